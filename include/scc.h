@@ -1,0 +1,142 @@
+/*
+ * scc.h — C ABI of the MI355X scConsensus engine (libscc.so).
+ *
+ * Drop-in boundary for the data-parallel core of the reference R package
+ * (bbbranjan/scConsensus).  The reference has no native code and no FFI
+ * (NAMESPACE:3-6 has no useDynLib); these entry points are what its R
+ * functions bind through `.Call` (see INTEGRATION.md for the R glue):
+ *
+ *   reclusterDEConsensusFast()  R/reclusterDEConsensusFast.R:22-33
+ *       pair loop + ComputePairWiseDE + union      :57-392  -> scc_de_run(SCC_DE_FAST)
+ *       prcomp_irlba + dist                         :398-400 -> scc_distance(SCC_DIST_PCA_EUCLID)
+ *       `1 - cor(...)` (commented alternative)      :403     -> scc_distance(SCC_DIST_PEARSON)
+ *       nodg loop                                   :440-443 -> scc_de_result_nodg
+ *   reclusterDEConsensus()      R/reclusterDEConsensus.R:20-29
+ *       global threshold + pair loop + union        :32-227  -> scc_de_run(SCC_DE_SLOW)
+ *       prcomp_irlba + dist                         :234-236 -> scc_distance(SCC_DIST_PCA_EUCLID)
+ *
+ * Conventions: plain pointers and sizes, no C++ types, int status returns
+ * (SCC_OK == 0), no exceptions or longjmp across the ABI.  Inputs are borrowed
+ * read-only; the caller owns every output buffer.  Cluster selection (R's
+ * table()/grepl("grey")/locale order, Fast:40-53) stays in the caller, which
+ * passes integer codes: code[c] in [0, K) in the reference's cluster order,
+ * or -1 for cells whose cluster is not compared.  Pairs are (i<j) in the
+ * reference's nested-loop order: p = i*K - i*(i+1)/2 + (j-i-1).
+ */
+#ifndef SCC_H
+#define SCC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#define SCC_API __attribute__((visibility("default")))
+#else
+#define SCC_API
+#endif
+
+#define SCC_OK 0
+#define SCC_ERR_INVALID 1     /* bad argument / shape */
+#define SCC_ERR_HIP 2         /* HIP runtime error (no device, launch failure) */
+#define SCC_ERR_OOM 3         /* device allocation failed */
+#define SCC_ERR_NONFINITE 4   /* input holds NaN/Inf or out-of-range row index */
+#define SCC_ERR_RSTOP 5       /* the reference R code would stop() on this input */
+#define SCC_ERR_UNSUPPORTED 6 /* valid input outside this build's limits (e.g. K > 64) */
+
+#define SCC_DE_FAST 0 /* reclusterDEConsensusFast(method = "wilcox") */
+#define SCC_DE_SLOW 1 /* reclusterDEConsensus(method = "Wilcoxon") */
+
+#define SCC_DIST_PCA_EUCLID 0 /* dist(prcomp_irlba(t(X[U,]), n=min(|U|,15))$x) */
+#define SCC_DIST_PEARSON 1    /* as.dist(1 - cor(X[U,], method = "pearson")) */
+
+#define SCC_PTR_HOST 0   /* pointers are host memory (copied H2D by the engine) */
+#define SCC_PTR_DEVICE 1 /* pointers are device memory of the context's device */
+
+typedef struct scc_ctx scc_ctx;
+typedef struct scc_dataset scc_dataset;
+typedef struct scc_de_result scc_de_result;
+
+typedef struct {
+    int32_t device;      /* HIP device ordinal */
+    int32_t profile;     /* 1: time the dominant kernels with HIP events */
+    int32_t reserved[6];
+} scc_opts;
+
+typedef struct {
+    int32_t mode;               /* SCC_DE_FAST | SCC_DE_SLOW */
+    int32_t top_n;              /* FAST: NumbertopDEGenes (Fast:32); SLOW: 30 (slow:218) */
+    double q_val_thrs;          /* qValThrs */
+    double log_fc_thrs;         /* FAST: logFCThrs, natural log (Fast:26) */
+    double min_per_cent;        /* FAST: minPerCent (Fast:29) */
+    double fc_thrs;             /* SLOW: fcThrs, compared as log(fcThrs) (slow:167) */
+    double mean_scaling_factor; /* SLOW: meanScalingFactor (slow:23) */
+} scc_de_params;
+
+/* ---- context ---------------------------------------------------------- */
+SCC_API int scc_ctx_create(const scc_opts* opts, scc_ctx** out);
+SCC_API void scc_ctx_destroy(scc_ctx* ctx);
+SCC_API const char* scc_ctx_last_error(const scc_ctx* ctx);
+SCC_API int scc_ctx_synchronize(scc_ctx* ctx);
+/* Kernel timing (opts.profile = 1): total ms and launch count of a named
+ * kernel family since the last reset ("gene_rank", "dist", "gram", ...). */
+SCC_API int scc_ctx_kernel_time(const scc_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+SCC_API void scc_ctx_reset_timers(scc_ctx* ctx);
+
+/* ---- dataset: the genes x cells matrix as R holds it ------------------- */
+/* dgCMatrix (CSC over cells): indptr[N+1] (R @p), rows[nnz] (R @i, 0-based
+ * gene rows), vals[nnz] (R @x).  Replaces as.matrix(dataMatrix) (Fast:368). */
+SCC_API int scc_dataset_create_csc(scc_ctx* ctx, const int64_t* indptr, const int32_t* rows, const double* vals,
+                           int64_t n_genes, int64_t n_cells, int64_t nnz, int32_t ptr_kind,
+                           scc_dataset** out);
+/* base R matrix: G x N column-major doubles (slow:32 as.matrix). */
+SCC_API int scc_dataset_create_dense(scc_ctx* ctx, const double* x_colmajor, int64_t n_genes, int64_t n_cells,
+                             int32_t ptr_kind, scc_dataset** out);
+SCC_API void scc_dataset_destroy(scc_dataset* ds);
+
+/* ---- stage 1+2: per-cluster statistics, all-pairs Wilcoxon, BH, union --- */
+SCC_API int scc_de_run(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
+               const scc_de_params* params, scc_de_result** out);
+
+/* n_pairs = K(K-1)/2; n_rows = FAST tested rows over all pairs (0 for SLOW);
+ * n_union = |deGeneUnion|. */
+SCC_API int scc_de_result_counts(const scc_de_result* r, int32_t* n_pairs, int64_t* n_rows, int32_t* n_union);
+/* deGeneUnion as 0-based gene rows, in the reference's order (Fast:392 / slow:224). */
+SCC_API int scc_de_result_union(const scc_de_result* r, int32_t* genes);
+/* FAST rows, pair-major, inside a pair in R's order(p, -avg_logFC) (Fast:346):
+ * every tested feature of every pair.  flags bit0 = kept DE row
+ * (pair has > 1 row and q < qValThrs, Fast:376-377), bit1 = survives
+ * top_n (Fast:391).  u2 = 2 * W (W = wilcox STATISTIC); ties = sum(t^3 - t).
+ * Any pointer may be NULL. */
+SCC_API int scc_de_result_rows(const scc_de_result* r, int32_t* pair_rows /* [n_pairs] */, int32_t* gene,
+                       double* p, double* q, double* avg_logfc, double* pct1, double* pct2, int64_t* u2,
+                       int64_t* ties, uint8_t* flags);
+/* SLOW per-pair full vectors [n_pairs][G] (the qValueList/logFCList RDS dumps,
+ * slow:181-184,200-202) plus p, u2 and de (0/1).  Any pointer may be NULL. */
+SCC_API int scc_de_result_pair_vectors(const scc_de_result* r, double* p, double* q, double* logfc, int64_t* u2,
+                               uint8_t* de);
+/* log(meanScalingFactor * mean(expm1(X))) used by SLOW (slow:36,111). */
+SCC_API int scc_de_result_log_threshold(const scc_de_result* r, double* log_thr);
+/* nodg: number of genes with x > 0 per cell, all cells (Fast:440-443). */
+SCC_API int scc_de_result_nodg(const scc_de_result* r, int32_t* nodg /* [N] */);
+SCC_API void scc_de_result_destroy(scc_de_result* r);
+
+/* ---- stage 3: cell x cell distance on the DE-gene union ---------------- */
+/* Packed lower triangle in R `dist` order (column-major: (1,0),(2,0),...,
+ * (N-1,0),(2,1),...), length N(N-1)/2.  out_kind SCC_PTR_HOST copies to the
+ * caller's host buffer; SCC_PTR_DEVICE writes a device buffer of the ctx
+ * device (dist_out == NULL: the engine keeps it HBM-resident in its own
+ * workspace, valid until the next call).  ncomp <= 0 means min(n_union, 15) (Fast:398).  out_f32 != 0 writes
+ * float instead of double. */
+SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */, int32_t n_union,
+                 int32_t metric, int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32);
+/* PCA scores (N x ncomp, row-major) of the last PCA distance call. */
+SCC_API int scc_last_pca_scores(const scc_ctx* ctx, double* scores, int32_t* ncomp);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCC_H */

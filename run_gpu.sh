@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU session script: each GPU step under its own time limit; stop at the first
+# fault / abort / timeout (exit codes other than 0 = pass, 1 = test failures).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+mkdir -p gpurun_out
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name" ; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
+    testsall) step testsall 900 python -m pytest tests -m gpu -q ;;
+    bench) step bench 900 python bench.py ;;
+    benchq) step benchq 600 python bench.py --no-cpu-baseline ;;
+    prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,293 @@
+"""ctypes binding of ``lib/libscc.so`` — the C ABI declared in ``include/scc.h``.
+
+There is no fallback: if the HIP library is missing this module raises, and if
+no MI355X is visible ``Engine()`` raises ``SccError(SCC_ERR_HIP)``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libscc.so")
+
+SCC_OK = 0
+SCC_ERR_INVALID = 1
+SCC_ERR_HIP = 2
+SCC_ERR_OOM = 3
+SCC_ERR_NONFINITE = 4
+SCC_ERR_RSTOP = 5
+SCC_ERR_UNSUPPORTED = 6
+SCC_DE_FAST = 0
+SCC_DE_SLOW = 1
+SCC_DIST_PCA_EUCLID = 0
+SCC_DIST_PEARSON = 1
+SCC_PTR_HOST = 0
+SCC_PTR_DEVICE = 1
+
+# every symbol include/scc.h declares (tests check the library exports them all)
+EXPORTS = [
+    "scc_ctx_create", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_kernel_time",
+    "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_dense", "scc_dataset_destroy",
+    "scc_de_run", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
+    "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
+    "scc_distance", "scc_last_pca_scores",
+]
+
+
+class SccError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"scc error {code}: {msg}")
+        self.code = code
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("profile", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+
+
+class DeParams(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("top_n", ctypes.c_int32), ("q_val_thrs", ctypes.c_double),
+                ("log_fc_thrs", ctypes.c_double), ("min_per_cent", ctypes.c_double), ("fc_thrs", ctypes.c_double),
+                ("mean_scaling_factor", ctypes.c_double)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `python -m scconsensus_amd.build` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    P = ctypes.POINTER
+    i32, i64, dbl, u8 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_uint8
+    sig = {
+        "scc_ctx_create": (ctypes.c_int, [P(Opts), P(vp)]),
+        "scc_ctx_destroy": (None, [vp]),
+        "scc_ctx_last_error": (ctypes.c_char_p, [vp]),
+        "scc_ctx_synchronize": (ctypes.c_int, [vp]),
+        "scc_ctx_kernel_time": (ctypes.c_int, [vp, ctypes.c_char_p, P(dbl), P(i64)]),
+        "scc_ctx_reset_timers": (None, [vp]),
+        "scc_dataset_create_csc": (ctypes.c_int, [vp, vp, vp, vp, i64, i64, i64, i32, P(vp)]),
+        "scc_dataset_create_dense": (ctypes.c_int, [vp, vp, i64, i64, i32, P(vp)]),
+        "scc_dataset_destroy": (None, [vp]),
+        "scc_de_run": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), P(vp)]),
+        "scc_de_result_counts": (ctypes.c_int, [vp, P(i32), P(i64), P(i32)]),
+        "scc_de_result_union": (ctypes.c_int, [vp, vp]),
+        "scc_de_result_rows": (ctypes.c_int, [vp] + [vp] * 10),
+        "scc_de_result_pair_vectors": (ctypes.c_int, [vp] + [vp] * 5),
+        "scc_de_result_log_threshold": (ctypes.c_int, [vp, P(dbl)]),
+        "scc_de_result_nodg": (ctypes.c_int, [vp, vp]),
+        "scc_de_result_destroy": (None, [vp]),
+        "scc_distance": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp, i32, i32]),
+        "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+@dataclass
+class FastRows:
+    pair_tested: np.ndarray
+    row_pair: np.ndarray
+    gene: np.ndarray
+    p: np.ndarray
+    q: np.ndarray
+    avg_logfc: np.ndarray
+    pct1: np.ndarray
+    pct2: np.ndarray
+    u2: np.ndarray
+    ties: np.ndarray
+    de: np.ndarray
+    top: np.ndarray
+
+
+@dataclass
+class DeResult:
+    mode: int
+    K: int
+    n_pairs: int
+    union: np.ndarray
+    nodg: np.ndarray
+    rows: FastRows | None = None       # FAST
+    p: np.ndarray | None = None        # [P, G]
+    q: np.ndarray | None = None        # SLOW [P, G]
+    logfc: np.ndarray | None = None    # [P, G]
+    u2: np.ndarray | None = None       # [P, G]
+    de: np.ndarray | None = None       # SLOW [P, G]
+    log_thr: float = 0.0
+    status: int = 0
+    message: str = ""
+
+
+class Dataset:
+    def __init__(self, engine, handle, G, N):
+        self.engine, self.handle, self.G, self.N = engine, handle, G, N
+
+    def close(self):
+        if self.handle:
+            self.engine.lib.scc_dataset_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One MI355X device (``device`` = HIP ordinal)."""
+
+    def __init__(self, device: int = 0, profile: bool = False):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        o = Opts(device, 1 if profile else 0)
+        rc = self.lib.scc_ctx_create(ctypes.byref(o), ctypes.byref(h))
+        if rc != SCC_OK:
+            raise SccError(rc, "scc_ctx_create failed (no HIP device?)")
+        self.ctx = h
+        self._keep = []
+
+    def close(self):
+        if self.ctx:
+            self.lib.scc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != SCC_OK:
+            raise SccError(rc, self.lib.scc_ctx_last_error(self.ctx).decode())
+
+    # -------------------------------------------------------------- datasets
+    def dataset_csc(self, indptr, rows, vals, G, N) -> Dataset:
+        indptr = np.ascontiguousarray(indptr, np.int64)
+        rows = np.ascontiguousarray(rows, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        h = ctypes.c_void_p()
+        self._check(self.lib.scc_dataset_create_csc(self.ctx, _ptr(indptr), _ptr(rows), _ptr(vals), G, N, len(vals),
+                                                    SCC_PTR_HOST, ctypes.byref(h)))
+        return Dataset(self, h, G, N)
+
+    def dataset_csc_device(self, indptr_ptr, rows_ptr, vals_ptr, G, N, nnz) -> Dataset:
+        h = ctypes.c_void_p()
+        self._check(self.lib.scc_dataset_create_csc(self.ctx, ctypes.c_void_p(indptr_ptr), ctypes.c_void_p(rows_ptr),
+                                                    ctypes.c_void_p(vals_ptr), G, N, nnz, SCC_PTR_DEVICE,
+                                                    ctypes.byref(h)))
+        return Dataset(self, h, G, N)
+
+    def dataset_dense(self, X_gene_major) -> Dataset:
+        """X as a genes x cells array; passed to the engine in R's column-major layout."""
+        X = np.asarray(X_gene_major, np.float64)
+        G, N = X.shape
+        col = np.ascontiguousarray(X.T)  # N x G row-major == G x N column-major
+        h = ctypes.c_void_p()
+        self._check(self.lib.scc_dataset_create_dense(self.ctx, _ptr(col), G, N, SCC_PTR_HOST, ctypes.byref(h)))
+        return Dataset(self, h, G, N)
+
+    # -------------------------------------------------------------- DE
+    def de_run(self, ds: Dataset, code, K, mode=SCC_DE_FAST, q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0,
+               top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all") -> DeResult:
+        code = np.ascontiguousarray(code, np.int32)
+        prm = DeParams(mode, top_n, q_val_thrs, log_fc_thrs, min_per_cent, fc_thrs, mean_scaling_factor)
+        r = ctypes.c_void_p()
+        rc = self.lib.scc_de_run(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), ctypes.byref(r))
+        msg = ""
+        if rc != SCC_OK:
+            msg = self.lib.scc_ctx_last_error(self.ctx).decode()
+            if not r.value:
+                raise SccError(rc, msg)
+        try:
+            npairs, nrows, nu = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int32()
+            self._check(self.lib.scc_de_result_counts(r, ctypes.byref(npairs), ctypes.byref(nrows), ctypes.byref(nu)))
+            uni = np.zeros(nu.value, np.int32)
+            self._check(self.lib.scc_de_result_union(r, _ptr(uni)))
+            out = DeResult(mode, K, npairs.value, uni, np.zeros(0, np.int32), status=rc, message=msg)
+            if fetch == "union":
+                return out
+            nodg = np.zeros(ds.N, np.int32)
+            self._check(self.lib.scc_de_result_nodg(r, _ptr(nodg)))
+            out.nodg = nodg
+            P, G = npairs.value, ds.G
+            if mode == SCC_DE_FAST:
+                n = nrows.value
+                tested = np.zeros(P, np.int32)
+                a = dict(gene=np.zeros(n, np.int32), p=np.zeros(n), q=np.zeros(n), lfc=np.zeros(n),
+                         pct1=np.zeros(n), pct2=np.zeros(n), u2=np.zeros(n, np.int64), t=np.zeros(n, np.int64),
+                         fl=np.zeros(n, np.uint8))
+                self._check(self.lib.scc_de_result_rows(r, _ptr(tested), _ptr(a["gene"]), _ptr(a["p"]), _ptr(a["q"]),
+                                                        _ptr(a["lfc"]), _ptr(a["pct1"]), _ptr(a["pct2"]),
+                                                        _ptr(a["u2"]), _ptr(a["t"]), _ptr(a["fl"])))
+                out.rows = FastRows(tested, np.repeat(np.arange(P, dtype=np.int32), tested), a["gene"], a["p"],
+                                    a["q"], a["lfc"], a["pct1"], a["pct2"], a["u2"], a["t"], (a["fl"] & 1) > 0,
+                                    (a["fl"] & 2) > 0)
+                if fetch == "all":
+                    pv, lf, u2 = np.zeros((P, G)), np.zeros((P, G)), np.zeros((P, G), np.int64)
+                    self._check(self.lib.scc_de_result_pair_vectors(r, _ptr(pv), None, _ptr(lf), _ptr(u2), None))
+                    out.p, out.logfc, out.u2 = pv, lf, u2
+            else:
+                pv, qv, lf = np.zeros((P, G)), np.zeros((P, G)), np.zeros((P, G))
+                u2, de = np.zeros((P, G), np.int64), np.zeros((P, G), np.uint8)
+                self._check(self.lib.scc_de_result_pair_vectors(r, _ptr(pv), _ptr(qv), _ptr(lf), _ptr(u2), _ptr(de)))
+                out.p, out.q, out.logfc, out.u2, out.de = pv, qv, lf, u2, de
+                lt = ctypes.c_double()
+                self._check(self.lib.scc_de_result_log_threshold(r, ctypes.byref(lt)))
+                out.log_thr = lt.value
+            return out
+        finally:
+            self.lib.scc_de_result_destroy(r)
+
+    # -------------------------------------------------------------- distance
+    def distance(self, ds: Dataset, genes, metric=SCC_DIST_PCA_EUCLID, ncomp=0, out=None, f32=False,
+                 device_out_ptr=None):
+        genes = np.ascontiguousarray(genes, np.int32)
+        N = ds.N
+        npairs = N * (N - 1) // 2
+        if device_out_ptr is not None:  # 0 -> engine-owned HBM-resident output
+            self._check(self.lib.scc_distance(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp,
+                                              ctypes.c_void_p(device_out_ptr or None), SCC_PTR_DEVICE,
+                                              1 if f32 else 0))
+            return None
+        if out is None:
+            out = np.empty(npairs, np.float32 if f32 else np.float64)
+        self._check(self.lib.scc_distance(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, _ptr(out),
+                                          SCC_PTR_HOST, 1 if f32 else 0))
+        return out
+
+    def last_pca_scores(self, N):
+        k = ctypes.c_int32()
+        self._check(self.lib.scc_last_pca_scores(self.ctx, None, ctypes.byref(k)))
+        s = np.zeros((N, k.value))
+        self._check(self.lib.scc_last_pca_scores(self.ctx, _ptr(s), ctypes.byref(k)))
+        return s
+
+    # -------------------------------------------------------------- timers
+    def kernel_time(self, name):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._check(self.lib.scc_ctx_kernel_time(self.ctx, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def reset_timers(self):
+        self.lib.scc_ctx_reset_timers(self.ctx)
+
+    def synchronize(self):
+        self._check(self.lib.scc_ctx_synchronize(self.ctx))

@@ -1,0 +1,178 @@
+"""Host-side mirror of the reference R API (same names, argument meaning and
+error behaviour), running the data-parallel core on the MI355X engine.
+
+Reference signatures:
+  reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method = "wilcox",
+      qValThrs = 0.1, logFCThrs = 0.5, deepSplitValues = 1:4, minClusterSize = 10,
+      minPerCent = 20, filename = "de_gene_object.rds", plotName = "DE_Heatmap",
+      NumbertopDEGenes = 30, nCores = 1)              R/reclusterDEConsensusFast.R:22-33
+  reclusterDEConsensus(dataMatrix, consensusClusterLabels, method = "Wilcoxon",
+      meanScalingFactor = 5, qValThrs, fcThrs, deepSplitValues = 1:4,
+      minClusterSize = 10, filename = "de_gene_object.rds", plotName = "DE_Heatmap")
+                                                       R/reclusterDEConsensus.R:20-29
+
+What runs where: cluster selection (A0), printing and the
+saved object stay on the host like in R; the pairwise DE, BH/filters/union and
+the distance matrix run in libscc on the GPU; hclust(ward.D2) runs on the host
+(scipy's Ward linkage == R's "ward.D2") as the reference keeps it on the host.
+dynamicTreeCut::cutreeDynamic / WGCNA::labels2colors and the ComplexHeatmap
+plot are not part of this engine; ``dynamicColors`` is returned
+as ``None`` and ``plotName`` is ignored.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native as nat
+
+_ENGINES: dict = {}
+
+
+def _engine(device: int = 0) -> nat.Engine:
+    if device not in _ENGINES:
+        _ENGINES[device] = nat.Engine(device)
+    return _ENGINES[device]
+
+
+def select_clusters(labels, min_cluster_size: int, cluster_order=None):
+    """A0 (Fast:40-53, slow:39-54): table(labels); keep count > minClusterSize;
+    drop names containing "grey".  Returns (names, code[N]) with code = -1 for
+    cells not compared.  R orders table() names by the locale's collation;
+    the default here is code-point order (R's C locale) — pass
+    ``cluster_order`` to reproduce another collation."""
+    labels = np.asarray(labels).astype(str)
+    names, counts = np.unique(labels, return_counts=True)
+    if cluster_order is not None:
+        pos = {n: i for i, n in enumerate(cluster_order)}
+        idx = sorted(range(len(names)), key=lambda i: pos.get(names[i], len(pos) + i))
+        names, counts = names[idx], counts[idx]
+    keep = [str(n) for n, c in zip(names, counts) if c > min_cluster_size and "grey" not in str(n)]
+    lut = {n: i for i, n in enumerate(keep)}
+    code = np.fromiter((lut.get(s, -1) for s in labels), np.int32, len(labels))
+    return keep, code
+
+
+def _as_matrix(dataMatrix):
+    """Accept scipy.sparse (genes x cells), numpy dense (genes x cells) or a
+    synth.Dataset; return ('csc', indptr, rows, vals, G, N) or ('dense', X)."""
+    try:
+        import scipy.sparse as sp
+        if sp.issparse(dataMatrix):
+            m = dataMatrix.tocsc()
+            m.sort_indices()
+            return "csc", m.indptr.astype(np.int64), m.indices.astype(np.int32), m.data.astype(np.float64), \
+                m.shape[0], m.shape[1]
+    except ImportError:  # pragma: no cover
+        pass
+    if hasattr(dataMatrix, "indptr") and hasattr(dataMatrix, "labels"):
+        d = dataMatrix
+        return "csc", d.indptr, d.indices, d.data, d.G, d.N
+    X = np.asarray(dataMatrix, np.float64)
+    return "dense", X
+
+
+def _upload(eng, m):
+    if m[0] == "csc":
+        _, indptr, rows, vals, G, N = m
+        return eng.dataset_csc(indptr, rows, vals, G, N)
+    return eng.dataset_dense(m[1])
+
+
+def _hclust_ward_d2(dist_packed, N):
+    from scipy.cluster.hierarchy import linkage
+    return linkage(dist_packed, method="ward", preserve_input=True) if N > 1 else None
+
+
+def _save(obj, filename):
+    if not filename:
+        return
+    import pickle
+    with open(filename if filename.endswith(".pkl") else filename + ".pkl", "wb") as f:
+        pickle.dump(obj, f)
+
+
+def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox", qValThrs=0.1, logFCThrs=0.5,
+                             deepSplitValues=(1, 2, 3, 4), minClusterSize=10, minPerCent=20,
+                             filename="de_gene_object.rds", plotName="DE_Heatmap", NumbertopDEGenes=30, nCores=1,
+                             *, gene_names=None, cluster_order=None, device=0, save=False, return_details=False):
+    if method != "wilcox":
+        # Fast:306-333: "bimod"/"roc" need Seurat helpers the reference never
+        # loads; "t" is SURVEY §8(f) "next".
+        raise NotImplementedError(f"Unknown test: {method} (this engine implements test.use = 'wilcox')")
+    eng = _engine(device)
+    m = _as_matrix(dataMatrix)
+    N = m[-1] if m[0] == "csc" else m[1].shape[1]
+    G = m[-2] if m[0] == "csc" else m[1].shape[0]
+    names, code = select_clusters(consensusClusterLabels, minClusterSize, cluster_order)
+    if len(names) < 2:
+        raise ValueError("need at least two clusters with > minClusterSize cells")
+    ds = _upload(eng, m)
+    res = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
+                     min_per_cent=float(minPerCent), top_n=NumbertopDEGenes,
+                     fetch="rows" if return_details else "union")
+    if res.status == nat.SCC_ERR_RSTOP:
+        raise RuntimeError(res.message)
+    uni = res.union
+    gnames = np.asarray(gene_names if gene_names is not None else [f"gene{g}" for g in range(G)], dtype=object)
+    print(f" chr [1:{len(uni)}] " + " ".join(f'"{g}"' for g in gnames[uni[:5]]) + (" ..." if len(uni) > 5 else ""))
+    if len(uni) == 0:
+        raise RuntimeError("no DE genes (R fails on an empty deGenes data frame, Fast:386)")
+    d = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
+    tree = _hclust_ward_d2(d, N)
+    ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree, "dynamicColors": None}
+    if save:
+        _save(ret, filename)
+    if return_details:
+        ret["_details"] = {"clusters": names, "code": code, "de": res, "dist": d, "union_idx": uni}
+    ds.close()
+    return ret
+
+
+def reclusterDEConsensus(dataMatrix, consensusClusterLabels, method="Wilcoxon", meanScalingFactor=5, qValThrs=None,
+                         fcThrs=None, deepSplitValues=(1, 2, 3, 4), minClusterSize=10, filename="de_gene_object.rds",
+                         plotName="DE_Heatmap", *, gene_names=None, cluster_order=None, device=0, save=False,
+                         return_details=False):
+    if qValThrs is None or fcThrs is None:
+        raise TypeError('argument "qValThrs"/"fcThrs" is missing, with no default')
+    if method == "edgeR":
+        raise NotImplementedError("edgeR branch stays on the host in the reference design (SURVEY D3)")
+    if method != "Wilcoxon":
+        print("Incorrect method chosen.")  # slow:158-161
+        return None
+    eng = _engine(device)
+    m = _as_matrix(dataMatrix)
+    N = m[-1] if m[0] == "csc" else m[1].shape[1]
+    G = m[-2] if m[0] == "csc" else m[1].shape[0]
+    names, code = select_clusters(consensusClusterLabels, minClusterSize, cluster_order)
+    if len(names) < 2:
+        raise ValueError("need at least two clusters with > minClusterSize cells")
+    ds = _upload(eng, m)
+    res = eng.de_run(ds, code, len(names), nat.SCC_DE_SLOW, q_val_thrs=qValThrs, fc_thrs=fcThrs,
+                     mean_scaling_factor=float(meanScalingFactor), fetch="all")
+    if res.status == nat.SCC_ERR_RSTOP:
+        raise RuntimeError(res.message)
+    gnames = np.asarray(gene_names if gene_names is not None else [f"gene{g}" for g in range(G)], dtype=object)
+    K = len(names)
+    p = 0
+    qlist, lflist, delist = {}, {}, {}
+    for i in range(K - 1):
+        for j in range(i + 1, K):
+            n_de = int((res.de[p] == 1).sum())
+            print(f"{names[i]}, {names[j]} DE genes: {n_de}")  # slow:172-178
+            qlist[(names[i], names[j])] = res.q[p]
+            lflist[(names[i], names[j])] = res.logfc[p]
+            delist[(names[i], names[j])] = list(gnames[res.de[p] == 1])
+            p += 1
+    uni = res.union
+    if len(uni) == 0:
+        raise RuntimeError("empty DE gene union")
+    d = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
+    tree = _hclust_ward_d2(d, N)
+    ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree, "dynamicColors": None}
+    if save:
+        _save({"qValueList": qlist, "logFCList": lflist, "deGeneList": delist}, "de_lists")
+        _save(ret, filename)
+    if return_details:
+        ret["_details"] = {"clusters": names, "code": code, "de": res, "dist": d, "union_idx": uni}
+    ds.close()
+    return ret

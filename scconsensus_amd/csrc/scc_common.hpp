@@ -1,0 +1,187 @@
+// scc_common.hpp — device helpers shared by the scConsensus MI355X engine.
+//
+// Everything here is compiled with -ffp-contract=off: the compensated (double-
+// double) sums and the R-order p-value arithmetic depend on un-fused rounding.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned long long u64;
+typedef long long i64;
+typedef uint32_t u32;
+typedef uint8_t u8;
+
+#define SCC_WAVE 64
+
+// ------------------------------------------------------------ orderable keys
+// Bijective map fp64 -> u64 whose unsigned order is the IEEE total order for
+// finite values (-0 and +0 never reach it: zeros are the implicit tie group).
+__host__ __device__ inline u64 scc_key_of(double v)
+{
+    u64 b = (u64)__double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__host__ __device__ inline double scc_val_of(u64 k)
+{
+    u64 b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double((long long)b);
+}
+
+// ------------------------------------------------------------ double-double
+struct dd {
+    double hi, lo;
+};
+__device__ inline dd dd_two_sum(double a, double b)
+{
+    double s = a + b;
+    double bb = s - a;
+    double e = (a - (s - bb)) + (b - bb);
+    return dd{s, e};
+}
+__device__ inline dd dd_fast_two_sum(double a, double b)
+{
+    double s = a + b;
+    double e = b - (s - a);
+    return dd{s, e};
+}
+__device__ inline dd dd_add_d(dd x, double y)
+{
+    dd s = dd_two_sum(x.hi, y);
+    s.lo += x.lo;
+    return dd_fast_two_sum(s.hi, s.lo);
+}
+__device__ inline dd dd_add(dd x, dd y)
+{
+    dd s = dd_two_sum(x.hi, y.hi);
+    dd t = dd_two_sum(x.lo, y.lo);
+    s.lo += t.hi;
+    s = dd_fast_two_sum(s.hi, s.lo);
+    s.lo += t.lo;
+    return dd_fast_two_sum(s.hi, s.lo);
+}
+// (hi + lo) / n rounded to double (one correction step; exact enough that the
+// result is the correctly rounded mean except in measure-zero cases).
+__device__ inline double dd_div_n(dd x, double n)
+{
+    double q = x.hi / n;
+    double r = fma(-q, n, x.hi);  // exact remainder of hi - q*n
+    r += x.lo;
+    return q + r / n;
+}
+
+__device__ inline dd dd_shfl_xor(dd x, int m)
+{
+    return dd{__shfl_xor(x.hi, m, SCC_WAVE), __shfl_xor(x.lo, m, SCC_WAVE)};
+}
+// Deterministic butterfly: every lane ends with the same value.
+__device__ inline dd dd_wave_sum(dd x)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x = dd_add(x, dd_shfl_xor(x, m));
+    return x;
+}
+__device__ inline u64 u64_wave_sum(u64 x)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, SCC_WAVE);
+    return x;
+}
+__device__ inline u32 u32_wave_sum(u32 x)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, SCC_WAVE);
+    return x;
+}
+
+__host__ __device__ inline int scc_next_pow2(int n)
+{
+    int m = 1;
+    while (m < n) m <<= 1;
+    return m;
+}
+
+// ------------------------------------------------------------ pair indexing
+// Pairs (i<j) enumerated as R's nested loops: p = i*K - i*(i+1)/2 + (j-i-1).
+__host__ __device__ inline int scc_pair_index(int i, int j, int K)
+{
+    return i * K - i * (i + 1) / 2 + (j - i - 1);
+}
+
+// ------------------------------------------------------------ pnorm (R)
+// Two-sided normal p-value 2*min(pnorm(z), pnorm(z, lower.tail=FALSE)) with the
+// same evaluation as R's nmath/pnorm.c (Cody 1993, ACM TOMS 715), including its
+// underflow cut-offs (|z| >= 37.5193 -> 0).
+__device__ inline double scc_pnorm_small_tail(double z)
+{
+    // returns min(pnorm(z), pnorm(-z)) i.e. the tail beyond |z|, NaN for NaN
+    const double A[5] = {2.2352520354606839287, 161.02823106855587881, 1067.6894854603709582,
+                         18154.981253343561249, 0.065682337918207449113};
+    const double B[4] = {47.20258190468824187, 976.09855173777669322, 10260.932208618978205,
+                         45507.789335026729956};
+    const double C[9] = {0.39894151208813466764, 8.8831497943883759412, 93.506656132177855979,
+                         597.27027639480026226, 2494.5375852903726711, 6848.1904505362823326,
+                         11602.651437647350124, 9842.7148383839780218, 1.0765576773720192317e-8};
+    const double D[8] = {22.266688044328115691, 235.38790178262499861, 1519.377599407554805,
+                         6485.558298266760755, 18615.571640885098091, 34900.952721145977266,
+                         38912.003286093271411, 19685.429676859990727};
+    const double P[6] = {0.21589853405795699, 0.1274011611602473639, 0.022235277870649807,
+                         0.001421619193227893466, 2.9112874951168792e-5, 0.02307344176494017303};
+    const double Q[5] = {1.28426009614491121, 0.468238212480865118, 0.0659881378689285515,
+                         0.00378239633202758244, 7.29751555083966205e-5};
+    if (z != z) return z;
+    // R evaluates pnorm(z) (lower) and pnorm(z, lower=FALSE) (upper) separately;
+    // the smaller one is the tail on the far side of 0.  Restate each branch of
+    // pnorm_both for that tail with the same operation order.
+    double y = fabs(z);
+    double cum, ccum, temp, xnum, xden, xsq, del;
+    if (y <= 0.67448975) {
+        const double eps = 1.1102230246251565e-16;  // DBL_EPSILON * 0.5
+        if (y > eps) {
+            xsq = z * z;
+            xnum = A[4] * xsq;
+            xden = xsq;
+            for (int i = 0; i < 3; ++i) {
+                xnum = (xnum + A[i]) * xsq;
+                xden = (xden + B[i]) * xsq;
+            }
+        } else {
+            xnum = xden = 0.0;
+        }
+        temp = z * (xnum + A[3]) / (xden + B[3]);
+        cum = 0.5 + temp;
+        ccum = 0.5 - temp;
+        return cum < ccum ? cum : ccum;
+    } else if (y <= 5.656854249492380195206754896838) {
+        xnum = C[8] * y;
+        xden = y;
+        for (int i = 0; i < 7; ++i) {
+            xnum = (xnum + C[i]) * y;
+            xden = (xden + D[i]) * y;
+        }
+        temp = (xnum + C[7]) / (xden + D[7]);
+        xsq = trunc(y * 16.0) / 16.0;
+        del = (y - xsq) * (y + xsq);
+        cum = exp(-xsq * xsq * 0.5) * exp(-del * 0.5) * temp;
+        ccum = 1.0 - cum;
+        // cum is the tail beyond |z| on the far side; R swaps for z > 0 so the
+        // small tail is cum either way.
+        return cum < ccum ? cum : ccum;
+    } else {
+        // lower tail of z<0 valid for -37.5193 < z; upper tail of z>0 valid for z < 37.5193
+        if (!(y < 37.5193)) return 0.0;
+        double x = z;
+        xsq = 1.0 / (x * x);
+        xnum = P[5] * xsq;
+        xden = xsq;
+        for (int i = 0; i < 4; ++i) {
+            xnum = (xnum + P[i]) * xsq;
+            xden = (xden + Q[i]) * xsq;
+        }
+        temp = xsq * (xnum + P[4]) / (xden + Q[4]);
+        temp = (0.398942280401432677939946059934 - temp) / y;
+        xsq = trunc(x * 16.0) / 16.0;
+        del = (x - xsq) * (x + xsq);
+        cum = exp(-xsq * xsq * 0.5) * exp(-del * 0.5) * temp;
+        return cum;  // the small tail (R: cum for x<0, swapped into ccum for x>0)
+    }
+}

@@ -1,0 +1,389 @@
+// scc_dist.hip — stage 3: cell x cell distance on the DE-gene union.
+//
+// Reference: pca.data <- irlba::prcomp_irlba(t(X[U, ]), n = min(|U|, 15),
+// center = TRUE)$x; d <- dist(pca.data, "euclidean")
+// (R/reclusterDEConsensusFast.R:398-400; R/reclusterDEConsensus.R:234-236) and
+// the commented alternative as.dist(1 - cor(X[U, ])) (Fast:403, slow:239).
+//
+// Kernels
+//   k_gather_*      X[U, ] -> Xc (N x nu_pad, row-major fp64, zero padded)
+//   k_colsum/center R colMeans (LDOUBLE sum restated as double-double) and centring
+//   k_gram_f64      C = Xc^T Xc, fp64 MFMA (v_mfma_f64_16x16x4_f64), split over
+//                   cell chunks into slabs reduced in a fixed order (deterministic)
+//   k_scores        P = Xc V_k (N x 16, zero padded components)
+//   k_dist_euclid   packed lower triangle in R `dist` order; per element the
+//                   same sum of squared differences in component order + sqrt
+//   k_zscore / k_pearson_f32   Pearson: per-cell centring/scaling, then an
+//                   LDS-tiled FP32 MFMA (v_mfma_f32_32x32x2_f32) Gram with the
+//                   1 - r epilogue fused into the packed-triangle store.
+#include "scc_common.hpp"
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------ gather
+__global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indptr, const int* __restrict__ rows,
+                                                    const double* __restrict__ vals, int N,
+                                                    const int* __restrict__ umap, int ld, double* __restrict__ Xc)
+{
+    const int lane = threadIdx.x & 63;
+    const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int nw = gridDim.x * (blockDim.x >> 6);
+    for (int c = wid; c < N; c += nw) {
+        for (i64 k = indptr[c] + lane; k < indptr[c + 1]; k += 64) {
+            const int u = umap[rows[k]];
+            if (u >= 0) Xc[(size_t)c * ld + u] = vals[k];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gather_dense(const double* __restrict__ X, int G, int N,
+                                                      const int* __restrict__ genes, int nu, int ld,
+                                                      double* __restrict__ Xc)
+{
+    const size_t total = (size_t)N * nu;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e / nu), u = (int)(e % nu);
+        Xc[(size_t)c * ld + u] = X[(size_t)c * G + genes[u]];
+    }
+}
+
+// column sums in dd: grid (ceil(ld/256), nchunk); partial[chunk][u]
+__global__ void __launch_bounds__(256) k_colsum(const double* __restrict__ Xc, int N, int ld, int rows_per_chunk,
+                                                dd* __restrict__ part)
+{
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= ld) return;
+    const int c0 = blockIdx.y * rows_per_chunk, c1 = min(N, c0 + rows_per_chunk);
+    dd s{0.0, 0.0};
+    for (int c = c0; c < c1; ++c) s = dd_add_d(s, Xc[(size_t)c * ld + u]);
+    part[(size_t)blockIdx.y * ld + u] = s;
+}
+
+__global__ void __launch_bounds__(256) k_colmean(const dd* __restrict__ part, int nchunk, int ld, int N,
+                                                 double* __restrict__ mean)
+{
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= ld) return;
+    dd s{0.0, 0.0};
+    for (int k = 0; k < nchunk; ++k) s = dd_add(s, part[(size_t)k * ld + u]);
+    mean[u] = dd_div_n(s, (double)N);
+}
+
+__global__ void __launch_bounds__(256) k_center(double* __restrict__ Xc, int N, int nu, int ld,
+                                                const double* __restrict__ mean)
+{
+    const size_t total = (size_t)N * ld;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int u = (int)(e % ld);
+        if (u < nu) Xc[e] -= mean[u];
+    }
+}
+
+// ------------------------------------------------------------------ Gram (fp64 MFMA)
+// WG = 4 waves -> 64x64 tile of C (upper tiles only); wave -> 32x32 = 2x2 MFMA
+// 16x16x4 tiles.  Lane l holds A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15];
+// accumulator reg r is C[row = (l>>4) + 4r][col = l&15] (f64 layout).
+__global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc, int Npad, int ld, int ntile,
+                                                  int rows_per_chunk, double* __restrict__ slabs)
+{
+    // upper-triangular tile index -> (ti, tj), ti <= tj
+    int t = blockIdx.x, ti = 0;
+    while (t >= ntile - ti) {
+        t -= ntile - ti;
+        ++ti;
+    }
+    const int tj = ti + t;
+    const int chunk = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wi = (w >> 1) * 32, wj = (w & 1) * 32;
+    const int i0 = ti * 64 + wi, j0 = tj * 64 + wj;
+    const int c0 = chunk * rows_per_chunk, c1 = min(Npad, c0 + rows_per_chunk);
+    d4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int kr = lane >> 4, cc = lane & 15;
+    for (int c = c0; c < c1; c += 4) {
+        const double* row = Xc + (size_t)(c + kr) * ld;
+        const double a0 = row[i0 + cc], a1 = row[i0 + 16 + cc];
+        const double b0 = row[j0 + cc], b1 = row[j0 + 16 + cc];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    double* S = slabs + (size_t)chunk * ld * ld;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = i0 + a * 16 + kr + 4 * r;
+                const int col = j0 + b * 16 + cc;
+                S[(size_t)row * ld + col] = acc[a][b][r];
+            }
+}
+
+// C[i][j] = sum_k slabs[k][i][j] in chunk order for tiles ti <= tj, mirrored
+__global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ slabs, int nchunk, int ld,
+                                                     double* __restrict__ C)
+{
+    const size_t total = (size_t)ld * ld;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(e / ld), j = (int)(e % ld);
+        const int ti = i >> 6, tj = j >> 6;
+        const size_t src = (ti <= tj) ? e : ((size_t)j * ld + i);
+        double s = 0.0;
+        for (int k = 0; k < nchunk; ++k) s += slabs[(size_t)k * total + src];
+        C[e] = s;
+    }
+}
+
+// ------------------------------------------------------------------ scores
+// P[c][q] = sum_u Xc[c][u] * Z[u][q]; Z row-major [u][16] (PC1 first, columns
+// q >= k are zero).
+__global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, int N, int nu, int ld,
+                                                const double* __restrict__ Z16, int k, double* __restrict__ P)
+{
+    __shared__ double sv[64][16];
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+    for (int u0 = 0; u0 < nu; u0 += 64) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+            const int uu = e / 16, q = e % 16;
+            const int u = u0 + uu;
+            sv[uu][q] = (u < nu && q < k) ? Z16[(size_t)u * 16 + q] : 0.0;
+        }
+        __syncthreads();
+        if (c < N) {
+            const int ue = min(64, nu - u0);
+            const double* row = Xc + (size_t)c * ld + u0;
+            for (int uu = 0; uu < ue; ++uu) {
+                const double x = row[uu];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[q] = fma(x, sv[uu][q], acc[q]);
+            }
+        }
+    }
+    if (c < N) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) P[(size_t)c * 16 + q] = acc[q];
+    }
+}
+
+// ------------------------------------------------------------------ Euclidean dist
+// Tile = 256 rows (i) x 64 columns (j); stores for one column j are contiguous
+// in the packed R order: out[j*(2N-j-1)/2 + (i - j - 1)], i > j.
+template <bool F32>
+__global__ void __launch_bounds__(256) k_dist_euclid(const double* __restrict__ P, int N, void* __restrict__ out)
+{
+    __shared__ double sp[64][17];
+    const int rb = blockIdx.x, cb = blockIdx.y;
+    const int i = rb * 256 + threadIdx.x;
+    const int j0 = cb * 64;
+    if (rb * 256 + 255 <= j0) return;  // tile entirely on/above the diagonal
+    for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+        const int jj = e >> 4, q = e & 15;
+        const int j = j0 + jj;
+        sp[jj][q] = (j < N) ? P[(size_t)j * 16 + q] : 0.0;
+    }
+    double pi[16];
+    if (i < N) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) pi[q] = P[(size_t)i * 16 + q];
+    }
+    __syncthreads();
+    if (i >= N) return;
+    const int jend = min(min(N, j0 + 64), i);  // columns j < i only
+    for (int j = j0; j < jend; ++j) {
+        const int jj = j - j0;
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const double dv = pi[q] - sp[jj][q];
+            s += dv * dv;  // R: dist += dev * dev (no FMA contraction)
+        }
+        const double d = sqrt(s);
+        const size_t o = (size_t)j * (2 * (size_t)N - j - 1) / 2 + (size_t)(i - j - 1);
+        if (F32)
+            ((float*)out)[o] = (float)d;
+        else
+            ((double*)out)[o] = d;
+    }
+}
+
+// ------------------------------------------------------------------ Pearson
+// Z[c][u] = (x - mean_c) / sqrt(sum (x - mean_c)^2), fp32, padded to ldz
+__global__ void __launch_bounds__(256) k_zscore(const double* __restrict__ Xc, int N, int nu, int ld, int ldz,
+                                                float* __restrict__ Z)
+{
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= N) return;
+    const double* row = Xc + (size_t)c * ld;
+    dd s{0.0, 0.0};
+    for (int u = lane; u < nu; u += 64) s = dd_add_d(s, row[u]);
+    s = dd_wave_sum(s);
+    const double mean = dd_div_n(s, (double)nu);
+    dd ss{0.0, 0.0};
+    for (int u = lane; u < nu; u += 64) {
+        const double d = row[u] - mean;
+        ss = dd_add_d(ss, d * d);
+    }
+    ss = dd_wave_sum(ss);
+    const double inv = (ss.hi > 0.0) ? 1.0 / sqrt(ss.hi + ss.lo) : 0.0;
+    for (int u = lane; u < ldz; u += 64) Z[(size_t)c * ldz + u] = (u < nu) ? (float)((row[u] - mean) * inv) : 0.0f;
+}
+
+// 128 x 128 output tile per WG (4 waves, 64x64 each = 2x2 tiles of 32x32),
+// K staged through LDS in 16-wide steps.  v_mfma_f32_32x32x2_f32: lane l holds
+// A[i = l&31][k = l>>5], B[k = l>>5][j = l&31]; accumulator reg r is
+// C[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
+template <bool F32>
+__global__ void __launch_bounds__(256) k_pearson_f32(const float* __restrict__ Z, int N, int ldz, int ntile,
+                                                     void* __restrict__ out)
+{
+    // lower-triangular tile index (ti >= tj)
+    int t = blockIdx.x, ti = 0;
+    while (t > ti) {
+        t -= ti + 1;
+        ++ti;
+    }
+    const int tj = t;
+    (void)ntile;
+    __shared__ float sa[16][128 + 4];
+    __shared__ float sb[16][128 + 4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
+    const int I0 = ti * 128, J0 = tj * 128;
+    f16v acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+    for (int k0 = 0; k0 < ldz; k0 += 16) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 16 * 128; e += 256) {
+            const int rr = e >> 4, kk = e & 15;  // row within tile, k within step
+            const int gi = I0 + rr, gj = J0 + rr;
+            sa[kk][rr] = (gi < N) ? Z[(size_t)gi * ldz + k0 + kk] : 0.0f;
+            sb[kk][rr] = (gj < N) ? Z[(size_t)gj * ldz + k0 + kk] : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 2) {
+            const int kq = kk + (lane >> 5);
+            const float a0 = sa[kq][wi + (lane & 31)], a1 = sa[kq][wi + 32 + (lane & 31)];
+            const float b0 = sb[kq][wj + (lane & 31)], b1 = sb[kq][wj + 32 + (lane & 31)];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+    }
+    // epilogue: 1 - r for i > j, packed R order
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = I0 + wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int j = J0 + wj + b * 32 + (lane & 31);
+                if (i < N && j < i) {
+                    const size_t o = (size_t)j * (2 * (size_t)N - j - 1) / 2 + (size_t)(i - j - 1);
+                    const float d = 1.0f - acc[a][b][r];
+                    if (F32)
+                        ((float*)out)[o] = d;
+                    else
+                        ((double*)out)[o] = (double)d;
+                }
+            }
+}
+
+// ------------------------------------------------------------------ launchers
+extern "C" hipError_t scc_launch_union_map(int* umap, int G, const int* genes, int nu, hipStream_t st);
+
+__global__ void k_umap(int* umap, const int* genes, int nu)
+{
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < nu) umap[genes[u]] = u;
+}
+
+extern "C" hipError_t scc_launch_union_map(int* umap, int G, const int* genes, int nu, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(umap, 0xFF, sizeof(int) * G, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_umap, dim3((nu + 255) / 256), dim3(256), 0, st, umap, genes, nu);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, const double* vals, const double* dense,
+                                        int G, int N, const int* umap, const int* genes, int nu, int ld, double* Xc,
+                                        hipStream_t st)
+{
+    if (dense)
+        hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
+    else
+        hipLaunchKernelGGL(k_gather_csc, dim3(1024), dim3(256), 0, st, indptr, rows, vals, N, umap, ld, Xc);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nchunk, double* mean,
+                                        hipStream_t st)
+{
+    const int rpc = (N + nchunk - 1) / nchunk;
+    hipLaunchKernelGGL(k_colsum, dim3((ld + 255) / 256, nchunk), dim3(256), 0, st, Xc, N, ld, rpc, part);
+    hipLaunchKernelGGL(k_colmean, dim3((ld + 255) / 256), dim3(256), 0, st, part, nchunk, ld, N, mean);
+    hipLaunchKernelGGL(k_center, dim3(4096), dim3(256), 0, st, Xc, N, nu, ld, mean);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C,
+                                      hipStream_t st)
+{
+    const int ntile = ld / 64;
+    const int rpc = ((Npad + nchunk - 1) / nchunk + 3) & ~3;
+    hipLaunchKernelGGL(k_gram_f64, dim3(ntile * (ntile + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, ntile, rpc,
+                       slabs);
+    hipLaunchKernelGGL(k_gram_reduce, dim3(2048), dim3(256), 0, st, slabs, nchunk, ld, C);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
+                                        hipStream_t st)
+{
+    hipLaunchKernelGGL(k_scores, dim3((N + 255) / 256), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, void* out, int f32, hipStream_t st)
+{
+    dim3 grid((N + 255) / 256, (N + 63) / 64);
+    if (f32)
+        hipLaunchKernelGGL(k_dist_euclid<true>, grid, dim3(256), 0, st, P, N, out);
+    else
+        hipLaunchKernelGGL(k_dist_euclid<false>, grid, dim3(256), 0, st, P, N, out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, void* out,
+                                         int f32, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_zscore, dim3((N + 3) / 4), dim3(256), 0, st, Xc, N, nu, ld, ldz, Z);
+    const int nt = (N + 127) / 128;
+    const int ntri = nt * (nt + 1) / 2;
+    if (f32)
+        hipLaunchKernelGGL(k_pearson_f32<true>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, out);
+    else
+        hipLaunchKernelGGL(k_pearson_f32<false>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, out);
+    return hipGetLastError();
+}

@@ -1,0 +1,139 @@
+// scc_distance.cpp — C ABI for stage 3 (include/scc.h: scc_distance).
+//
+// PCA path (parity default, reference Fast:398-400): gather X[U, ] for ALL
+// cells, centre columns (R colMeans), fp64 MFMA Gram C = Xc^T Xc, top-k
+// eigenpairs of the |U| x |U| Gram (Householder + multisection + inverse
+// iteration, exact to fp64 backward error), scores
+// P = Xc V_k, then the packed Euclidean `dist`.  The eigensolve is this
+// engine's own single-workgroup dense solver (scc_eigen.hip), no vendor BLAS.  The exact truncated SVD is
+// the deterministic quantity irlba approximates.
+// Pearson path (reference Fast:403, commented out there): per-cell z-scores
+// over U and an FP32 MFMA Gram with the 1 - r epilogue fused into the store.
+#include "scc_internal.hpp"
+
+using namespace scc_rt;
+
+extern "C" {
+hipError_t scc_launch_union_map(int* umap, int G, const int* genes, int nu, hipStream_t st);
+hipError_t scc_launch_gather(const long long* indptr, const int* rows, const double* vals, const double* dense,
+                             int G, int N, const int* umap, const int* genes, int nu, int ld, double* Xc,
+                             hipStream_t st);
+hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nchunk, double* mean, hipStream_t st);
+hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C, hipStream_t st);
+hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
+                             hipStream_t st);
+hipError_t scc_launch_dist_euclid(const double* P, int N, void* out, int f32, hipStream_t st);
+hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, void* out, int f32,
+                              hipStream_t st);
+hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
+                                 hipStream_t st);
+}
+
+extern "C" void scc_distance_release(scc_ctx*) {}
+
+extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
+                            int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32)
+{
+    if (!c || !ds || !genes) return fail(c, SCC_ERR_INVALID, "scc_distance: null argument");
+    if (!dist_out && out_kind != SCC_PTR_DEVICE) return fail(c, SCC_ERR_INVALID, "scc_distance: null output");
+    if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
+    if (nu < 1) return fail(c, SCC_ERR_INVALID, "empty gene union");
+    if (metric != SCC_DIST_PCA_EUCLID && metric != SCC_DIST_PEARSON) return fail(c, SCC_ERR_INVALID, "bad metric");
+    const int G = (int)ds->G, N = (int)ds->N;
+    if (N < 2) return fail(c, SCC_ERR_INVALID, "need at least two cells");
+    for (int u = 0; u < nu; ++u)
+        if (genes[u] < 0 || genes[u] >= G) return fail(c, SCC_ERR_INVALID, "gene index out of range");
+    int k = ncomp > 0 ? ncomp : std::min(nu, 15);
+    if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    const int ld = (nu + 63) & ~63;
+    const int Npad = (N + 15) & ~15;
+    const size_t npairs = (size_t)N * (N - 1) / 2;
+    int rc;
+    int *d_genes, *d_umap;
+    double *d_X, *d_mean;
+    void* d_part;
+#define WS(name, n, ptr)                                       \
+    do {                                                       \
+        if ((rc = ws(c, name, (size_t)(n), &(ptr)))) return rc; \
+    } while (0)
+    WS("d_genes", nu, d_genes);
+    WS("d_umap", G, d_umap);
+    WS("d_X", (size_t)Npad * ld, d_X);
+    WS("d_mean", ld, d_mean);
+    const int nchunk_mean = 64;
+    if ((rc = ws_get(c, "d_part", sizeof(double) * 2 * (size_t)nchunk_mean * ld, &d_part))) return rc;
+    void* d_out = dist_out;
+    if (out_kind == SCC_PTR_HOST || !dist_out) {  // NULL device output: keep it in the workspace
+        if ((rc = ws_get(c, "d_dist", npairs * (out_f32 ? 4 : 8), &d_out))) return rc;
+    }
+    HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
+    {
+        Scope sc(c, "gather", s0);
+        HIPCHK(c, hipMemsetAsync(d_X, 0, sizeof(double) * (size_t)Npad * ld, s0));
+        HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
+        HIPCHK(c, scc_launch_gather(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, N, d_umap, d_genes, nu, ld,
+                                    d_X, s0));
+    }
+    if (metric == SCC_DIST_PCA_EUCLID) {
+        double *d_slabs, *d_C, *d_W, *d_Z, *d_P, *d_escr;
+        const int nchunk = std::max(1, std::min(32, Npad / 512));
+        WS("d_slabs", (size_t)nchunk * ld * ld, d_slabs);
+        WS("d_C", (size_t)ld * ld, d_C);
+        WS("d_W", ld, d_W);
+        WS("d_Z", (size_t)ld * 16, d_Z);
+        WS("d_P", (size_t)N * 16, d_P);
+        WS("d_escr", (size_t)84 * ld + 64, d_escr);
+        {
+            Scope sc(c, "center", s0);
+            HIPCHK(c, scc_launch_center(d_X, N, nu, ld, (dd*)d_part, nchunk_mean, d_mean, s0));
+        }
+        {
+            Scope sc(c, "gram", s0);
+            HIPCHK(c, scc_launch_gram(d_X, Npad, ld, nchunk, d_slabs, d_C, s0));
+        }
+        {
+            Scope sc(c, "eigen", s0);
+            HIPCHK(c, scc_launch_syevx_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, s0));
+        }
+        {
+            Scope sc(c, "scores", s0);
+            HIPCHK(c, scc_launch_scores(d_X, N, nu, ld, d_Z, k, d_P, s0));
+        }
+        {
+            Scope sc(c, "dist", s0);
+            HIPCHK(c, scc_launch_dist_euclid(d_P, N, d_out, out_f32, s0));
+        }
+        c->d_last_scores = d_P;
+        c->last_n = N;
+        c->last_ncomp = k;
+    } else {
+        float* d_Zp;
+        const int ldz = (nu + 15) & ~15;
+        WS("d_Zp", (size_t)N * ldz, d_Zp);
+        Scope sc(c, "pearson", s0);
+        HIPCHK(c, scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, d_out, out_f32, s0));
+    }
+    if (out_kind == SCC_PTR_HOST) {
+        HIPCHK(c, hipMemcpyAsync(dist_out, d_out, npairs * (out_f32 ? 4 : 8), hipMemcpyDeviceToHost, s0));
+    }
+    HIPCHK(c, hipStreamSynchronize(s0));
+    return SCC_OK;
+#undef WS
+}
+
+extern "C" int scc_last_pca_scores(const scc_ctx* c, double* scores, int32_t* ncomp)
+{
+    if (!c) return SCC_ERR_INVALID;
+    if (ncomp) *ncomp = c->last_ncomp;
+    if (scores && c->last_ncomp > 0 && c->d_last_scores) {
+        scc_ctx* cc = const_cast<scc_ctx*>(c);
+        hipSetDevice(c->device);
+        std::vector<double> buf((size_t)c->last_n * 16);
+        HIPCHK(cc, hipMemcpy(buf.data(), c->d_last_scores, sizeof(double) * buf.size(), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < (size_t)c->last_n; ++i)
+            for (int q = 0; q < c->last_ncomp; ++q) scores[i * c->last_ncomp + q] = buf[i * 16 + q];
+    }
+    return SCC_OK;
+}

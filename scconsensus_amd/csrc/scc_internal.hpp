@@ -1,0 +1,231 @@
+// scc_internal.hpp — runtime-internal state shared by the C ABI translation
+// units (scc_runtime.cpp: context/dataset/DE; scc_distance.cpp: stage 3).
+#pragma once
+#include "scc.h"
+#include "scc_kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace scc_rt {
+
+constexpr int kCapSmall = 2048;    // LDS rank kernel, 256 threads
+constexpr int kCapMedium = 12288;  // LDS rank kernel, 1024 threads
+constexpr int kChunkBig = 8192;    // staged sort chunk for larger genes
+constexpr int kSelectCap = 2048;   // per-pair records sorted in LDS
+constexpr int kUnionCap = 4096;
+constexpr int kMaxK = 64;
+
+struct Timer {
+    double ms = 0.0;
+    int64_t n = 0;
+};
+
+struct PendingEv {
+    std::string name;
+    hipEvent_t a, b;
+};
+
+}  // namespace scc_rt
+
+struct scc_ctx {
+    int device = 0;
+    hipStream_t s0 = nullptr, s1 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    std::string err;
+    // workspace slots (grow-only)
+    std::map<std::string, std::pair<void*, size_t>> ws;
+    // exact-test table
+    double* d_wtab = nullptr;
+    int* d_woff = nullptr;
+    bool wtab_ready = false;
+    // profiling
+    bool profile = false;
+    std::vector<scc_rt::PendingEv> pending;
+    std::vector<hipEvent_t> ev_pool;
+    std::map<std::string, scc_rt::Timer> timers;
+    uint64_t generation = 0;
+    // last PCA
+    const double* d_last_scores = nullptr;  // N x 16 in the workspace
+    int last_n = 0;
+    int last_ncomp = 0;
+};
+
+struct scc_dataset {
+    scc_ctx* ctx = nullptr;
+    int64_t G = 0, N = 0, nnz = 0;
+    bool dense = false;
+    long long* d_indptr = nullptr;
+    int* d_rows = nullptr;
+    double* d_vals = nullptr;
+    double* d_dense = nullptr;
+    bool owned = false;
+};
+
+struct scc_de_result {
+    scc_ctx* ctx = nullptr;
+    uint64_t generation = 0;
+    int mode = 0, K = 0, P = 0;
+    int64_t G = 0, N = 0;
+    int64_t n_rows = 0;
+    std::vector<int32_t> union_genes;
+    std::vector<int32_t> pair_tested;
+    double log_thr = 0.0;
+    // device views into the context workspace (valid while generation matches)
+    const int* d_nodg = nullptr;
+    const int* d_row_gene = nullptr;
+    const double *d_row_p = nullptr, *d_row_q = nullptr, *d_row_lfc = nullptr, *d_row_pct1 = nullptr,
+                 *d_row_pct2 = nullptr;
+    const long long *d_row_u2 = nullptr, *d_row_t = nullptr;
+    const uint8_t* d_row_flags = nullptr;
+    const double *d_p = nullptr, *d_q = nullptr, *d_lfc = nullptr;
+    const long long* d_u2 = nullptr;
+    const uint8_t* d_de = nullptr;
+};
+
+namespace scc_rt {
+
+inline int fail(scc_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                              \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess)                                                                          \
+            return fail((ctx), SCC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
+    } while (0)
+
+// grow-only named workspace buffer
+inline int ws_get(scc_ctx* c, const char* name, size_t bytes, void** out)
+{
+    bytes = std::max<size_t>(bytes, 256);
+    auto it = c->ws.find(name);
+    if (it != c->ws.end() && it->second.second >= bytes) {
+        *out = it->second.first;
+        return SCC_OK;
+    }
+    if (it != c->ws.end()) {
+        hipStreamSynchronize(c->s0);
+        hipStreamSynchronize(c->s1);
+        hipFree(it->second.first);
+        c->ws.erase(it);
+    }
+    void* p = nullptr;
+    size_t grow = bytes + bytes / 8;
+    if (hipMalloc(&p, grow) != hipSuccess) {
+        hipGetLastError();
+        return fail(c, SCC_ERR_OOM, std::string("hipMalloc failed for workspace ") + name);
+    }
+    c->ws[name] = {p, grow};
+    *out = p;
+    return SCC_OK;
+}
+
+template <class T>
+inline int ws(scc_ctx* c, const char* name, size_t count, T** out)
+{
+    void* p = nullptr;
+    int rc = ws_get(c, name, count * sizeof(T), &p);
+    *out = (T*)p;
+    return rc;
+}
+
+inline hipEvent_t ev_take(scc_ctx* c)
+{
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+inline int env_int(const char* name, int dflt)
+{
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+// SCC_DEBUG_SYNC=1: synchronise after every stage and report it on stderr
+// (locates a faulting kernel; never set in timed runs).
+inline bool debug_sync()
+{
+    static int v = env_int("SCC_DEBUG_SYNC", 0);
+    return v != 0;
+}
+
+struct Scope {
+    scc_ctx* c;
+    const char* name;
+    hipStream_t st;
+    hipEvent_t a = nullptr;
+    Scope(scc_ctx* c_, const char* n, hipStream_t s) : c(c_), name(n), st(s)
+    {
+        if (c->profile) {
+            a = ev_take(c);
+            hipEventRecord(a, st);
+        }
+        if (debug_sync()) fprintf(stderr, "[scc] %s: start\n", name);
+    }
+    ~Scope()
+    {
+        if (c->profile) {
+            hipEvent_t b = ev_take(c);
+            hipEventRecord(b, st);
+            c->pending.push_back({name, a, b});
+        }
+        if (debug_sync()) {
+            hipError_t e0 = hipStreamSynchronize(c->s0), e1 = hipStreamSynchronize(c->s1);
+            fprintf(stderr, "[scc] %s: done (%s / %s)\n", name, hipGetErrorString(e0), hipGetErrorString(e1));
+            fflush(stderr);
+        }
+    }
+};
+
+inline void resolve_timers(scc_ctx* c)
+{
+    if (c->pending.empty()) return;
+    hipStreamSynchronize(c->s0);
+    hipStreamSynchronize(c->s1);
+    for (auto& pe : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            auto& t = c->timers[pe.name];
+            t.ms += ms;
+            t.n += 1;
+        }
+        c->ev_pool.push_back(pe.a);
+        c->ev_pool.push_back(pe.b);
+    }
+    c->pending.clear();
+}
+
+inline int ensure_wtab(scc_ctx* c)
+{
+    if (c->wtab_ready) return SCC_OK;
+    std::vector<int> woff(50 * 50);
+    const int total = scc_wilcox_table_layout(woff.data());
+    int rc = ws(c, "wtab", (size_t)total, &c->d_wtab);
+    if (rc) return rc;
+    rc = ws(c, "woff", woff.size(), &c->d_woff);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_woff, woff.data(), woff.size() * sizeof(int), hipMemcpyHostToDevice, c->s0));
+    HIPCHK(c, scc_launch_wilcox_table(c->d_wtab, c->d_woff, c->s0));
+    c->wtab_ready = true;
+    return SCC_OK;
+}
+
+}  // namespace scc_rt

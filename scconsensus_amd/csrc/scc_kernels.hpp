@@ -1,0 +1,112 @@
+// scc_kernels.hpp — internal launcher interface between the runtime
+// (scc_runtime.cpp) and the HIP kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#ifndef SCC_DE_FAST
+#define SCC_DE_FAST 0
+#define SCC_DE_SLOW 1
+#endif
+
+struct dd;
+
+struct ScRankLaunch {
+    const int* gene_list;
+    const int* list_count;
+    const long long* seg_off;
+    unsigned long long* keys;
+    uint8_t* codes_scratch;
+    int G, K, cap, grid;
+    const int* n_clu;
+    double* mean_x;
+    double* mean_e;
+    uint32_t* cnt_pos;
+    long long* u2_base;
+    long long* t_base;
+    unsigned long long* tie_e;
+    unsigned long long* tie_x;
+};
+
+struct ScTestLaunch {
+    int K, G, P, mode;
+    double min_pct, lfc_thr, log_thr;
+    const int* n_clu;
+    const double* mean_x;
+    const double* mean_e;
+    const uint32_t* cnt_pos;
+    const long long* u2_base;
+    const long long* t_base;
+    const unsigned long long* tie_e;
+    const unsigned long long* tie_x;
+    const double* wtab;
+    const int* woff;
+    double* out_p;
+    double* out_lfc;
+    double* out_pct1;
+    double* out_pct2;
+    long long* out_u2;
+    long long* out_t;
+    uint8_t* out_flags;
+};
+
+struct ScSelectLaunch {
+    int K, G, P, mode, top_n, cap;
+    double q_thr, lfc_cut;
+    const double* p;
+    const double* lfc;
+    const double* pct1;
+    const double* pct2;
+    const long long* u2;
+    const long long* t;
+    const uint8_t* flags;
+    const long long* row_off;
+    void* rec_scratch;
+    void* key_scratch;
+    int* row_gene;
+    double* row_p;
+    double* row_q;
+    double* row_lfc;
+    double* row_pct1;
+    double* row_pct2;
+    long long* row_u2;
+    long long* row_t;
+    uint8_t* row_flags;
+    double* slow_q;
+    uint8_t* slow_de;
+    unsigned long long* first_occ;
+    int* err;
+};
+
+extern "C" {
+hipError_t scc_launch_ingest_count(const long long* indptr, const int* rows, const double* vals,
+                                   const double* dense, int N, int G, int K, const int* code, uint32_t* cnt,
+                                   uint32_t* neg, int* nodg, dd* wave_expm1, int nwaves, int want_expm1, int* err,
+                                   hipStream_t st);
+hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, const double* vals,
+                                     const double* dense, int N, int G, int K, const int* code,
+                                     const long long* seg_off, uint32_t* cursor, unsigned long long* keys,
+                                     int nwaves, hipStream_t st);
+hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
+                           long long* total, hipStream_t st);
+int scc_scan_scratch_blocks(long long n);
+hipError_t scc_launch_reduce_dd(const dd* parts, int n, dd* out, hipStream_t st);
+
+hipError_t scc_launch_classify(const long long* seg_off, int G, int K, int cap_s, int cap_m, int* lists,
+                               int* counts, hipStream_t st);
+size_t scc_rank_lds_bytes(int cls, int cap, int K);
+hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st);
+
+hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st);
+int scc_wilcox_table_layout(int* woff);
+hipError_t scc_launch_pair_test(const ScTestLaunch* L, hipStream_t st);
+hipError_t scc_launch_count_tested(const uint8_t* flags, int G, int P, int* tested, long long* row_off,
+                                   hipStream_t st);
+size_t scc_select_lds_bytes(int cap);
+size_t scc_select_rec_bytes(void);
+size_t scc_select_key_bytes(void);
+hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_t st);
+hipError_t scc_launch_union(const unsigned long long* first_occ, int G, void* scratch, int cap, int* out,
+                            int* n_out, hipStream_t st);
+}

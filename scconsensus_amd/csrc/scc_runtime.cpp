@@ -1,0 +1,566 @@
+// scc_runtime.cpp — host runtime behind the C ABI (include/scc.h).
+//
+// Owns the HIP device, two streams, a grow-only HBM workspace, the exact
+// Wilcoxon count table, and optional HIP-event kernel timers.  The whole DE
+// stage is one stream-ordered launch sequence (the bigger genes run on a side
+// stream concurrently with the LDS-resident ones); the host synchronises once
+// per call to read the union size.  No CPU fallback exists: without a HIP
+// device every entry point returns SCC_ERR_HIP.
+#include "scc_internal.hpp"
+
+using namespace scc_rt;
+
+// ====================================================================== ctx
+extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
+{
+    if (!out) return SCC_ERR_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        hipGetLastError();
+        return SCC_ERR_HIP;
+    }
+    scc_ctx* c = new scc_ctx();
+    c->device = opts ? opts->device : 0;
+    c->profile = opts ? (opts->profile != 0) : false;
+    if (c->device < 0 || c->device >= ndev) {
+        delete c;
+        return SCC_ERR_INVALID;
+    }
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->s0, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s1, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipGetLastError();
+        delete c;
+        return SCC_ERR_HIP;
+    }
+    *out = c;
+    return SCC_OK;
+}
+
+extern "C" void scc_distance_release(scc_ctx* c);
+
+extern "C" void scc_ctx_destroy(scc_ctx* c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    scc_distance_release(c);
+    hipStreamSynchronize(c->s0);
+    hipStreamSynchronize(c->s1);
+    for (auto& kv : c->ws) hipFree(kv.second.first);
+    for (auto& pe : c->pending) {
+        hipEventDestroy(pe.a);
+        hipEventDestroy(pe.b);
+    }
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    hipEventDestroy(c->ev_fork);
+    hipEventDestroy(c->ev_join);
+    hipStreamDestroy(c->s0);
+    hipStreamDestroy(c->s1);
+    delete c;
+}
+
+extern "C" const char* scc_ctx_last_error(const scc_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int scc_ctx_synchronize(scc_ctx* c)
+{
+    if (!c) return SCC_ERR_INVALID;
+    hipSetDevice(c->device);
+    HIPCHK(c, hipStreamSynchronize(c->s0));
+    HIPCHK(c, hipStreamSynchronize(c->s1));
+    return SCC_OK;
+}
+
+extern "C" int scc_ctx_kernel_time(const scc_ctx* cc, const char* name, double* total_ms, int64_t* launches)
+{
+    scc_ctx* c = const_cast<scc_ctx*>(cc);
+    if (!c || !name) return SCC_ERR_INVALID;
+    hipSetDevice(c->device);
+    resolve_timers(c);
+    auto it = c->timers.find(name);
+    if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.ms;
+    if (launches) *launches = it == c->timers.end() ? 0 : it->second.n;
+    return SCC_OK;
+}
+
+extern "C" void scc_ctx_reset_timers(scc_ctx* c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    resolve_timers(c);
+    c->timers.clear();
+}
+
+// ====================================================================== dataset
+extern "C" int scc_dataset_create_csc(scc_ctx* c, const int64_t* indptr, const int32_t* rows, const double* vals,
+                                      int64_t G, int64_t N, int64_t nnz, int32_t kind, scc_dataset** out)
+{
+    if (!c || !out || !indptr || G <= 0 || N <= 0 || nnz < 0 || (nnz > 0 && (!rows || !vals)))
+        return fail(c, SCC_ERR_INVALID, "scc_dataset_create_csc: bad arguments");
+    if (G > INT32_MAX || N > INT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "dimensions exceed int32");
+    hipSetDevice(c->device);
+    scc_dataset* d = new scc_dataset();
+    d->ctx = c;
+    d->G = G;
+    d->N = N;
+    d->nnz = nnz;
+    if (kind == SCC_PTR_DEVICE) {
+        d->d_indptr = (long long*)indptr;
+        d->d_rows = (int*)rows;
+        d->d_vals = (double*)vals;
+        d->owned = false;
+    } else {
+        d->owned = true;
+        if (hipMalloc(&d->d_indptr, sizeof(long long) * (N + 1)) != hipSuccess ||
+            hipMalloc(&d->d_rows, sizeof(int) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
+            hipMalloc(&d->d_vals, sizeof(double) * std::max<int64_t>(nnz, 1)) != hipSuccess) {
+            hipGetLastError();
+            scc_dataset_destroy(d);
+            return fail(c, SCC_ERR_OOM, "dataset allocation failed");
+        }
+        hipMemcpyAsync(d->d_indptr, indptr, sizeof(long long) * (N + 1), hipMemcpyHostToDevice, c->s0);
+        if (nnz > 0) {
+            hipMemcpyAsync(d->d_rows, rows, sizeof(int) * nnz, hipMemcpyHostToDevice, c->s0);
+            hipMemcpyAsync(d->d_vals, vals, sizeof(double) * nnz, hipMemcpyHostToDevice, c->s0);
+        }
+        if (hipStreamSynchronize(c->s0) != hipSuccess) {
+            hipGetLastError();
+            scc_dataset_destroy(d);
+            return fail(c, SCC_ERR_HIP, "dataset upload failed");
+        }
+    }
+    *out = d;
+    return SCC_OK;
+}
+
+extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, int64_t N, int32_t kind,
+                                        scc_dataset** out)
+{
+    if (!c || !out || !x || G <= 0 || N <= 0) return fail(c, SCC_ERR_INVALID, "scc_dataset_create_dense: bad arguments");
+    if (G > INT32_MAX || N > INT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "dimensions exceed int32");
+    hipSetDevice(c->device);
+    scc_dataset* d = new scc_dataset();
+    d->ctx = c;
+    d->G = G;
+    d->N = N;
+    d->nnz = G * N;
+    d->dense = true;
+    if (kind == SCC_PTR_DEVICE) {
+        d->d_dense = (double*)x;
+    } else {
+        d->owned = true;
+        if (hipMalloc(&d->d_dense, sizeof(double) * G * N) != hipSuccess) {
+            hipGetLastError();
+            delete d;
+            return fail(c, SCC_ERR_OOM, "dataset allocation failed");
+        }
+        if (hipMemcpy(d->d_dense, x, sizeof(double) * G * N, hipMemcpyHostToDevice) != hipSuccess) {
+            hipGetLastError();
+            scc_dataset_destroy(d);
+            return fail(c, SCC_ERR_HIP, "dataset upload failed");
+        }
+    }
+    *out = d;
+    return SCC_OK;
+}
+
+extern "C" void scc_dataset_destroy(scc_dataset* d)
+{
+    if (!d) return;
+    if (d->owned) {
+        hipSetDevice(d->ctx->device);
+        hipStreamSynchronize(d->ctx->s0);
+        hipFree(d->d_indptr);
+        hipFree(d->d_rows);
+        hipFree(d->d_vals);
+        hipFree(d->d_dense);
+    }
+    delete d;
+}
+
+// ====================================================================== DE
+extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                          const scc_de_params* prm, scc_de_result** out)
+{
+    if (!c || !ds || !code || !prm || !out) return fail(c, SCC_ERR_INVALID, "scc_de_run: null argument");
+    *out = nullptr;
+    if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
+    if (prm->mode != SCC_DE_FAST && prm->mode != SCC_DE_SLOW) return fail(c, SCC_ERR_INVALID, "bad mode");
+    if (K < 2) return fail(c, SCC_ERR_INVALID, "need at least two clusters");
+    if (K > kMaxK) return fail(c, SCC_ERR_UNSUPPORTED, "K > 64 clusters is not supported by this build");
+    hipSetDevice(c->device);
+    const int G = (int)ds->G, N = (int)ds->N, P = K * (K - 1) / 2;
+    const bool fast = prm->mode == SCC_DE_FAST;
+    // cluster sizes (host: the codes are a host array at the R boundary)
+    std::vector<int> nclu(K, 0);
+    for (int i = 0; i < N; ++i) {
+        const int a = code[i];
+        if (a < -1 || a >= K) return fail(c, SCC_ERR_INVALID, "code out of range");
+        if (a >= 0) nclu[a]++;
+    }
+    for (int a = 0; a < K; ++a) {
+        if (nclu[a] == 0) return fail(c, SCC_ERR_INVALID, "empty cluster");
+        // ComputePairWiseDE: min.cells.group = 3 (Fast:76,208-213)
+        if (fast && nclu[a] < 3) return fail(c, SCC_ERR_RSTOP, "cluster has fewer than 3 cells (R stop())");
+    }
+    const int64_t GK = (int64_t)G * K;
+    const size_t PG = (size_t)P * G;
+    int rc;
+    int *d_code, *d_nclu, *d_nodg, *d_lists, *d_counts, *d_err, *d_tested, *d_union, *d_nu;
+    uint32_t *d_cnt, *d_neg, *d_cursor, *d_cntpos;
+    long long *d_segoff, *d_scan, *d_rowoff;
+    unsigned long long* d_keys;
+    uint8_t* d_codes;
+    dd* d_wexp;
+    dd* d_gexp;
+    double *d_mx, *d_me;
+    long long *d_u2b, *d_tb, *d_u2, *d_t;
+    unsigned long long *d_tie_e, *d_tie_x, *d_first;
+    double *d_p, *d_lfc, *d_pct1, *d_pct2;
+    uint8_t* d_flags;
+    const int nwaves = 4096;
+#define WS(name, n, ptr)                                  \
+    do {                                                  \
+        if ((rc = ws(c, name, (size_t)(n), &(ptr)))) return rc; \
+    } while (0)
+    WS("code", N, d_code);
+    WS("nclu", K, d_nclu);
+    WS("nodg", N, d_nodg);
+    WS("cnt", GK, d_cnt);
+    WS("neg", GK, d_neg);
+    WS("cursor", GK, d_cursor);
+    WS("segoff", GK + 1, d_segoff);
+    WS("scan", scc_scan_scratch_blocks(GK) + 1, d_scan);
+    WS("keys", std::max<int64_t>(ds->nnz, 1), d_keys);
+    WS("codes", std::max<int64_t>(ds->nnz, 1), d_codes);
+    {
+        void* p;
+        if ((rc = ws_get(c, "wexp", sizeof(double) * 2 * (nwaves + 1), &p))) return rc;
+        d_wexp = (dd*)p;
+        d_gexp = (dd*)((char*)p + sizeof(double) * 2 * nwaves);
+    }
+    WS("lists", 3 * (size_t)G, d_lists);
+    WS("counts", 4, d_counts);
+    WS("err", 4, d_err);
+    WS("mx", GK, d_mx);
+    WS("me", GK, d_me);
+    WS("cntpos", GK, d_cntpos);
+    WS("u2b", PG, d_u2b);
+    WS("tb", PG, d_tb);
+    WS("tie_e", PG, d_tie_e);
+    WS("tie_x", PG, d_tie_x);
+    WS("p", PG, d_p);
+    WS("lfc", PG, d_lfc);
+    WS("pct1", fast ? PG : 1, d_pct1);
+    WS("pct2", fast ? PG : 1, d_pct2);
+    WS("u2", PG, d_u2);
+    WS("t", PG, d_t);
+    WS("flags", PG, d_flags);
+    WS("tested", P, d_tested);
+    WS("rowoff", P + 1, d_rowoff);
+    WS("first", G, d_first);
+    WS("union", G, d_union);
+    WS("nu", 4, d_nu);
+    if ((rc = ensure_wtab(c))) return rc;
+    hipStream_t s0 = c->s0, s1 = c->s1;
+    c->generation++;
+
+    HIPCHK(c, hipMemcpyAsync(d_code, code, sizeof(int) * N, hipMemcpyHostToDevice, s0));
+    HIPCHK(c, hipMemcpyAsync(d_nclu, nclu.data(), sizeof(int) * K, hipMemcpyHostToDevice, s0));
+    {
+        Scope sc(c, "ingest", s0);
+        HIPCHK(c, hipMemsetAsync(d_cnt, 0, sizeof(uint32_t) * GK, s0));
+        HIPCHK(c, hipMemsetAsync(d_neg, 0, sizeof(uint32_t) * GK, s0));
+        HIPCHK(c, hipMemsetAsync(d_cursor, 0, sizeof(uint32_t) * GK, s0));
+        HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
+        HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 4, s0));
+        HIPCHK(c, scc_launch_ingest_count(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, K, d_code, d_cnt,
+                                          d_neg, d_nodg, d_wexp, nwaves, fast ? 0 : 1, d_err, s0));
+        HIPCHK(c, scc_launch_scan(d_cnt, GK, d_segoff, d_scan, d_segoff + GK, s0));
+        HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, K, d_code,
+                                            d_segoff, d_cursor, d_keys, nwaves, s0));
+        if (!fast) HIPCHK(c, scc_launch_reduce_dd(d_wexp, nwaves, d_gexp, s0));
+    }
+    {
+        Scope sc(c, "gene_rank", s0);
+        HIPCHK(c, hipMemsetAsync(d_tie_e, 0, sizeof(unsigned long long) * PG, s0));
+        HIPCHK(c, hipMemsetAsync(d_tie_x, 0, sizeof(unsigned long long) * PG, s0));
+        // size classes (env overrides exist to exercise the big-gene path on small test data)
+        const int cap_s = env_int("SCC_CAP_SMALL", kCapSmall), cap_m = env_int("SCC_CAP_MEDIUM", kCapMedium);
+        const int chunk_big = env_int("SCC_CHUNK_BIG", kChunkBig);
+        HIPCHK(c, scc_launch_classify(d_segoff, G, K, cap_s, cap_m, d_lists, d_counts, s0));
+        HIPCHK(c, hipEventRecord(c->ev_fork, s0));
+        HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
+        ScRankLaunch L{};
+        L.seg_off = d_segoff;
+        L.keys = d_keys;
+        L.codes_scratch = d_codes;
+        L.G = G;
+        L.K = K;
+        L.n_clu = d_nclu;
+        L.mean_x = d_mx;
+        L.mean_e = d_me;
+        L.cnt_pos = d_cntpos;
+        L.u2_base = d_u2b;
+        L.t_base = d_tb;
+        L.tie_e = d_tie_e;
+        L.tie_x = d_tie_x;
+        L.grid = G;
+        // big genes first on the side stream
+        L.gene_list = d_lists + 2 * (size_t)G;
+        L.list_count = d_counts + 2;
+        L.cap = chunk_big;
+        HIPCHK(c, scc_launch_gene_rank(2, &L, s1));
+        L.gene_list = d_lists + (size_t)G;
+        L.list_count = d_counts + 1;
+        L.cap = cap_m;
+        HIPCHK(c, scc_launch_gene_rank(1, &L, s0));
+        L.gene_list = d_lists;
+        L.list_count = d_counts;
+        L.cap = cap_s;
+        HIPCHK(c, scc_launch_gene_rank(0, &L, s0));
+        HIPCHK(c, hipEventRecord(c->ev_join, s1));
+        HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
+    }
+    // SLOW: log(meanScalingFactor * mean(expm1(X))) on device would need one
+    // more kernel; it is a scalar, read back together with the union below.
+    double log_thr = 0.0;
+    if (!fast) {
+        double gx[2];
+        HIPCHK(c, hipMemcpyAsync(gx, d_gexp, sizeof(double) * 2, hipMemcpyDeviceToHost, s0));
+        HIPCHK(c, hipStreamSynchronize(s0));
+        // R: LDOUBLE two-pass mean over G*N entries (zeros included) -> double
+        const double tot = (double)G * (double)N;
+        double q = gx[0] / tot;
+        double r = std::fma(-q, tot, gx[0]) + gx[1];
+        const double mean = q + r / tot;
+        log_thr = std::log(prm->mean_scaling_factor * mean);
+    }
+    {
+        Scope sc(c, "pair_test", s0);
+        ScTestLaunch T{};
+        T.K = K;
+        T.G = G;
+        T.P = P;
+        T.mode = prm->mode;
+        T.min_pct = prm->min_per_cent;
+        T.lfc_thr = prm->log_fc_thrs;
+        T.log_thr = log_thr;
+        T.n_clu = d_nclu;
+        T.mean_x = d_mx;
+        T.mean_e = d_me;
+        T.cnt_pos = d_cntpos;
+        T.u2_base = d_u2b;
+        T.t_base = d_tb;
+        T.tie_e = d_tie_e;
+        T.tie_x = d_tie_x;
+        T.wtab = c->d_wtab;
+        T.woff = c->d_woff;
+        T.out_p = d_p;
+        T.out_lfc = d_lfc;
+        T.out_pct1 = d_pct1;
+        T.out_pct2 = d_pct2;
+        T.out_u2 = d_u2;
+        T.out_t = d_t;
+        T.out_flags = d_flags;
+        HIPCHK(c, scc_launch_pair_test(&T, s0));
+    }
+    // rows (FAST) / per-pair vectors (SLOW)
+    int* d_row_gene = nullptr;
+    double *d_row_p = nullptr, *d_row_q = nullptr, *d_row_lfc = nullptr, *d_row_pct1 = nullptr, *d_row_pct2 = nullptr;
+    long long *d_row_u2 = nullptr, *d_row_t = nullptr;
+    uint8_t* d_row_flags = nullptr;
+    double* d_slow_q = nullptr;
+    uint8_t* d_slow_de = nullptr;
+    void *d_rec = nullptr, *d_key = nullptr;
+    const size_t rowcap = fast ? PG : 1;
+    WS("row_gene", rowcap, d_row_gene);
+    WS("row_p", rowcap, d_row_p);
+    WS("row_q", rowcap, d_row_q);
+    WS("row_lfc", rowcap, d_row_lfc);
+    WS("row_pct1", rowcap, d_row_pct1);
+    WS("row_pct2", rowcap, d_row_pct2);
+    WS("row_u2", rowcap, d_row_u2);
+    WS("row_t", rowcap, d_row_t);
+    WS("row_flags", rowcap, d_row_flags);
+    WS("slow_q", fast ? 1 : PG, d_slow_q);
+    WS("slow_de", fast ? 1 : PG, d_slow_de);
+    if ((rc = ws_get(c, "rec_scratch", PG * scc_select_rec_bytes(), &d_rec))) return rc;
+    if ((rc = ws_get(c, "key_scratch", std::max<size_t>(PG, G) * scc_select_key_bytes(), &d_key))) return rc;
+    {
+        Scope sc(c, "pair_select", s0);
+        HIPCHK(c, hipMemsetAsync(d_first, 0xFF, sizeof(unsigned long long) * G, s0));
+        if (fast) HIPCHK(c, scc_launch_count_tested(d_flags, G, P, d_tested, d_rowoff, s0));
+        ScSelectLaunch S{};
+        S.K = K;
+        S.G = G;
+        S.P = P;
+        S.mode = prm->mode;
+        S.top_n = fast ? prm->top_n : 30;
+        S.cap = env_int("SCC_SELECT_CAP", kSelectCap);
+        S.q_thr = prm->q_val_thrs;
+        S.lfc_cut = fast ? 0.0 : std::log(prm->fc_thrs);
+        S.p = d_p;
+        S.lfc = d_lfc;
+        S.pct1 = d_pct1;
+        S.pct2 = d_pct2;
+        S.u2 = d_u2;
+        S.t = d_t;
+        S.flags = d_flags;
+        S.row_off = d_rowoff;
+        S.rec_scratch = d_rec;
+        S.key_scratch = d_key;
+        S.row_gene = d_row_gene;
+        S.row_p = d_row_p;
+        S.row_q = d_row_q;
+        S.row_lfc = d_row_lfc;
+        S.row_pct1 = d_row_pct1;
+        S.row_pct2 = d_row_pct2;
+        S.row_u2 = d_row_u2;
+        S.row_t = d_row_t;
+        S.row_flags = d_row_flags;
+        S.slow_q = d_slow_q;
+        S.slow_de = d_slow_de;
+        S.first_occ = d_first;
+        S.err = d_err;
+        HIPCHK(c, scc_launch_pair_select(&S, s0));
+        HIPCHK(c, scc_launch_union(d_first, G, d_key, env_int("SCC_UNION_CAP", kUnionCap), d_union, d_nu, s0));
+    }
+    int hdr[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(&hdr[0], d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
+    HIPCHK(c, hipMemcpyAsync(&hdr[1], d_err, sizeof(int), hipMemcpyDeviceToHost, s0));
+    HIPCHK(c, hipStreamSynchronize(s0));
+    if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values or bad row indices");
+    scc_de_result* r = new scc_de_result();
+    r->ctx = c;
+    r->generation = c->generation;
+    r->mode = prm->mode;
+    r->K = K;
+    r->P = P;
+    r->G = G;
+    r->N = N;
+    r->log_thr = log_thr;
+    r->union_genes.resize(hdr[0]);
+    if (hdr[0] > 0)
+        HIPCHK(c, hipMemcpy(r->union_genes.data(), d_union, sizeof(int) * hdr[0], hipMemcpyDeviceToHost));
+    if (fast) {
+        r->pair_tested.resize(P);
+        long long nrows = 0;
+        HIPCHK(c, hipMemcpy(r->pair_tested.data(), d_tested, sizeof(int) * P, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(&nrows, d_rowoff + P, sizeof(long long), hipMemcpyDeviceToHost));
+        r->n_rows = nrows;
+    }
+    r->d_nodg = d_nodg;
+    r->d_row_gene = d_row_gene;
+    r->d_row_p = d_row_p;
+    r->d_row_q = d_row_q;
+    r->d_row_lfc = d_row_lfc;
+    r->d_row_pct1 = d_row_pct1;
+    r->d_row_pct2 = d_row_pct2;
+    r->d_row_u2 = d_row_u2;
+    r->d_row_t = d_row_t;
+    r->d_row_flags = d_row_flags;
+    r->d_p = d_p;
+    r->d_q = d_slow_q;
+    r->d_lfc = d_lfc;
+    r->d_u2 = d_u2;
+    r->d_de = d_slow_de;
+    *out = r;
+    if (hdr[1] & 4) return fail(c, SCC_ERR_RSTOP, "NA in the DE logical vector: R stops at if(sum(...) <= 1)");
+    if (hdr[1] & 2) return fail(c, SCC_ERR_RSTOP, "NA adjusted p-value in a kept pair (R builds NA rows)");
+    return SCC_OK;
+#undef WS
+}
+
+static int check_live(const scc_de_result* r)
+{
+    if (!r) return SCC_ERR_INVALID;
+    if (r->generation != r->ctx->generation)
+        return fail(r->ctx, SCC_ERR_INVALID, "result is stale: copy it out before the next scc_de_run");
+    hipSetDevice(r->ctx->device);
+    return SCC_OK;
+}
+
+extern "C" int scc_de_result_counts(const scc_de_result* r, int32_t* n_pairs, int64_t* n_rows, int32_t* n_union)
+{
+    if (!r) return SCC_ERR_INVALID;
+    if (n_pairs) *n_pairs = r->P;
+    if (n_rows) *n_rows = r->n_rows;
+    if (n_union) *n_union = (int32_t)r->union_genes.size();
+    return SCC_OK;
+}
+
+extern "C" int scc_de_result_union(const scc_de_result* r, int32_t* genes)
+{
+    if (!r || !genes) return SCC_ERR_INVALID;
+    std::copy(r->union_genes.begin(), r->union_genes.end(), genes);
+    return SCC_OK;
+}
+
+template <class T>
+static int d2h(scc_ctx* c, T* dst, const T* src, size_t n)
+{
+    if (!dst || n == 0) return SCC_OK;
+    HIPCHK(c, hipMemcpy(dst, src, sizeof(T) * n, hipMemcpyDeviceToHost));
+    return SCC_OK;
+}
+
+extern "C" int scc_de_result_rows(const scc_de_result* r, int32_t* pair_rows, int32_t* gene, double* p, double* q,
+                                  double* lfc, double* pct1, double* pct2, int64_t* u2, int64_t* ties,
+                                  uint8_t* flags)
+{
+    int rc = check_live(r);
+    if (rc) return rc;
+    if (r->mode != SCC_DE_FAST) return fail(r->ctx, SCC_ERR_INVALID, "rows exist for SCC_DE_FAST only");
+    scc_ctx* c = r->ctx;
+    const size_t n = (size_t)r->n_rows;
+    if (pair_rows) std::copy(r->pair_tested.begin(), r->pair_tested.end(), pair_rows);
+    if ((rc = d2h(c, gene, r->d_row_gene, n))) return rc;
+    if ((rc = d2h(c, p, r->d_row_p, n))) return rc;
+    if ((rc = d2h(c, q, r->d_row_q, n))) return rc;
+    if ((rc = d2h(c, lfc, r->d_row_lfc, n))) return rc;
+    if ((rc = d2h(c, pct1, r->d_row_pct1, n))) return rc;
+    if ((rc = d2h(c, pct2, r->d_row_pct2, n))) return rc;
+    if ((rc = d2h(c, (long long*)u2, r->d_row_u2, n))) return rc;
+    if ((rc = d2h(c, (long long*)ties, r->d_row_t, n))) return rc;
+    if ((rc = d2h(c, flags, r->d_row_flags, n))) return rc;
+    return SCC_OK;
+}
+
+extern "C" int scc_de_result_pair_vectors(const scc_de_result* r, double* p, double* q, double* lfc, int64_t* u2,
+                                          uint8_t* de)
+{
+    int rc = check_live(r);
+    if (rc) return rc;
+    scc_ctx* c = r->ctx;
+    const size_t n = (size_t)r->P * (size_t)r->G;
+    if ((rc = d2h(c, p, r->d_p, n))) return rc;
+    if ((rc = d2h(c, lfc, r->d_lfc, n))) return rc;
+    if ((rc = d2h(c, (long long*)u2, r->d_u2, n))) return rc;
+    if (r->mode == SCC_DE_SLOW) {
+        if ((rc = d2h(c, q, r->d_q, n))) return rc;
+        if ((rc = d2h(c, de, r->d_de, n))) return rc;
+    } else if (q || de) {
+        return fail(c, SCC_ERR_INVALID, "q/de vectors exist for SCC_DE_SLOW only");
+    }
+    return SCC_OK;
+}
+
+extern "C" int scc_de_result_log_threshold(const scc_de_result* r, double* log_thr)
+{
+    if (!r || !log_thr) return SCC_ERR_INVALID;
+    *log_thr = r->log_thr;
+    return SCC_OK;
+}
+
+extern "C" int scc_de_result_nodg(const scc_de_result* r, int32_t* nodg)
+{
+    int rc = check_live(r);
+    if (rc) return rc;
+    return d2h(r->ctx, nodg, r->d_nodg, (size_t)r->N);
+}
+
+extern "C" void scc_de_result_destroy(scc_de_result* r) { delete r; }
+
+// distance entry points live in scc_distance.cpp

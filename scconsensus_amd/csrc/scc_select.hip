@@ -1,0 +1,674 @@
+// scc_select.hip — per-(pair, gene) test epilogue and per-pair selection.
+//
+//  k_wilcox_table   R's cwilcox counts (nmath/wilcox.c recursion, memo table
+//                   w[i][j][k]) for the exact test, built once per context.
+//  k_pair_test      per (pair, gene): Fast feature filters (Fast:229-291) or
+//                   slow mean-diff + expression gate (slow:104-113), and the
+//                   wilcox.test p-value (exact / normal rule) from exact 2U, T.
+//  k_pair_select    per pair: R's row order order(p, -avg_logFC) (Fast:346),
+//                   BH (Fast:347 lazy n / slow:116-121 n = G), q filter and
+//                   the dim > 1 rule (Fast:376-378), top_n with ties
+//                   (Fast:391) / first-30 of sort(|logfc|) (slow:214-222),
+//                   and first-occurrence keys for the union.
+//  k_union          unique(Gene) in row order (Fast:392) / union() (slow:224).
+#include "scc_common.hpp"
+#include "scc_kernels.hpp"
+#include "scc_sort.hpp"
+
+#define WT_DIM 50  // exact test when both clusters < 50 cells
+#define SEL_T 256
+
+// -------------------------------------------------------- cwilcox table
+__device__ inline double cw_lookup(int k, int m, int n, const double* W, const int* woff)
+{
+    for (;;) {
+        const int u = m * n;
+        if (k < 0 || k > u) return 0.0;
+        const int c = u / 2;
+        if (k > c) k = u - k;
+        const int i = m < n ? m : n, j = m < n ? n : m;
+        if (j == 0) return (k == 0) ? 1.0 : 0.0;
+        if (k < j) {  // cwilcox(k, i, k)
+            m = i;
+            n = k;
+            continue;
+        }
+        return W[woff[i * WT_DIM + j] + k];
+    }
+}
+
+// single workgroup; level s = i + j ascending, all entries of a level in parallel
+__global__ void __launch_bounds__(1024) k_wilcox_table(double* W, const int* woff)
+{
+    for (int s = 2; s <= 2 * (WT_DIM - 1); ++s) {
+        for (int i = 1; i < WT_DIM; ++i) {
+            const int j = s - i;
+            if (j < i || j >= WT_DIM) continue;
+            const int c = (i * j) / 2;
+            double* row = W + woff[i * WT_DIM + j];
+            for (int k = threadIdx.x; k <= c; k += blockDim.x) {
+                if (k < j) {
+                    row[k] = -1.0;  // never read (reduced to cwilcox(k, i, k))
+                } else {
+                    row[k] = cw_lookup(k - j, i - 1, j, W, woff) + cw_lookup(k, i, j - 1, W, woff);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__device__ inline double r_choose(double n, double k)
+{
+    if (n - k < k) k = n - k;
+    if (k < 0) return 0.0;
+    if (k == 0) return 1.0;
+    double r = n;
+    for (int j = 2; j <= (int)k; ++j) r *= (n - j + 1) / j;
+    return rint(r);
+}
+
+__device__ inline double r_pwilcox(double q, int m, int n, bool lower, const double* W, const int* woff)
+{
+    q = floor(q + 1e-7);
+    const double mn = (double)m * n;
+    if (q < 0.0) return lower ? 0.0 : 1.0;
+    if (q >= mn) return lower ? 1.0 : 0.0;
+    const double c = r_choose((double)m + n, (double)n);
+    double p = 0.0;
+    if (q <= mn / 2) {
+        for (int i = 0; i <= (int)q; ++i) p += cw_lookup(i, m, n, W, woff) / c;
+    } else {
+        q = mn - q;
+        for (int i = 0; i < (int)q; ++i) p += cw_lookup(i, m, n, W, woff) / c;
+        lower = !lower;
+    }
+    return lower ? p : (0.5 - p + 0.5);
+}
+
+// stats:::wilcox.test.default two-sided, correct = TRUE, exact = NULL, from
+// the exact statistic W = 2U/2 and tie term T = sum(NTIES^3 - NTIES).
+__device__ inline double wilcox_p(i64 u2, i64 tie, int nx, int ny, const double* W, const int* woff, u8* exact_used)
+{
+    const double dnx = (double)nx, dny = (double)ny;
+    const double stat = (double)u2 * 0.5;
+    if (nx < 50 && ny < 50 && tie == 0) {
+        *exact_used = 1;
+        double p;
+        if (stat > (dnx * dny / 2))
+            p = r_pwilcox(stat - 1, nx, ny, false, W, woff);
+        else
+            p = r_pwilcox(stat, nx, ny, true, W, woff);
+        return fmin(2 * p, 1.0);
+    }
+    *exact_used = 0;
+    double z = stat - dnx * dny / 2;
+    const double sigma =
+        sqrt((dnx * dny / 12) * ((dnx + dny + 1) - (double)tie / ((dnx + dny) * (dnx + dny - 1))));
+    const double corr = (z > 0) ? 0.5 : ((z < 0) ? -0.5 : 0.0);
+    z = (z - corr) / sigma;
+    return 2 * scc_pnorm_small_tail(z);
+}
+
+// -------------------------------------------------------- per (pair, gene)
+struct TestArgs {
+    int K, G, P, mode;
+    double min_pct, lfc_thr, log_thr;  // FAST: minPerCent, logFCThrs; SLOW: log(meanExprsThrs)
+    const int* n_clu;
+    const double* mean_x;
+    const double* mean_e;
+    const u32* cnt_pos;
+    const i64* u2_base;
+    const i64* t_base;
+    const u64* tie_e;
+    const u64* tie_x;
+    const double* wtab;
+    const int* woff;
+    double* out_p;     // [P][G]
+    double* out_lfc;   // [P][G]
+    double* out_pct1;  // [P][G] (FAST)
+    double* out_pct2;
+    i64* out_u2;       // [P][G]
+    i64* out_t;        // [P][G]
+    u8* out_flags;     // [P][G]: bit0 tested, bit1 gate (SLOW), bit2 exact test
+};
+
+__global__ void __launch_bounds__(256) k_pair_test(TestArgs A)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = blockIdx.y;
+    if (g >= A.G) return;
+    int a = 0, rem = p;
+    while (rem >= A.K - 1 - a) {
+        rem -= A.K - 1 - a;
+        ++a;
+    }
+    const int b = a + 1 + rem;
+    const size_t pg = (size_t)p * A.G + g;
+    const i64 u2 = A.u2_base[pg] + (i64)A.tie_e[pg];
+    const i64 t = A.t_base[pg] + 3 * (i64)A.tie_x[pg];
+    const int na = A.n_clu[a], nb = A.n_clu[b];
+    u8 ex = 0;
+    const double pv = wilcox_p(u2, t, na, nb, A.wtab, A.woff, &ex);
+    u8 fl = (u8)(ex << 2);
+    double lfc;
+    if (A.mode == SCC_DE_FAST) {
+        // Fast:230-239  round(100 * rowSums(x > 0) / n, 16): the round is the identity here
+        const double pct1 = (100.0 * (double)A.cnt_pos[(size_t)a * A.G + g]) / (double)na;
+        const double pct2 = (100.0 * (double)A.cnt_pos[(size_t)b * A.G + g]) / (double)nb;
+        const double amax = pct1 > pct2 ? pct1 : pct2;
+        // Fast:259-272 log(mean(expm1(x)) + 1)
+        const double m1 = log(A.mean_e[(size_t)a * A.G + g] + 1.0);
+        const double m2 = log(A.mean_e[(size_t)b * A.G + g] + 1.0);
+        lfc = m1 - m2;
+        const bool pass_pct = amax > A.min_pct;
+        const bool pass_expr = (expm1(m1) > 0.0) || (expm1(m2) > 0.0);  // Fast:275
+        const bool pass_fc = fabs(lfc) > A.lfc_thr;                       // Fast:285
+        if (pass_pct && pass_expr && pass_fc) fl |= 1;
+        A.out_pct1[pg] = pct1;
+        A.out_pct2[pg] = pct2;
+    } else {
+        const double mi = A.mean_x[(size_t)a * A.G + g], mj = A.mean_x[(size_t)b * A.G + g];
+        lfc = mi - mj;  // slow:105
+        fl |= 1;
+        if (mi > A.log_thr || mj > A.log_thr) fl |= 2;  // slow:110-113
+    }
+    A.out_p[pg] = pv;
+    A.out_lfc[pg] = lfc;
+    A.out_u2[pg] = u2;
+    A.out_t[pg] = t;
+    A.out_flags[pg] = fl;
+}
+
+// -------------------------------------------------------- per pair counts
+__global__ void __launch_bounds__(256) k_count_tested(const u8* flags, int G, int* tested)
+{
+    const int p = blockIdx.x;
+    int c = 0;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) c += flags[(size_t)p * G + g] & 1;
+    c = (int)u32_wave_sum((u32)c);
+    __shared__ int s[4];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tested[p] = s[0] + s[1] + s[2] + s[3];
+}
+
+// exclusive prefix over P pair counts (single block; P <= a few thousand)
+__global__ void __launch_bounds__(1024) k_prefix_pairs(const int* cnt, int P, i64* off)
+{
+    __shared__ i64 s[1024];
+    i64 carry = 0;
+    for (int base = 0; base < P; base += 1024) {
+        const int i = base + threadIdx.x;
+        const i64 v = (i < P) ? cnt[i] : 0;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const i64 t = ((int)threadIdx.x >= o) ? s[threadIdx.x - o] : 0;
+            __syncthreads();
+            s[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < P) off[i] = carry + s[threadIdx.x] - v;
+        const i64 blk = s[1023];
+        __syncthreads();
+        carry += blk;
+    }
+    if (threadIdx.x == 0) off[P] = carry;
+}
+
+// -------------------------------------------------------- per pair selection
+// Record order = R's order(p, -avg_logFC) with NA last, ties by gene index
+// (the original feature order: R's radix order is stable).
+struct RowRec {
+    u64 k1;  // orderable p (NaN -> max)
+    u64 k2;  // orderable -logFC (FAST) / 0 (SLOW)
+    u32 g;
+    u32 pad;
+    __device__ bool operator<(const RowRec& o) const
+    {
+        if (k1 != o.k1) return k1 < o.k1;
+        if (k2 != o.k2) return k2 < o.k2;
+        return g < o.g;
+    }
+};
+
+struct KeyRec {  // (u64 key, u32 payload) ascending by key then payload
+    u64 k;
+    u32 g;
+    u32 pad;
+    __device__ bool operator<(const KeyRec& o) const { return k != o.k ? k < o.k : g < o.g; }
+};
+
+__device__ inline u64 p_key(double p) { return (p != p) ? ~0ull : scc_key_of(p + 0.0); }
+
+struct SelectArgs {
+    int K, G, P, mode, top_n, cap;
+    double q_thr;
+    double lfc_cut;          // SLOW: log(fcThrs)
+    const double* p;         // [P][G]
+    const double* lfc;
+    const double* pct1;
+    const double* pct2;
+    const i64* u2;
+    const i64* t;
+    const u8* flags;
+    const i64* row_off;      // [P+1] (FAST rows = tested genes per pair)
+    RowRec* rec_scratch;     // [P][G] global scratch for large pairs
+    KeyRec* key_scratch;     // [P][G]
+    // FAST row outputs
+    int* row_gene;
+    double* row_p;
+    double* row_q;
+    double* row_lfc;
+    double* row_pct1;
+    double* row_pct2;
+    i64* row_u2;
+    i64* row_t;
+    u8* row_flags;           // bit0 DE (q < thr and pair kept), bit1 top_n survivor
+    // SLOW outputs [P][G]
+    double* slow_q;
+    u8* slow_de;             // 0/1, 2 = NA (R would stop())
+    u64* first_occ;          // [G] (pair << 32 | rank), min-reduced
+    int* err;
+};
+
+// block-wide exclusive scan helper (T threads, returns exclusive prefix, total)
+template <int T>
+__device__ int block_excl_scan(int v, int* s, int& total)
+{
+    const int tid = threadIdx.x;
+    s[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < T; o <<= 1) {
+        const int t = (tid >= o) ? s[tid - o] : 0;
+        __syncthreads();
+        s[tid] += t;
+        __syncthreads();
+    }
+    total = s[T - 1];
+    const int ex = s[tid] - v;
+    __syncthreads();
+    return ex;
+}
+
+template <int T>
+__global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // dynamic LDS: RowRec[cap] | KeyRec[cap] | sred[T] | sc[T] | sthr
+    const size_t tail = (size_t)A.cap * (sizeof(RowRec) + sizeof(KeyRec));
+    double* sred = (double*)(smem + tail);
+    int* sc = (int*)(smem + tail + sizeof(double) * T);
+    u64& sthr = *(u64*)(smem + tail + (sizeof(double) + sizeof(int)) * T);
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int G = A.G;
+    const size_t pb = (size_t)p * G;
+    // 1) compact tested genes (gene order) into records
+    int m = 0;
+    const bool fast = (A.mode == SCC_DE_FAST);
+    RowRec* rec = (RowRec*)smem;
+    // count first to decide LDS vs HBM
+    {
+        int c = 0;
+        for (int g = tid; g < G; g += T) c += A.flags[pb + g] & 1;
+        int tot;
+        block_excl_scan<T>(c, sc, tot);
+        m = tot;
+    }
+    const bool big = m > A.cap;
+    if (big) rec = A.rec_scratch + pb;
+    {
+        // chunked compaction keeping gene order
+        int base = 0;
+        for (int g0 = 0; g0 < G; g0 += T) {
+            const int g = g0 + tid;
+            const bool t = (g < G) && (A.flags[pb + g] & 1);
+            int tot;
+            const int ex = block_excl_scan<T>(t ? 1 : 0, sc, tot);
+            if (t) {
+                RowRec r;
+                r.k1 = p_key(A.p[pb + g]);
+                r.k2 = fast ? scc_key_of(-A.lfc[pb + g] + 0.0) : 0ull;
+                r.g = (u32)g;
+                r.pad = 0;
+                rec[base + ex] = r;
+            }
+            base += tot;
+        }
+    }
+    __syncthreads();
+    // 2) sort into R's row order
+    if (big) {
+        AccAoS<RowRec> gacc{rec}, sacc{(RowRec*)smem};
+        block_bitonic_staged(gacc, m, sacc, A.cap, tid, T);
+    } else {
+        AccAoS<RowRec> acc{rec};
+        block_bitonic(acc, m, tid, T);
+    }
+    // 3) BH: non-NaN prefix length, then suffix-min of (n / rank) * p
+    int mnn = 0;
+    {
+        int c = 0;
+        for (int i = tid; i < m; i += T) c += (rec[i].k1 != ~0ull);
+        int tot;
+        block_excl_scan<T>(c, sc, tot);
+        mnn = tot;
+    }
+    const double nbh = fast ? (double)mnn : (double)G;
+    // suffix min processed in chunks of T from the end; carry = min so far
+    double carry = INFINITY;
+    const int nchunks = (mnn + T - 1) / T;
+    for (int cidx = nchunks - 1; cidx >= 0; --cidx) {
+        const int i = cidx * T + tid;
+        double v = INFINITY;
+        double pv = 0.0;
+        u32 gg = 0;
+        if (i < mnn) {
+            gg = rec[i].g;
+            pv = A.p[pb + gg];
+            v = (nbh / (double)(i + 1)) * pv;
+        }
+        // inclusive suffix min within chunk (Hillis-Steele towards lower index)
+        sred[tid] = v;
+        __syncthreads();
+        for (int o = 1; o < T; o <<= 1) {
+            const double t2 = (tid + o < T) ? sred[tid + o] : INFINITY;
+            __syncthreads();
+            sred[tid] = fmin(sred[tid], t2);
+            __syncthreads();
+        }
+        const double sm = fmin(sred[tid], carry);
+        const double q = fmin(1.0, sm);
+        if (i < mnn) {
+            if (fast) {
+                A.row_q[A.row_off[p] + i] = q;
+            } else {
+                A.slow_q[pb + gg] = q;
+            }
+        }
+        const double cmin = fmin(sred[0], carry);
+        __syncthreads();
+        carry = cmin;
+    }
+    for (int i = mnn + tid; i < m; i += T) {
+        if (fast) A.row_q[A.row_off[p] + i] = NAN;
+        else A.slow_q[pb + rec[i].g] = NAN;
+    }
+    __syncthreads();
+    __threadfence_block();
+    if (fast) {
+        // 4) rows in R order, DE flag (q < thr, pair kept only when > 1 row)
+        const i64 ro = A.row_off[p];
+        int nde = 0;
+        for (int i = tid; i < m; i += T) {
+            const u32 g = rec[i].g;
+            const double q = A.row_q[ro + i];
+            const bool de = (m > 1) && (q < A.q_thr);
+            A.row_gene[ro + i] = (int)g;
+            A.row_p[ro + i] = A.p[pb + g];
+            A.row_lfc[ro + i] = A.lfc[pb + g];
+            A.row_pct1[ro + i] = A.pct1[pb + g];
+            A.row_pct2[ro + i] = A.pct2[pb + g];
+            A.row_u2[ro + i] = A.u2[pb + g];
+            A.row_t[ro + i] = A.t[pb + g];
+            A.row_flags[ro + i] = de ? 1 : 0;
+            nde += de;
+            if (m > 1 && q != q) atomicOr(A.err, 2);  // NA q in a kept pair: R builds an NA row
+        }
+        int d;
+        block_excl_scan<T>(nde, sc, d);
+        // 5) top_n: keep DE rows with min_rank(desc(|lfc|)) <= top_n  <=>  w >= v,
+        //    v = top_n-th largest |lfc| among DE rows (all kept when d <= top_n)
+        if (tid == 0) sthr = 0ull;
+        __syncthreads();
+        if (d > A.top_n) {
+            // sort |lfc| keys of DE rows (ascending) in the record buffer's KeyRec view
+            KeyRec* kr = (d <= A.cap) ? (KeyRec*)(smem + (size_t)A.cap * sizeof(RowRec))
+                                      : (A.key_scratch + pb);
+            int base = 0;
+            for (int i0 = 0; i0 < m; i0 += T) {
+                const int i = i0 + tid;
+                const bool de = (i < m) && (A.row_flags[ro + i] & 1);
+                int tot;
+                const int ex = block_excl_scan<T>(de ? 1 : 0, sc, tot);
+                if (de) {
+                    KeyRec r;
+                    r.k = scc_key_of(fabs(A.row_lfc[ro + i]));
+                    r.g = (u32)i;
+                    r.pad = 0;
+                    kr[base + ex] = r;
+                }
+                base += tot;
+            }
+            __syncthreads();
+            if (d <= A.cap) {
+                AccAoS<KeyRec> acc{kr};
+                block_bitonic(acc, d, tid, T);
+            } else {
+                AccAoS<KeyRec> gacc{kr}, sacc{(KeyRec*)smem};
+                block_bitonic_staged(gacc, d, sacc, A.cap, tid, T);
+            }
+            if (tid == 0) sthr = kr[d - A.top_n].k;
+            __syncthreads();
+        }
+        const u64 thr = sthr;
+        for (int i = tid; i < m; i += T) {
+            if (A.row_flags[ro + i] & 1) {
+                const u64 w = scc_key_of(fabs(A.row_lfc[ro + i]));
+                if (w >= thr) {
+                    A.row_flags[ro + i] |= 2;
+                    atomicMin((unsigned long long*)&A.first_occ[A.row_gene[ro + i]],
+                              (unsigned long long)(((u64)p << 32) | (u64)i));
+                }
+            }
+        }
+    } else {
+        // SLOW: DE = q < thr & |logfc| > log(fcThrs) & gate (R NA logic), then
+        // first 30 of sort(|logfc|, decreasing) (stable: gene order on ties)
+        int nde = 0;
+        for (int g = tid; g < G; g += T) {
+            const double q = A.slow_q[pb + g];
+            const bool bterm = (fabs(A.lfc[pb + g]) > A.lfc_cut) && (A.flags[pb + g] & 2);
+            u8 de;
+            if (q != q) {
+                de = bterm ? 2 : 0;
+                if (bterm) atomicOr(A.err, 4);
+            } else {
+                de = (q < A.q_thr) && bterm;
+            }
+            A.slow_de[pb + g] = de;
+            nde += (de == 1);
+        }
+        int d;
+        block_excl_scan<T>(nde, sc, d);
+        __syncthreads();
+        KeyRec* kr = (d <= A.cap) ? (KeyRec*)(smem + (size_t)A.cap * sizeof(RowRec)) : (A.key_scratch + pb);
+        int base = 0;
+        for (int g0 = 0; g0 < G; g0 += T) {
+            const int g = g0 + tid;
+            const bool de = (g < G) && (A.slow_de[pb + g] == 1);
+            int tot;
+            const int ex = block_excl_scan<T>(de ? 1 : 0, sc, tot);
+            if (de) {
+                KeyRec r;
+                // descending |logfc| -> ascending key of -|logfc|; ties by gene (stable)
+                r.k = scc_key_of(-fabs(A.lfc[pb + g]));
+                r.g = (u32)g;
+                r.pad = 0;
+                kr[base + ex] = r;
+            }
+            base += tot;
+        }
+        __syncthreads();
+        if (d <= A.cap) {
+            AccAoS<KeyRec> acc{kr};
+            block_bitonic(acc, d, tid, T);
+        } else {
+            AccAoS<KeyRec> gacc{kr}, sacc{(KeyRec*)smem};
+            block_bitonic_staged(gacc, d, sacc, A.cap, tid, T);
+        }
+        const int take = d < 30 ? d : 30;
+        for (int i = tid; i < take; i += T)
+            atomicMin((unsigned long long*)&A.first_occ[kr[i].g], (unsigned long long)(((u64)p << 32) | (u64)i));
+    }
+}
+
+// -------------------------------------------------------- union
+template <int T>
+__global__ void __launch_bounds__(T) k_union(const u64* first_occ, int G, KeyRec* scratch, int cap, int* out,
+                                             int* n_out)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* sc = (int*)(smem + (size_t)cap * sizeof(KeyRec));
+    const int tid = threadIdx.x;
+    int c = 0;
+    for (int g = tid; g < G; g += T) c += (first_occ[g] != ~0ull);
+    int tot;
+    block_excl_scan<T>(c, sc, tot);
+    const int nu = tot;
+    KeyRec* kr = (nu <= cap) ? (KeyRec*)smem : scratch;
+    int base = 0;
+    for (int g0 = 0; g0 < G; g0 += T) {
+        const int g = g0 + tid;
+        const bool in = (g < G) && (first_occ[g] != ~0ull);
+        int t2;
+        const int ex = block_excl_scan<T>(in ? 1 : 0, sc, t2);
+        if (in) {
+            KeyRec r;
+            r.k = first_occ[g];
+            r.g = (u32)g;
+            r.pad = 0;
+            kr[base + ex] = r;
+        }
+        base += t2;
+    }
+    __syncthreads();
+    if (nu <= cap) {
+        AccAoS<KeyRec> acc{kr};
+        block_bitonic(acc, nu, tid, T);
+    } else {
+        AccAoS<KeyRec> gacc{kr}, sacc{(KeyRec*)smem};
+        block_bitonic_staged(gacc, nu, sacc, cap, tid, T);
+    }
+    for (int i = tid; i < nu; i += T) out[i] = (int)kr[i].g;
+    if (tid == 0) *n_out = nu;
+}
+
+// -------------------------------------------------------- launchers
+extern "C" hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_wilcox_table, dim3(1), dim3(1024), 0, st, W, woff);
+    return hipGetLastError();
+}
+
+extern "C" int scc_wilcox_table_layout(int* woff /* WT_DIM*WT_DIM */)
+{
+    int o = 0;
+    for (int i = 0; i < WT_DIM; ++i)
+        for (int j = 0; j < WT_DIM; ++j) {
+            if (i >= 1 && j >= i) {
+                woff[i * WT_DIM + j] = o;
+                o += (i * j) / 2 + 1;
+            } else {
+                woff[i * WT_DIM + j] = 0;
+            }
+        }
+    return o;
+}
+
+extern "C" hipError_t scc_launch_pair_test(const ScTestLaunch* L, hipStream_t st)
+{
+    TestArgs A;
+    A.K = L->K;
+    A.G = L->G;
+    A.P = L->P;
+    A.mode = L->mode;
+    A.min_pct = L->min_pct;
+    A.lfc_thr = L->lfc_thr;
+    A.log_thr = L->log_thr;
+    A.n_clu = L->n_clu;
+    A.mean_x = L->mean_x;
+    A.mean_e = L->mean_e;
+    A.cnt_pos = L->cnt_pos;
+    A.u2_base = L->u2_base;
+    A.t_base = L->t_base;
+    A.tie_e = L->tie_e;
+    A.tie_x = L->tie_x;
+    A.wtab = L->wtab;
+    A.woff = L->woff;
+    A.out_p = L->out_p;
+    A.out_lfc = L->out_lfc;
+    A.out_pct1 = L->out_pct1;
+    A.out_pct2 = L->out_pct2;
+    A.out_u2 = L->out_u2;
+    A.out_t = L->out_t;
+    A.out_flags = L->out_flags;
+    hipLaunchKernelGGL(k_pair_test, dim3((L->G + 255) / 256, L->P), dim3(256), 0, st, A);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_count_tested(const u8* flags, int G, int P, int* tested, i64* row_off,
+                                              hipStream_t st)
+{
+    hipLaunchKernelGGL(k_count_tested, dim3(P), dim3(256), 0, st, flags, G, tested);
+    hipLaunchKernelGGL(k_prefix_pairs, dim3(1), dim3(1024), 0, st, tested, P, row_off);
+    return hipGetLastError();
+}
+
+extern "C" size_t scc_select_lds_bytes(int cap)
+{
+    return (size_t)cap * (sizeof(RowRec) + sizeof(KeyRec)) + (sizeof(double) + sizeof(int)) * SEL_T + 16;
+}
+extern "C" size_t scc_select_rec_bytes(void) { return sizeof(RowRec); }
+extern "C" size_t scc_select_key_bytes(void) { return sizeof(KeyRec); }
+
+extern "C" hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_t st)
+{
+    SelectArgs A;
+    A.K = L->K;
+    A.G = L->G;
+    A.P = L->P;
+    A.mode = L->mode;
+    A.top_n = L->top_n;
+    A.cap = L->cap;
+    A.q_thr = L->q_thr;
+    A.lfc_cut = L->lfc_cut;
+    A.p = L->p;
+    A.lfc = L->lfc;
+    A.pct1 = L->pct1;
+    A.pct2 = L->pct2;
+    A.u2 = L->u2;
+    A.t = L->t;
+    A.flags = L->flags;
+    A.row_off = L->row_off;
+    A.rec_scratch = (RowRec*)L->rec_scratch;
+    A.key_scratch = (KeyRec*)L->key_scratch;
+    A.row_gene = L->row_gene;
+    A.row_p = L->row_p;
+    A.row_q = L->row_q;
+    A.row_lfc = L->row_lfc;
+    A.row_pct1 = L->row_pct1;
+    A.row_pct2 = L->row_pct2;
+    A.row_u2 = L->row_u2;
+    A.row_t = L->row_t;
+    A.row_flags = L->row_flags;
+    A.slow_q = L->slow_q;
+    A.slow_de = L->slow_de;
+    A.first_occ = L->first_occ;
+    A.err = L->err;
+    const size_t lds = scc_select_lds_bytes(L->cap);
+    hipFuncSetAttribute((const void*)k_pair_select<SEL_T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_pair_select<SEL_T>, dim3(L->P), dim3(SEL_T), lds, st, A);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_union(const u64* first_occ, int G, void* scratch, int cap, int* out, int* n_out,
+                                       hipStream_t st)
+{
+    const size_t lds = (size_t)cap * sizeof(KeyRec) + sizeof(int) * SEL_T;
+    hipFuncSetAttribute((const void*)k_union<SEL_T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_union<SEL_T>, dim3(1), dim3(SEL_T), lds, st, first_occ, G, (KeyRec*)scratch, cap, out,
+                       n_out);
+    return hipGetLastError();
+}

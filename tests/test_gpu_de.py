@@ -1,0 +1,189 @@
+"""GPU parity: the MI355X DE engine (through the C ABI) vs the CPU oracle.
+
+Bar (BASELINE.json north_star): rank sums / U statistics and selected-gene
+sets bit-exact; p/q within 1e-6 relative.  logFC is compared at 1e-12
+relative (GPU expm1/log vs glibc; documented in DESIGN.md)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from scconsensus_amd import api, synth
+
+pytestmark = pytest.mark.gpu
+
+P_RTOL = 1e-6
+LFC_RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from scconsensus_amd import _native
+    return _native.Engine(0)
+
+
+@pytest.fixture(scope="module")
+def cfg_a():
+    d = synth.generate("A")
+    names, code = api.select_clusters(d.labels, 10)
+    return d, d.dense(), names, code
+
+
+@pytest.fixture(scope="module")
+def edge():
+    d = synth.edge_fixture()
+    names, code = api.select_clusters(d.labels, 10)
+    return d, d.dense(), names, code
+
+
+def _fast_compare(eng, ds, X, code, K, **kw):
+    from scconsensus_amd import _native as nat
+    g = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows", **kw)
+    o = O.de_fast(X, code, K, **kw)
+    r = g.rows
+    np.testing.assert_array_equal(r.pair_tested, o.pair_tested)      # tested feature sets (sizes)
+    np.testing.assert_array_equal(r.gene, o.row_gene)                 # sets AND R's row order
+    np.testing.assert_array_equal(r.u2, np.round(2 * o.row_W).astype(np.int64))  # exact U
+    np.testing.assert_array_equal(r.ties, np.round(o.row_ties).astype(np.int64))
+    np.testing.assert_allclose(r.p, o.row_p, rtol=P_RTOL, atol=0)
+    np.testing.assert_allclose(r.q, o.row_q, rtol=P_RTOL, atol=0)
+    np.testing.assert_allclose(r.avg_logfc, o.row_lfc, rtol=LFC_RTOL, atol=1e-15)
+    np.testing.assert_array_equal(r.pct1, o.row_pct1)
+    np.testing.assert_array_equal(r.pct2, o.row_pct2)
+    np.testing.assert_array_equal(r.de, o.row_de)
+    np.testing.assert_array_equal(r.top, o.row_top)
+    np.testing.assert_array_equal(g.union, o.union)                   # deGeneUnion, in order
+    return g, o
+
+
+def test_fast_config_a(eng, cfg_a):
+    d, X, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g, o = _fast_compare(eng, ds, X, code, len(names))
+    assert len(o.union) > 50
+    # the p-values agree far tighter than the bar
+    assert np.max(np.abs(g.rows.p - o.row_p) / np.maximum(o.row_p, 1e-300)) < 1e-12
+    np.testing.assert_array_equal(g.nodg, O.nodg(X))
+
+
+def test_fast_config_a_dense_input(eng, cfg_a):
+    d, X, names, code = cfg_a
+    ds = eng.dataset_dense(X)
+    _fast_compare(eng, ds, X, code, len(names))
+
+
+@pytest.mark.parametrize("kw", [dict(q_val_thrs=0.05, log_fc_thrs=0.25, min_per_cent=10.0, top_n=5),
+                                dict(q_val_thrs=0.5, log_fc_thrs=1.0, min_per_cent=40.0, top_n=100)])
+def test_fast_config_a_params(eng, cfg_a, kw):
+    d, X, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _fast_compare(eng, ds, X, code, len(names), **kw)
+
+
+def test_fast_edge_fixture(eng, edge):
+    d, X, names, code = edge
+    assert "grey" not in names and "grey60" not in names and "tiny" not in names
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g, o = _fast_compare(eng, ds, X, code, len(names), log_fc_thrs=0.1, min_per_cent=15.0)
+    from scconsensus_amd import _native as nat
+    full = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, log_fc_thrs=0.1, min_per_cent=15.0, fetch="rows")
+    assert full.rows is not None
+
+
+def test_exact_branch_is_exercised(eng, edge):
+    """Tie-free genes between the 20- and 15-cell clusters use R's exact pwilcox."""
+    from scconsensus_amd import _native as nat
+    d, X, names, code = edge
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="all")
+    a, b = names.index("brown"), names.index("yellow")
+    K = len(names)
+    p = a * K - a * (a + 1) // 2 + (b - a - 1)
+    for gene in range(30, 36):
+        x = X[gene, code == a]
+        y = X[gene, code == b]
+        po, W, T, meth = O.wilcox_test(x, y)
+        assert meth == "exact"
+        assert g.u2[p, gene] == int(2 * W)
+        assert g.p[p, gene] == pytest.approx(po, rel=1e-13)
+
+
+def _slow_compare(eng, ds, X, code, K, qthr=0.05, fc=1.5, msf=5.0):
+    from scconsensus_amd import _native as nat
+    g = eng.de_run(ds, code, K, nat.SCC_DE_SLOW, q_val_thrs=qthr, fc_thrs=fc, mean_scaling_factor=msf, fetch="all")
+    o = O.de_slow(X, code, K, qthr, fc, msf)
+    assert g.log_thr == pytest.approx(o.log_thr, rel=1e-14)
+    np.testing.assert_array_equal(g.u2, np.round(2 * o.W).astype(np.int64))
+    np.testing.assert_allclose(g.p, o.p, rtol=P_RTOL, atol=0, equal_nan=True)
+    np.testing.assert_allclose(g.q, o.q, rtol=P_RTOL, atol=0, equal_nan=True)
+    np.testing.assert_allclose(g.logfc, o.lfc, rtol=LFC_RTOL, atol=1e-15)
+    np.testing.assert_array_equal(g.de, o.de)
+    np.testing.assert_array_equal(g.union, o.union)
+    return g, o
+
+
+def test_slow_config_a_subset(eng, cfg_a):
+    d, X, names, code = cfg_a
+    Xs = X[:600]
+    sub = synth.from_dense(Xs, d.labels)
+    ds = eng.dataset_csc(sub.indptr, sub.indices, sub.data, sub.G, sub.N)
+    g, o = _slow_compare(eng, ds, Xs, code, len(names))
+    assert len(o.union) > 0
+
+
+def test_slow_edge_fixture(eng, edge):
+    d, X, names, code = edge
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _slow_compare(eng, ds, X, code, len(names), qthr=0.2, fc=1.2, msf=0.5)
+
+
+def test_repeat_is_bitwise_deterministic(eng, cfg_a):
+    from scconsensus_amd import _native as nat
+    d, X, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    a = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="all")
+    b = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="all")
+    np.testing.assert_array_equal(a.p, b.p)
+    np.testing.assert_array_equal(a.logfc, b.logfc)
+    np.testing.assert_array_equal(a.union, b.union)
+
+
+def test_invalid_inputs_fail_loudly(eng, cfg_a):
+    from scconsensus_amd import _native as nat
+    d, X, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    bad = code.copy()
+    bad[0] = len(names)
+    with pytest.raises(nat.SccError):
+        eng.de_run(ds, bad, len(names), nat.SCC_DE_FAST)
+    vals = d.data.copy()
+    vals[5] = np.nan
+    ds2 = eng.dataset_csc(d.indptr, d.indices, vals, d.G, d.N)
+    with pytest.raises(nat.SccError) as e:
+        eng.de_run(ds2, code, len(names), nat.SCC_DE_FAST)
+    assert e.value.code == nat.SCC_ERR_NONFINITE
+
+
+def test_config_b_sampled_parity(eng):
+    """PBMC-26k shape: exact U/ties/p on a seeded sample of (pair, gene) cells
+    against the oracle's R-style rank sums, plus full-size properties."""
+    from scconsensus_amd import _native as nat
+    d = synth.generate("B")
+    names, code = api.select_clusters(d.labels, 10)
+    K = len(names)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="all")
+    n = np.bincount(code[code >= 0], minlength=K).astype(np.int64)
+    pairs = [(i, j) for i in range(K - 1) for j in range(i + 1, K)]
+    nn = np.array([n[i] * n[j] for i, j in pairs])
+    assert np.all(g.u2 >= 0) and np.all(g.u2 <= 2 * nn[:, None])
+    csr = d.scipy_csc().tocsr()
+    rng = np.random.default_rng(0)
+    for _ in range(60):
+        p = int(rng.integers(len(pairs)))
+        gene = int(rng.integers(d.G))
+        i, j = pairs[p]
+        row = np.asarray(csr[gene].todense()).ravel()
+        po, W, T, _ = O.wilcox_test(row[code == i], row[code == j])
+        assert g.u2[p, gene] == int(round(2 * W))
+        assert g.p[p, gene] == pytest.approx(po, rel=P_RTOL)
+    assert 100 < len(g.union) <= 30 * len(pairs) * 2

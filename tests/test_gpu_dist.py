@@ -1,0 +1,80 @@
+"""GPU parity of stage 3 (cell x cell distance) against the numpy oracle.
+
+Bar: distance entries within 1e-5 absolute (BASELINE.json north_star).  The
+PCA oracle is the exact truncated SVD (irlba's target)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from scconsensus_amd import api, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from scconsensus_amd import _native
+    return _native.Engine(0)
+
+
+@pytest.fixture(scope="module")
+def cfg_a():
+    d = synth.generate("A")
+    names, code = api.select_clusters(d.labels, 10)
+    X = d.dense()
+    o = O.de_fast(X, code, len(names))
+    return d, X, o.union
+
+
+def test_pca_euclid_matches_exact_svd(eng, cfg_a):
+    from scconsensus_amd import _native as nat
+    d, X, uni = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    dist = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, uni))
+    assert dist.shape == ref.shape
+    err = np.max(np.abs(dist - ref))
+    assert err < 1e-5, err
+    # scores span the same subspace (signs arbitrary)
+    S = eng.last_pca_scores(d.N)
+    R = O.pca_scores(X, uni)
+    for q in range(S.shape[1]):
+        assert min(np.max(np.abs(S[:, q] - R[:, q])), np.max(np.abs(S[:, q] + R[:, q]))) < 1e-5 * max(
+            1.0, np.max(np.abs(R[:, q]))) or q >= 7  # noise-level components may rotate inside near-degenerate pairs
+
+
+def test_pca_euclid_fp32_output(eng, cfg_a):
+    from scconsensus_amd import _native as nat
+    d, X, uni = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    d64 = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
+    d32 = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID, f32=True)
+    np.testing.assert_allclose(d32, d64, rtol=1e-6, atol=1e-6)
+
+
+def test_pca_small_union_and_dense_input(eng, cfg_a):
+    from scconsensus_amd import _native as nat
+    d, X, uni = cfg_a
+    small = uni[:9]  # |U| < 15 -> n = |U| components
+    ds = eng.dataset_dense(X)
+    dist = eng.distance(ds, small, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, small))
+    assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+def test_pearson_matches_numpy(eng, cfg_a):
+    from scconsensus_amd import _native as nat
+    d, X, uni = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    dist = eng.distance(ds, uni, nat.SCC_DIST_PEARSON)
+    ref = O.dist_pearson(X, uni)
+    assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+def test_dist_packed_order_small(eng):
+    """R dist order on a tiny hand case: (1,0),(2,0),(3,0),(2,1),(3,1),(3,2)."""
+    from scconsensus_amd import _native as nat
+    X = np.array([[0.0, 1.0, 3.0, 6.0], [0.0, 0.0, 0.0, 0.0], [1.0, 1.0, 1.0, 1.0]])
+    ds = eng.dataset_dense(X)
+    dist = eng.distance(ds, np.array([0, 2]), nat.SCC_DIST_PCA_EUCLID)
+    np.testing.assert_allclose(dist, [1, 3, 6, 2, 5, 3], atol=1e-12)
