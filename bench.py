@@ -75,22 +75,15 @@ def cpu_baseline(d, code, K, union, sample_genes, seed=0):
 
 def main():
     a = _args()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")  # RCCL
-        dist = (torch, tdist)
+    from scconsensus_amd import parallel
+    dist = parallel.init()  # RCCL ("nccl") when launched by torchrun with N > 1
+    rank, world, local = dist.rank, dist.world, dist.local_rank
     from scconsensus_amd import _native as nat
     from scconsensus_amd import api, synth
     from scconsensus_amd.synth import CONFIGS
 
     cfg = CONFIGS[a.config]
-    d = synth.generate(a.config, seed=cfg["seed"] + 1000 * rank)
+    d = synth.generate(a.config, seed=parallel.job_seed(cfg["seed"], rank))
     names, code = api.select_clusters(d.labels, 10)
     K = len(names)
     P = K * (K - 1) // 2
@@ -103,9 +96,7 @@ def main():
         eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
         return r
 
-    def barrier():
-        if dist:
-            dist[1].barrier()
+    barrier = dist.barrier
 
     for _ in range(a.warmup):
         r = step()
@@ -119,12 +110,7 @@ def main():
     eng.synchronize()
     barrier()
     t1 = time.perf_counter()
-    dt = t1 - t0
-    if dist:
-        torch, tdist = dist
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = dist.max_over_ranks(t1 - t0)
     ms = dt / a.steps * 1e3
     fams = ["ingest", "gene_rank", "pair_test", "pair_select", "gather", "center", "gram", "eigen", "scores", "dist"]
     times = {f: eng.kernel_time(f) for f in fams}
@@ -176,8 +162,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(d, code, K, r.union, a.cpu_sample_genes)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist:
-        dist[1].destroy_process_group()
+    dist.close()
 
 
 if __name__ == "__main__":

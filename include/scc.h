@@ -95,6 +95,7 @@ SCC_API int scc_dataset_create_csc(scc_ctx* ctx, const int64_t* indptr, const in
 /* base R matrix: G x N column-major doubles (slow:32 as.matrix). */
 SCC_API int scc_dataset_create_dense(scc_ctx* ctx, const double* x_colmajor, int64_t n_genes, int64_t n_cells,
                              int32_t ptr_kind, scc_dataset** out);
+/* Destroy every dataset before the context it was created on. */
 SCC_API void scc_dataset_destroy(scc_dataset* ds);
 
 /* ---- stage 1+2: per-cluster statistics, all-pairs Wilcoxon, BH, union --- */

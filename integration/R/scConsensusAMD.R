@@ -1,0 +1,116 @@
+# scConsensusAMD.R — drop-in R wrappers that route the data-parallel core of
+# scConsensus to the MI355X engine (libscc via .Call; see INTEGRATION.md).
+#
+# Signatures and return objects are those of the reference:
+#   reclusterDEConsensusFast  R/reclusterDEConsensusFast.R:22-33, returns :446-450
+#   reclusterDEConsensus      R/reclusterDEConsensus.R:20-29,      returns :278-282
+# Kept in R (host), exactly as the reference does them: cluster selection
+# (table / grepl("grey") / locale order), hclust(ward.D2), cutreeDynamic,
+# labels2colors, silhouette, saveRDS, printing and cellTypeDEPlot.
+
+.scc_codes <- function(labels, minClusterSize) {
+  counts <- table(labels)                       # locale collation, as in R
+  keep <- names(counts)[counts > minClusterSize]
+  keep <- keep[!grepl("grey", keep)]
+  code <- match(as.character(labels), keep) - 1L
+  code[is.na(code)] <- -1L
+  list(clusters = keep, code = as.integer(code))
+}
+
+.scc_slots <- function(m) {
+  if (inherits(m, "dgCMatrix")) {
+    list(x = m@x, p = m@p, i = m@i, dim = dim(m))
+  } else {
+    m <- as.matrix(m)
+    storage.mode(m) <- "double"
+    list(x = m, p = NULL, i = NULL, dim = dim(m))
+  }
+}
+
+.scc_dist <- function(s, genes, n_cells, metric = 0L) {
+  d <- .Call("C_scc_distance", s$x, s$p, s$i, s$dim, as.integer(genes), as.integer(metric), 0L)
+  structure(d, Size = n_cells, Diag = FALSE, Upper = FALSE,
+            method = if (metric == 0L) "euclidean" else "pearson", class = "dist")
+}
+
+.scc_tree_and_colors <- function(d, deepSplitValues, minClusterSize, with_si) {
+  tree <- if (requireNamespace("fastcluster", quietly = TRUE)) fastcluster::hclust(d, method = "ward.D2")
+          else stats::hclust(d, method = "ward.D2")
+  dm <- as.matrix(d)
+  colors <- list()
+  for (dsv in deepSplitValues) {
+    grp <- dynamicTreeCut::cutreeDynamic(dendro = tree, distM = dm, deepSplit = dsv,
+                                         pamStage = FALSE, minClusterSize = minClusterSize)
+    colors[[paste("deepsplit:", dsv)]] <- WGCNA::labels2colors(grp)
+    if (with_si) invisible(cluster::silhouette(grp, dmatrix = dm))
+  }
+  names(colors) <- paste("deepsplit:", deepSplitValues)
+  list(tree = tree, colors = colors)
+}
+
+reclusterDEConsensusFast <- function(dataMatrix, consensusClusterLabels, method = "wilcox",
+                                     qValThrs = 0.1, logFCThrs = 0.5, deepSplitValues = 1:4,
+                                     minClusterSize = 10, minPerCent = 20,
+                                     filename = "de_gene_object.rds", plotName = "DE_Heatmap",
+                                     NumbertopDEGenes = 30, nCores = 1) {
+  if (method != "wilcox") stop("Unknown test: ", method)
+  if (is.null(names(consensusClusterLabels))) names(consensusClusterLabels) <- colnames(dataMatrix)
+  labels <- consensusClusterLabels[colnames(dataMatrix)]
+  sel <- .scc_codes(labels, minClusterSize)
+  s <- .scc_slots(dataMatrix)
+  res <- .Call("C_scc_de_fast", s$x, s$p, s$i, s$dim, sel$code, length(sel$clusters),
+               as.double(qValThrs), as.double(logFCThrs), as.double(minPerCent),
+               as.integer(NumbertopDEGenes))
+  deGeneUnion <- rownames(dataMatrix)[res[[1]]]
+  print(str(deGeneUnion))
+  d <- .scc_dist(s, res[[1]], ncol(dataMatrix))
+  tc <- .scc_tree_and_colors(d, deepSplitValues, minClusterSize, with_si = TRUE)
+  out <- list("deGeneUnion" = deGeneUnion, "cellTree" = tc$tree, "dynamicColors" = tc$colors)
+  saveRDS(object = out, file = filename)
+  cellTypeDEPlot(dataMatrix = dataMatrix[deGeneUnion, ], nodg = res[[2]], cellTree = tc$tree,
+                 clusterLabels = consensusClusterLabels, dynamicColorsList = tc$colors,
+                 colScheme = "violet", filename = plotName)
+  out
+}
+
+reclusterDEConsensus <- function(dataMatrix, consensusClusterLabels, method = "Wilcoxon",
+                                 meanScalingFactor = 5, qValThrs, fcThrs, deepSplitValues = 1:4,
+                                 minClusterSize = 10, filename = "de_gene_object.rds",
+                                 plotName = "DE_Heatmap") {
+  if (method != "Wilcoxon") {
+    print("Incorrect method chosen.")
+    return(NULL)
+  }
+  if (is.null(names(consensusClusterLabels))) names(consensusClusterLabels) <- colnames(dataMatrix)
+  labels <- consensusClusterLabels[colnames(dataMatrix)]
+  sel <- .scc_codes(labels, minClusterSize)
+  s <- .scc_slots(dataMatrix)
+  res <- .Call("C_scc_de_slow", s$x, s$p, s$i, s$dim, sel$code, length(sel$clusters),
+               as.double(qValThrs), as.double(fcThrs), as.double(meanScalingFactor))
+  K <- length(sel$clusters)
+  qValueList <- rep(list(list()), K); logFCList <- rep(list(list()), K); deGeneList <- rep(list(list()), K)
+  pcol <- 0L
+  for (a in seq_len(K - 1)) for (b in (a + 1):K) {
+    pcol <- pcol + 1L
+    de <- as.integer(res[[4]][, pcol]) == 1L
+    print(paste0(sel$clusters[a], ", ", sel$clusters[b], " DE genes: ", sum(de)))
+    qValueList[[a]][[b]] <- res[[2]][, pcol]
+    logFCList[[a]][[b]] <- res[[3]][, pcol]
+    deGeneList[[a]][[b]] <- rownames(dataMatrix)[de]
+  }
+  names(qValueList) <- names(logFCList) <- names(deGeneList) <- sel$clusters
+  saveRDS(object = qValueList, file = "qValueList.rds")
+  saveRDS(object = logFCList, file = "logFCList.rds")
+  saveRDS(object = deGeneList, file = "deGeneList.rds")
+  deGeneUnion <- rownames(dataMatrix)[res[[1]]]
+  print(str(deGeneUnion))
+  saveRDS(deGeneUnion, file = "deGeneUnion.rds")
+  d <- .scc_dist(s, res[[1]], ncol(dataMatrix))
+  tc <- .scc_tree_and_colors(d, deepSplitValues, minClusterSize, with_si = FALSE)
+  out <- list("deGeneUnion" = deGeneUnion, "cellTree" = tc$tree, "dynamicColors" = tc$colors)
+  saveRDS(object = out, file = filename)
+  cellTypeDEPlot(dataMatrix = as.matrix(dataMatrix)[deGeneUnion, ], nodg = res[[5]], cellTree = tc$tree,
+                 clusterLabels = consensusClusterLabels, dynamicColorsList = tc$colors,
+                 colScheme = "violet", filename = plotName)
+  out
+}

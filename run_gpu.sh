@@ -15,8 +15,8 @@ step() {  # step <name> <timeout_s> <cmd...>
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
-    testsall) step testsall 900 python -m pytest tests -m gpu -q ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 ;;
+    testsall) step testsall 900 python -u -m pytest tests -m gpu -v --timeout 300 ;;
     bench) step bench 900 python bench.py ;;
     benchq) step benchq 600 python bench.py --no-cpu-baseline ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;

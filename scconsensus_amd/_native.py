@@ -5,8 +5,10 @@ no MI355X is visible ``Engine()`` raises ``SccError(SCC_ERR_HIP)``.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -55,6 +57,21 @@ class DeParams(ctypes.Structure):
 
 
 _lib = None
+_live_datasets: "weakref.WeakSet" = weakref.WeakSet()
+_live_engines: "weakref.WeakSet" = weakref.WeakSet()
+_shutdown = False
+
+
+@atexit.register
+def _teardown():
+    # release device objects in dependency order while the HIP runtime is
+    # still alive (interpreter-exit __del__ order is arbitrary)
+    global _shutdown
+    for d in list(_live_datasets):
+        d.close()
+    for e in list(_live_engines):
+        e.close()
+    _shutdown = True
 
 
 def load():
@@ -137,11 +154,12 @@ class DeResult:
 class Dataset:
     def __init__(self, engine, handle, G, N):
         self.engine, self.handle, self.G, self.N = engine, handle, G, N
+        _live_datasets.add(self)
 
     def close(self):
-        if self.handle:
+        if self.handle and not _shutdown:
             self.engine.lib.scc_dataset_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
     def __del__(self):
         try:
@@ -161,12 +179,15 @@ class Engine:
         if rc != SCC_OK:
             raise SccError(rc, "scc_ctx_create failed (no HIP device?)")
         self.ctx = h
-        self._keep = []
+        _live_engines.add(self)
 
     def close(self):
-        if self.ctx:
+        if self.ctx and not _shutdown:
+            for d in list(_live_datasets):
+                if d.engine is self:
+                    d.close()
             self.lib.scc_ctx_destroy(self.ctx)
-            self.ctx = None
+        self.ctx = None
 
     def __del__(self):
         try:

@@ -1,147 +1,124 @@
 // scc_ingest.hip — boundary ingest: the R dgCMatrix (CSC over cells) or dense
-// column-major matrix, plus per-cell cluster codes, becomes a per-(gene,
-// cluster) bucketed array of orderable 64-bit keys resident in HBM.
+// column-major matrix plus per-cell cluster codes become a gene-major array of
+// (orderable 64-bit value key, cluster code) for the kept nonzeros, resident
+// in HBM.  Replaces the reference's per-pair `as.matrix(dataMatrix)` and
+// name-indexed column subsets (R/reclusterDEConsensusFast.R:361-368).
 //
-// Replaces the reference's per-pair `as.matrix(dataMatrix)` + name-indexed
-// column subsets (R/reclusterDEConsensusFast.R:361-368) with one streaming pass.
-// Layout out:  seg_off[g*K + a] .. seg_off[g*K + a + 1]  = keys of gene g,
-// cluster a (value != 0, cell kept).  Zeros are implicit (the tie group every
-// Wilcoxon statistic treats in closed form).
+// A block-local counting sort (no global atomics):
+//   k_ing_hist     one workgroup per chunk of cells: LDS histogram over genes
+//                  (kept nonzeros), nodg per cell (Fast:440-443, x > 0 over ALL
+//                  cells), optional sum of expm1 over all entries (slow:36),
+//                  non-finite / bad-row flag; histogram row -> cnt[w][g]
+//   k_ing_colscan  per gene: exclusive prefix over chunks (in place), total[g]
+//   scan           gene starts gstart[G+1] (three-kernel device scan)
+//   k_ing_scatter  per chunk: LDS cursors = gstart[g] + cnt[w][g]; write keys
+//                  and codes.
+// Zeros are implicit (the tie group every Wilcoxon statistic handles in
+// closed form).  Within a gene the order is chunk-major (cell order across
+// chunks); the rank kernel sorts each gene anyway.
 #include "scc_common.hpp"
 #include "scc_kernels.hpp"
 
-// One wave per cell: lanes stride the cell's stored entries (coalesced).
-// Counts kept nonzeros per (gene, cluster), negatives per (gene, cluster),
-// nodg per cell (Fast:440-443, x > 0 over ALL cells), non-finite flag, and
-// optionally the global sum of expm1 over all entries (slow:36).
-__global__ void __launch_bounds__(256) k_ingest_count(const i64* __restrict__ indptr, const int* __restrict__ rows,
-                                                      const double* __restrict__ vals, int N, int G, int K,
-                                                      const int* __restrict__ code, u32* __restrict__ cnt,
-                                                      u32* __restrict__ neg, int* __restrict__ nodg,
-                                                      dd* __restrict__ wave_expm1, int want_expm1,
-                                                      int* __restrict__ err)
+#define ING_T 256
+
+template <bool DENSE>
+__device__ inline void cell_range(const i64* indptr, int c, int G, i64& b, i64& e)
 {
-    const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x >> 6;
-    const int wid = blockIdx.x * wpb + (threadIdx.x >> 6);
-    const int nw = gridDim.x * wpb;
+    if (DENSE) {
+        b = (i64)c * G;
+        e = b + G;
+    } else {
+        b = indptr[c];
+        e = indptr[c + 1];
+    }
+}
+
+template <bool DENSE>
+__global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
+                                                    const double* __restrict__ vals, int N, int G, int cells_per_wg,
+                                                    const int* __restrict__ code, u32* __restrict__ cnt,
+                                                    int* __restrict__ nodg, dd* __restrict__ wave_expm1,
+                                                    int want_expm1, int* __restrict__ err)
+{
+    extern __shared__ __attribute__((aligned(16))) u32 hist[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int g = threadIdx.x; g < G; g += ING_T) hist[g] = 0;
+    __syncthreads();
+    const int c0 = blockIdx.x * cells_per_wg, c1 = min(N, c0 + cells_per_wg);
     dd se{0.0, 0.0};
     int bad = 0;
-    for (int c = wid; c < N; c += nw) {
-        const i64 b = indptr[c], e = indptr[c + 1];
+    for (int c = c0 + wv; c < c1; c += ING_T / 64) {
+        i64 b, e;
+        cell_range<DENSE>(indptr, c, G, b, e);
         const int a = code[c];
         u32 pos = 0;
         for (i64 k = b + lane; k < e; k += 64) {
             const double x = vals[k];
-            const int g = rows[k];
-            bad |= !(x - x == 0.0) | (g < 0) | (g >= G);
+            const int g = DENSE ? (int)(k - b) : rows[k];
+            const bool gok = (g >= 0) & (g < G);
+            bad |= !(x - x == 0.0) | !gok;
             pos += (x > 0.0);
             if (want_expm1) se = dd_add_d(se, expm1(x));
-            if (a >= 0 && x != 0.0 && g >= 0 && g < G) {
-                atomicAdd(&cnt[(size_t)g * K + a], 1u);
-                if (x < 0.0) atomicAdd(&neg[(size_t)g * K + a], 1u);
-            }
+            if (a >= 0 && x != 0.0 && gok) atomicAdd(&hist[g], 1u);
         }
         pos = u32_wave_sum(pos);
         if (lane == 0) nodg[c] = (int)pos;
     }
     if (want_expm1) {
         se = dd_wave_sum(se);
-        if (lane == 0) wave_expm1[wid] = se;
+        if (lane == 0) wave_expm1[blockIdx.x * (ING_T / 64) + wv] = se;
     }
     if (bad) atomicOr(err, 1);
+    __syncthreads();
+    u32* row = cnt + (size_t)blockIdx.x * G;
+    for (int g = threadIdx.x; g < G; g += ING_T) row[g] = hist[g];
 }
 
-// Dense R matrix (G x N column-major): same outputs.  One wave per cell column.
-__global__ void __launch_bounds__(256) k_ingest_count_dense(const double* __restrict__ X, int N, int G, int K,
-                                                            const int* __restrict__ code, u32* __restrict__ cnt,
-                                                            u32* __restrict__ neg, int* __restrict__ nodg,
-                                                            dd* __restrict__ wave_expm1, int want_expm1,
-                                                            int* __restrict__ err)
+__global__ void __launch_bounds__(256) k_ing_colscan(u32* __restrict__ cnt, int nwg, int G, u32* __restrict__ total)
 {
-    const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x >> 6;
-    const int wid = blockIdx.x * wpb + (threadIdx.x >> 6);
-    const int nw = gridDim.x * wpb;
-    dd se{0.0, 0.0};
-    int bad = 0;
-    for (int c = wid; c < N; c += nw) {
-        const double* col = X + (size_t)c * G;
-        const int a = code[c];
-        u32 pos = 0;
-        for (int g = lane; g < G; g += 64) {
-            const double x = col[g];
-            bad |= !(x - x == 0.0);
-            pos += (x > 0.0);
-            if (want_expm1) se = dd_add_d(se, expm1(x));
-            if (a >= 0 && x != 0.0) {
-                atomicAdd(&cnt[(size_t)g * K + a], 1u);
-                if (x < 0.0) atomicAdd(&neg[(size_t)g * K + a], 1u);
-            }
-        }
-        pos = u32_wave_sum(pos);
-        if (lane == 0) nodg[c] = (int)pos;
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= G) return;
+    u32 run = 0;
+    for (int w = 0; w < nwg; ++w) {
+        const u32 v = cnt[(size_t)w * G + g];
+        cnt[(size_t)w * G + g] = run;
+        run += v;
     }
-    if (want_expm1) {
-        se = dd_wave_sum(se);
-        if (lane == 0) wave_expm1[wid] = se;
-    }
-    if (bad) atomicOr(err, 1);
+    total[g] = run;
 }
 
-// Scatter kept nonzeros into their (gene, cluster) bucket as orderable keys.
-__global__ void __launch_bounds__(256) k_ingest_scatter(const i64* __restrict__ indptr, const int* __restrict__ rows,
-                                                        const double* __restrict__ vals, int N, int G, int K,
-                                                        const int* __restrict__ code, const i64* __restrict__ seg_off,
-                                                        u32* __restrict__ cursor, u64* __restrict__ keys)
+template <bool DENSE>
+__global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ indptr, const int* __restrict__ rows,
+                                                       const double* __restrict__ vals, int N, int G,
+                                                       int cells_per_wg, const int* __restrict__ code,
+                                                       const u32* __restrict__ cnt, const i64* __restrict__ gstart,
+                                                       u64* __restrict__ keys, u8* __restrict__ codes)
 {
-    const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x >> 6;
-    const int wid = blockIdx.x * wpb + (threadIdx.x >> 6);
-    const int nw = gridDim.x * wpb;
-    for (int c = wid; c < N; c += nw) {
+    extern __shared__ __attribute__((aligned(16))) u32 cur[];  // offset inside the gene
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u32* row = cnt + (size_t)blockIdx.x * G;
+    for (int g = threadIdx.x; g < G; g += ING_T) cur[g] = row[g];
+    __syncthreads();
+    const int c0 = blockIdx.x * cells_per_wg, c1 = min(N, c0 + cells_per_wg);
+    for (int c = c0 + wv; c < c1; c += ING_T / 64) {
         const int a = code[c];
         if (a < 0) continue;
-        const i64 b = indptr[c], e = indptr[c + 1];
+        i64 b, e;
+        cell_range<DENSE>(indptr, c, G, b, e);
         for (i64 k = b + lane; k < e; k += 64) {
             const double x = vals[k];
-            const int g = rows[k];
+            const int g = DENSE ? (int)(k - b) : rows[k];
             if (x != 0.0 && g >= 0 && g < G) {
-                const size_t s = (size_t)g * K + a;
-                const u32 slot = atomicAdd(&cursor[s], 1u);
-                keys[seg_off[s] + slot] = scc_key_of(x);
-            }
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256) k_ingest_scatter_dense(const double* __restrict__ X, int N, int G, int K,
-                                                              const int* __restrict__ code,
-                                                              const i64* __restrict__ seg_off,
-                                                              u32* __restrict__ cursor, u64* __restrict__ keys)
-{
-    const int lane = threadIdx.x & 63;
-    const int wpb = blockDim.x >> 6;
-    const int wid = blockIdx.x * wpb + (threadIdx.x >> 6);
-    const int nw = gridDim.x * wpb;
-    for (int c = wid; c < N; c += nw) {
-        const int a = code[c];
-        if (a < 0) continue;
-        const double* col = X + (size_t)c * G;
-        for (int g = lane; g < G; g += 64) {
-            const double x = col[g];
-            if (x != 0.0) {
-                const size_t s = (size_t)g * K + a;
-                const u32 slot = atomicAdd(&cursor[s], 1u);
-                keys[seg_off[s] + slot] = scc_key_of(x);
+                const u64 pos = (u64)gstart[g] + atomicAdd(&cur[g], 1u);
+                keys[pos] = scc_key_of(x);
+                codes[pos] = (u8)a;
             }
         }
     }
 }
 
 // ------------------------------------------------------------ exclusive scan
-// Three-kernel device-wide exclusive scan of u32 counts into i64 offsets
-// (n up to G*K = 2M buckets at the 1M-cell config).
+// Three-kernel device-wide exclusive scan of u32 counts into i64 offsets.
 #define SCAN_T 256
 #define SCAN_PER 8
 __global__ void __launch_bounds__(SCAN_T) k_scan_block_sums(const u32* __restrict__ in, i64 n, i64* __restrict__ bsum)
@@ -190,6 +167,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_apply(const u32* __restrict__ i
                                                        i64* __restrict__ out)
 {
     __shared__ i64 s[SCAN_T * SCAN_PER];
+    __shared__ i64 t[SCAN_T];
     const i64 base = (i64)blockIdx.x * SCAN_T * SCAN_PER;
     for (int k = 0; k < SCAN_PER; ++k) {
         int li = k * SCAN_T + threadIdx.x;
@@ -197,8 +175,6 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_apply(const u32* __restrict__ i
         s[li] = (i < n) ? (i64)in[i] : 0;
     }
     __syncthreads();
-    // each thread scans SCAN_PER contiguous, then block scan of thread totals
-    __shared__ i64 t[SCAN_T];
     i64 acc = 0;
     for (int k = 0; k < SCAN_PER; ++k) acc += s[threadIdx.x * SCAN_PER + k];
     t[threadIdx.x] = acc;
@@ -228,32 +204,54 @@ __global__ void k_reduce_dd(const dd* __restrict__ parts, int n, dd* __restrict_
 }
 
 // ------------------------------------------------------------ host launchers
-extern "C" hipError_t scc_launch_ingest_count(const i64* indptr, const int* rows, const double* vals,
-                                              const double* dense, int N, int G, int K, const int* code,
-                                              u32* cnt, u32* neg, int* nodg, dd* wave_expm1, int nwaves,
-                                              int want_expm1, int* err, hipStream_t st)
+extern "C" int scc_ingest_chunks(int N, int* cells_per_wg)
 {
-    int blocks = nwaves / 4;
-    if (dense)
-        hipLaunchKernelGGL(k_ingest_count_dense, dim3(blocks), dim3(256), 0, st, dense, N, G, K, code, cnt, neg, nodg,
-                           wave_expm1, want_expm1, err);
-    else
-        hipLaunchKernelGGL(k_ingest_count, dim3(blocks), dim3(256), 0, st, indptr, rows, vals, N, G, K, code, cnt, neg,
-                           nodg, wave_expm1, want_expm1, err);
+    int nwg = N / 16;
+    if (nwg > 1024) nwg = 1024;
+    if (nwg < 1) nwg = 1;
+    *cells_per_wg = (N + nwg - 1) / nwg;
+    return (N + *cells_per_wg - 1) / *cells_per_wg;
+}
+
+extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows, const double* vals,
+                                             const double* dense, int N, int G, int nwg, int cells_per_wg,
+                                             const int* code, u32* cnt, int* nodg, dd* wave_expm1, int want_expm1,
+                                             int* err, hipStream_t st)
+{
+    const size_t lds = sizeof(u32) * (size_t)G;
+    if (dense) {
+        hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_ing_hist<true>, dim3(nwg), dim3(ING_T), lds, st, nullptr, nullptr, dense, N, G,
+                           cells_per_wg, code, cnt, nodg, wave_expm1, want_expm1, err);
+    } else {
+        hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_ing_hist<false>, dim3(nwg), dim3(ING_T), lds, st, indptr, rows, vals, N, G, cells_per_wg,
+                           code, cnt, nodg, wave_expm1, want_expm1, err);
+    }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nwg, int G, u32* total, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_ing_colscan, dim3((G + 255) / 256), dim3(256), 0, st, cnt, nwg, G, total);
     return hipGetLastError();
 }
 
 extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* rows, const double* vals,
-                                                const double* dense, int N, int G, int K, const int* code,
-                                                const i64* seg_off, u32* cursor, u64* keys, int nwaves, hipStream_t st)
+                                                const double* dense, int N, int G, int nwg, int cells_per_wg,
+                                                const int* code, const u32* cnt, const i64* gstart, u64* keys,
+                                                u8* codes, hipStream_t st)
 {
-    int blocks = nwaves / 4;
-    if (dense)
-        hipLaunchKernelGGL(k_ingest_scatter_dense, dim3(blocks), dim3(256), 0, st, dense, N, G, K, code, seg_off,
-                           cursor, keys);
-    else
-        hipLaunchKernelGGL(k_ingest_scatter, dim3(blocks), dim3(256), 0, st, indptr, rows, vals, N, G, K, code, seg_off,
-                           cursor, keys);
+    const size_t lds = sizeof(u32) * (size_t)G;
+    if (dense) {
+        hipFuncSetAttribute((const void*)k_ing_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_ing_scatter<true>, dim3(nwg), dim3(ING_T), lds, st, nullptr, nullptr, dense, N, G,
+                           cells_per_wg, code, cnt, gstart, keys, codes);
+    } else {
+        hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_ing_scatter<false>, dim3(nwg), dim3(ING_T), lds, st, indptr, rows, vals, N, G,
+                           cells_per_wg, code, cnt, gstart, keys, codes);
+    }
     return hipGetLastError();
 }
 

@@ -60,7 +60,8 @@ struct scc_ctx {
 };
 
 struct scc_dataset {
-    scc_ctx* ctx = nullptr;
+    scc_ctx* ctx = nullptr;  // borrowed; the dataset must be destroyed before its context
+    int device = 0;
     int64_t G = 0, N = 0, nnz = 0;
     bool dense = false;
     long long* d_indptr = nullptr;

@@ -15,9 +15,9 @@ struct dd;
 struct ScRankLaunch {
     const int* gene_list;
     const int* list_count;
-    const long long* seg_off;
+    const long long* gstart;
     unsigned long long* keys;
-    uint8_t* codes_scratch;
+    uint8_t* codes;
     int G, K, cap, grid;
     const int* n_clu;
     double* mean_x;
@@ -80,21 +80,22 @@ struct ScSelectLaunch {
 };
 
 extern "C" {
-hipError_t scc_launch_ingest_count(const long long* indptr, const int* rows, const double* vals,
-                                   const double* dense, int N, int G, int K, const int* code, uint32_t* cnt,
-                                   uint32_t* neg, int* nodg, dd* wave_expm1, int nwaves, int want_expm1, int* err,
-                                   hipStream_t st);
+int scc_ingest_chunks(int N, int* cells_per_wg);
+hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
+                                  int N, int G, int nwg, int cells_per_wg, const int* code, uint32_t* cnt, int* nodg,
+                                  dd* wave_expm1, int want_expm1, int* err, hipStream_t st);
+hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nwg, int G, uint32_t* total, hipStream_t st);
 hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, const double* vals,
-                                     const double* dense, int N, int G, int K, const int* code,
-                                     const long long* seg_off, uint32_t* cursor, unsigned long long* keys,
-                                     int nwaves, hipStream_t st);
+                                     const double* dense, int N, int G, int nwg, int cells_per_wg, const int* code,
+                                     const uint32_t* cnt, const long long* gstart, unsigned long long* keys,
+                                     uint8_t* codes, hipStream_t st);
 hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
                            long long* total, hipStream_t st);
 int scc_scan_scratch_blocks(long long n);
 hipError_t scc_launch_reduce_dd(const dd* parts, int n, dd* out, hipStream_t st);
 
-hipError_t scc_launch_classify(const long long* seg_off, int G, int K, int cap_s, int cap_m, int* lists,
-                               int* counts, hipStream_t st);
+hipError_t scc_launch_classify(const long long* gstart, int G, int cap_s, int cap_m, int* lists, int* counts,
+                               hipStream_t st);
 size_t scc_rank_lds_bytes(int cls, int cap, int K);
 hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st);
 

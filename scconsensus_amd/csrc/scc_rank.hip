@@ -6,8 +6,8 @@
 // per-pair log-mean/pct statistics (Fast:229-271, slow:104-113).
 //
 // One workgroup per gene:
-//   1. per-cluster statistics from the (gene, cluster) buckets (dd sums of x
-//      and expm1(x), counts of x > 0 / x < 0)                      [exact ints]
+//   1. per-cluster statistics (dd sums of x and expm1(x), counts of x > 0 /
+//      x < 0), one wave per cluster over the gene's (key, code) pairs
 //   2. sort the gene's kept nonzeros by (value, cluster code)         [bitonic]
 //   3. one sweep: S[a][b] = #{b-elements before an a-element}.  With ties
 //      ordered by code, for a < b this is exactly #{(x in a, y in b): x > y}
@@ -37,9 +37,9 @@ __device__ inline void pair_decode(int p, int K, int& a, int& b)
 struct RankArgs {
     const int* gene_list;
     const int* list_count;
-    const i64* seg_off;  // [G*K+1]
-    u64* keys;           // bucketed keys (sorted in place for big genes)
-    u8* codes_scratch;   // per-nnz scratch codes (big genes only)
+    const i64* gstart;   // [G+1] gene segment starts
+    u64* keys;           // kept nonzeros' value keys (sorted in place for big genes)
+    u8* codes;           // their cluster codes
     int G, K, P;
     const int* n_clu;    // kept cells per cluster
     double* mean_x;      // [K][G]
@@ -130,31 +130,35 @@ __device__ void rank_sweep_finalize(const RankArgs& A, int g, int n, const u64* 
     }
 }
 
-// Per-cluster statistics from the unsorted (gene, cluster) buckets.
+// Per-cluster statistics: wave w takes clusters a = w, w+W, ... and scans the
+// gene's n (key, code) pairs for its cluster (order-insensitive dd sums).
 template <int T>
-__device__ void cluster_stats(const RankArgs& A, int g, const int* off, const u64* key, u32* posc, u32* negc)
+__device__ void cluster_stats(const RankArgs& A, int g, int n, const u64* key, const u8* code, u32* posc, u32* negc)
 {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int W = T / 64;
     for (int a = w; a < A.K; a += W) {
         dd sx{0.0, 0.0}, se{0.0, 0.0};
-        u32 pos = 0;
-        for (int i = off[a] + lane; i < off[a + 1]; i += 64) {
+        u32 pos = 0, neg = 0;
+        for (int i = lane; i < n; i += 64) {
+            if (code[i] != a) continue;
             const double x = scc_val_of(key[i]);
             sx = dd_add_d(sx, x);
             se = dd_add_d(se, expm1(x));
             pos += (x > 0.0);
+            neg += (x < 0.0);
         }
         sx = dd_wave_sum(sx);
         se = dd_wave_sum(se);
         pos = u32_wave_sum(pos);
+        neg = u32_wave_sum(neg);
         if (lane == 0) {
             const double na = (double)A.n_clu[a];
             A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
             A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
             A.cnt_pos[(size_t)a * A.G + g] = pos;
             posc[a] = pos;
-            negc[a] = (u32)(off[a + 1] - off[a]) - pos;
+            negc[a] = neg;
         }
     }
 }
@@ -220,25 +224,15 @@ __global__ void __launch_bounds__(T) k_gene_rank_lds(RankArgs A, int cap)
     const int g = A.gene_list[blockIdx.x];
     const int K = A.K, tid = threadIdx.x;
     RankLds L = carve<T>(smem, cap, K, 4);
-    const i64* so = A.seg_off + (size_t)g * K;
-    const i64 base = so[0];
-    const int n = (int)(so[K] - base);
-    for (int i = tid; i <= K; i += T) L.off[i] = (int)(so[i] - base);
+    const i64 base = A.gstart[g];
+    const int n = (int)(A.gstart[g + 1] - base);
     zero_lds<T, u32>(L, K);
-    __syncthreads();
     for (int i = tid; i < n; i += T) {
         L.skey[i] = A.keys[base + i];
-        // cluster of position i: largest a with off[a] <= i (skip empty buckets)
-        int lo = 0, hi = K;  // off[lo] <= i < off[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (L.off[mid] <= i) lo = mid;
-            else hi = mid;
-        }
-        L.scode[i] = (u8)lo;
+        L.scode[i] = A.codes[base + i];
     }
     __syncthreads();
-    cluster_stats<T>(A, g, L.off, L.skey, L.posc, L.negc);
+    cluster_stats<T>(A, g, n, L.skey, L.scode, L.posc, L.negc);
     __syncthreads();  // stats read the unsorted buckets
     AccKeyCode acc{L.skey, L.scode};
     block_bitonic(acc, n, tid, T);  // ends with a barrier
@@ -254,17 +248,12 @@ __global__ void __launch_bounds__(T) k_gene_rank_big(RankArgs A, int chunk)
     const int g = A.gene_list[blockIdx.x];
     const int K = A.K, tid = threadIdx.x;
     RankLds L = carve<T>(smem, chunk, K, 8);
-    const i64* so = A.seg_off + (size_t)g * K;
-    const i64 base = so[0];
-    const int n = (int)(so[K] - base);
+    const i64 base = A.gstart[g];
+    const int n = (int)(A.gstart[g + 1] - base);
     u64* gkey = A.keys + base;
-    u8* gcode = A.codes_scratch + base;
-    for (int i = tid; i <= K; i += T) L.off[i] = (int)(so[i] - base);
+    u8* gcode = A.codes + base;
     zero_lds<T, u64>(L, K);
-    __syncthreads();
-    for (int a = 0; a < K; ++a)
-        for (int i = L.off[a] + tid; i < L.off[a + 1]; i += T) gcode[i] = (u8)a;
-    cluster_stats<T>(A, g, L.off, gkey, L.posc, L.negc);
+    cluster_stats<T>(A, g, n, gkey, gcode, L.posc, L.negc);
     __syncthreads();
     AccKeyCode gacc{gkey, gcode}, sacc{L.skey, L.scode};
     block_bitonic_staged(gacc, n, sacc, chunk, tid, T);
@@ -272,22 +261,20 @@ __global__ void __launch_bounds__(T) k_gene_rank_big(RankArgs A, int chunk)
 }
 
 // Size classes: 0 small (n <= cap_s), 1 medium (n <= cap_m), 2 big.
-__global__ void k_classify(const i64* __restrict__ seg_off, int G, int K, int cap_s, int cap_m, int* lists,
-                           int* counts)
+__global__ void k_classify(const i64* __restrict__ gstart, int G, int cap_s, int cap_m, int* lists, int* counts)
 {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
-    const i64 n = seg_off[(size_t)(g + 1) * K] - seg_off[(size_t)g * K];
+    const i64 n = gstart[g + 1] - gstart[g];
     const int cls = (n <= cap_s) ? 0 : ((n <= cap_m) ? 1 : 2);
     const int slot = atomicAdd(&counts[cls], 1);
     lists[(size_t)cls * G + slot] = g;
 }
 
-extern "C" hipError_t scc_launch_classify(const i64* seg_off, int G, int K, int cap_s, int cap_m, int* lists,
-                                          int* counts, hipStream_t st)
+extern "C" hipError_t scc_launch_classify(const i64* gstart, int G, int cap_s, int cap_m, int* lists, int* counts,
+                                          hipStream_t st)
 {
-    hipLaunchKernelGGL(k_classify, dim3((G + 255) / 256), dim3(256), 0, st, seg_off, G, K, cap_s, cap_m, lists,
-                       counts);
+    hipLaunchKernelGGL(k_classify, dim3((G + 255) / 256), dim3(256), 0, st, gstart, G, cap_s, cap_m, lists, counts);
     return hipGetLastError();
 }
 
@@ -301,9 +288,9 @@ extern "C" hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipSt
     RankArgs A;
     A.gene_list = L->gene_list;
     A.list_count = L->list_count;
-    A.seg_off = L->seg_off;
+    A.gstart = L->gstart;
     A.keys = L->keys;
-    A.codes_scratch = L->codes_scratch;
+    A.codes = L->codes;
     A.G = L->G;
     A.K = L->K;
     A.P = L->K * (L->K - 1) / 2;

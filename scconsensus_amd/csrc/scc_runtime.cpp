@@ -102,6 +102,7 @@ extern "C" int scc_dataset_create_csc(scc_ctx* c, const int64_t* indptr, const i
     hipSetDevice(c->device);
     scc_dataset* d = new scc_dataset();
     d->ctx = c;
+    d->device = c->device;
     d->G = G;
     d->N = N;
     d->nnz = nnz;
@@ -142,6 +143,7 @@ extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, 
     hipSetDevice(c->device);
     scc_dataset* d = new scc_dataset();
     d->ctx = c;
+    d->device = c->device;
     d->G = G;
     d->N = N;
     d->nnz = G * N;
@@ -169,8 +171,8 @@ extern "C" void scc_dataset_destroy(scc_dataset* d)
 {
     if (!d) return;
     if (d->owned) {
-        hipSetDevice(d->ctx->device);
-        hipStreamSynchronize(d->ctx->s0);
+        hipSetDevice(d->device);
+        hipDeviceSynchronize();
         hipFree(d->d_indptr);
         hipFree(d->d_rows);
         hipFree(d->d_vals);
@@ -208,8 +210,8 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     const size_t PG = (size_t)P * G;
     int rc;
     int *d_code, *d_nclu, *d_nodg, *d_lists, *d_counts, *d_err, *d_tested, *d_union, *d_nu;
-    uint32_t *d_cnt, *d_neg, *d_cursor, *d_cntpos;
-    long long *d_segoff, *d_scan, *d_rowoff;
+    uint32_t *d_cnt, *d_total, *d_cntpos;
+    long long *d_gstart, *d_scan, *d_rowoff;
     unsigned long long* d_keys;
     uint8_t* d_codes;
     dd* d_wexp;
@@ -219,7 +221,9 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     unsigned long long *d_tie_e, *d_tie_x, *d_first;
     double *d_p, *d_lfc, *d_pct1, *d_pct2;
     uint8_t* d_flags;
-    const int nwaves = 4096;
+    int cells_per_wg = 1;
+    const int nwg = scc_ingest_chunks(N, &cells_per_wg);
+    const int nwaves = nwg * 4;
 #define WS(name, n, ptr)                                  \
     do {                                                  \
         if ((rc = ws(c, name, (size_t)(n), &(ptr)))) return rc; \
@@ -227,11 +231,10 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     WS("code", N, d_code);
     WS("nclu", K, d_nclu);
     WS("nodg", N, d_nodg);
-    WS("cnt", GK, d_cnt);
-    WS("neg", GK, d_neg);
-    WS("cursor", GK, d_cursor);
-    WS("segoff", GK + 1, d_segoff);
-    WS("scan", scc_scan_scratch_blocks(GK) + 1, d_scan);
+    WS("cnt", (size_t)nwg * G, d_cnt);
+    WS("total", G, d_total);
+    WS("gstart", G + 1, d_gstart);
+    WS("scan", scc_scan_scratch_blocks(G) + 1, d_scan);
     WS("keys", std::max<int64_t>(ds->nnz, 1), d_keys);
     WS("codes", std::max<int64_t>(ds->nnz, 1), d_codes);
     {
@@ -270,16 +273,14 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     HIPCHK(c, hipMemcpyAsync(d_nclu, nclu.data(), sizeof(int) * K, hipMemcpyHostToDevice, s0));
     {
         Scope sc(c, "ingest", s0);
-        HIPCHK(c, hipMemsetAsync(d_cnt, 0, sizeof(uint32_t) * GK, s0));
-        HIPCHK(c, hipMemsetAsync(d_neg, 0, sizeof(uint32_t) * GK, s0));
-        HIPCHK(c, hipMemsetAsync(d_cursor, 0, sizeof(uint32_t) * GK, s0));
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
         HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 4, s0));
-        HIPCHK(c, scc_launch_ingest_count(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, K, d_code, d_cnt,
-                                          d_neg, d_nodg, d_wexp, nwaves, fast ? 0 : 1, d_err, s0));
-        HIPCHK(c, scc_launch_scan(d_cnt, GK, d_segoff, d_scan, d_segoff + GK, s0));
-        HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, K, d_code,
-                                            d_segoff, d_cursor, d_keys, nwaves, s0));
+        HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, nwg, cells_per_wg,
+                                         d_code, d_cnt, d_nodg, d_wexp, fast ? 0 : 1, d_err, s0));
+        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nwg, G, d_total, s0));
+        HIPCHK(c, scc_launch_scan(d_total, G, d_gstart, d_scan, d_gstart + G, s0));
+        HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, nwg,
+                                            cells_per_wg, d_code, d_cnt, d_gstart, d_keys, d_codes, s0));
         if (!fast) HIPCHK(c, scc_launch_reduce_dd(d_wexp, nwaves, d_gexp, s0));
     }
     {
@@ -289,13 +290,13 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         // size classes (env overrides exist to exercise the big-gene path on small test data)
         const int cap_s = env_int("SCC_CAP_SMALL", kCapSmall), cap_m = env_int("SCC_CAP_MEDIUM", kCapMedium);
         const int chunk_big = env_int("SCC_CHUNK_BIG", kChunkBig);
-        HIPCHK(c, scc_launch_classify(d_segoff, G, K, cap_s, cap_m, d_lists, d_counts, s0));
+        HIPCHK(c, scc_launch_classify(d_gstart, G, cap_s, cap_m, d_lists, d_counts, s0));
         HIPCHK(c, hipEventRecord(c->ev_fork, s0));
         HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
         ScRankLaunch L{};
-        L.seg_off = d_segoff;
+        L.gstart = d_gstart;
         L.keys = d_keys;
-        L.codes_scratch = d_codes;
+        L.codes = d_codes;
         L.G = G;
         L.K = K;
         L.n_clu = d_nclu;
