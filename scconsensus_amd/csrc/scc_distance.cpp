@@ -25,8 +25,6 @@ hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const doub
 hipError_t scc_launch_dist_euclid(const double* P, int N, void* out, int f32, hipStream_t st);
 hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, void* out, int f32,
                               hipStream_t st);
-hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
-                                 hipStream_t st);
 }
 
 extern "C" void scc_distance_release(scc_ctx*) {}
@@ -95,7 +93,16 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         }
         {
             Scope sc(c, "eigen", s0);
-            HIPCHK(c, scc_launch_syevx_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, s0));
+            unsigned long long* st_buf = nullptr;
+            if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 8, st_buf);
+            HIPCHK(c, scc_launch_syevx_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, st_buf, s0));
+            if (st_buf) {
+                unsigned long long h[8];
+                HIPCHK(c, hipMemcpyAsync(h, st_buf, sizeof(h), hipMemcpyDeviceToHost, s0));
+                HIPCHK(c, hipStreamSynchronize(s0));
+                fprintf(stderr, "[scc stamps] eigen n=%d: tridiag %llu, bisect %llu, inviter %llu, backtr %llu cycles\n",
+                        nu, h[1] - h[0], h[2] - h[1], h[3] - h[2], h[4] - h[3]);
+            }
         }
         {
             Scope sc(c, "scores", s0);

@@ -55,84 +55,201 @@ __device__ inline int sturm_count(const double* d, const double* e, int n, doubl
     return c;
 }
 
-// A: n x n symmetric (full), row-major, leading dimension lda; destroyed.
-// scratch doubles: 4*n + 80*n.  Z: n x 16 out.  W: k out (descending).
-__global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z,
-                                                      double* W)
+// Fused pass of step k (see k_syevx_topk): rows i = 1..m-1 of the trailing
+// block T (local (i,j) at T[(off+i)*ld + off+j]) are updated by the rank-2
+// term of step k, and the same sweep forms p' = tau' * T' v' for step k+1.
+// Output rows go to O (ld_o, off_o) — the same storage, or LDS on the switch.
+template <class TP, class OP>
+__device__ __forceinline__ void fused_pass(TP T, int ld, int off, OP O, int ldo, int offo, int m, const double* v,
+                                           const double* w, const double* vn, double taun, double* pn)
 {
-    __shared__ double red[EIG_W];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = 1 + wv; i < m; i += EIG_W) {
+        const size_t ri = (size_t)(off + i) * ld + off;
+        const size_t ro = (size_t)(offo + i - 1) * ldo + offo - 1;
+        const double vi = v[i], wi = w[i];
+        double s = 0.0;
+        for (int j = 1 + lane; j < m; j += 64) {
+            const double r = T[ri + j] - vi * w[j] - wi * v[j];
+            O[ro + j] = r;
+            s += r * vn[j - 1];
+        }
+        s = wave_sum_d(s);
+        if (lane == 0) pn[i - 1] = taun * s;
+    }
+}
+
+// A: n x n symmetric (full), row-major, leading dimension lda; destroyed
+// (the reflectors are left in its rows).  scratch doubles: 84 n.
+// Z: n x 16 out.  W: k out (descending).  Dynamic LDS: 3 n + 16 doubles plus
+// an mlds x mlds tail block.
+#define ESTAMP(ph)                                                          \
+    do {                                                                    \
+        if (stamps && threadIdx.x == 0) stamps[ph] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+
+__global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z,
+                                                      double* W, int mlds, u64* stamps)
+{
+    ESTAMP(0);
+    extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ double sh[8];
+    double* red = sm;                 // EIG_W
+    double* vb = sm + 16;             // n   current reflector v (v[0] = 1)
+    double* wb = vb + n;              // n   w = p - tau/2 (p.v) v
+    double* pb = wb + n;              // n   p = tau A22 v
+    double* Tl = pb + n;              // mlds * mlds (LDS-resident tail)
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double* d = scratch;          // n
     double* e = d + n;            // n
     double* tau = e + n;          // n
-    double* p = tau + n;          // n (symv result / w)
+    double* p = tau + n;          // n (unused scratch)
     double* lu = p + n;           // 5n per eigenvector (<= 16): LU factors of T - lambda I
+    (void)p;
     // ---------------------------------------------------------------- 1. tridiagonalise
-    for (int kk = 0; kk < n - 2; ++kk) {
-        double* rowk = A + (size_t)kk * lda;
-        const int m = n - kk - 1;          // length of x = A[kk][kk+1 .. n-1]
-        double part = 0.0;
-        for (int i = 1 + tid; i < m; i += EIG_T) {
-            const double xv = rowk[kk + 1 + i];
-            part += xv * xv;
-        }
-        const double xnorm2 = block_sum(part, red);
-        const double alpha = rowk[kk + 1];
-        double taui = 0.0, beta = alpha, scal = 0.0;
-        if (xnorm2 > 0.0) {
-            beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
-            taui = (beta - alpha) / beta;
-            scal = 1.0 / (alpha - beta);
-        }
-        // v stored in place: rowk[kk+1] = 1 (implicit), rowk[kk+1+i] *= scal
-        __syncthreads();
-        for (int i = 1 + tid; i < m; i += EIG_T) rowk[kk + 1 + i] *= scal;
+    // LAPACK dsytd2 (lower) order.  Reflector k is kept in row k of A
+    // (A[k][k+1] = 1, A[k][k+2..] = v tail) for the back-transformation.
+    if (n <= 2) {
         if (tid == 0) {
-            d[kk] = rowk[kk];
-            e[kk] = beta;
-            tau[kk] = taui;
-            rowk[kk + 1] = 1.0;
+            d[0] = A[0];
+            e[0] = (n == 2) ? A[1] : 0.0;
+            tau[0] = 0.0;
+            if (n == 2) {
+                d[1] = A[(size_t)lda + 1];
+                e[1] = 0.0;
+                tau[1] = 0.0;
+            }
         }
-        __syncthreads();
-        if (taui != 0.0) {
-            // p = taui * A22 v  (A22 = A[kk+1.., kk+1..]); one wave per row
-            const double* v = rowk + kk + 1;
+    } else {
+        // reflector 0 from row 0
+        {
+            const int m = n - 1;
+            double part = 0.0;
+            for (int j = 2 + tid; j < n; j += EIG_T) part += A[j] * A[j];
+            const double xn2 = block_sum(part, red);
+            const double alpha = A[1];
+            double t = 0.0, beta = alpha, scal = 0.0;
+            if (xn2 > 0.0) {
+                beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+                t = (beta - alpha) / beta;
+                scal = 1.0 / (alpha - beta);
+            }
+            for (int j = tid; j < m; j += EIG_T) vb[j] = (j == 0) ? 1.0 : A[1 + j] * scal;
+            __syncthreads();
+            for (int j = tid; j < m; j += EIG_T) A[1 + j] = vb[j];
+            if (tid == 0) {
+                d[0] = A[0];
+                e[0] = beta;
+                tau[0] = t;
+                sh[0] = t;
+            }
+            __syncthreads();
+            // p = tau A22 v
+            const double tt = sh[0];
             for (int i = wv; i < m; i += EIG_W) {
-                const double* ri = A + (size_t)(kk + 1 + i) * lda + kk + 1;
+                const double* ri = A + (size_t)(1 + i) * lda + 1;
                 double s = 0.0;
-                for (int j = lane; j < m; j += 64) s += ri[j] * v[j];
+                for (int j = lane; j < m; j += 64) s += ri[j] * vb[j];
                 s = wave_sum_d(s);
-                if (lane == 0) p[i] = taui * s;
+                if (lane == 0) pb[i] = tt * s;
             }
             __syncthreads();
+        }
+        bool in_lds = false;
+        int lds_base = 0, lds_ld = 0;  // step index at the switch, LDS leading dimension
+        for (int kk = 0; kk <= n - 3; ++kk) {
+            const int m = n - kk - 1;  // trailing block A22 = rows/cols kk+1 .. n-1
+            const double t = sh[0];
+            // w = p - tau/2 (p.v) v
             double pv = 0.0;
-            for (int i = tid; i < m; i += EIG_T) pv += p[i] * v[i];
+            for (int i = tid; i < m; i += EIG_T) pv += pb[i] * vb[i];
             const double dot = block_sum(pv, red);
-            const double alpha2 = -0.5 * taui * dot;
-            for (int i = tid; i < m; i += EIG_T) p[i] += alpha2 * v[i];
+            const double a2 = -0.5 * t * dot;
+            for (int i = tid; i < m; i += EIG_T) wb[i] = (t != 0.0) ? pb[i] + a2 * vb[i] : 0.0;
             __syncthreads();
-            // A22 -= v w^T + w v^T (full square, rows stay symmetric)
-            for (int i = wv; i < m; i += EIG_W) {
-                double* ri = A + (size_t)(kk + 1 + i) * lda + kk + 1;
-                const double vi = v[i], wi = p[i];
-                for (int j = lane; j < m; j += 64) ri[j] -= vi * p[j] + wi * v[j];
+            // locate row 0 of A22 (global row kk+1)
+            const double* row0;
+            int off0, ld0;
+            if (in_lds) {
+                off0 = kk + 1 - lds_base;
+                ld0 = lds_ld;
+                row0 = Tl + (size_t)off0 * ld0 + off0;
+            } else {
+                off0 = kk + 1;
+                ld0 = lda;
+                row0 = A + (size_t)off0 * ld0 + off0;
+            }
+            // updated row 0: x_j = A22[0][j] - v0 w_j - w0 v_j
+            const double v0 = vb[0], w0 = wb[0];
+            if (kk == n - 3) {  // 2 x 2 remainder
+                if (tid == 0) {
+                    const double a00 = row0[0] - 2.0 * v0 * w0;
+                    const double a01 = row0[1] - v0 * wb[1] - w0 * vb[1];
+                    const double* row1 = row0 + ld0;
+                    const double a11 = row1[1] - 2.0 * vb[1] * wb[1];
+                    d[n - 2] = a00;
+                    e[n - 2] = a01;
+                    d[n - 1] = a11;
+                    e[n - 1] = 0.0;
+                    tau[n - 2] = 0.0;
+                    tau[n - 1] = 0.0;
+                }
+                break;
+            }
+            double part = 0.0;
+            for (int j = 2 + tid; j < m; j += EIG_T) {
+                const double x = row0[j] - v0 * wb[j] - w0 * vb[j];
+                part += x * x;
+            }
+            const double xn2 = block_sum(part, red);
+            const double alpha = row0[1] - v0 * wb[1] - w0 * vb[1];
+            double tn = 0.0, beta = alpha, scal = 0.0;
+            if (xn2 > 0.0) {
+                beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+                tn = (beta - alpha) / beta;
+                scal = 1.0 / (alpha - beta);
+            }
+            // v' (length m-1) reuses p's LDS buffer: p of step kk is consumed (w formed)
+            double* vn = pb;
+            for (int j = 1 + tid; j < m; j += EIG_T) {
+                const double x = row0[j] - v0 * wb[j] - w0 * vb[j];
+                vn[j - 1] = (j == 1) ? 1.0 : x * scal;
+            }
+            if (tid == 0) {
+                d[kk + 1] = row0[0] - 2.0 * v0 * w0;
+                e[kk + 1] = beta;
+                tau[kk + 1] = tn;
             }
             __syncthreads();
+            double* refl = A + (size_t)(kk + 1) * lda + kk + 2;
+            for (int j = tid; j < m - 1; j += EIG_T) refl[j] = vn[j];
+            // fused pass: rows 1..m-1 of A22 updated (v, w read), p' to scratch
+            double* pn = lu;  // free until the inverse iteration
+            const int mn = m - 1;
+            if (!in_lds && mn <= mlds) {
+                // switch: the updated trailing block is written to LDS
+                fused_pass(A, lda, kk + 1, Tl, mn, 0, m, vb, wb, vn, tn, pn);
+                in_lds = true;
+                lds_base = kk + 2;
+                lds_ld = mn;
+            } else if (in_lds) {
+                const int o = kk + 1 - lds_base;
+                fused_pass(Tl, lds_ld, o, Tl, lds_ld, o + 1, m, vb, wb, vn, tn, pn);
+            } else {
+                fused_pass(A, lda, kk + 1, A, lda, kk + 2, m, vb, wb, vn, tn, pn);
+            }
+            __syncthreads();
+            // next step: v <- v', p <- p'
+            for (int j = tid; j < mn; j += EIG_T) {
+                vb[j] = vn[j];
+                pb[j] = pn[j];
+            }
+            if (tid == 0) sh[0] = tn;
+            __syncthreads();
         }
-        // the reflector lives in rowk[kk+1..]; keep the beta in e[kk]
-    }
-    if (tid == 0) {
-        if (n >= 2) {
-            d[n - 2] = A[(size_t)(n - 2) * lda + n - 2];
-            e[n - 2] = A[(size_t)(n - 2) * lda + n - 1];
-            tau[n - 2] = 0.0;
-        }
-        d[n - 1] = A[(size_t)(n - 1) * lda + n - 1];
-        e[n - 1] = 0.0;
-        tau[n - 1] = 0.0;
     }
     __syncthreads();
+    ESTAMP(1);
     // ---------------------------------------------------------------- 2. eigenvalues
     // Gershgorin bounds, pivmin as LAPACK dstebz
     if (tid == 0) {
@@ -172,6 +289,7 @@ __global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda,
         if (lane == 0) W[q] = 0.5 * (lo + hi);
     }
     __syncthreads();
+    ESTAMP(2);
     // ---------------------------------------------------------------- 3. inverse iteration
     // Each wave factors T - lambda_q I (dgttrf order, partial pivoting) for its
     // q and solves; between solves wave 0 re-orthogonalises cluster members
@@ -227,7 +345,7 @@ __global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda,
         }
         __threadfence_block();
         __syncthreads();
-        for (int iter = 0; iter < 4; ++iter) {
+        for (int iter = 0; iter < 3; ++iter) {
             for (int q = wv; q < k; q += EIG_W) {
                 if (lane == 0) {
                     const double* dd = lu + (size_t)q * 5 * n;
@@ -276,6 +394,7 @@ __global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda,
             __syncthreads();
         }
     }
+    ESTAMP(3);
     // ---------------------------------------------------------------- 4. back-transform
     // eigenvector of A = H_0 H_1 ... H_{n-3} y; apply from the last reflector.
     // One wave per vector q.
@@ -314,11 +433,20 @@ __global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda,
     __syncthreads();
     for (int i = tid; i < n * 16; i += EIG_T)
         if ((i & 15) >= k) Z[i] = 0.0;
+    ESTAMP(4);
 }
 
 extern "C" hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
-                                            hipStream_t st)
+                                            u64* stamps, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_syevx_topk, dim3(1), dim3(EIG_T), 0, st, A, n, lda, k, scratch, Z, W);
+    // LDS: red(16) + v, w, p (3n) + the largest square tail that fits in 156 KiB
+    const size_t budget = 156 * 1024;
+    const size_t fixed = sizeof(double) * (16 + 3 * (size_t)n);
+    if (fixed > budget) return hipErrorInvalidValue;
+    int mlds = (int)floor(sqrt((double)(budget - fixed) / sizeof(double)));
+    if (mlds > n) mlds = n;
+    const size_t lds = fixed + sizeof(double) * (size_t)mlds * mlds;
+    hipFuncSetAttribute((const void*)k_syevx_topk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_syevx_topk, dim3(1), dim3(EIG_T), lds, st, A, n, lda, k, scratch, Z, W, mlds, stamps);
     return hipGetLastError();
 }

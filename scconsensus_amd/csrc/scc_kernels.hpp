@@ -27,6 +27,7 @@ struct ScRankLaunch {
     long long* t_base;
     unsigned long long* tie_e;
     unsigned long long* tie_x;
+    unsigned long long* stamps;  // diagnostic only
 };
 
 struct ScTestLaunch {
@@ -98,6 +99,8 @@ hipError_t scc_launch_classify(const long long* gstart, int G, int cap_s, int ca
                                hipStream_t st);
 size_t scc_rank_lds_bytes(int cls, int cap, int K);
 hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st);
+hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
+                                 unsigned long long* stamps, hipStream_t st);
 
 hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st);
 int scc_wilcox_table_layout(int* woff);

@@ -49,7 +49,14 @@ struct RankArgs {
     i64* t_base;         // [P][G]
     u64* tie_e;          // [P][G] (zeroed; atomically accumulated)
     u64* tie_x;          // [P][G]
+    u64* stamps;         // diagnostic phase clocks [block][8] (nullptr in normal runs)
 };
+
+#define STAMP(A, ph)                                                                      \
+    do {                                                                                  \
+        if ((A).stamps && threadIdx.x == 0)                                               \
+            (A).stamps[(size_t)blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memtime();    \
+    } while (0)
 
 // Shared tail of both kernels: given keys/codes (LDS or HBM) sorted, and the
 // per-cluster counts, do the sweep, tie groups and per-pair outputs.
@@ -65,6 +72,7 @@ __device__ void rank_sweep_finalize(const RankArgs& A, int g, int n, const u64* 
     const int c0 = min(n, w * ch), c1 = min(n, c0 + ch);
     for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&whist[w * K + scode[i]], 1u);
     __syncthreads();
+    STAMP(A, 3);
     // ---- sweep: lane b keeps the running count of cluster b before position i
     if (lane < K) {
         u32 C = 0;
@@ -116,6 +124,7 @@ __device__ void rank_sweep_finalize(const RankArgs& A, int g, int n, const u64* 
         }
     }
     __syncthreads();
+    STAMP(A, 4);
     // ---- per pair outputs
     for (int p = tid; p < A.P; p += T) {
         int a, b;
@@ -128,6 +137,7 @@ __device__ void rank_sweep_finalize(const RankArgs& A, int g, int n, const u64* 
         A.u2_base[(size_t)p * A.G + g] = (i64)u2;
         A.t_base[(size_t)p * A.G + g] = (i64)t;
     }
+    STAMP(A, 5);
 }
 
 // Per-cluster statistics: wave w takes clusters a = w, w+W, ... and scans the
@@ -223,6 +233,7 @@ __global__ void __launch_bounds__(T) k_gene_rank_lds(RankArgs A, int cap)
     if ((int)blockIdx.x >= *A.list_count) return;
     const int g = A.gene_list[blockIdx.x];
     const int K = A.K, tid = threadIdx.x;
+    STAMP(A, 0);
     RankLds L = carve<T>(smem, cap, K, 4);
     const i64 base = A.gstart[g];
     const int n = (int)(A.gstart[g + 1] - base);
@@ -232,10 +243,13 @@ __global__ void __launch_bounds__(T) k_gene_rank_lds(RankArgs A, int cap)
         L.scode[i] = A.codes[base + i];
     }
     __syncthreads();
+    STAMP(A, 1);
     cluster_stats<T>(A, g, n, L.skey, L.scode, L.posc, L.negc);
     __syncthreads();  // stats read the unsorted buckets
+    STAMP(A, 2);
     AccKeyCode acc{L.skey, L.scode};
     block_bitonic(acc, n, tid, T);  // ends with a barrier
+    STAMP(A, 6);
     rank_sweep_finalize<T, u32>(A, g, n, L.skey, L.scode, (u32*)L.S, L.whist, L.F, L.posc, L.negc);
 }
 
@@ -247,16 +261,20 @@ __global__ void __launch_bounds__(T) k_gene_rank_big(RankArgs A, int chunk)
     if ((int)blockIdx.x >= *A.list_count) return;
     const int g = A.gene_list[blockIdx.x];
     const int K = A.K, tid = threadIdx.x;
+    STAMP(A, 0);
     RankLds L = carve<T>(smem, chunk, K, 8);
     const i64 base = A.gstart[g];
     const int n = (int)(A.gstart[g + 1] - base);
     u64* gkey = A.keys + base;
     u8* gcode = A.codes + base;
     zero_lds<T, u64>(L, K);
+    STAMP(A, 1);
     cluster_stats<T>(A, g, n, gkey, gcode, L.posc, L.negc);
     __syncthreads();
+    STAMP(A, 2);
     AccKeyCode gacc{gkey, gcode}, sacc{L.skey, L.scode};
     block_bitonic_staged(gacc, n, sacc, chunk, tid, T);
+    STAMP(A, 6);
     rank_sweep_finalize<T, u64>(A, g, n, gkey, gcode, (u64*)L.S, L.whist, L.F, L.posc, L.negc);
 }
 
@@ -302,6 +320,7 @@ extern "C" hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipSt
     A.t_base = L->t_base;
     A.tie_e = L->tie_e;
     A.tie_x = L->tie_x;
+    A.stamps = L->stamps;
     const int grid = L->grid;
     if (grid <= 0) return hipSuccess;
     if (cls == 0) {

@@ -308,21 +308,56 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         L.tie_e = d_tie_e;
         L.tie_x = d_tie_x;
         L.grid = G;
+        unsigned long long* st_buf = nullptr;
+        const bool stamps = env_int("SCC_STAMPS", 0) != 0;
+        if (stamps) {
+            WS("d_rstamps", (size_t)3 * G * 8, st_buf);
+            HIPCHK(c, hipMemsetAsync(st_buf, 0, sizeof(unsigned long long) * 3 * G * 8, s0));
+        }
         // big genes first on the side stream
         L.gene_list = d_lists + 2 * (size_t)G;
         L.list_count = d_counts + 2;
         L.cap = chunk_big;
+        L.stamps = stamps ? st_buf + (size_t)2 * G * 8 : nullptr;
         HIPCHK(c, scc_launch_gene_rank(2, &L, s1));
         L.gene_list = d_lists + (size_t)G;
         L.list_count = d_counts + 1;
         L.cap = cap_m;
+        L.stamps = stamps ? st_buf + (size_t)G * 8 : nullptr;
         HIPCHK(c, scc_launch_gene_rank(1, &L, s0));
         L.gene_list = d_lists;
         L.list_count = d_counts;
         L.cap = cap_s;
+        L.stamps = stamps ? st_buf : nullptr;
         HIPCHK(c, scc_launch_gene_rank(0, &L, s0));
         HIPCHK(c, hipEventRecord(c->ev_join, s1));
         HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
+        if (stamps) {
+            std::vector<unsigned long long> h((size_t)3 * G * 8);
+            int cnts[4];
+            HIPCHK(c, hipMemcpyAsync(h.data(), st_buf, h.size() * 8, hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipMemcpyAsync(cnts, d_counts, sizeof(cnts), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            const char* ph[] = {"load", "stats", "sort", "hist", "sweep+ties", "final"};
+            for (int cls = 0; cls < 3; ++cls) {
+                double acc[6] = {0, 0, 0, 0, 0, 0};
+                int nb = 0;
+                for (int b = 0; b < cnts[cls]; ++b) {
+                    const unsigned long long* t = &h[((size_t)cls * G + b) * 8];
+                    if (!t[0] || !t[5]) continue;
+                    acc[0] += (double)(t[1] - t[0]);
+                    acc[1] += (double)(t[2] - t[1]);
+                    acc[2] += (double)(t[6] - t[2]);
+                    acc[3] += (double)(t[3] - t[6]);
+                    acc[4] += (double)(t[4] - t[3]);
+                    acc[5] += (double)(t[5] - t[4]);
+                    ++nb;
+                }
+                fprintf(stderr, "[scc stamps] rank class %d: %d genes, mean cycles:", cls, nb);
+                for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.0f", ph[q], nb ? acc[q] / nb : 0.0);
+                fprintf(stderr, "\n");
+            }
+        }
     }
     // SLOW: log(meanScalingFactor * mean(expm1(X))) on device would need one
     // more kernel; it is a scalar, read back together with the union below.
