@@ -19,6 +19,7 @@ for s in "$@"; do
     testsall) step testsall 900 python -u -m pytest tests -m gpu -v --timeout 300 ;;
     bench) step bench 900 python bench.py ;;
     benchq) step benchq 600 python bench.py --no-cpu-baseline ;;
+    stamps) SCC_STAMPS=1 step stamps 300 python scripts/diag_gpu.py B ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

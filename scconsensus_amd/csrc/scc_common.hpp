@@ -93,6 +93,10 @@ __device__ inline u32 u32_wave_sum(u32 x)
     return x;
 }
 
+// wave index inside the workgroup, as a wave-uniform (SGPR) value: loops
+// bounded by it stay scalar instead of being treated as divergent
+__device__ inline int scc_wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 __host__ __device__ inline int scc_next_pow2(int n)
 {
     int m = 1;

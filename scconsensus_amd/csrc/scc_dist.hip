@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indp
                                                     const int* __restrict__ umap, int ld, double* __restrict__ Xc)
 {
     const int lane = threadIdx.x & 63;
-    const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int wid = blockIdx.x * (blockDim.x >> 6) + scc_wave_id();
     const int nw = gridDim.x * (blockDim.x >> 6);
     for (int c = wid; c < N; c += nw) {
         for (i64 k = indptr[c] + lane; k < indptr[c + 1]; k += 64) {
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
     }
     const int tj = ti + t;
     const int chunk = blockIdx.y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = scc_wave_id();
     const int wi = (w >> 1) * 32, wj = (w & 1) * 32;
     const int i0 = ti * 64 + wi, j0 = tj * 64 + wj;
     const int c0 = chunk * rows_per_chunk, c1 = min(Npad, c0 + rows_per_chunk);
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(256) k_zscore(const double* __restrict__ Xc, i
                                                 float* __restrict__ Z)
 {
     const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int c = blockIdx.x * 4 + scc_wave_id();
     if (c >= N) return;
     const double* row = Xc + (size_t)c * ld;
     dd s{0.0, 0.0};
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(256) k_pearson_f32(const float* __restrict__ Z
     (void)ntile;
     __shared__ float sa[16][128 + 4];
     __shared__ float sb[16][128 + 4];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = scc_wave_id();
     const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
     const int I0 = ti * 128, J0 = tj * 128;
     f16v acc[2][2];

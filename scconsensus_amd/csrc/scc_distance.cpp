@@ -82,7 +82,7 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         WS("d_W", ld, d_W);
         WS("d_Z", (size_t)ld * 16, d_Z);
         WS("d_P", (size_t)N * 16, d_P);
-        WS("d_escr", (size_t)84 * ld + 64, d_escr);
+        WS("d_escr", (size_t)104 * ld + 64, d_escr);
         {
             Scope sc(c, "center", s0);
             HIPCHK(c, scc_launch_center(d_X, N, nu, ld, (dd*)d_part, nchunk_mean, d_mean, s0));

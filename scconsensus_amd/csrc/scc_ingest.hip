@@ -1,21 +1,30 @@
-// scc_ingest.hip — boundary ingest: the R dgCMatrix (CSC over cells) or dense
-// column-major matrix plus per-cell cluster codes become a gene-major array of
-// (orderable 64-bit value key, cluster code) for the kept nonzeros, resident
-// in HBM.  Replaces the reference's per-pair `as.matrix(dataMatrix)` and
-// name-indexed column subsets (R/reclusterDEConsensusFast.R:361-368).
+// scc_ingest.hip — boundary ingest: the R dgCMatrix (CSC over cells, row
+// indices sorted inside each column) or a dense column-major matrix, plus the
+// per-cell cluster codes, become a gene-major array of orderable 64-bit value
+// keys of the kept nonzeros, resident in HBM.  Replaces the reference's
+// per-pair `as.matrix(dataMatrix)` and name-indexed column subsets
+// (R/reclusterDEConsensusFast.R:361-368).
 //
-// A block-local counting sort (no global atomics):
-//   k_ing_hist     one workgroup per chunk of cells: LDS histogram over genes
-//                  (kept nonzeros), nodg per cell (Fast:440-443, x > 0 over ALL
+// Cells are visited in cluster order (host permutation `perm`: kept cells by
+// code, then the unkept ones), in "count chunks" of <= 32 cells that never
+// straddle two clusters.  Inside every gene segment the keys are therefore
+// grouped by cluster: cluster a of gene g occupies
+//     [cnt[cl_cc[a]][g], cnt[cl_cc[a+1]][g])     (offsets inside the segment)
+// so per-cluster statistics are contiguous reductions and no code array is
+// stored.  A block-local counting sort, no global atomics:
+//   k_ing_hist     one workgroup per count chunk: LDS histogram over genes (kept
+//                  nonzeros), nodg per cell (Fast:440-443, x > 0 over ALL
 //                  cells), optional sum of expm1 over all entries (slow:36),
-//                  non-finite / bad-row flag; histogram row -> cnt[w][g]
-//   k_ing_colscan  per gene: exclusive prefix over chunks (in place), total[g]
-//   scan           gene starts gstart[G+1] (three-kernel device scan)
-//   k_ing_scatter  per chunk: LDS cursors = gstart[g] + cnt[w][g]; write keys
-//                  and codes.
-// Zeros are implicit (the tie group every Wilcoxon statistic handles in
-// closed form).  Within a gene the order is chunk-major (cell order across
-// chunks); the rank kernel sorts each gene anyway.
+//                  non-finite / bad-row / unsorted-row flags, and each cell's
+//                  entry boundaries at every gene tile (bnd)
+//   k_ing_colscan  per gene: exclusive prefix over count chunks (in place);
+//                  row nc = per-gene totals
+//   scan           gene starts gstart[G+1]
+//   k_ing_scatter  one workgroup per (scatter chunk of <= 4 count chunks of one
+//                  cluster, gene tile): the tile's entries are counting-sorted
+//                  by gene in LDS, then written out as per-gene runs (~15
+//                  consecutive keys each at PBMC density) instead of 8-byte
+//                  scattered stores.
 #include "scc_common.hpp"
 #include "scc_kernels.hpp"
 
@@ -33,33 +42,53 @@ __device__ inline void cell_range(const i64* indptr, int c, int G, i64& b, i64& 
     }
 }
 
+// err bits: 1 non-finite value, 2 row index out of range, 4 rows not sorted
 template <bool DENSE>
 __global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
-                                                    const double* __restrict__ vals, int N, int G, int cells_per_wg,
-                                                    const int* __restrict__ code, u32* __restrict__ cnt,
+                                                    const double* __restrict__ vals, int G, const int* __restrict__ perm,
+                                                    const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
+                                                    int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
                                                     int* __restrict__ nodg, dd* __restrict__ wave_expm1,
                                                     int want_expm1, int* __restrict__ err)
 {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int g = threadIdx.x; g < G; g += ING_T) hist[g] = 0;
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    const int ch = blockIdx.x;
+    const int a = cc_code[ch];
+    if (a >= 0)
+        for (int g = threadIdx.x; g < G; g += ING_T) hist[g] = 0;
     __syncthreads();
-    const int c0 = blockIdx.x * cells_per_wg, c1 = min(N, c0 + cells_per_wg);
+    const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
     dd se{0.0, 0.0};
     int bad = 0;
-    for (int c = c0 + wv; c < c1; c += ING_T / 64) {
+    for (int p = p0 + wv; p < p1; p += ING_T / 64) {
+        const int c = perm[p];
         i64 b, e;
         cell_range<DENSE>(indptr, c, G, b, e);
-        const int a = code[c];
         u32 pos = 0;
+        i64* bp = bnd + (size_t)p * (ntile + 1);
         for (i64 k = b + lane; k < e; k += 64) {
             const double x = vals[k];
             const int g = DENSE ? (int)(k - b) : rows[k];
             const bool gok = (g >= 0) & (g < G);
-            bad |= !(x - x == 0.0) | !gok;
+            bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
             pos += (x > 0.0);
             if (want_expm1) se = dd_add_d(se, expm1(x));
             if (a >= 0 && x != 0.0 && gok) atomicAdd(&hist[g], 1u);
+            if (!DENSE && a >= 0) {
+                // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
+                const int gp = (k > b) ? rows[k - 1] : -1;
+                if (k > b && gp >= g) bad |= 4;
+                const int tp = (gp < 0) ? -1 : min(gp / gt, ntile - 1);
+                const int tg = gok ? g / gt : (g < 0 ? -1 : ntile - 1);
+                for (int t = tp + 1; t <= tg; ++t) bp[t] = k;
+            }
+        }
+        if (!DENSE && a >= 0) {
+            // tiles after the last entry (and every tile of an empty cell) end at e
+            const int gl = (e > b) ? rows[e - 1] : -1;
+            const int tl = (gl < 0) ? -1 : min(gl / gt, ntile - 1);
+            for (int t = tl + 1 + lane; t <= ntile; t += 64) bp[t] = e;
         }
         pos = u32_wave_sum(pos);
         if (lane == 0) nodg[c] = (int)pos;
@@ -68,52 +97,135 @@ __global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indp
         se = dd_wave_sum(se);
         if (lane == 0) wave_expm1[blockIdx.x * (ING_T / 64) + wv] = se;
     }
-    if (bad) atomicOr(err, 1);
+    if (bad) atomicOr(err, bad);
+    if (a < 0) return;
     __syncthreads();
-    u32* row = cnt + (size_t)blockIdx.x * G;
+    u32* row = cnt + (size_t)ch * G;
     for (int g = threadIdx.x; g < G; g += ING_T) row[g] = hist[g];
 }
 
-__global__ void __launch_bounds__(256) k_ing_colscan(u32* __restrict__ cnt, int nwg, int G, u32* __restrict__ total)
+// per gene: exclusive prefix over the nc count chunks; row nc = total
+__global__ void __launch_bounds__(256) k_ing_colscan(u32* __restrict__ cnt, int nc, int nc_kept, int G)
 {
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= G) return;
     u32 run = 0;
-    for (int w = 0; w < nwg; ++w) {
+    for (int w = 0; w < nc_kept; ++w) {
         const u32 v = cnt[(size_t)w * G + g];
         cnt[(size_t)w * G + g] = run;
         run += v;
     }
-    total[g] = run;
+    for (int w = nc_kept; w <= nc; ++w) cnt[(size_t)w * G + g] = run;  // unkept chunks add nothing
 }
+
+#define SC_GT 256       // genes per tile (== ING_T: one scan lane per gene)
+#define SC_CAP 6144     // staged entries per round (u64 key + u16 gene = 10 B each): 2 blocks per CU
 
 template <bool DENSE>
 __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ indptr, const int* __restrict__ rows,
-                                                       const double* __restrict__ vals, int N, int G,
-                                                       int cells_per_wg, const int* __restrict__ code,
-                                                       const u32* __restrict__ cnt, const i64* __restrict__ gstart,
-                                                       u64* __restrict__ keys, u8* __restrict__ codes)
+                                                       const double* __restrict__ vals, int G,
+                                                       const int* __restrict__ perm, const int* __restrict__ cc_p0,
+                                                       const int* __restrict__ sc_cc0, const u32* __restrict__ cnt,
+                                                       const i64* __restrict__ gstart, const i64* __restrict__ bnd,
+                                                       int ntile, u64* __restrict__ keys)
 {
-    extern __shared__ __attribute__((aligned(16))) u32 cur[];  // offset inside the gene
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const u32* row = cnt + (size_t)blockIdx.x * G;
-    for (int g = threadIdx.x; g < G; g += ING_T) cur[g] = row[g];
+    __shared__ u32 loff[SC_GT + 1];
+    __shared__ u32 cur[SC_GT];
+    __shared__ u32 lcnt[SC_GT];
+    __shared__ i64 gdst[SC_GT];
+    __shared__ int rnd[SC_GT + 2];
+    __shared__ int nrnd;
+    __shared__ u32 wsum[ING_T / 64];
+    extern __shared__ __attribute__((aligned(16))) u64 skey[];  // [SC_CAP]
+    unsigned short* sg = (unsigned short*)(skey + SC_CAP);     // [SC_CAP]
+    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    const int s = blockIdx.x, t = blockIdx.y;
+    const int g0 = t * SC_GT, g1 = min(G, g0 + SC_GT), ng = g1 - g0;
+    const int cc0 = sc_cc0[s], cc1 = sc_cc0[s + 1];
+    const int p0 = cc_p0[cc0], p1 = cc_p0[cc1];
+    // local counts and destinations of this (chunk, tile) per gene
+    u32 myc = 0;
+    if (tid < ng) {
+        const int g = g0 + tid;
+        const u32 o0 = cnt[(size_t)cc0 * G + g];
+        myc = cnt[(size_t)cc1 * G + g] - o0;
+        lcnt[tid] = myc;
+        gdst[tid] = gstart[g] + o0;
+    }
+    // inclusive scan of the counts (ING_T == SC_GT)
+    u32 inc = myc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
     __syncthreads();
-    const int c0 = blockIdx.x * cells_per_wg, c1 = min(N, c0 + cells_per_wg);
-    for (int c = c0 + wv; c < c1; c += ING_T / 64) {
-        const int a = code[c];
-        if (a < 0) continue;
-        i64 b, e;
-        cell_range<DENSE>(indptr, c, G, b, e);
-        for (i64 k = b + lane; k < e; k += 64) {
-            const double x = vals[k];
-            const int g = DENSE ? (int)(k - b) : rows[k];
-            if (x != 0.0 && g >= 0 && g < G) {
-                const u64 pos = (u64)gstart[g] + atomicAdd(&cur[g], 1u);
-                keys[pos] = scc_key_of(x);
-                codes[pos] = (u8)a;
+    for (int v = 0; v < wv; ++v) inc += wsum[v];
+    // rounds of <= SC_CAP entries over consecutive genes
+    if (tid == 0) {
+        u32 tot = 0;
+        for (int v = 0; v < ING_T / 64; ++v) tot += wsum[v];
+        int nr = 0;
+        rnd[0] = 0;
+        if (tot <= SC_CAP) {
+            nr = 1;
+            rnd[1] = ng;
+        } else {
+            u32 acc = 0;
+            for (int gl = 0; gl < ng; ++gl) {
+                if (acc + lcnt[gl] > SC_CAP) {
+                    rnd[++nr] = gl;
+                    acc = 0;
+                }
+                acc += lcnt[gl];
+            }
+            rnd[++nr] = ng;
+        }
+        nrnd = nr;
+    }
+    if (tid < ng) loff[tid + 1] = inc;  // global-in-tile inclusive prefix
+    if (tid == 0) loff[0] = 0;
+    __syncthreads();
+    const int nr = nrnd;
+    for (int r = 0; r < nr; ++r) {
+        const int r0 = rnd[r], r1 = rnd[r + 1];
+        const u32 base = loff[r0];
+        for (int gl = tid; gl < SC_GT; gl += ING_T) cur[gl] = 0;
+        __syncthreads();
+        for (int p = p0 + wv; p < p1; p += ING_T / 64) {
+            const int c = perm[p];
+            i64 kb, ke;
+            if (DENSE) {
+                kb = (i64)c * G + g0 + r0;
+                ke = (i64)c * G + g0 + r1;
+            } else {
+                // clamp: bnd is only trustworthy when the hist pass saw sorted
+                // rows (err bit 4 otherwise); reads must stay in bounds anyway
+                const i64* bp = bnd + (size_t)p * (ntile + 1);
+                const i64 cb = indptr[c], ce = indptr[c + 1];
+                kb = min(max(bp[t], cb), ce);
+                ke = min(max(bp[t + 1], kb), ce);
+            }
+            for (i64 k = kb + lane; k < ke; k += 64) {
+                const double x = vals[k];
+                const int gl = DENSE ? (int)(k - (i64)c * G) - g0 : rows[k] - g0;
+                if (x != 0.0 && gl >= r0 && gl < r1) {
+                    const u32 o = atomicAdd(&cur[gl], 1u);
+                    if (o < lcnt[gl]) {  // always, for valid input
+                        const u32 pos = loff[gl] - base + o;
+                        skey[pos] = scc_key_of(x);
+                        sg[pos] = (unsigned short)gl;
+                    }
+                }
             }
         }
+        __syncthreads();
+        const int E = (int)(loff[r1] - base);
+        for (int i = tid; i < E; i += ING_T) {
+            const int gl = sg[i];
+            keys[gdst[gl] + (i64)(i - (int)(loff[gl] - base))] = skey[i];
+        }
+        __syncthreads();
     }
 }
 
@@ -204,54 +316,48 @@ __global__ void k_reduce_dd(const dd* __restrict__ parts, int n, dd* __restrict_
 }
 
 // ------------------------------------------------------------ host launchers
-extern "C" int scc_ingest_chunks(int N, int* cells_per_wg)
-{
-    int nwg = N / 16;
-    if (nwg > 1024) nwg = 1024;
-    if (nwg < 1) nwg = 1;
-    *cells_per_wg = (N + nwg - 1) / nwg;
-    return (N + *cells_per_wg - 1) / *cells_per_wg;
-}
+extern "C" int scc_ingest_gene_tile(void) { return SC_GT; }
 
 extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows, const double* vals,
-                                             const double* dense, int N, int G, int nwg, int cells_per_wg,
-                                             const int* code, u32* cnt, int* nodg, dd* wave_expm1, int want_expm1,
-                                             int* err, hipStream_t st)
+                                             const double* dense, int G, const int* perm, const int* cc_p0,
+                                             const int* cc_code, int nc, int ntile, u32* cnt, i64* bnd, int* nodg,
+                                             dd* wave_expm1, int want_expm1, int* err, hipStream_t st)
 {
     const size_t lds = sizeof(u32) * (size_t)G;
     if (dense) {
         hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_hist<true>, dim3(nwg), dim3(ING_T), lds, st, nullptr, nullptr, dense, N, G,
-                           cells_per_wg, code, cnt, nodg, wave_expm1, want_expm1, err);
+        hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, err);
     } else {
         hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_hist<false>, dim3(nwg), dim3(ING_T), lds, st, indptr, rows, vals, N, G, cells_per_wg,
-                           code, cnt, nodg, wave_expm1, want_expm1, err);
+        hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, err);
     }
     return hipGetLastError();
 }
 
-extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nwg, int G, u32* total, hipStream_t st)
+extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, int G, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ing_colscan, dim3((G + 255) / 256), dim3(256), 0, st, cnt, nwg, G, total);
+    hipLaunchKernelGGL(k_ing_colscan, dim3((G + 255) / 256), dim3(256), 0, st, cnt, nc, nc_kept, G);
     return hipGetLastError();
 }
 
 extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* rows, const double* vals,
-                                                const double* dense, int N, int G, int nwg, int cells_per_wg,
-                                                const int* code, const u32* cnt, const i64* gstart, u64* keys,
-                                                u8* codes, hipStream_t st)
+                                                const double* dense, int G, const int* perm, const int* cc_p0,
+                                                const int* sc_cc0, int ns, const u32* cnt, const i64* gstart,
+                                                const i64* bnd, int ntile, u64* keys, hipStream_t st)
 {
-    const size_t lds = sizeof(u32) * (size_t)G;
-    if (dense) {
-        hipFuncSetAttribute((const void*)k_ing_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_scatter<true>, dim3(nwg), dim3(ING_T), lds, st, nullptr, nullptr, dense, N, G,
-                           cells_per_wg, code, cnt, gstart, keys, codes);
-    } else {
-        hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_scatter<false>, dim3(nwg), dim3(ING_T), lds, st, indptr, rows, vals, N, G,
-                           cells_per_wg, code, cnt, gstart, keys, codes);
-    }
+    if (ns <= 0) return hipSuccess;
+    const dim3 grid(ns, ntile);
+    const size_t lds = (size_t)SC_CAP * (8 + 2);
+    hipFuncSetAttribute((const void*)k_ing_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (dense)
+        hipLaunchKernelGGL(k_ing_scatter<true>, grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
+                           sc_cc0, cnt, gstart, bnd, ntile, keys);
+    else
+        hipLaunchKernelGGL(k_ing_scatter<false>, grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0, sc_cc0,
+                           cnt, gstart, bnd, ntile, keys);
     return hipGetLastError();
 }
 

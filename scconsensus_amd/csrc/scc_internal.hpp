@@ -18,8 +18,10 @@
 namespace scc_rt {
 
 constexpr int kCapSmall = 2048;    // LDS rank kernel, 256 threads
-constexpr int kCapMedium = 12288;  // LDS rank kernel, 1024 threads
-constexpr int kChunkBig = 8192;    // staged sort chunk for larger genes
+constexpr int kCapMedium = 8192;   // LDS rank kernel, 1024 threads (larger genes: HBM index arrays)
+constexpr int kCountChunk = 32;    // cells per ingest count chunk (one cluster each)
+constexpr int kScatterCC = 4;      // count chunks per ingest scatter chunk
+constexpr int kMaxGenesLds = 40960;  // ingest histogram of one chunk lives in LDS
 constexpr int kSelectCap = 2048;   // per-pair records sorted in LDS
 constexpr int kUnionCap = 4096;
 constexpr int kMaxK = 64;
@@ -53,6 +55,7 @@ struct scc_ctx {
     std::vector<hipEvent_t> ev_pool;
     std::map<std::string, scc_rt::Timer> timers;
     uint64_t generation = 0;
+    std::vector<int> host_tables;  // cell permutation + chunk tables of the last scc_de_run
     // last PCA
     const double* d_last_scores = nullptr;  // N x 16 in the workspace
     int last_n = 0;

@@ -16,17 +16,20 @@ struct ScRankLaunch {
     const int* gene_list;
     const int* list_count;
     const long long* gstart;
-    unsigned long long* keys;
-    uint8_t* codes;
+    const unsigned long long* keys;
     int G, K, cap, grid;
     const int* n_clu;
+    const uint32_t* coff;
+    const int* cl_cc;
+    uint32_t* gix;
+    uint8_t* guc;
+    uint8_t* gsc;
+    long long nnz;
     double* mean_x;
     double* mean_e;
     uint32_t* cnt_pos;
     long long* u2_base;
     long long* t_base;
-    unsigned long long* tie_e;
-    unsigned long long* tie_x;
     unsigned long long* stamps;  // diagnostic only
 };
 
@@ -39,8 +42,6 @@ struct ScTestLaunch {
     const uint32_t* cnt_pos;
     const long long* u2_base;
     const long long* t_base;
-    const unsigned long long* tie_e;
-    const unsigned long long* tie_x;
     const double* wtab;
     const int* woff;
     double* out_p;
@@ -81,15 +82,16 @@ struct ScSelectLaunch {
 };
 
 extern "C" {
-int scc_ingest_chunks(int N, int* cells_per_wg);
+int scc_ingest_gene_tile(void);
 hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
-                                  int N, int G, int nwg, int cells_per_wg, const int* code, uint32_t* cnt, int* nodg,
-                                  dd* wave_expm1, int want_expm1, int* err, hipStream_t st);
-hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nwg, int G, uint32_t* total, hipStream_t st);
+                                  int G, const int* perm, const int* cc_p0, const int* cc_code, int nc, int ntile,
+                                  uint32_t* cnt, long long* bnd, int* nodg, dd* wave_expm1, int want_expm1, int* err,
+                                  hipStream_t st);
+hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nc, int nc_kept, int G, hipStream_t st);
 hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, const double* vals,
-                                     const double* dense, int N, int G, int nwg, int cells_per_wg, const int* code,
-                                     const uint32_t* cnt, const long long* gstart, unsigned long long* keys,
-                                     uint8_t* codes, hipStream_t st);
+                                     const double* dense, int G, const int* perm, const int* cc_p0, const int* sc_cc0,
+                                     int ns, const uint32_t* cnt, const long long* gstart, const long long* bnd,
+                                     int ntile, unsigned long long* keys, hipStream_t st);
 hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
                            long long* total, hipStream_t st);
 int scc_scan_scratch_blocks(long long n);
@@ -98,6 +100,7 @@ hipError_t scc_launch_reduce_dd(const dd* parts, int n, dd* out, hipStream_t st)
 hipError_t scc_launch_classify(const long long* gstart, int G, int cap_s, int cap_m, int* lists, int* counts,
                                hipStream_t st);
 size_t scc_rank_lds_bytes(int cls, int cap, int K);
+int scc_rank_cap(int cls, int want, int K);
 hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st);
 hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
                                  unsigned long long* stamps, hipStream_t st);

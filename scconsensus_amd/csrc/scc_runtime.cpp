@@ -206,37 +206,85 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         // ComputePairWiseDE: min.cells.group = 3 (Fast:76,208-213)
         if (fast && nclu[a] < 3) return fail(c, SCC_ERR_RSTOP, "cluster has fewer than 3 cells (R stop())");
     }
+    if (G > kMaxGenesLds) return fail(c, SCC_ERR_UNSUPPORTED, "more than 40960 genes is not supported by this build");
     const int64_t GK = (int64_t)G * K;
     const size_t PG = (size_t)P * G;
+    // Cells in cluster order: kept cells by code, then unkept ones.  Count
+    // chunks of <= kCountChunk cells never straddle clusters; scatter chunks
+    // group <= kScatterCC count chunks of one cluster.
+    std::vector<int>& H = c->host_tables;
+    std::vector<int> start(K + 1, 0);
+    for (int a = 0; a < K; ++a) start[a + 1] = start[a] + nclu[a];
+    const int nkept = start[K];
+    std::vector<int> perm(N), fill(start.begin(), start.end() - 1);
+    {
+        int u = nkept;
+        for (int i = 0; i < N; ++i) perm[code[i] >= 0 ? fill[code[i]]++ : u++] = i;
+    }
+    std::vector<int> cc_p0, cc_code, sc_cc0, cl_cc(K + 1);
+    for (int a = 0; a < K; ++a) {
+        cl_cc[a] = (int)cc_code.size();
+        for (int p = start[a]; p < start[a + 1]; p += kCountChunk) {
+            cc_p0.push_back(p);
+            cc_code.push_back(a);
+        }
+    }
+    const int nc_kept = (int)cc_code.size();
+    cl_cc[K] = nc_kept;
+    for (int a = 0; a < K; ++a)
+        for (int q = cl_cc[a]; q < cl_cc[a + 1]; q += kScatterCC) sc_cc0.push_back(q);
+    const int ns = (int)sc_cc0.size();
+    sc_cc0.push_back(nc_kept);
+    for (int p = nkept; p < N; p += kCountChunk) {
+        cc_p0.push_back(p);
+        cc_code.push_back(-1);
+    }
+    const int nc = (int)cc_code.size();
+    cc_p0.push_back(N);
+    const int gt = scc_ingest_gene_tile();
+    const int ntile = (G + gt - 1) / gt;
+    H.clear();
+    H.insert(H.end(), perm.begin(), perm.end());
+    const size_t o_ccp0 = H.size();
+    H.insert(H.end(), cc_p0.begin(), cc_p0.end());
+    const size_t o_cccode = H.size();
+    H.insert(H.end(), cc_code.begin(), cc_code.end());
+    const size_t o_sccc0 = H.size();
+    H.insert(H.end(), sc_cc0.begin(), sc_cc0.end());
+    const size_t o_clcc = H.size();
+    H.insert(H.end(), cl_cc.begin(), cl_cc.end());
+    const size_t o_nclu = H.size();
+    H.insert(H.end(), nclu.begin(), nclu.end());
+
     int rc;
-    int *d_code, *d_nclu, *d_nodg, *d_lists, *d_counts, *d_err, *d_tested, *d_union, *d_nu;
-    uint32_t *d_cnt, *d_total, *d_cntpos;
-    long long *d_gstart, *d_scan, *d_rowoff;
+    int *d_tab, *d_nodg, *d_lists, *d_counts, *d_err, *d_tested, *d_union, *d_nu;
+    uint32_t *d_cnt, *d_cntpos, *d_gix;
+    long long *d_gstart, *d_scan, *d_rowoff, *d_bnd;
     unsigned long long* d_keys;
-    uint8_t* d_codes;
+    uint8_t *d_guc, *d_gsc;
     dd* d_wexp;
     dd* d_gexp;
     double *d_mx, *d_me;
     long long *d_u2b, *d_tb, *d_u2, *d_t;
-    unsigned long long *d_tie_e, *d_tie_x, *d_first;
+    unsigned long long* d_first;
     double *d_p, *d_lfc, *d_pct1, *d_pct2;
     uint8_t* d_flags;
-    int cells_per_wg = 1;
-    const int nwg = scc_ingest_chunks(N, &cells_per_wg);
-    const int nwaves = nwg * 4;
+    const int nwaves = nc * 4;
+    const int64_t nnz1 = std::max<int64_t>(ds->nnz, 1);
 #define WS(name, n, ptr)                                  \
     do {                                                  \
         if ((rc = ws(c, name, (size_t)(n), &(ptr)))) return rc; \
     } while (0)
-    WS("code", N, d_code);
-    WS("nclu", K, d_nclu);
+    WS("tables", H.size(), d_tab);
     WS("nodg", N, d_nodg);
-    WS("cnt", (size_t)nwg * G, d_cnt);
-    WS("total", G, d_total);
+    WS("cnt", (size_t)(nc + 1) * G, d_cnt);
+    WS("bnd", ds->dense ? 1 : (size_t)N * (ntile + 1), d_bnd);
     WS("gstart", G + 1, d_gstart);
     WS("scan", scc_scan_scratch_blocks(G) + 1, d_scan);
-    WS("keys", std::max<int64_t>(ds->nnz, 1), d_keys);
-    WS("codes", std::max<int64_t>(ds->nnz, 1), d_codes);
+    WS("keys", nnz1, d_keys);
+    WS("gix", 2 * (size_t)nnz1, d_gix);
+    WS("guc", nnz1, d_guc);
+    WS("gsc", nnz1, d_gsc);
     {
         void* p;
         if ((rc = ws_get(c, "wexp", sizeof(double) * 2 * (nwaves + 1), &p))) return rc;
@@ -251,8 +299,6 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     WS("cntpos", GK, d_cntpos);
     WS("u2b", PG, d_u2b);
     WS("tb", PG, d_tb);
-    WS("tie_e", PG, d_tie_e);
-    WS("tie_x", PG, d_tie_x);
     WS("p", PG, d_p);
     WS("lfc", PG, d_lfc);
     WS("pct1", fast ? PG : 1, d_pct1);
@@ -268,45 +314,52 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     if ((rc = ensure_wtab(c))) return rc;
     hipStream_t s0 = c->s0, s1 = c->s1;
     c->generation++;
+    const int* d_perm = d_tab;
+    const int* d_ccp0 = d_tab + o_ccp0;
+    const int* d_cccode = d_tab + o_cccode;
+    const int* d_sccc0 = d_tab + o_sccc0;
+    const int* d_clcc = d_tab + o_clcc;
+    const int* d_nclu = d_tab + o_nclu;
 
-    HIPCHK(c, hipMemcpyAsync(d_code, code, sizeof(int) * N, hipMemcpyHostToDevice, s0));
-    HIPCHK(c, hipMemcpyAsync(d_nclu, nclu.data(), sizeof(int) * K, hipMemcpyHostToDevice, s0));
+    HIPCHK(c, hipMemcpyAsync(d_tab, H.data(), sizeof(int) * H.size(), hipMemcpyHostToDevice, s0));
     {
         Scope sc(c, "ingest", s0);
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
         HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 4, s0));
-        HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, nwg, cells_per_wg,
-                                         d_code, d_cnt, d_nodg, d_wexp, fast ? 0 : 1, d_err, s0));
-        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nwg, G, d_total, s0));
+        HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
+                                         d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, d_err, s0));
+        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, s0));
+        const uint32_t* d_total = d_cnt + (size_t)nc * G;
         HIPCHK(c, scc_launch_scan(d_total, G, d_gstart, d_scan, d_gstart + G, s0));
-        HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, N, G, nwg,
-                                            cells_per_wg, d_code, d_cnt, d_gstart, d_keys, d_codes, s0));
+        HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
+                                            d_sccc0, ns, d_cnt, d_gstart, d_bnd, ntile, d_keys, s0));
         if (!fast) HIPCHK(c, scc_launch_reduce_dd(d_wexp, nwaves, d_gexp, s0));
     }
     {
         Scope sc(c, "gene_rank", s0);
-        HIPCHK(c, hipMemsetAsync(d_tie_e, 0, sizeof(unsigned long long) * PG, s0));
-        HIPCHK(c, hipMemsetAsync(d_tie_x, 0, sizeof(unsigned long long) * PG, s0));
-        // size classes (env overrides exist to exercise the big-gene path on small test data)
-        const int cap_s = env_int("SCC_CAP_SMALL", kCapSmall), cap_m = env_int("SCC_CAP_MEDIUM", kCapMedium);
-        const int chunk_big = env_int("SCC_CHUNK_BIG", kChunkBig);
+        // size classes (env overrides exist to exercise the HBM-resident path on small test data)
+        const int cap_s = scc_rank_cap(0, env_int("SCC_CAP_SMALL", kCapSmall), K);
+        const int cap_m = std::max(cap_s, scc_rank_cap(1, env_int("SCC_CAP_MEDIUM", kCapMedium), K));
         HIPCHK(c, scc_launch_classify(d_gstart, G, cap_s, cap_m, d_lists, d_counts, s0));
         HIPCHK(c, hipEventRecord(c->ev_fork, s0));
         HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
         ScRankLaunch L{};
         L.gstart = d_gstart;
         L.keys = d_keys;
-        L.codes = d_codes;
         L.G = G;
         L.K = K;
         L.n_clu = d_nclu;
+        L.coff = d_cnt;
+        L.cl_cc = d_clcc;
+        L.gix = d_gix;
+        L.guc = d_guc;
+        L.gsc = d_gsc;
+        L.nnz = nnz1;
         L.mean_x = d_mx;
         L.mean_e = d_me;
         L.cnt_pos = d_cntpos;
         L.u2_base = d_u2b;
         L.t_base = d_tb;
-        L.tie_e = d_tie_e;
-        L.tie_x = d_tie_x;
         L.grid = G;
         unsigned long long* st_buf = nullptr;
         const bool stamps = env_int("SCC_STAMPS", 0) != 0;
@@ -317,7 +370,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         // big genes first on the side stream
         L.gene_list = d_lists + 2 * (size_t)G;
         L.list_count = d_counts + 2;
-        L.cap = chunk_big;
+        L.cap = 0;
         L.stamps = stamps ? st_buf + (size_t)2 * G * 8 : nullptr;
         HIPCHK(c, scc_launch_gene_rank(2, &L, s1));
         L.gene_list = d_lists + (size_t)G;
@@ -389,8 +442,6 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         T.cnt_pos = d_cntpos;
         T.u2_base = d_u2b;
         T.t_base = d_tb;
-        T.tie_e = d_tie_e;
-        T.tie_x = d_tie_x;
         T.wtab = c->d_wtab;
         T.woff = c->d_woff;
         T.out_p = d_p;
@@ -467,7 +518,9 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     HIPCHK(c, hipMemcpyAsync(&hdr[0], d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
     HIPCHK(c, hipMemcpyAsync(&hdr[1], d_err, sizeof(int), hipMemcpyDeviceToHost, s0));
     HIPCHK(c, hipStreamSynchronize(s0));
-    if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values or bad row indices");
+    if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
+    if (hdr[1] & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
+    if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
     scc_de_result* r = new scc_de_result();
     r->ctx = c;
     r->generation = c->generation;

@@ -120,8 +120,6 @@ struct TestArgs {
     const u32* cnt_pos;
     const i64* u2_base;
     const i64* t_base;
-    const u64* tie_e;
-    const u64* tie_x;
     const double* wtab;
     const int* woff;
     double* out_p;     // [P][G]
@@ -145,8 +143,8 @@ __global__ void __launch_bounds__(256) k_pair_test(TestArgs A)
     }
     const int b = a + 1 + rem;
     const size_t pg = (size_t)p * A.G + g;
-    const i64 u2 = A.u2_base[pg] + (i64)A.tie_e[pg];
-    const i64 t = A.t_base[pg] + 3 * (i64)A.tie_x[pg];
+    const i64 u2 = A.u2_base[pg];  // exact 2U and tie term from the rank kernel
+    const i64 t = A.t_base[pg];
     const int na = A.n_clu[a], nb = A.n_clu[b];
     u8 ex = 0;
     const double pv = wilcox_p(u2, t, na, nb, A.wtab, A.woff, &ex);
@@ -414,7 +412,7 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
             A.row_t[ro + i] = A.t[pb + g];
             A.row_flags[ro + i] = de ? 1 : 0;
             nde += de;
-            if (m > 1 && q != q) atomicOr(A.err, 2);  // NA q in a kept pair: R builds an NA row
+            if (m > 1 && q != q) atomicOr(A.err, 0x100);  // NA q in a kept pair: R builds an NA row (informational)
         }
         int d;
         block_excl_scan<T>(nde, sc, d);
@@ -473,7 +471,7 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
             u8 de;
             if (q != q) {
                 de = bterm ? 2 : 0;
-                if (bterm) atomicOr(A.err, 4);
+                if (bterm) atomicOr(A.err, 0x200);  // informational
             } else {
                 de = (q < A.q_thr) && bterm;
             }
@@ -593,8 +591,6 @@ extern "C" hipError_t scc_launch_pair_test(const ScTestLaunch* L, hipStream_t st
     A.cnt_pos = L->cnt_pos;
     A.u2_base = L->u2_base;
     A.t_base = L->t_base;
-    A.tie_e = L->tie_e;
-    A.tie_x = L->tie_x;
     A.wtab = L->wtab;
     A.woff = L->woff;
     A.out_p = L->out_p;

@@ -2,6 +2,7 @@
 tests/engine_model.py, mirroring scc_rank.hip) equals R's rank definition
 (the oracle) exactly, including zeros, negatives and cross-cluster ties."""
 import numpy as np
+import pytest
 from hypothesis import given, settings
 from hypothesis import strategies as st
 
@@ -43,3 +44,21 @@ def test_count_formula_continuous():
         rng.shuffle(codes)
         vals = np.where(rng.random(len(codes)) < 0.5, 0.0, np.log1p(rng.gamma(2, 2, len(codes))))
         _check(vals, codes, sizes)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("W", [1, 3, 16])
+def test_sweep_tie_terms_match(seed, W):
+    """Chunked sweep with G-counts (the kernel's tie statistics, including
+    tie groups that straddle wave chunks) == explicit tie-group walk."""
+    from engine_model import gene_u2_ties, gene_u2_ties_sweep
+    rng = np.random.default_rng(seed)
+    K = int(rng.integers(2, 7))
+    N = int(rng.integers(5, 120))
+    codes = rng.integers(0, K, N)
+    codes[:K] = np.arange(K)
+    vals = rng.choice([-2.0, -1.0, 0.0, 0.0, 1.0, 1.5, 2.0, 3.0], N) if seed % 2 else np.round(rng.normal(0, 1, N), 1)
+    n_clu = np.bincount(codes, minlength=K)
+    a = gene_u2_ties(vals, codes, n_clu)
+    b = gene_u2_ties_sweep(vals, codes, n_clu, W)
+    assert a == b

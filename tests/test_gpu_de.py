@@ -190,3 +190,65 @@ def test_config_b_sampled_parity(eng):
         else:
             assert g.p[p, gene] == pytest.approx(po, rel=P_RTOL)
     assert 100 < len(g.union) <= 30 * len(pairs) * 2
+
+
+def _near_tie_dataset(seed=5):
+    """Genes whose values differ only in the last bits next to far larger
+    values: the rank kernel's 32-bit key window merges them (mixed runs of
+    <= 64 and > 64 elements) and must restore the exact order."""
+    rng = np.random.default_rng(seed)
+    K, per = 4, 60
+    labels = np.repeat(np.array(["red", "blue", "green", "cyan"], dtype=object), per)
+    rng.shuffle(labels)
+    N = len(labels)
+    G = 6
+    X = np.zeros((G, N))
+    one = np.nextafter(1.0, 2.0) - 1.0
+    # gene 0: 20 near-equal values + a far value (short mixed runs)
+    idx = rng.choice(N, 40, replace=False)
+    X[0, idx[:20]] = 1.0 + one * rng.permutation(20)
+    X[0, idx[20:]] = rng.uniform(0.1, 20.0, 20)
+    # gene 1: 150 near-equal values + far values (a run > 64: full re-sort)
+    idx = rng.choice(N, 200, replace=False)
+    X[1, idx[:150]] = 2.0 + 2 * one * rng.permutation(150)
+    X[1, idx[150:]] = rng.uniform(1e-3, 20.0, 50)
+    # gene 2: exact ties mixed with near ties
+    idx = rng.choice(N, 120, replace=False)
+    X[2, idx] = np.where(rng.random(120) < 0.5, 3.0, 3.0 + one * 2 * rng.integers(1, 4, 120))
+    X[2, idx[:5]] = 15.0
+    # gene 3: negative and positive with tiny separations
+    idx = rng.choice(N, 100, replace=False)
+    X[3, idx] = rng.choice([-1.0, -1.0 - one, 1.0, 1.0 + one, 1e-300, -1e-300, 15.0], 100)
+    # genes 4, 5: ordinary
+    X[4] = np.where(rng.random(N) < 0.4, rng.gamma(2.0, 1.0, N), 0.0)
+    X[5] = np.where(rng.random(N) < 0.9, np.round(rng.gamma(2.0, 1.0, N), 1), 0.0)
+    return synth.from_dense(X, labels), X
+
+
+def test_near_ties_exact_order(eng):
+    from scconsensus_amd import _native as nat
+    d, X = _near_tie_dataset()
+    names, code = api.select_clusters(d.labels, 10)
+    K = len(names)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="all")
+    for p, (i, j) in enumerate([(i, j) for i in range(K - 1) for j in range(i + 1, K)]):
+        for gene in range(d.G):
+            po, W, T, _ = O.wilcox_test(X[gene, code == i], X[gene, code == j])
+            assert g.u2[p, gene] == int(round(2 * W)), (p, gene)
+            if np.isnan(po):
+                assert np.isnan(g.p[p, gene])
+            else:
+                assert g.p[p, gene] == pytest.approx(po, rel=1e-12), (p, gene)
+    _fast_compare(eng, ds, X, code, K, log_fc_thrs=0.01, min_per_cent=1.0)
+
+
+@pytest.mark.parametrize("caps", [("64", "256"), ("128", "128")])
+def test_rank_size_classes(eng, cfg_a, caps, monkeypatch):
+    """Small caps push most genes to the 1024-thread LDS class and the
+    HBM-resident class: same results bit for bit."""
+    monkeypatch.setenv("SCC_CAP_SMALL", caps[0])
+    monkeypatch.setenv("SCC_CAP_MEDIUM", caps[1])
+    d, X, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _fast_compare(eng, ds, X, code, len(names))
