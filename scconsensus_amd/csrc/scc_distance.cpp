@@ -5,7 +5,7 @@
 // eigenpairs of the |U| x |U| Gram (Householder + multisection + inverse
 // iteration, exact to fp64 backward error), scores
 // P = Xc V_k, then the packed Euclidean `dist`.  The eigensolve is this
-// engine's own single-workgroup dense solver (scc_eigen.hip), no vendor BLAS.  The exact truncated SVD is
+// engine's own multi-workgroup dense solver (scc_eigen.hip), no vendor BLAS.  The exact truncated SVD is
 // the deterministic quantity irlba approximates.
 // Pearson path (reference Fast:403, commented out there): per-cell z-scores
 // over U and an FP32 MFMA Gram with the 1 - r epilogue fused into the store.
@@ -82,7 +82,7 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         WS("d_W", ld, d_W);
         WS("d_Z", (size_t)ld * 16, d_Z);
         WS("d_P", (size_t)N * 16, d_P);
-        WS("d_escr", (size_t)104 * ld + 64, d_escr);
+        WS("d_escr", scc_eigen_scratch_doubles(nu, ld, k), d_escr);
         {
             Scope sc(c, "center", s0);
             HIPCHK(c, scc_launch_center(d_X, N, nu, ld, (dd*)d_part, nchunk_mean, d_mean, s0));
@@ -91,17 +91,35 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
             Scope sc(c, "gram", s0);
             HIPCHK(c, scc_launch_gram(d_X, Npad, ld, nchunk, d_slabs, d_C, s0));
         }
+        unsigned int* d_eig_err = nullptr;
         {
             Scope sc(c, "eigen", s0);
-            unsigned long long* st_buf = nullptr;
-            if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 8, st_buf);
-            HIPCHK(c, scc_launch_syevx_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, st_buf, s0));
-            if (st_buf) {
-                unsigned long long h[8];
-                HIPCHK(c, hipMemcpyAsync(h, st_buf, sizeof(h), hipMemcpyDeviceToHost, s0));
-                HIPCHK(c, hipStreamSynchronize(s0));
-                fprintf(stderr, "[scc stamps] eigen n=%d: tridiag %llu, bisect %llu, inviter %llu, backtr %llu cycles\n",
-                        nu, h[1] - h[0], h[2] - h[1], h[3] - h[2], h[4] - h[3]);
+            hipEvent_t mk[6];
+            hipEvent_t* marks = nullptr;
+            if (c->profile) {  // per-kernel split of the eigensolve
+                for (auto& m : mk) m = ev_take(c);
+                marks = mk;
+            }
+            HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, nullptr, marks, s0));
+            if (marks) {
+                c->pending.push_back({"eig_tridiag", mk[0], mk[1]});
+                c->pending.push_back({"eig_vec", mk[2], mk[3]});
+                c->pending.push_back({"eig_fin", mk[4], mk[5]});
+            }
+        }
+        HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
+        if (env_int("SCC_EIG_DUMP", 0)) {  // debug: eigenvalues and vectors on stderr
+            std::vector<double> w(k), z((size_t)nu * 16);
+            HIPCHK(c, hipMemcpyAsync(w.data(), d_W, sizeof(double) * k, hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipMemcpyAsync(z.data(), d_Z, sizeof(double) * z.size(), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            fprintf(stderr, "[scc eig] n=%d k=%d err=%u W:", nu, k, c->eig_err);
+            for (int q = 0; q < k; ++q) fprintf(stderr, " %.6g", w[q]);
+            fprintf(stderr, "\n");
+            for (int u = 0; u < std::min(nu, 8); ++u) {
+                fprintf(stderr, "[scc eig] Z[%d]:", u);
+                for (int q = 0; q < k; ++q) fprintf(stderr, " %.4g", z[(size_t)u * 16 + q]);
+                fprintf(stderr, "\n");
             }
         }
         {
@@ -126,6 +144,8 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         HIPCHK(c, hipMemcpyAsync(dist_out, d_out, npairs * (out_f32 ? 4 : 8), hipMemcpyDeviceToHost, s0));
     }
     HIPCHK(c, hipStreamSynchronize(s0));
+    if (metric == SCC_DIST_PCA_EUCLID && c->eig_err)
+        return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
     return SCC_OK;
 #undef WS
 }

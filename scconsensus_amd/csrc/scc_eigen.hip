@@ -1,32 +1,45 @@
 // scc_eigen.hip — top-k eigenpairs of the |U| x |U| fp64 Gram matrix.
 //
 // Dense symmetric eigensolver for the PCA step of stage 3 (reference:
-// irlba::prcomp_irlba, R/reclusterDEConsensusFast.R:398).  The spectrum of
-// the centred union-gene Gram is a few cluster "spikes" over a noise bulk, so
-// the 15th/16th eigenvalues are routinely within 1e-3 relative of each other
-// (SURVEY D5): Krylov/subspace iterations need hundreds of steps there, while
-// a direct method is exact to fp64 backward error.  One workgroup (16 waves):
-//   1. Householder tridiagonalisation, LAPACK dsytd2 order.  One fused sweep
-//      per step: the rank-2 update of step k and the symv of step k+1 share a
-//      pass over the trailing block (3 rows in flight per wave); the trailing
-//      block moves from L2 into LDS once it fits.  5 barriers per step.
-//   2. the k largest eigenvalues of T by multisection (64 Sturm counts per
-//      wave per round), T resident in LDS
-//   3. eigenvectors of T by inverse iteration (dgttrf/dgttrs LU with partial
-//      pivoting, factors in LDS), re-orthogonalised inside eigenvalue clusters
-//      (|dl| <= 1e-3 ||T||, as LAPACK dstein)
-//   4. back-transformation by the stored reflectors, vectors in LDS
-// Output Z[u*16 + q] = q-th largest eigenvector (q < k), zero padded to 16.
-// Every LDS array has a global fall-back in `scratch` for very large |U|.
+// irlba::prcomp_irlba, R/reclusterDEConsensusFast.R:398; R/reclusterDEConsensus.R:234).
+// The spectrum of the centred union-gene Gram is a few cluster "spikes" over a
+// noise bulk, so the 15th/16th eigenvalues are routinely within 1e-3 relative
+// of each other: Krylov/subspace iterations need hundreds of steps
+// there, while a direct method is exact to fp64 backward error.
+//
+// Three launches:
+//   1. k_tridiag  — Householder tridiagonalisation (LAPACK dsytd2, lower) on
+//      `nwg` persistent workgroups.  Rows are dealt cyclically (row r lives in
+//      workgroup r % nwg) and stay in that CU's LDS for the whole reduction,
+//      so the matrix never goes back to L2/HBM.  One cross-workgroup hand-off
+//      per column: every workgroup publishes tau*A22*v for its rows (and the
+//      owner of the next column publishes that row), then all workgroups
+//      redundantly and deterministically form w and the next reflector.  The
+//      hand-off is write-through (`sc1`) stores + one agent-scope counter add
+//      per workgroup; readers poll the counter and read with `sc1` loads
+//      (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off row).
+//   2. k_tri_vectors — one workgroup per wanted eigenpair: multisection on
+//      Sturm counts (256 points per round), inverse iteration with the
+//      partially pivoted LU of T - lambda I (LAPACK dgttrf/dgttrs order),
+//      then the back-transformation by the stored reflectors.
+//   3. k_eig_finish — Gram-Schmidt inside eigenvalue clusters
+//      (|dl| <= 1e-3 ||T||, the LAPACK dstein criterion), normalisation and a
+//      deterministic sign (largest-magnitude component positive).
+// Output Z[u*16 + q] = q-th largest eigenvector (q < k), zero padded to 16;
+// W[q] the q-th largest eigenvalue.
 #include "scc_common.hpp"
 
-#define EIG_T 1024
-#define EIG_W (EIG_T / 64)
-#ifndef EIG_RU
-#define EIG_RU 3  // rows in flight per wave in the fused sweep (4 spills at 128 VGPRs)
-#endif
-#define EIG_LDS_BYTES (156 * 1024)
-#define EIG_LDS_DBL (EIG_LDS_BYTES / 8)
+#define TRI_T 256
+#define TRI_W (TRI_T / 64)
+#define VEC_T 256
+#define VEC_W (VEC_T / 64)
+#define FIN_T 1024
+#define FIN_W (FIN_T / 64)
+#define EIG_LDS_MAX (160 * 1024)
+#define EIG_MAX_WG 256
+#define EIG_SPIN_LIMIT (1u << 22)
+
+static constexpr double kEps = 2.220446049250313e-16;
 
 __device__ inline double wave_sum_d(double v)
 {
@@ -35,19 +48,225 @@ __device__ inline double wave_sum_d(double v)
     return v;
 }
 
+// write-through / L1-bypassing accessors for the cross-workgroup hand-off
+__device__ inline double ld_sc1(const double* p)
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ inline void st_sc1(double* p, double v)
+{
+    __hip_atomic_store((u64*)p, (u64)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// deterministic block sum over W waves (every thread returns the same value)
+template <int W>
 __device__ inline double block_sum(double v, double* red)
 {
-    const int lane = threadIdx.x & 63, w = scc_wave_id();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     v = wave_sum_d(v);
-    __syncthreads();
-    if (lane == 0) red[w] = v;
+    if (lane == 0) red[wv] = v;
     __syncthreads();
     double s = 0.0;
-    for (int i = 0; i < EIG_W; ++i) s += red[i];  // fixed order: deterministic
+#pragma unroll
+    for (int i = 0; i < W; ++i) s += red[i];
+    __syncthreads();
     return s;
 }
 
-// number of eigenvalues of T (d, e^2) strictly below x (Sturm sequence)
+// ---------------------------------------------------------------------------
+// 1. tridiagonalisation
+struct TriArgs {
+    const double* A;  // n x n symmetric, row-major, lda
+    int n, lda, nwg, rows_lds;
+    double* d;        // [n] diagonal of T
+    double* e;        // [n] off-diagonal (e[i] = T[i+1][i])
+    double* tau;      // [n]
+    double* refl;     // reflector i in row i: refl[i*lda + j], j >= i+1 (refl[i][i+1] = 1)
+    double* pbuf;     // [2][lda] tau*A22*v of the current column (hand-off)
+    double* rowbuf;   // [2][lda] row i+1 of A^(i-1) (hand-off)
+    double* pdot;     // [2][EIG_MAX_WG] per-workgroup partial of p.v (hand-off)
+    double* work;     // own rows when they do not fit LDS: [nwg][R][n]
+    u32* counter;     // arrivals (monotonic, zeroed before the launch)
+    u32* err;         // 1: a hand-off timed out
+};
+
+// Householder reflector from y[lo..n-1] (alpha = y[lo], x = y[lo+1..]), LAPACK
+// dlarfg: v[lo] = 1, v[j] = x_j / (alpha - beta); returns beta and tau.
+template <int T>
+__device__ inline void house(const double* y, int lo, int n, double* v, double* red, double& beta, double& tau)
+{
+    const int tid = threadIdx.x;
+    double part = 0.0;
+    for (int j = lo + 1 + tid; j < n; j += T) part += y[j] * y[j];
+    const double xn2 = block_sum<T / 64>(part, red);
+    const double alpha = y[lo];
+    double scal = 0.0;
+    beta = alpha;
+    tau = 0.0;
+    if (xn2 > 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+        tau = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+    }
+    for (int j = lo + tid; j < n; j += T) v[j] = (j == lo) ? 1.0 : y[j] * scal;
+}
+
+__global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ int s_abort;
+    const int n = a.n, nwg = a.nwg, me = blockIdx.x, lda = a.lda;
+    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    const int R = (n + nwg - 1) / nwg;
+    double* vA = sm;           // v_i   (support i+1..n-1)
+    double* vB = vA + n;       // v_{i-1}, then v_{i+1}
+    double* wp = vB + n;       // w_{i-1}, then w_i
+    double* y = wp + n;        // hand-off row / scratch
+    double* red = y + n;       // 64
+    double* part = red + 64;   // EIG_MAX_WG
+    double* rows = a.rows_lds ? (part + EIG_MAX_WG) : (a.work + (size_t)me * R * n);
+    const int nown = (me < n) ? (n - me + nwg - 1) / nwg : 0;
+    if (tid == 0) s_abort = 0;
+    for (int l = 0; l < nown; ++l) {
+        const double* src = a.A + (size_t)(me + nwg * l) * lda;
+        for (int j = tid; j < n; j += TRI_T) rows[(size_t)l * n + j] = src[j];
+    }
+    for (int j = tid; j < n; j += TRI_T) y[j] = a.A[j];  // row 0
+    __syncthreads();
+    if (n == 1) {
+        if (me == 0 && tid == 0) {
+            a.d[0] = y[0];
+            a.e[0] = 0.0;
+            a.tau[0] = 0.0;
+        }
+        return;
+    }
+    double* vc = vA;
+    double* vp = vB;
+    double beta, tc;
+    house<TRI_T>(y, 1, n, vc, red, beta, tc);
+    if (me == 0) {
+        if (tid == 0) {
+            a.d[0] = y[0];
+            a.e[0] = beta;
+            a.tau[0] = tc;
+        }
+        for (int j = 1 + tid; j < n; j += TRI_T) a.refl[j] = vc[j];
+    }
+    double tp = 0.0;  // tau_{i-1}
+    __syncthreads();
+    for (int i = 0; i <= n - 2; ++i) {
+        const int par = i & 1;
+        double* pb = a.pbuf + (size_t)par * lda;
+        double* rb = a.rowbuf + (size_t)par * lda;
+        const bool prev = (i >= 1) && (tp != 0.0);
+        // ---- phase B: own rows r >= i+1: apply update i-1, p_r = tau_i A_r. v_i
+        double pd = 0.0;
+        const int l0 = (i + 1 > me) ? (i + 1 - me + nwg - 1) / nwg : 0;
+        for (int l = l0 + wv; l < nown; l += TRI_W) {
+            const int r = me + nwg * l;
+            double* row = rows + (size_t)l * n;
+            const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
+            const bool pub = (r == i + 1);
+            double s = 0.0;
+            for (int j = i + 1 + lane; j < n; j += 64) {
+                double x = row[j];
+                if (prev) {
+                    x = x - vr * wp[j] - wr * vp[j];
+                    row[j] = x;
+                }
+                if (pub) st_sc1(rb + j, x);
+                s += x * vc[j];
+            }
+            s = wave_sum_d(s);
+            const double p = tc * s;
+            if (lane == 0) {
+                st_sc1(pb + r, p);
+                pd += p * vc[r];
+            }
+        }
+        if (lane == 0) red[wv] = pd;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int q = 0; q < TRI_W; ++q) s += red[q];
+            st_sc1(a.pdot + (size_t)par * EIG_MAX_WG + me, s);
+        }
+        // ---- hand-off: every storing wave drains, one lane signals
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u32 target = (u32)(i + 1) * (u32)nwg;
+            u32 spins = 0;
+            while (__hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > EIG_SPIN_LIMIT) {
+                    __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_abort = 1;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_abort) return;
+        // ---- phase C (every workgroup, identical arithmetic): w_i, row i+1 of
+        // A^(i), d[i+1], and reflector i+1 into the free v buffer
+        if (tid < nwg) part[tid] = ld_sc1(a.pdot + (size_t)par * EIG_MAX_WG + tid);
+        for (int j = i + 1 + tid; j < n; j += TRI_T) {
+            wp[j] = ld_sc1(pb + j);
+            y[j] = ld_sc1(rb + j);
+        }
+        __syncthreads();
+        double pdt = 0.0;
+        for (int q = 0; q < nwg; ++q) pdt += part[q];
+        const double a2 = -0.5 * tc * pdt;
+        for (int j = i + 1 + tid; j < n; j += TRI_T) wp[j] = (tc != 0.0) ? wp[j] + a2 * vc[j] : 0.0;
+        __syncthreads();
+        const double v1 = vc[i + 1], w1 = wp[i + 1];
+        for (int j = i + 1 + tid; j < n; j += TRI_T) y[j] = y[j] - v1 * wp[j] - w1 * vc[j];
+        __syncthreads();
+        if (i + 1 <= n - 2) {
+            double bn, tn;
+            house<TRI_T>(y, i + 2, n, vp, red, bn, tn);
+            if (me == 0) {
+                if (tid == 0) {
+                    a.d[i + 1] = y[i + 1];
+                    a.e[i + 1] = bn;
+                    a.tau[i + 1] = tn;
+                }
+                for (int j = i + 2 + tid; j < n; j += TRI_T) a.refl[(size_t)(i + 1) * lda + j] = vp[j];
+            }
+            tp = tc;
+            tc = tn;
+            double* t = vc;  // v_i becomes the previous reflector
+            vc = vp;
+            vp = t;
+        } else if (me == 0 && tid == 0) {
+            a.d[n - 1] = y[n - 1];
+            a.e[n - 1] = 0.0;
+            a.tau[n - 1] = 0.0;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 2. eigenvalue q (q-th largest) and its eigenvector, one workgroup each
+struct VecArgs {
+    const double* d;
+    const double* e;
+    const double* tau;
+    const double* refl;
+    int n, lda, k, lu_lds;
+    double* lu;     // global LU slots [k][5n] when they do not fit LDS
+    double* Zq;     // [16][lda] back-transformed vectors (unnormalised sign)
+    double* W;      // [k]
+    double* tnorm;  // [1]
+};
+
+// number of eigenvalues of T (d, e^2) strictly below x (Sturm sequence, dstebz)
 __device__ inline int sturm_count(const double* d, const double* e2, int n, double x, double pivmin)
 {
     int c = 0;
@@ -62,436 +281,388 @@ __device__ inline int sturm_count(const double* d, const double* e2, int n, doub
     return c;
 }
 
-// Fused sweep of step k: rows i = 1..m-1 of the trailing block T (local
-// (i,j) at T[(off+i)*ld + off+j]) get the rank-2 update of step k, and the
-// same sweep forms p' = tau' T' v' for step k+1 (written to pn) plus each
-// wave's partial of p'.v' (pdot[wave]).  Output rows go to O (ldo, offo).
-template <class TP, class OP>
-__device__ __forceinline__ void fused_pass(TP T, int ld, int off, OP O, int ldo, int offo, int m, const double* v,
-                                           const double* w, const double* vn, double taun, double* pn, double* pdot)
-{
-    const int lane = threadIdx.x & 63, wv = scc_wave_id();
-    double dacc = 0.0;
-    for (int i0 = 1 + wv; i0 < m; i0 += EIG_RU * EIG_W) {
-        int r[EIG_RU];
-        bool ok[EIG_RU];
-        double vi[EIG_RU], wi[EIG_RU], s[EIG_RU];
-#pragma unroll
-        for (int u = 0; u < EIG_RU; ++u) {
-            r[u] = i0 + u * EIG_W;
-            ok[u] = r[u] < m;
-            vi[u] = ok[u] ? v[r[u]] : 0.0;
-            wi[u] = ok[u] ? w[r[u]] : 0.0;
-            s[u] = 0.0;
-        }
-        for (int j = 1 + lane; j < m; j += 64) {
-            const double vj = v[j], wj = w[j], vnj = vn[j - 1];
-            double x[EIG_RU];
-#pragma unroll
-            for (int u = 0; u < EIG_RU; ++u) x[u] = ok[u] ? T[(size_t)(off + r[u]) * ld + off + j] : 0.0;
-#pragma unroll
-            for (int u = 0; u < EIG_RU; ++u) {
-                if (ok[u]) {
-                    const double y = x[u] - vi[u] * wj - wi[u] * vj;
-                    O[(size_t)(offo + r[u] - 1) * ldo + offo - 1 + j] = y;
-                    s[u] += y * vnj;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < EIG_RU; ++u) {
-            const double su = wave_sum_d(s[u]) * taun;
-            if (ok[u] && lane == 0) {
-                pn[r[u] - 1] = su;
-                dacc += su * vn[r[u] - 1];
-            }
-        }
-    }
-    if (lane == 0) pdot[wv] = dacc;
-}
-
-#define ESTAMP(ph)                                                                  \
-    do {                                                                            \
-        if (stamps && threadIdx.x == 0) stamps[ph] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-
-// A: n x n symmetric (full), row-major, leading dimension lda; destroyed (the
-// reflectors are left in its rows: A[k][k+1] = 1, A[k][k+2..] = v tail).
-// scratch doubles: 104 n.  Z: n x 16 out.  W: k out (descending).
-__global__ void __launch_bounds__(EIG_T) k_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z,
-                                                      double* W, u64* stamps)
+__global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    __shared__ double sh[8];
-    ESTAMP(0);
-    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
-    double* red = sm;        // 16
-    double* pdot = sm + 16;  // 16
-    double* d = scratch;     // n
-    double* e = d + n;       // n
-    double* tau = e + n;     // n
-    double* gbuf = tau + n;  // global fall-back space (99 n)
-    // ---------------------------------------------------------------- 1. tridiagonalise
-    const bool vec_lds = (32 + 4 * (size_t)n) <= EIG_LDS_DBL;
-    double* vbuf0 = vec_lds ? sm + 32 : gbuf;
-    double* vbuf1 = vbuf0 + n;
-    double* wbuf = vbuf1 + n;
-    double* pbuf = wbuf + n;
-    int mlds = 0;
-    if (vec_lds) {
-        mlds = (int)sqrt((double)(EIG_LDS_DBL - 32 - 4 * (size_t)n));
-        if (mlds > n) mlds = n;
-    }
-    double* Tl = sm + 32 + 4 * (size_t)n;
-    if (n <= 2) {
-        if (tid == 0) {
-            d[0] = A[0];
-            e[0] = (n == 2) ? A[1] : 0.0;
-            tau[0] = 0.0;
-            if (n == 2) {
-                d[1] = A[(size_t)lda + 1];
-                e[1] = 0.0;
-                tau[1] = 0.0;
-            }
-        }
-    } else {
-        {  // reflector 0 from row 0, then p = tau A22 v
-            const int m = n - 1;
-            double part = 0.0;
-            for (int j = 2 + tid; j < n; j += EIG_T) part += A[j] * A[j];
-            const double xn2 = block_sum(part, red);
-            const double alpha = A[1];
-            double t = 0.0, beta = alpha, scal = 0.0;
-            if (xn2 > 0.0) {
-                beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-                t = (beta - alpha) / beta;
-                scal = 1.0 / (alpha - beta);
-            }
-            for (int j = tid; j < m; j += EIG_T) vbuf0[j] = (j == 0) ? 1.0 : A[1 + j] * scal;
-            __syncthreads();
-            for (int j = tid; j < m; j += EIG_T) A[1 + j] = vbuf0[j];
-            if (tid == 0) {
-                d[0] = A[0];
-                e[0] = beta;
-                tau[0] = t;
-                sh[0] = t;
-            }
-            double dacc = 0.0;
-            for (int i = wv; i < m; i += EIG_W) {
-                const double* ri = A + (size_t)(1 + i) * lda + 1;
-                double s = 0.0;
-                for (int j = lane; j < m; j += 64) s += ri[j] * vbuf0[j];
-                s = wave_sum_d(s) * t;
-                if (lane == 0) {
-                    pbuf[i] = s;
-                    dacc += s * vbuf0[i];
-                }
-            }
-            if (lane == 0) pdot[wv] = dacc;
-            __syncthreads();
-        }
-        bool in_lds = false;
-        int lds_base = 0, lds_ld = 0;
-        int cur = 0;
-        for (int kk = 0; kk <= n - 3; ++kk) {
-            const int m = n - kk - 1;  // trailing block A22 = rows/cols kk+1 .. n-1
-            double* v = cur ? vbuf1 : vbuf0;
-            double* vn = cur ? vbuf0 : vbuf1;
-            const double t = sh[0];
-            double dot = 0.0;
-            for (int i = 0; i < EIG_W; ++i) dot += pdot[i];
-            const double a2 = -0.5 * t * dot;
-            for (int i = tid; i < m; i += EIG_T) wbuf[i] = (t != 0.0) ? pbuf[i] + a2 * v[i] : 0.0;
-            __syncthreads();
-            const double* row0;
-            int ld0;
-            if (in_lds) {
-                const int o = kk + 1 - lds_base;
-                ld0 = lds_ld;
-                row0 = Tl + (size_t)o * ld0 + o;
-            } else {
-                ld0 = lda;
-                row0 = A + (size_t)(kk + 1) * ld0 + kk + 1;
-            }
-            const double v0 = v[0], w0 = wbuf[0];
-            if (kk == n - 3) {  // 2 x 2 remainder
-                if (tid == 0) {
-                    d[n - 2] = row0[0] - 2.0 * v0 * w0;
-                    e[n - 2] = row0[1] - v0 * wbuf[1] - w0 * v[1];
-                    d[n - 1] = row0[ld0 + 1] - 2.0 * v[1] * wbuf[1];
-                    e[n - 1] = 0.0;
-                    tau[n - 2] = 0.0;
-                    tau[n - 1] = 0.0;
-                }
-                break;
-            }
-            double part = 0.0;
-            for (int j = 2 + tid; j < m; j += EIG_T) {
-                const double x = row0[j] - v0 * wbuf[j] - w0 * v[j];
-                part += x * x;
-            }
-            const double xn2 = block_sum(part, red);
-            const double alpha = row0[1] - v0 * wbuf[1] - w0 * v[1];
-            double tn = 0.0, beta = alpha, scal = 0.0;
-            if (xn2 > 0.0) {
-                beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-                tn = (beta - alpha) / beta;
-                scal = 1.0 / (alpha - beta);
-            }
-            for (int j = 1 + tid; j < m; j += EIG_T) {
-                const double x = row0[j] - v0 * wbuf[j] - w0 * v[j];
-                vn[j - 1] = (j == 1) ? 1.0 : x * scal;
-            }
-            if (tid == 0) {
-                d[kk + 1] = row0[0] - 2.0 * v0 * w0;
-                e[kk + 1] = beta;
-                tau[kk + 1] = tn;
-                sh[0] = tn;
-            }
-            __syncthreads();
-            double* refl = A + (size_t)(kk + 1) * lda + kk + 2;
-            for (int j = tid; j < m - 1; j += EIG_T) refl[j] = vn[j];
-            const int mn = m - 1;
-            if (!in_lds && mn <= mlds) {
-                fused_pass(A, lda, kk + 1, Tl, mn, 0, m, v, wbuf, vn, tn, pbuf, pdot);
-                in_lds = true;
-                lds_base = kk + 2;
-                lds_ld = mn;
-            } else if (in_lds) {
-                const int o = kk + 1 - lds_base;
-                fused_pass(Tl, lds_ld, o, Tl, lds_ld, o + 1, m, v, wbuf, vn, tn, pbuf, pdot);
-            } else {
-                fused_pass(A, lda, kk + 1, A, lda, kk + 2, m, v, wbuf, vn, tn, pbuf, pdot);
-            }
-            __syncthreads();
-            cur ^= 1;
-        }
-    }
-    __syncthreads();
-    ESTAMP(1);
-    // ---------------------------------------------------------------- 2. eigenvalues
-    // T into LDS (d, e, e^2), then the eigenvector block Zl (n x 16) and LU slots
-    const bool t_lds = (32 + 19 * (size_t)n) <= EIG_LDS_DBL;
-    double* dl = t_lds ? sm + 32 : gbuf;
+    __shared__ double red[16];
+    __shared__ int ired[VEC_W];
+    const int n = a.n, q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    double* dl = sm;
     double* el = dl + n;
     double* e2l = el + n;
-    double* Zl = e2l + n;  // n x 16
-    for (int i = tid; i < n; i += EIG_T) {
-        dl[i] = d[i];
-        el[i] = e[i];
-        e2l[i] = e[i] * e[i];
+    double* y = e2l + n;
+    double* lu = a.lu_lds ? (y + n) : (a.lu + (size_t)q * 5 * n);
+    for (int i = tid; i < n; i += VEC_T) {
+        dl[i] = a.d[i];
+        el[i] = a.e[i];
+        e2l[i] = a.e[i] * a.e[i];
     }
-    for (int i = tid; i < 16 * n; i += EIG_T) Zl[i] = 0.0;
     __syncthreads();
-    if (tid == 0) {  // Gershgorin bounds, pivmin as LAPACK dstebz
-        double gl = dl[0], gu = dl[0], emax2 = 0.0;
+    // Gershgorin bounds and pivmin (LAPACK dstebz)
+    double gl = INFINITY, gu = -INFINITY, em = 0.0;
+    for (int i = tid; i < n; i += VEC_T) {
+        const double r = (i > 0 ? fabs(el[i - 1]) : 0.0) + (i < n - 1 ? fabs(el[i]) : 0.0);
+        gl = fmin(gl, dl[i] - r);
+        gu = fmax(gu, dl[i] + r);
+        if (i < n - 1) em = fmax(em, e2l[i]);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        gl = fmin(gl, __shfl_xor(gl, m, 64));
+        gu = fmax(gu, __shfl_xor(gu, m, 64));
+        em = fmax(em, __shfl_xor(em, m, 64));
+    }
+    if (lane == 0) {
+        red[wv] = gl;
+        red[4 + wv] = gu;
+        red[8 + wv] = em;
+    }
+    __syncthreads();
+    gl = red[0];
+    gu = red[4];
+    em = red[8];
+    for (int w = 1; w < VEC_W; ++w) {
+        gl = fmin(gl, red[w]);
+        gu = fmax(gu, red[4 + w]);
+        em = fmax(em, red[8 + w]);
+    }
+    __syncthreads();
+    const double tnorm = fmax(fabs(gl), fabs(gu));
+    const double pivmin = fmax(2.2250738585072014e-308 * fmax(1.0, em), 1e-300);
+    double lo = gl - 2.0 * tnorm * kEps * n - 1e-300;
+    double hi = gu + 2.0 * tnorm * kEps * n + 1e-300;
+    // ---- multisection: 256 Sturm counts per round
+    const int target = n - 1 - q;  // ascending index of the q-th largest
+    for (int it = 0; it < 64; ++it) {
+        const double x = lo + (hi - lo) * (double)(tid + 1) / (double)(VEC_T + 1);
+        const int c = sturm_count(dl, e2l, n, x, pivmin);
+        const unsigned long long above = __ballot(c > target);  // lambda_target < x
+        if (lane == 0) ired[wv] = above ? wv * 64 + __builtin_ctzll(above) : VEC_T;
+        __syncthreads();
+        int first = VEC_T;
+        for (int w = 0; w < VEC_W; ++w) first = min(first, ired[w]);
+        __syncthreads();
+        const double nlo = (first == 0) ? lo : lo + (hi - lo) * (double)first / (double)(VEC_T + 1);
+        const double nhi = (first == VEC_T) ? hi : lo + (hi - lo) * (double)(first + 1) / (double)(VEC_T + 1);
+        if (nlo == lo && nhi == hi) break;
+        lo = nlo;
+        hi = nhi;
+        if (hi - lo <= 2.0 * kEps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
+    }
+    const double lam = 0.5 * (lo + hi);
+    if (tid == 0) {
+        a.W[q] = lam;
+        if (q == 0) a.tnorm[0] = tnorm;
+    }
+    // ---- inverse iteration (dgttrf / dgttrs), lane 0 of wave 0
+    double* fd = lu;
+    double* fu = fd + n;
+    double* fu2 = fu + n;
+    double* fl = fu2 + n;
+    double* fp = fl + n;
+    const double tiny = kEps * tnorm + 1e-300;
+    if (tid == 0) {
         for (int i = 0; i < n; ++i) {
-            const double r = (i > 0 ? fabs(el[i - 1]) : 0.0) + (i < n - 1 ? fabs(el[i]) : 0.0);
-            gl = fmin(gl, dl[i] - r);
-            gu = fmax(gu, dl[i] + r);
-            if (i < n - 1) emax2 = fmax(emax2, e2l[i]);
+            fd[i] = dl[i] - lam;
+            fu[i] = (i < n - 1) ? el[i] : 0.0;
+            fl[i] = (i < n - 1) ? el[i] : 0.0;
+            fu2[i] = 0.0;
+            fp[i] = 0.0;
         }
-        const double tnorm = fmax(fabs(gl), fabs(gu));
-        const double eps = 2.220446049250313e-16;
-        sh[0] = gl - 2.0 * tnorm * eps * n - 1e-300;
-        sh[1] = gu + 2.0 * tnorm * eps * n + 1e-300;
-        sh[2] = fmax(2.2250738585072014e-308 * fmax(1.0, emax2), 1e-300);
-        sh[3] = tnorm;
-    }
-    __syncthreads();
-    const double pivmin = sh[2], tnorm = sh[3];
-    for (int q = wv; q < k; q += EIG_W) {
-        const int target = n - 1 - q;  // ascending index of the q-th largest
-        double lo = sh[0], hi = sh[1];
-        for (int it = 0; it < 40; ++it) {
-            const double x = lo + (hi - lo) * (double)(lane + 1) / 65.0;
-            const int c = sturm_count(dl, e2l, n, x, pivmin);
-            const unsigned long long above = __ballot(c > target);  // lambda_target < x
-            const int first = above ? __builtin_ctzll(above) : 64;
-            const double nlo = (first == 0) ? lo : lo + (hi - lo) * (double)first / 65.0;
-            const double nhi = (first == 64) ? hi : lo + (hi - lo) * (double)(first + 1) / 65.0;
-            if (nlo == lo && nhi == hi) break;
-            lo = nlo;
-            hi = nhi;
-            if (hi - lo <= 2.0 * 2.220446049250313e-16 * fmax(fabs(lo), fabs(hi)) + pivmin) break;
-        }
-        if (lane == 0) W[q] = 0.5 * (lo + hi);
-    }
-    __syncthreads();
-    ESTAMP(2);
-    // ---------------------------------------------------------------- 3. inverse iteration
-    // Waves factor T - lambda_q I into their LU slot and solve in place on
-    // column q of Zl; between solves wave 0 re-orthogonalises each vector
-    // against the earlier members of its eigenvalue cluster and normalises.
-    {
-        const double eps = 2.220446049250313e-16;
-        const double tiny = eps * tnorm + 1e-300;
-        const size_t slot = 5 * (size_t)n;
-        double* slots = nullptr;
-        int nslots = 0;
-        if (t_lds) {
-            const size_t used = 32 + 19 * (size_t)n;
-            nslots = (int)((EIG_LDS_DBL - used) / slot);
-            slots = sm + used;
-        }
-        if (nslots < 1) {  // global fall-back (very large |U|)
-            slots = gbuf + 19 * (size_t)n;
-            nslots = EIG_W;
-        }
-        if (nslots > EIG_W) nslots = EIG_W;
-        for (int q0 = 0; q0 < k; q0 += nslots) {
-            const int q = q0 + wv;
-            const bool act = (wv < nslots) && (q < k);
-            double* dd = slots + (size_t)wv * slot;
-            double* du = dd + n;
-            double* du2 = du + n;
-            double* dlw = du2 + n;
-            double* piv = dlw + n;
-            if (act) {
-                const double lam = W[q];
-                if (lane == 0) {
-                    for (int i = 0; i < n; ++i) {
-                        dd[i] = dl[i] - lam;
-                        du[i] = (i < n - 1) ? el[i] : 0.0;
-                        dlw[i] = (i < n - 1) ? el[i] : 0.0;
-                        du2[i] = 0.0;
-                        piv[i] = 0.0;
-                    }
-                    for (int i = 0; i < n - 1; ++i) {
-                        if (fabs(dd[i]) >= fabs(dlw[i])) {
-                            if (dd[i] == 0.0) dd[i] = tiny;
-                            const double f = dlw[i] / dd[i];
-                            dlw[i] = f;
-                            dd[i + 1] -= f * du[i];
-                        } else {
-                            const double f = dd[i] / dlw[i];
-                            dd[i] = dlw[i];
-                            dlw[i] = f;
-                            const double tt = du[i];
-                            du[i] = dd[i + 1];
-                            dd[i + 1] = tt - f * dd[i + 1];
-                            if (i < n - 2) {
-                                du2[i] = du[i + 1];
-                                du[i + 1] = -f * du[i + 1];
-                            }
-                            piv[i] = 1.0;
-                        }
-                    }
-                    if (dd[n - 1] == 0.0) dd[n - 1] = tiny;
+        for (int i = 0; i < n - 1; ++i) {
+            if (fabs(fd[i]) >= fabs(fl[i])) {
+                if (fd[i] == 0.0) fd[i] = tiny;
+                const double f = fl[i] / fd[i];
+                fl[i] = f;
+                fd[i + 1] -= f * fu[i];
+            } else {
+                const double f = fd[i] / fl[i];
+                fd[i] = fl[i];
+                fl[i] = f;
+                const double tt = fu[i];
+                fu[i] = fd[i + 1];
+                fd[i + 1] = tt - f * fd[i + 1];
+                if (i < n - 2) {
+                    fu2[i] = fu[i + 1];
+                    fu[i + 1] = -f * fu[i + 1];
                 }
-                for (int i = lane; i < n; i += 64) {  // deterministic pseudo-random start
-                    unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)q * 40503u + 12345u);
-                    h ^= h >> 13;
-                    h *= 0x5bd1e995u;
-                    h ^= h >> 15;
-                    Zl[(size_t)i * 16 + q] = 0.5 + (double)(h & 0xffff) / 65536.0;
-                }
-            }
-            __syncthreads();
-            for (int iter = 0; iter < 3; ++iter) {
-                if (act && lane == 0) {
-                    double* b = Zl + q;  // stride 16
-                    for (int i = 0; i < n - 1; ++i) {
-                        if (piv[i] == 0.0) {
-                            b[(size_t)(i + 1) * 16] -= dlw[i] * b[(size_t)i * 16];
-                        } else {
-                            const double tt = b[(size_t)i * 16];
-                            b[(size_t)i * 16] = b[(size_t)(i + 1) * 16];
-                            b[(size_t)(i + 1) * 16] = tt - dlw[i] * b[(size_t)i * 16];
-                        }
-                    }
-                    b[(size_t)(n - 1) * 16] /= dd[n - 1];
-                    if (n >= 2)
-                        b[(size_t)(n - 2) * 16] =
-                            (b[(size_t)(n - 2) * 16] - du[n - 2] * b[(size_t)(n - 1) * 16]) / dd[n - 2];
-                    for (int i = n - 3; i >= 0; --i)
-                        b[(size_t)i * 16] = (b[(size_t)i * 16] - du[i] * b[(size_t)(i + 1) * 16] -
-                                             du2[i] * b[(size_t)(i + 2) * 16]) /
-                                            dd[i];
-                }
-                __syncthreads();
-                if (wv == 0) {
-                    const int qe = min(k, q0 + nslots);
-                    for (int qq = q0; qq < qe; ++qq) {
-                        for (int rr = qq - 1; rr >= 0 && fabs(W[rr] - W[rr + 1]) <= 1e-3 * tnorm; --rr) {
-                            double s = 0.0;
-                            for (int i = lane; i < n; i += 64) s += Zl[(size_t)i * 16 + rr] * Zl[(size_t)i * 16 + qq];
-                            s = wave_sum_d(s);
-                            for (int i = lane; i < n; i += 64) Zl[(size_t)i * 16 + qq] -= s * Zl[(size_t)i * 16 + rr];
-                        }
-                        double s = 0.0;
-                        for (int i = lane; i < n; i += 64) s += Zl[(size_t)i * 16 + qq] * Zl[(size_t)i * 16 + qq];
-                        s = wave_sum_d(s);
-                        const double inv = 1.0 / sqrt(s);
-                        for (int i = lane; i < n; i += 64) Zl[(size_t)i * 16 + qq] *= inv;
-                    }
-                }
-                __syncthreads();
+                fp[i] = 1.0;
             }
         }
+        if (fd[n - 1] == 0.0) fd[n - 1] = tiny;
     }
-    ESTAMP(3);
-    // ---------------------------------------------------------------- 4. back-transform
-    // eigenvector of A = H_0 H_1 ... H_{n-3} y, applied from the last reflector;
-    // one wave per vector, vectors in LDS, reflectors read from A's rows.
-    for (int q = wv; q < k; q += EIG_W) {
-        for (int kk = n - 3; kk >= 0; --kk) {
-            const double t = tau[kk];
-            if (t == 0.0) continue;
-            const double* v = A + (size_t)kk * lda + kk + 1;  // v[0] = 1
-            double* zc = Zl + (size_t)(kk + 1) * 16 + q;
-            const int m = n - kk - 1;
-            double vr[8];
+    for (int i = tid; i < n; i += VEC_T) {  // deterministic pseudo-random start
+        unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)q * 40503u + 12345u);
+        h ^= h >> 13;
+        h *= 0x5bd1e995u;
+        h ^= h >> 15;
+        y[i] = 0.5 + (double)(h & 0xffff) / 65536.0;
+    }
+    __syncthreads();
+    for (int iter = 0; iter < 3; ++iter) {
+        if (tid == 0) {
+            double bi = y[0];
+            for (int i = 0; i < n - 1; ++i) {
+                const double bn = y[i + 1];
+                if (fp[i] == 0.0) {
+                    y[i] = bi;
+                    bi = bn - fl[i] * bi;
+                } else {
+                    y[i] = bn;
+                    bi = bi - fl[i] * bn;
+                }
+            }
+            y[n - 1] = bi;
+            double z1 = y[n - 1] / fd[n - 1];
+            y[n - 1] = z1;
+            double z2 = 0.0;
+            if (n >= 2) {
+                z2 = (y[n - 2] - fu[n - 2] * z1) / fd[n - 2];
+                y[n - 2] = z2;
+            }
+            for (int i = n - 3; i >= 0; --i) {
+                const double z0 = (y[i] - fu[i] * z2 - fu2[i] * z1) / fd[i];
+                y[i] = z0;
+                z1 = z2;
+                z2 = z0;
+            }
+        }
+        __syncthreads();
+        // scale by the largest magnitude first (a solve can grow y by 1/pivot ~ 1e300)
+        double mx = 0.0;
+        for (int i = tid; i < n; i += VEC_T) mx = fmax(mx, fabs(y[i]));
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) mx = fmax(mx, __shfl_xor(mx, m, 64));
+        if (lane == 0) red[8 + wv] = mx;
+        __syncthreads();
+        mx = red[8];
+        for (int w = 1; w < VEC_W; ++w) mx = fmax(mx, red[8 + w]);
+        const double sc = (mx > 0.0 && mx < INFINITY) ? 1.0 / mx : 1.0;
+        double s = 0.0;
+        for (int i = tid; i < n; i += VEC_T) {
+            const double v = y[i] * sc;
+            s += v * v;
+        }
+        s = block_sum<VEC_W>(s, red);
+        const double inv = sc / sqrt(s);
+        for (int i = tid; i < n; i += VEC_T) y[i] *= inv;
+        __syncthreads();
+    }
+    // ---- back-transformation: z = H_0 H_1 ... H_{n-3} y (last reflector first)
+    for (int kk = n - 3; kk >= 0; --kk) {
+        const double t = a.tau[kk];
+        if (t == 0.0) continue;
+        const double* v = a.refl + (size_t)kk * a.lda;  // v[kk+1] = 1
+        double s = 0.0;
+        for (int j = kk + 1 + tid; j < n; j += VEC_T) s += v[j] * y[j];
+        s = block_sum<VEC_W>(s, red) * t;
+        for (int j = kk + 1 + tid; j < n; j += VEC_T) y[j] -= s * v[j];
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += VEC_T) a.Zq[(size_t)q * a.lda + i] = y[i];
+}
+
+// ---------------------------------------------------------------------------
+// 3. cluster re-orthogonalisation, normalisation, sign, transposed store
+__global__ void __launch_bounds__(FIN_T) k_eig_finish(double* Zq, int n, int lda, int k, const double* W,
+                                                     const double* tnorm_p, double* Z)
+{
+    __shared__ double red[FIN_W];
+    __shared__ int ired[FIN_W];
+    __shared__ double sbest[FIN_W];
+    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    const double tnorm = tnorm_p[0];
+    for (int qq = 0; qq < k; ++qq) {  // vectors live in global memory (one workgroup)
+        double* z = Zq + (size_t)qq * lda;
+        for (int rr = qq - 1; rr >= 0 && fabs(W[rr] - W[rr + 1]) <= 1e-3 * tnorm; --rr) {
+            const double* zr = Zq + (size_t)rr * lda;
             double s = 0.0;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int j = lane + 64 * u;
-                vr[u] = (j < m) ? v[j] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int j = lane + 64 * u;
-                if (j < m) s += vr[u] * zc[(size_t)j * 16];
-            }
-            for (int j = lane + 512; j < m; j += 64) s += v[j] * zc[(size_t)j * 16];
-            s = wave_sum_d(s) * t;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int j = lane + 64 * u;
-                if (j < m) zc[(size_t)j * 16] -= s * vr[u];
-            }
-            for (int j = lane + 512; j < m; j += 64) zc[(size_t)j * 16] -= s * v[j];
+            for (int i = tid; i < n; i += FIN_T) s += zr[i] * z[i];
+            s = block_sum<FIN_W>(s, red);
+            for (int i = tid; i < n; i += FIN_T) z[i] -= s * zr[i];
+            __syncthreads();
         }
-        // deterministic sign: largest-magnitude component positive
-        double best = 0.0;
+        double s = 0.0;
+        for (int i = tid; i < n; i += FIN_T) s += z[i] * z[i];
+        s = block_sum<FIN_W>(s, red);
+        const double inv = 1.0 / sqrt(s);
+        // deterministic sign: largest-magnitude component positive (lowest index on ties)
+        double best = -1.0;
         int bi = 0;
-        for (int i = lane; i < n; i += 64) {
-            const double a = fabs(Zl[(size_t)i * 16 + q]);
-            if (a > best) {
-                best = a;
+        for (int i = tid; i < n; i += FIN_T) {
+            const double v = fabs(z[i]);
+            if (v > best) {
+                best = v;
                 bi = i;
             }
         }
-        for (int m2 = 32; m2 >= 1; m2 >>= 1) {
-            const double ob = __shfl_xor(best, m2, 64);
-            const int oi = __shfl_xor(bi, m2, 64);
+        for (int m = 32; m >= 1; m >>= 1) {
+            const double ob = __shfl_xor(best, m, 64);
+            const int oi = __shfl_xor(bi, m, 64);
             if (ob > best || (ob == best && oi < bi)) {
                 best = ob;
                 bi = oi;
             }
         }
-        const double sgn = (Zl[(size_t)bi * 16 + q] < 0.0) ? -1.0 : 1.0;
-        for (int i = lane; i < n; i += 64) Zl[(size_t)i * 16 + q] *= sgn;
+        if (lane == 0) {
+            sbest[wv] = best;
+            ired[wv] = bi;
+        }
+        __syncthreads();
+        best = sbest[0];
+        bi = ired[0];
+        for (int w = 1; w < FIN_W; ++w)
+            if (sbest[w] > best || (sbest[w] == best && ired[w] < bi)) {
+                best = sbest[w];
+                bi = ired[w];
+            }
+        const double sg = (z[bi] < 0.0) ? -inv : inv;
+        __syncthreads();
+        for (int i = tid; i < n; i += FIN_T) z[i] *= sg;
+        __syncthreads();
     }
-    __syncthreads();
-    for (int i = tid; i < n * 16; i += EIG_T) Z[i] = ((i & 15) < k) ? Zl[i] : 0.0;
-    ESTAMP(4);
+    for (int i = tid; i < n * 16; i += FIN_T) {
+        const int u = i >> 4, q = i & 15;
+        Z[i] = (q < k) ? Zq[(size_t)q * lda + u] : 0.0;
+    }
 }
 
-extern "C" hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
-                                            u64* stamps, hipStream_t st)
+// ---------------------------------------------------------------------------
+// host side
+struct EigLayout {
+    size_t d, e, tau, tnorm, flags, pbuf, rowbuf, pdot, zq, refl, lu, work, total;
+};
+
+static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool lu_lds)
 {
-    hipFuncSetAttribute((const void*)k_syevx_topk, hipFuncAttributeMaxDynamicSharedMemorySize, EIG_LDS_BYTES);
-    hipLaunchKernelGGL(k_syevx_topk, dim3(1), dim3(EIG_T), EIG_LDS_BYTES, st, A, n, lda, k, scratch, Z, W, stamps);
+    EigLayout L;
+    size_t o = 0;
+    auto take = [&](size_t cnt) {
+        const size_t at = o;
+        o += (cnt + 31) & ~(size_t)31;  // 256-B aligned pieces
+        return at;
+    };
+    L.d = take(n);
+    L.e = take(n);
+    L.tau = take(n);
+    L.tnorm = take(1);
+    L.flags = take(2);  // counter, err (u32 in doubles' space)
+    L.pbuf = take(2 * (size_t)lda);
+    L.rowbuf = take(2 * (size_t)lda);
+    L.pdot = take(2 * EIG_MAX_WG);
+    L.zq = take(16 * (size_t)lda);
+    L.refl = take((size_t)n * lda);
+    L.lu = lu_lds ? o : take((size_t)16 * 5 * n);
+    const int R = (n + nwg - 1) / nwg;
+    L.work = rows_lds ? o : take((size_t)nwg * R * n);
+    L.total = o;
+    (void)k;
+    return L;
+}
+
+static size_t tri_lds_bytes(int n, int R, bool rows_lds)
+{
+    return sizeof(double) * (4 * (size_t)n + 64 + EIG_MAX_WG + (rows_lds ? (size_t)R * n : 0));
+}
+
+static int eig_nwg(int n)
+{
+    static int cus = -1;
+    if (cus < 0) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 64;
+    }
+    const char* env = getenv("SCC_EIG_NWG");
+    int nwg = (env && *env) ? atoi(env) : (n + 9) / 10;
+    nwg = nwg < 8 ? 8 : nwg;
+    if (nwg > cus) nwg = cus;
+    if (nwg > EIG_MAX_WG) nwg = EIG_MAX_WG;
+    if (nwg > n) nwg = n;
+    if (nwg < 1) nwg = 1;
+    return nwg;
+}
+
+static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
+{
+    nwg = eig_nwg(n);
+    const int R = (n + nwg - 1) / nwg;
+    rows_lds = tri_lds_bytes(n, R, true) <= EIG_LDS_MAX;
+    lu_lds = sizeof(double) * 9 * (size_t)n <= EIG_LDS_MAX;
+}
+
+extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
+{
+    int nwg;
+    bool rl, ll;
+    eig_plan(n, nwg, rl, ll);
+    return eig_layout(n, lda, k, nwg, rl, ll).total;
+}
+
+// A: n x n symmetric (full), row-major, lda (read only).  scratch: see
+// scc_eigen_scratch_doubles.  Z: n x 16 out, W: k out (descending).
+// *err_dev (device u32 inside scratch) is set to 1 if a hand-off timed out.
+// marks (optional): 6 events recorded before/after each of the three launches.
+extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
+                                            double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
+                                            hipStream_t st)
+{
+    int nwg;
+    bool rows_lds, lu_lds;
+    eig_plan(n, nwg, rows_lds, lu_lds);
+    const EigLayout L = eig_layout(n, lda, k, nwg, rows_lds, lu_lds);
+    u32* flags = (u32*)(scratch + L.flags);
+    if (err_dev) *err_dev = flags + 1;
+    if (nwg_out) *nwg_out = nwg;
+    hipError_t e = hipMemsetAsync(flags, 0, 8, st);
+    if (e != hipSuccess) return e;
+    TriArgs t;
+    t.A = A;
+    t.n = n;
+    t.lda = lda;
+    t.nwg = nwg;
+    t.rows_lds = rows_lds ? 1 : 0;
+    t.d = scratch + L.d;
+    t.e = scratch + L.e;
+    t.tau = scratch + L.tau;
+    t.refl = scratch + L.refl;
+    t.pbuf = scratch + L.pbuf;
+    t.rowbuf = scratch + L.rowbuf;
+    t.pdot = scratch + L.pdot;
+    t.work = scratch + L.work;
+    t.counter = flags;
+    t.err = flags + 1;
+    const int R = (n + nwg - 1) / nwg;
+    // at least 82 KB so that every workgroup has a CU of its own
+    size_t lds = tri_lds_bytes(n, R, rows_lds);
+    if (lds < 82 * 1024) lds = 82 * 1024;
+    hipFuncSetAttribute((const void*)k_tridiag, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (marks) hipEventRecord(marks[0], st);
+    hipLaunchKernelGGL(k_tridiag, dim3(nwg), dim3(TRI_T), lds, st, t);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (marks) hipEventRecord(marks[1], st);
+    VecArgs v;
+    v.d = t.d;
+    v.e = t.e;
+    v.tau = t.tau;
+    v.refl = t.refl;
+    v.n = n;
+    v.lda = lda;
+    v.k = k;
+    v.lu_lds = lu_lds ? 1 : 0;
+    v.lu = scratch + L.lu;
+    v.Zq = scratch + L.zq;
+    v.W = W;
+    v.tnorm = scratch + L.tnorm;
+    const size_t vlds = sizeof(double) * (lu_lds ? 9 : 4) * (size_t)n;
+    hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
+    if (marks) hipEventRecord(marks[2], st);
+    hipLaunchKernelGGL(k_tri_vectors, dim3(k), dim3(VEC_T), vlds, st, v);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (marks) hipEventRecord(marks[3], st);
+    if (marks) hipEventRecord(marks[4], st);
+    hipLaunchKernelGGL(k_eig_finish, dim3(1), dim3(FIN_T), 0, st, v.Zq, n, lda, k, W, v.tnorm, Z);
+    if (marks) hipEventRecord(marks[5], st);
     return hipGetLastError();
 }

@@ -60,6 +60,7 @@ struct scc_ctx {
     const double* d_last_scores = nullptr;  // N x 16 in the workspace
     int last_n = 0;
     int last_ncomp = 0;
+    unsigned int eig_err = 0;  // hand-off timeout flag of the last eigensolve (host copy)
 };
 
 struct scc_dataset {

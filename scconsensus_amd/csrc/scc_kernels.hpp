@@ -102,8 +102,9 @@ hipError_t scc_launch_classify(const long long* gstart, int G, int cap_s, int ca
 size_t scc_rank_lds_bytes(int cls, int cap, int K);
 int scc_rank_cap(int cls, int want, int K);
 hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st);
-hipError_t scc_launch_syevx_topk(double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
-                                 unsigned long long* stamps, hipStream_t st);
+size_t scc_eigen_scratch_doubles(int n, int lda, int k);
+hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
+                                 unsigned int** err_dev, int* nwg_out, hipEvent_t* marks, hipStream_t st);
 
 hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st);
 int scc_wilcox_table_layout(int* woff);

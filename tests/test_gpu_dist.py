@@ -78,3 +78,50 @@ def test_dist_packed_order_small(eng):
     ds = eng.dataset_dense(X)
     dist = eng.distance(ds, np.array([0, 2]), nat.SCC_DIST_PCA_EUCLID)
     np.testing.assert_allclose(dist, [1, 3, 6, 2, 5, 3], atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 17, 40, 130, 700])
+def test_eigensolver_sizes(eng, n):
+    """Multi-workgroup tridiagonalisation + per-eigenpair vectors at many |U|
+    (workgroup counts 2..70, rows in LDS) against numpy's exact SVD."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(100 + n)
+    X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+def test_eigensolver_repeated_eigenvalues(eng):
+    """Exactly repeated eigenvalues inside the top 15 (cluster re-orthogonalisation);
+    the 15/16 boundary itself is well separated so the distance is defined."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(7)
+    n, N = 40, 500
+    sv = np.array([9.0] * 3 + [7.0] * 4 + [5.0] * 2 + [4.0] * 6 + [1.0] * (n - 15))
+    Q, _ = np.linalg.qr(rng.standard_normal((N, n)))
+    Q -= Q.mean(axis=0)  # centred cells -> the Gram is exactly V diag(sv^2) V'
+    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    M = Q @ np.diag(sv) @ V.T  # cells x genes
+    X = M.T
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+def test_eigensolver_rows_beyond_lds(eng):
+    """|U| = 2100: each workgroup's rows no longer fit its LDS (global row store)."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(11)
+    n, N = 2100, 1200
+    X = rng.standard_normal((n, N)) * np.linspace(3.0, 0.5, n)[:, None]
+    X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, N)) * 4.0  # a few spikes
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
