@@ -112,7 +112,8 @@ def main():
     t1 = time.perf_counter()
     dt = dist.max_over_ranks(t1 - t0)
     ms = dt / a.steps * 1e3
-    fams = ["ingest", "gene_rank", "pair_test", "pair_select", "gather", "center", "gram", "eigen", "scores", "dist"]
+    fams = ["ingest", "gene_stats", "pair_filter", "gene_rank", "pair_test", "pair_select", "gather", "center", "gram",
+            "eigen", "eig_tridiag", "eig_vec", "eig_fin", "scores", "dist"]
     times = {f: eng.kernel_time(f) for f in fams}
     stage_ms = {f: (t[0] / max(t[1], 1)) for f, t in times.items()}
     # algorithmic work per launch of each kernel family

@@ -74,6 +74,9 @@ typedef struct {
     double min_per_cent;        /* FAST: minPerCent (Fast:29) */
     double fc_thrs;             /* SLOW: fcThrs, compared as log(fcThrs) (slow:167) */
     double mean_scaling_factor; /* SLOW: meanScalingFactor (slow:23) */
+    int32_t test_all;           /* FAST: 1 = also compute U / p for the (pair, gene) cells the
+                                   feature filters drop (diagnostics; R never tests them) */
+    int32_t reserved;
 } scc_de_params;
 
 /* ---- context ---------------------------------------------------------- */

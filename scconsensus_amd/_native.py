@@ -53,7 +53,8 @@ class Opts(ctypes.Structure):
 class DeParams(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("top_n", ctypes.c_int32), ("q_val_thrs", ctypes.c_double),
                 ("log_fc_thrs", ctypes.c_double), ("min_per_cent", ctypes.c_double), ("fc_thrs", ctypes.c_double),
-                ("mean_scaling_factor", ctypes.c_double)]
+                ("mean_scaling_factor", ctypes.c_double), ("test_all", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 _lib = None
@@ -227,9 +228,15 @@ class Engine:
 
     # -------------------------------------------------------------- DE
     def de_run(self, ds: Dataset, code, K, mode=SCC_DE_FAST, q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0,
-               top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all") -> DeResult:
+               top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all", test_all=None) -> DeResult:
+        """test_all (FAST): also compute U / p for the (pair, gene) cells the
+        feature filters drop; default: only when the full per-pair vectors are
+        fetched (fetch="all")."""
         code = np.ascontiguousarray(code, np.int32)
-        prm = DeParams(mode, top_n, q_val_thrs, log_fc_thrs, min_per_cent, fc_thrs, mean_scaling_factor)
+        if test_all is None:
+            test_all = fetch == "all"
+        prm = DeParams(mode, top_n, q_val_thrs, log_fc_thrs, min_per_cent, fc_thrs, mean_scaling_factor,
+                       1 if test_all else 0, 0)
         r = ctypes.c_void_p()
         rc = self.lib.scc_de_run(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), ctypes.byref(r))
         msg = ""

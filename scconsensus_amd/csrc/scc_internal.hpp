@@ -17,8 +17,9 @@
 
 namespace scc_rt {
 
-constexpr int kCapSmall = 2048;    // LDS rank kernel, 256 threads
-constexpr int kCapMedium = 8192;   // LDS rank kernel, 1024 threads (larger genes: HBM index arrays)
+constexpr int kCapSmall = 2048;    // rank work item in LDS, 256 threads
+constexpr int kCapMedium = 16384;  // rank work item in LDS, 1024 threads (capped by the LDS budget);
+                                   // larger genes are split into value buckets
 constexpr int kCountChunk = 32;    // cells per ingest count chunk (one cluster each)
 constexpr int kScatterCC = 4;      // count chunks per ingest scatter chunk
 constexpr int kMaxGenesLds = 40960;  // ingest histogram of one chunk lives in LDS
@@ -40,6 +41,7 @@ struct PendingEv {
 
 struct scc_ctx {
     int device = 0;
+    int n_cu = 256;
     hipStream_t s0 = nullptr, s1 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;

@@ -12,25 +12,51 @@
 
 struct dd;
 
-struct ScRankLaunch {
-    const int* gene_list;
-    const int* list_count;
+struct ScStatsLaunch {
     const long long* gstart;
     const unsigned long long* keys;
-    int G, K, cap, grid;
+    int G, K;
     const int* n_clu;
     const uint32_t* coff;
     const int* cl_cc;
-    uint32_t* gix;
-    uint8_t* guc;
-    uint8_t* gsc;
+    double* mean_x;     // [K][G]
+    double* mean_e;     // [K][G]
+    uint32_t* cnt_pos;  // [K][G]
+    uint32_t* cnt_neg;  // [K][G]
+};
+
+// one unit of rank work: a whole gene (src 0: the ingest's cluster-grouped
+// segment) or one value bucket of a split gene (src 1: keys2 / codes2)
+struct ScRankItem {
+    long long base;
+    int n, gene, src;
+};
+
+struct ScRankLaunch {
+    const long long* gstart;
+    const unsigned long long* keys;
+    int G, K, P, all_pairs;
+    const uint32_t* coff;
+    const int* cl_cc;
+    const uint8_t* flags;  // [P][G] bit0: the pair tests the gene
+    int cap_s, cap_m, cap_lds, bucket_target, ntp_max, item_cap;
+    int med_wide;          // medium items: 1024 threads, one workgroup per CU
+    ScRankItem* items;     // [3][item_cap]
+    int* counts;           // [0..2] items per class, [3] split genes
+    int* split_genes;      // [G]
+    unsigned long long* keys2;  // [nnz] bucket-ordered keys of split genes
+    uint8_t* codes2;            // [nnz]
+    uint32_t* gix;              // [2][nnz] index ping-pong of HBM-resident items
+    uint32_t* gwin;             // [nnz] key windows of HBM-resident items
+    uint8_t* gcode;             // [nnz]
+    uint8_t* gsc;               // [nnz]
     long long nnz;
-    double* mean_x;
-    double* mean_e;
-    uint32_t* cnt_pos;
-    long long* u2_base;
-    long long* t_base;
-    unsigned long long* stamps;  // diagnostic only
+    unsigned long long* accS;   // [P][G] #{x > y}, nonzeros
+    unsigned long long* accE;   // [P][G] cross-cluster equal pairs
+    unsigned long long* accX;   // [P][G] sum c_a c_b (c_a + c_b) over tie groups
+    unsigned long long* accF;   // [K][G] sum c^3 - c over within-cluster runs
+    unsigned long long* stamps; // diagnostic phase clocks [item][8] (nullptr normally)
+    int stamp_base[3];
 };
 
 struct ScTestLaunch {
@@ -40,8 +66,12 @@ struct ScTestLaunch {
     const double* mean_x;
     const double* mean_e;
     const uint32_t* cnt_pos;
-    const long long* u2_base;
-    const long long* t_base;
+    const uint32_t* cnt_neg;
+    const unsigned long long* accS;
+    const unsigned long long* accE;
+    const unsigned long long* accX;
+    const unsigned long long* accF;
+    int all_pairs;
     const double* wtab;
     const int* woff;
     double* out_p;
@@ -97,11 +127,14 @@ hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long
 int scc_scan_scratch_blocks(long long n);
 hipError_t scc_launch_reduce_dd(const dd* parts, int n, dd* out, hipStream_t st);
 
-hipError_t scc_launch_classify(const long long* gstart, int G, int cap_s, int cap_m, int* lists, int* counts,
-                               hipStream_t st);
-size_t scc_rank_lds_bytes(int cls, int cap, int K);
-int scc_rank_cap(int cls, int want, int K);
-hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st);
+hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st);
+hipError_t scc_launch_rank_classify(const ScRankLaunch* L, hipStream_t st);
+size_t scc_rank_item_lds(int cls, int cap, int ntp_max, int K);
+int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim);
+size_t scc_rank_split_lds(int K);
+hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st);
+hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st);
+hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st);
 size_t scc_eigen_scratch_doubles(int n, int lda, int k);
 hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
                                  unsigned int** err_dev, int* nwg_out, hipEvent_t* marks, hipStream_t st);

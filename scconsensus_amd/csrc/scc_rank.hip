@@ -1,46 +1,46 @@
-// scc_rank.hip — per-gene Wilcoxon rank-sum engine (all cluster pairs at once).
+// scc_rank.hip — per-gene statistics and the all-pairs Wilcoxon rank-sum engine.
 //
-// Replaces, for every gene and every cluster pair (i<j) simultaneously, the
-// reference's per-(pair, gene) `wilcox.test(data.use[x, ] ~ group)` call
-// (R/reclusterDEConsensusFast.R:78-91; R/reclusterDEConsensus.R:99-103) and the
-// per-pair log-mean/pct statistics (Fast:229-271, slow:104-113).
+// Replaces the reference's per-(pair, gene) `wilcox.test(data.use[x, ] ~ group)`
+// calls (R/reclusterDEConsensusFast.R:78-91; R/reclusterDEConsensus.R:99-103)
+// and the per-cluster log-mean / detection statistics (Fast:229-271,
+// slow:104-113).  Exact integer arithmetic throughout: R's statistic
+// W = 2U/2 and its tie term sum(NTIES^3 - NTIES) are reproduced bit for bit.
 //
-// One workgroup per gene.  The ingest leaves each gene's kept nonzeros
-// grouped by cluster (cluster a at [off_a, off_a+1) of the segment), so:
-//   1. per-cluster statistics (dd sums of x and expm1(x), counts of x > 0 /
-//      x < 0) are contiguous reductions over <= K + W balanced pieces
-//   2. the segment is sorted by value with a stable LSD radix sort of an index
-//      permutation (8-bit digits, wave match-ranking, no compare network) on a
-//      32-bit window of the orderable key: bits [sh, sh+32) of key - kmin.
-//      Equal windows with different doubles ("mixed runs", values closer than
-//      2^-28 relative) are re-sorted exactly by one wave each; if any is
-//      longer than 64 the gene is re-sorted on all bits.  Stability keeps
-//      equal values in cluster order, which the sweep relies on.
-//   3. one sweep per wave chunk (register accumulators): S[a][b] = #{b before
-//      an a-element}; with ties ordered by code, for a < b this is exactly
-//      #{(x in a, y in b): x > y}.  The same sweep counts, per tie group,
-//      E_ab = c_a c_b, X_ab = c_a c_b (c_a + c_b) and F_a = sum c_a^3 - c_a
-//   5. per pair:  2U = 2*(S + z_a*neg_b + pos_a*z_b) + z_a*z_b + E_ab
-//                 T  = F_a + F_b + 3*z_a*z_b*(z_a+z_b) + 3*X_ab
-//      where z = implicit zeros of the cluster; T = sum(NTIES^3 - NTIES).
-// 2U and T are exact int64 — R's W = 2U/2 and its tie term bit for bit.
-// Genes too large for LDS keep their index arrays in HBM (same code).
+// Kernels (one launch each, all on the nonzeros the ingest grouped by
+// (gene, cluster); zeros are never materialised):
+//   k_gene_stats   one workgroup per gene: per-cluster double-double sums of
+//                  x and expm1(x), counts of x > 0 and x < 0, fixed reduction
+//                  order (bitwise deterministic).
+//   k_rank_classify  per gene: does any cluster pair test it (FAST filters
+//                  ran before the rank stage, exactly as ComputePairWiseDE
+//                  only tests the features that pass, Fast:242-291)?  Genes
+//                  that fit a workgroup's LDS become work items; larger ones
+//                  go to the splitter.
+//   k_rank_split   one workgroup per large gene: 2048-bin histogram of the
+//                  value key, bins packed into value-range buckets of <= cap
+//                  elements, buckets scattered to their own ranges, and the
+//                  cross-bucket part of every tested pair's rank sum from the
+//                  per-bucket cluster histograms.  Equal values never straddle
+//                  buckets, so ties stay inside one work item.
+//   k_rank_item    one workgroup per work item (a gene or a bucket): stable
+//                  LSD radix sort (8-bit digits, wave match-ranking, no atomic
+//                  conflicts) on a 32-bit window of the orderable key with an
+//                  exact fix-up of windows that merged distinct doubles; the
+//                  sorted positions partitioned by cluster; for every tested
+//                  pair (a, b) the within-item count #{x in a, y in b: x > y}
+//                  by binary searches of the smaller cluster's positions in
+//                  the larger's; tie groups (runs of equal values) give
+//                  E_ab = sum c_a c_b, X_ab = sum c_a c_b (c_a + c_b) and
+//                  F_a = sum (c_a^3 - c_a).  Everything is added with integer
+//                  atomics into per-(pair, gene) accumulators (order-free).
+// The pair-test kernel (scc_select.hip) adds the implicit zero group in closed
+// form:  2U = 2 (S + z_a neg_b + pos_a z_b) + z_a z_b + E,
+//        T  = F_a + F_b + f(z_a) + f(z_b) + 3 z_a z_b (z_a + z_b) + 3 X.
 #include "scc_common.hpp"
 #include "scc_kernels.hpp"
 #include <type_traits>
 
 __device__ inline u64 f_tie(u64 c) { return c * c * c - c; }
-
-__device__ inline void pair_decode(int p, int K, int& a, int& b)
-{
-    a = 0;
-    int rem = p;
-    while (rem >= K - 1 - a) {
-        rem -= K - 1 - a;
-        ++a;
-    }
-    b = a + 1 + rem;
-}
 
 __device__ inline u32 lanes_below(u64 m)  // popcount of m over lanes < this lane
 {
@@ -53,81 +53,186 @@ __device__ inline u64 shfl_xor_u64(u64 v, int m)
     return ((u64)hi << 32) | lo;
 }
 
-struct RankArgs {
-    const int* gene_list;
-    const int* list_count;
-    const i64* gstart;   // [G+1] gene segment starts
-    const u64* keys;     // kept nonzeros' value keys, cluster-grouped per gene
-    int G, K, P;
-    const int* n_clu;    // kept cells per cluster
-    const u32* coff;     // [nc+1][G] per-gene offsets of the count chunks
-    const int* cl_cc;    // [K+1] first count chunk of each cluster
-    double* mean_x;      // [K][G]
-    double* mean_e;      // [K][G]
-    u32* cnt_pos;        // [K][G]
-    i64* u2_base;        // [P][G]
-    i64* t_base;         // [P][G]
-    u32* gix;            // [2][nnz] index ping-pong of HBM-resident genes
-    u8* guc;             // [nnz] code by segment position (HBM-resident genes)
-    u8* gsc;             // [nnz] sorted codes (HBM-resident genes)
-    i64 nnz;
-    u64* stamps;         // diagnostic phase clocks [block][8] (nullptr in normal runs)
-};
+__device__ inline void pair_decode(int p, int K, int& a, int& b)
+{
+    a = 0;
+    int rem = p;
+    while (rem >= K - 1 - a) {
+        rem -= K - 1 - a;
+        ++a;
+    }
+    b = a + 1 + rem;
+}
 
-#define STAMP(A, ph)                                                                      \
-    do {                                                                                  \
-        if ((A).stamps && threadIdx.x == 0)                                               \
-            (A).stamps[(size_t)blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memtime();    \
-    } while (0)
+// lanes whose value of the low `bits` bits of d equals this lane's (among `act`)
+template <int BITS>
+__device__ inline u64 match_bits(u32 d, u64 act)
+{
+    u64 peers = act;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const u64 bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    return peers;
+}
 
-#define RK_RUNS 256  // mixed-run list capacity
+// ===================================================================== stats
+#define ST_T 256
+#define ST_W (ST_T / 64)
 
 struct StatItem {
     double sx_hi, sx_lo, se_hi, se_lo;
-    u64 kmin, kmax;
     u32 pos, neg;
 };
 
-// small per-block LDS state (both variants)
-template <int T>
-struct RankSmall {
-    static constexpr int W = T / 64;
+__global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
+{
+    __shared__ int off[65];
+    __shared__ StatItem item[64 + ST_W + 4];
+    const int g = blockIdx.x, K = A.K, tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    const i64 base = A.gstart[g];
+    const int n = (int)(A.gstart[g + 1] - base);
+    const u64* key = A.keys + base;
+    if (tid <= K) off[tid] = (int)A.coff[(size_t)A.cl_cc[tid] * A.G + g];
+    __syncthreads();
+    // balanced pieces that never straddle clusters, combined in a fixed order
+    const int Lp = max(64, (((n + ST_W - 1) / ST_W) + 63) & ~63);
+    for (int it = w;; it += ST_W) {
+        int a = 0, acc = 0, ni = 0;
+        for (; a < K; ++a) {
+            ni = (off[a + 1] - off[a] + Lp - 1) / Lp;
+            if (it < acc + ni) break;
+            acc += ni;
+        }
+        if (a == K) break;
+        const int s0 = off[a] + (it - acc) * Lp, s1 = min(off[a + 1], s0 + Lp);
+        dd sx{0.0, 0.0}, se{0.0, 0.0};
+        u32 pos = 0, neg = 0;
+        for (int i = s0 + lane; i < s1; i += 64) {
+            const double x = scc_val_of(key[i]);
+            sx = dd_add_d(sx, x);
+            se = dd_add_d(se, expm1(x));
+            pos += (x > 0.0);
+            neg += (x < 0.0);
+        }
+        sx = dd_wave_sum(sx);
+        se = dd_wave_sum(se);
+        pos = u32_wave_sum(pos);
+        neg = u32_wave_sum(neg);
+        if (lane == 0) item[it] = StatItem{sx.hi, sx.lo, se.hi, se.lo, pos, neg};
+    }
+    __syncthreads();
+    if (tid < K) {
+        const int a = tid;
+        int first = 0;
+        for (int b = 0; b < a; ++b) first += (off[b + 1] - off[b] + Lp - 1) / Lp;
+        const int ni = (off[a + 1] - off[a] + Lp - 1) / Lp;
+        dd sx{0.0, 0.0}, se{0.0, 0.0};
+        u32 pos = 0, neg = 0;
+        for (int q = first; q < first + ni; ++q) {
+            sx = dd_add(sx, dd{item[q].sx_hi, item[q].sx_lo});
+            se = dd_add(se, dd{item[q].se_hi, item[q].se_lo});
+            pos += item[q].pos;
+            neg += item[q].neg;
+        }
+        const double na = (double)A.n_clu[a];
+        A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
+        A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
+        A.cnt_pos[(size_t)a * A.G + g] = pos;
+        A.cnt_neg[(size_t)a * A.G + g] = neg;
+    }
+}
+
+extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st)
+{
+    if (L->G <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gene_stats, dim3(L->G), dim3(ST_T), 0, st, *L);
+    return hipGetLastError();
+}
+
+// ===================================================================== classify
+// counts: [0] small items, [1] medium items, [2] global-memory items, [3] split genes
+__global__ void k_rank_classify(ScRankLaunch A)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= A.G) return;
+    const i64 base = A.gstart[g];
+    const i64 n = A.gstart[g + 1] - base;
+    if (n <= 0) return;
+    if (!A.all_pairs) {
+        bool any = false;
+        for (int p = 0; p < A.P && !any; ++p) any = (A.flags[(size_t)p * A.G + g] & 1) != 0;
+        if (!any) return;
+    }
+    if (n > A.cap_m) {
+        const int s = atomicAdd(&A.counts[3], 1);
+        A.split_genes[s] = g;
+        return;
+    }
+    const int cls = (n <= A.cap_s) ? 0 : 1;
+    const int s = atomicAdd(&A.counts[cls], 1);
+    A.items[(size_t)cls * A.item_cap + s] = ScRankItem{base, (int)n, g, 0};
+}
+
+extern "C" hipError_t scc_launch_rank_classify(const ScRankLaunch* L, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_rank_classify, dim3((L->G + 255) / 256), dim3(256), 0, st, *L);
+    return hipGetLastError();
+}
+
+// ===================================================================== radix
+// LDS block state of the radix passes (W waves)
+template <int W>
+struct RadixLds {
     u32 hist[W * 256];
     u32 dtot[256 + W];
-    u32 whist[W * 64];
-    u32 posc[64], negc[64];
-    u64 F[64];
-    int off[65];
-    StatItem item[64 + W];
-    int run_s[RK_RUNS], run_l[RK_RUNS];
-    int nruns, flag, redo, pad;
-    u64 kmin, kmax;
 };
 
-// One stable LSD pass on digit (key[id] - kmin) >> shift & 255: in -> out.
-// Each wave owns a contiguous range; per-(wave, digit) offsets; inside a
-// 64-element tile, equal digits are ranked by lane order (match by ballots).
-template <int T, class KP, class IX>
-__device__ void radix_pass(KP key, u64 kmin, int shift, const IX* in, IX* out, int n, RankSmall<T>& L)
+// One stable LSD pass of the digit dig(id) (< 2^BITS, BITS <= 8): in -> out.
+// Each wave owns a contiguous range and per-(wave, digit) counters; inside a
+// 64-element tile equal digits are ranked by lane (match by ballots), so one
+// leader lane per distinct digit touches the counter: no LDS atomic ever
+// conflicts.  Two tiles are in flight per wave; the returning adds of the
+// scatter execute in tile order, which keeps the pass stable.
+template <int W, int BITS, class IX, class DIG>
+__device__ void radix_pass(DIG dig, const IX* in, IX* out, int n, RadixLds<W>& L)
 {
-    constexpr int W = T / 64;
+    constexpr int U = 2;
     const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
     const int R = (((n + W - 1) / W) + 63) & ~63;
     const int lo = min(n, w * R), hi = min(n, lo + R);
     u32* hw = L.hist + w * 256;
     for (int d = lane; d < 256; d += 64) hw[d] = 0;
-    for (int i = lo + lane; i < hi; i += 64) {
-        const u32 d = (u32)((key[in[i]] - kmin) >> shift) & 255u;
-        atomicAdd(&hw[d], 1u);
+    __builtin_amdgcn_wave_barrier();
+    for (int i0 = lo; i0 < hi; i0 += 64 * U) {
+        u32 d[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + 64 * u + lane;
+            ok[u] = i < hi;
+            d[u] = ok[u] ? dig(in[i]) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 peers = match_bits<BITS>(d[u], __ballot(ok[u]));
+            if (ok[u] && lanes_below(peers) == 0)
+                __hip_atomic_fetch_add(&hw[d[u]], (u32)__popcll(peers), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
     }
     __syncthreads();
     u32 tot = 0, incl = 0;
     if (tid < 256) {
+        u32 c[W];
+#pragma unroll
+        for (int v = 0; v < W; ++v) c[v] = L.hist[v * 256 + tid];
         u32 s = 0;
+#pragma unroll
         for (int v = 0; v < W; ++v) {
-            const u32 c = L.hist[v * 256 + tid];
             L.hist[v * 256 + tid] = s;
-            s += c;
+            s += c[v];
         }
         tot = s;
         incl = s;
@@ -135,228 +240,341 @@ __device__ void radix_pass(KP key, u64 kmin, int shift, const IX* in, IX* out, i
             const u32 y = __shfl_up(incl, o, 64);
             if (lane >= o) incl += y;
         }
-        if (lane == 63) L.dtot[256 + w] = incl;
+        if (lane == 63) L.dtot[256 + (tid >> 6)] = incl;
     }
     __syncthreads();
     if (tid < 256) {
         u32 base = incl - tot;
-        for (int v = 0; v < w; ++v) base += L.dtot[256 + v];
+        for (int v = 0; v < (tid >> 6); ++v) base += L.dtot[256 + v];
+#pragma unroll
         for (int v = 0; v < W; ++v) L.hist[v * 256 + tid] += base;
     }
     __syncthreads();
-    for (int i0 = lo; i0 < hi; i0 += 64) {
-        const int i = i0 + lane;
-        const bool ok = i < hi;
-        const IX id = ok ? in[i] : (IX)0;
-        const u32 d = ok ? ((u32)((key[id] - kmin) >> shift) & 255u) : 0u;
-        u64 peers = __ballot(ok);
+    for (int i0 = lo; i0 < hi; i0 += 64 * U) {
+        u32 d[U];
+        IX id[U];
+        bool ok[U];
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const u64 bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + 64 * u + lane;
+            ok[u] = i < hi;
+            id[u] = ok[u] ? in[i] : (IX)0;
+            d[u] = ok[u] ? dig(id[u]) : 0u;
         }
-        if (ok) {
-            const u32 rank = lanes_below(peers);
-            const u32 base = hw[d];
-            out[base + rank] = id;
-            if (rank == 0) hw[d] = base + (u32)__popcll(peers);
+        u32 b[U], rank[U];
+        int leader[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u64 peers = match_bits<BITS>(d[u], __ballot(ok[u]));
+            rank[u] = lanes_below(peers);
+            leader[u] = __builtin_ctzll(peers ? peers : 1ull);
+            b[u] = 0;
+            if (ok[u] && rank[u] == 0)
+                b[u] = __hip_atomic_fetch_add(&hw[d[u]], (u32)__popcll(peers), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32 bb = (u32)__shfl((int)b[u], leader[u], 64);
+            if (ok[u]) out[bb + rank[u]] = id[u];
         }
     }
     __syncthreads();
 }
 
-// exact order of one mixed run (length <= 64) by (key, index): one wave
+// exact order of one mixed run (length <= 64) by (key, cluster, index): one wave
 template <class KP, class IX>
-__device__ void wave_sort_run(KP key, IX* ix, int s, int len)
+__device__ void wave_sort_run(KP key, const u8* code, IX* ix, int s, int len)
 {
     const int lane = threadIdx.x & 63;
     u64 k = ~0ull;
-    u32 id = 0x80000000u + lane;
+    u32 id = 0xffffffffu;
     if (lane < len) {
         id = (u32)ix[s + lane];
         k = key[id];
     }
+    // secondary key: cluster code above the index (ties of equal doubles keep cluster order)
+    u64 k2 = (lane < len) ? (((u64)code[id] << 32) | id) : ~0ull;
     for (int size = 2; size <= 64; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             const u64 ok = shfl_xor_u64(k, stride);
-            const u32 oid = __shfl_xor(id, stride, 64);
+            const u64 ok2 = shfl_xor_u64(k2, stride);
             const bool up = (lane & size) == 0 || size == 64;
             const bool lower = (lane & stride) == 0;
-            const bool other_less = (ok < k) || (ok == k && oid < id);
+            const bool other_less = (ok < k) || (ok == k && ok2 < k2);
             const bool take = (lower == up) ? other_less : !other_less;
             if (take) {
                 k = ok;
-                id = oid;
+                k2 = ok2;
             }
         }
     }
-    if (lane < len) ix[s + lane] = (IX)id;
+    if (lane < len) ix[s + lane] = (IX)(u32)k2;
 }
 
-template <int T, bool BIG>
-__global__ void __launch_bounds__(T) k_gene_rank(RankArgs A, int cap)
+// ===================================================================== item
+#define RK_RUNS 256
+
+template <int W>
+struct ItemLds {
+    RadixLds<W> rx;
+    u32 m[64];         // nonzeros per cluster in this item
+    u32 po[65];        // position-list offsets
+    u64 F[64];         // per-cluster tie term
+    u64 red64[2 * W];  // min / max keys
+    u32 redu[W + 1];
+    int run_s[RK_RUNS], run_l[RK_RUNS];
+    int nruns, flag, redo, anytie;
+    int ntp, nchunk;
+    u64 kmin, kmax;
+    // tested pairs: packed (p | a << 16 | b << 22 | small-is-b << 28), chunk prefix
+    u32 tp[1];  // dynamic tail: tp[ntp_max], cp[ntp_max + 1], eacc[ntp_max], xacc[ntp_max] (u64),
+                // pmap[K * K] (u16: tested-pair slot + 1, 0 = untested)
+};
+
+__device__ inline int tp_p(u32 v) { return (int)(v & 0xffffu); }
+__device__ inline int tp_a(u32 v) { return (int)((v >> 16) & 63u); }
+__device__ inline int tp_b(u32 v) { return (int)((v >> 22) & 63u); }
+__device__ inline bool tp_sb(u32 v) { return ((v >> 28) & 1u) != 0; }
+
+// lower_bound of x in the ascending array s[0..len)
+template <class IX>
+__device__ inline u32 lower_bound_ix(const IX* s, u32 len, u32 x)
 {
-    using IX = typename std::conditional<BIG, u32, unsigned short>::type;
-    using ST = typename std::conditional<BIG, u64, u32>::type;
-    constexpr int W = T / 64;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if ((int)blockIdx.x >= *A.list_count) return;
-    const int g = A.gene_list[blockIdx.x];
-    const int K = A.K, tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
-    STAMP(A, 0);
-    RankSmall<T>& L = *(RankSmall<T>*)smem;
-    u64* const EX = (u64*)(smem + sizeof(RankSmall<T>));  // tie terms E[K][K], X[K][K]
-    ST* S = (ST*)(smem + sizeof(RankSmall<T>) + 16 * (size_t)K * K);
-    char* big = (char*)S + ((sizeof(ST) * K * K + 15) & ~(size_t)15);
-    const i64 base = A.gstart[g];
-    const int n = (int)(A.gstart[g + 1] - base);
-    const u64* gkey = A.keys + base;
-    u64* lkey = (u64*)big;
-    IX* ix0;
-    IX* ix1;
-    u8* uc;
-    u8* sc;
-    if (BIG) {
-        ix0 = (IX*)(A.gix + base);
-        ix1 = (IX*)(A.gix + A.nnz + base);
-        uc = A.guc + base;
-        sc = A.gsc + base;
-    } else {
-        ix0 = (IX*)(lkey + cap);
-        ix1 = ix0 + cap;
-        uc = (u8*)(ix1 + cap);
-        sc = uc + cap;
+    u32 lo = 0;
+    while (len > 0) {
+        const u32 half = len >> 1;
+        const bool lt = (u32)s[lo + half] < x;
+        lo = lt ? lo + half + 1 : lo;
+        len = lt ? len - half - 1 : half;
     }
-    const u64* key = BIG ? gkey : (const u64*)lkey;
-    for (int i = tid; i < K * K; i += T) S[i] = 0;
-    for (int i = tid; i < 2 * K * K; i += T) EX[i] = 0;
-    for (int i = tid; i < W * K; i += T) L.whist[i] = 0;
-    for (int i = tid; i < K; i += T) L.F[i] = 0;
-    if (tid <= K) L.off[tid] = (int)A.coff[(size_t)A.cl_cc[tid] * A.G + g];
+    return lo;
+}
+
+// GLOBALMEM: every per-element array lives in HBM scratch (items too large
+// for LDS); otherwise the key window, indices, codes and sorted codes are in
+// LDS and the 64-bit keys stay in registers / L2.  KPT: keys per thread held
+// in registers during the setup (LDS items: cap <= KPT * T).
+template <int T, bool GLOBALMEM, int KPT>
+__device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int item_no, char* smem)
+{
+    constexpr int W = T / 64;
+    using IX = typename std::conditional<GLOBALMEM, u32, unsigned short>::type;
+    const int K = A.K, P = A.P, G = A.G, g = it.gene, n = it.n;
+    const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    ItemLds<W>& L = *(ItemLds<W>*)smem;
+    u32* tp = L.tp;
+    u32* cp = tp + A.ntp_max;
+    u64* eacc = (u64*)(((uintptr_t)(cp + A.ntp_max + 1) + 7) & ~(uintptr_t)7);
+    u64* xacc = eacc + A.ntp_max;
+    unsigned short* pmap = (unsigned short*)(xacc + A.ntp_max);
+    char* big = (char*)(pmap + K * K);
+    big = (char*)(((uintptr_t)big + 15) & ~(uintptr_t)15);
+    u64* const stamps = A.stamps ? A.stamps + (size_t)item_no * 8 : nullptr;
+#define ISTAMP(ph)                                                                   \
+    do {                                                                             \
+        if (stamps && threadIdx.x == 0) stamps[ph] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+    ISTAMP(0);
+    // ---- per-element arrays
+    const u64* key = (it.src ? A.keys2 : A.keys) + it.base;  // HBM / L2
+    u32* win;
+    u8 *code, *sc;
+    IX *ix0, *ix1;
+    if (GLOBALMEM) {
+        win = A.gwin + it.base;
+        code = it.src ? (A.codes2 + it.base) : (A.gcode + it.base);
+        sc = A.gsc + it.base;
+        ix0 = (IX*)(A.gix + it.base);
+        ix1 = (IX*)(A.gix + A.nnz + it.base);
+    } else {
+        win = (u32*)big;
+        ix0 = (IX*)(win + A.cap_lds);
+        ix1 = ix0 + A.cap_lds;
+        code = (u8*)(ix1 + A.cap_lds);
+        sc = code + A.cap_lds;
+    }
+    // ---- setup: every global read issued before the first barrier
+    int off_r = 0;
+    if (it.src == 0 && tid <= K) off_r = (int)A.coff[(size_t)A.cl_cc[tid] * G + g];
+    u64 kr[KPT];
+    u64 kmn = ~0ull, kmx = 0;
+    if (!GLOBALMEM) {
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const int i = u * T + tid;
+            kr[u] = (i < n) ? key[i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            if (u * T + tid < n) {
+                kmn = kr[u] < kmn ? kr[u] : kmn;
+                kmx = kr[u] > kmx ? kr[u] : kmx;
+            }
+        }
+    } else {
+        for (int i = tid; i < n; i += T) {
+            const u64 k = key[i];
+            kmn = k < kmn ? k : kmn;
+            kmx = k > kmx ? k : kmx;
+        }
+    }
+    for (int m2 = 32; m2 >= 1; m2 >>= 1) {
+        const u64 o1 = shfl_xor_u64(kmn, m2), o2 = shfl_xor_u64(kmx, m2);
+        kmn = o1 < kmn ? o1 : kmn;
+        kmx = o2 > kmx ? o2 : kmx;
+    }
+    if (tid < 64) {
+        L.m[tid] = 0;
+        L.F[tid] = 0;
+    }
+    for (int i = tid; i < K * K; i += T) pmap[i] = 0;
+    if (lane == 0) {
+        L.red64[w] = kmn;
+        L.red64[W + w] = kmx;
+    }
     if (tid == 0) {
         L.nruns = 0;
         L.flag = 0;
         L.redo = 0;
+        L.anytie = 0;
     }
-    if (!BIG)
-        for (int i = tid; i < n; i += T) lkey[i] = gkey[i];
-    __syncthreads();
-    STAMP(A, 1);
-    // ---- 1. statistics over balanced cluster pieces
-    const int Lp = max(64, (((n + W - 1) / W) + 63) & ~63);
-    for (int it = w;; it += W) {
-        int a = 0, acc = 0, ni = 0;
-        for (; a < K; ++a) {
-            const int len = L.off[a + 1] - L.off[a];
-            ni = (len + Lp - 1) / Lp;
-            if (it < acc + ni) break;
-            acc += ni;
+    int* off = (int*)L.po;  // cluster offsets of a gene segment, until the position offsets exist
+    if (it.src == 0 && tid <= K) off[tid] = off_r;
+    // tested pairs of this gene, compacted in pair order (all of them in SLOW / test-all)
+    {
+        u32 basep = 0;
+        for (int p0 = 0; p0 < P; p0 += T) {
+            const int p = p0 + tid;
+            const bool t = p < P && (A.all_pairs || (A.flags[(size_t)p * G + g] & 1));
+            const u64 bal = __ballot(t);
+            if (lane == 0) L.redu[w] = (u32)__popcll(bal);
+            __syncthreads();
+            u32 o = basep;
+            for (int v = 0; v < w; ++v) o += L.redu[v];
+            if (t) tp[o + lanes_below(bal)] = (u32)p;
+            for (int v = 0; v < W; ++v) basep += L.redu[v];
+            __syncthreads();
         }
-        if (a == K) break;
-        const int s0 = L.off[a] + (it - acc) * Lp, s1 = min(L.off[a + 1], s0 + Lp);
-        dd sx{0.0, 0.0}, se{0.0, 0.0};
-        u32 pos = 0, neg = 0;
-        u64 kmn = ~0ull, kmx = 0;
-        for (int i = s0 + lane; i < s1; i += 64) {
-            const u64 kk = key[i];
-            uc[i] = (u8)a;
-            const double x = scc_val_of(kk);
-            sx = dd_add_d(sx, x);
-            se = dd_add_d(se, expm1(x));
-            pos += (x > 0.0);
-            neg += (x < 0.0);
-            kmn = kk < kmn ? kk : kmn;
-            kmx = kk > kmx ? kk : kmx;
-        }
-        sx = dd_wave_sum(sx);
-        se = dd_wave_sum(se);
-        pos = u32_wave_sum(pos);
-        neg = u32_wave_sum(neg);
-        for (int m = 32; m >= 1; m >>= 1) {
-            const u64 o1 = shfl_xor_u64(kmn, m), o2 = shfl_xor_u64(kmx, m);
-            kmn = o1 < kmn ? o1 : kmn;
-            kmx = o2 > kmx ? o2 : kmx;
-        }
-        if (lane == 0) {
-            StatItem& I = L.item[it];
-            I.sx_hi = sx.hi;
-            I.sx_lo = sx.lo;
-            I.se_hi = se.hi;
-            I.se_lo = se.lo;
-            I.pos = pos;
-            I.neg = neg;
-            I.kmin = kmn;
-            I.kmax = kmx;
-        }
+        if (tid == 0) L.ntp = (int)basep;
     }
-    __syncthreads();
-    if (tid < K) {  // combine the pieces of cluster a in order
-        const int a = tid;
-        int first = 0;
-        for (int b = 0; b < a; ++b) first += (L.off[b + 1] - L.off[b] + Lp - 1) / Lp;
-        const int ni = (L.off[a + 1] - L.off[a] + Lp - 1) / Lp;
-        dd sx{0.0, 0.0}, se{0.0, 0.0};
-        u32 pos = 0, neg = 0;
-        for (int q = first; q < first + ni; ++q) {
-            sx = dd_add(sx, dd{L.item[q].sx_hi, L.item[q].sx_lo});
-            se = dd_add(se, dd{L.item[q].se_hi, L.item[q].se_lo});
-            pos += L.item[q].pos;
-            neg += L.item[q].neg;
-        }
-        const double na = (double)A.n_clu[a];
-        A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
-        A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
-        A.cnt_pos[(size_t)a * A.G + g] = pos;
-        L.posc[a] = pos;
-        L.negc[a] = neg;
+    // key range -> 32-bit window of (key - kmin)
+    kmn = L.red64[0];
+    kmx = L.red64[W];
+    for (int v = 1; v < W; ++v) {
+        kmn = L.red64[v] < kmn ? L.red64[v] : kmn;
+        kmx = L.red64[W + v] > kmx ? L.red64[W + v] : kmx;
     }
-    if (tid == 0) {
-        int nit = 0;
-        for (int b = 0; b < K; ++b) nit += (L.off[b + 1] - L.off[b] + Lp - 1) / Lp;
-        u64 kmn = ~0ull, kmx = 0;
-        for (int q = 0; q < nit; ++q) {
-            kmn = L.item[q].kmin < kmn ? L.item[q].kmin : kmn;
-            kmx = L.item[q].kmax > kmx ? L.item[q].kmax : kmx;
-        }
-        L.kmin = kmn;
-        L.kmax = kmx;
-    }
-    for (int i = tid; i < n; i += T) ix0[i] = (IX)i;
-    __syncthreads();
-    STAMP(A, 2);
-    // ---- 2. stable radix sort of the index permutation
-    const u64 kmin = L.kmin;
-    const u64 range = (n > 0) ? L.kmax - kmin : 0;
+    const u64 kmin = kmn, kmax = kmx;
+    const u64 range = kmax - kmin;
     const int bits = range ? 64 - __clzll((long long)range) : 0;
     const int sh = bits > 32 ? bits - 32 : 0;
+    if (!GLOBALMEM) {
+#pragma unroll
+        for (int u = 0; u < KPT; ++u) {
+            const int i = u * T + tid;
+            if (i < n) win[i] = (u32)((kr[u] - kmin) >> sh);
+        }
+    } else {
+        for (int i = tid; i < n; i += T) win[i] = (u32)((key[i] - kmin) >> sh);
+    }
+    if (it.src == 0) {  // the ingest's cluster-grouped gene segment: codes from the offsets
+        for (int a = 0; a < K; ++a) {
+            const int s0 = off[a], s1 = off[a + 1];
+            if (tid == 0) L.m[a] = (u32)(s1 - s0);
+            for (int i = s0 + tid; i < s1; i += T) code[i] = (u8)a;
+        }
+    } else {
+        for (int i0 = 0; i0 < n; i0 += T) {  // bucket: codes and cluster counts
+            const int i = i0 + tid;
+            const bool ok = i < n;
+            const u32 c = ok ? A.codes2[it.base + i] : 0u;
+            if (ok && !GLOBALMEM) code[i] = (u8)c;
+            const u64 peers = match_bits<6>(c, __ballot(ok));
+            if (ok && lanes_below(peers) == 0) atomicAdd(&L.m[c], (u32)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // pack (pair, a, b, smaller side) and chunk the smaller side by 64
+        u32 c = 0;
+        for (int j = 0; j < L.ntp; ++j) {
+            int a2, b2;
+            pair_decode((int)tp[j], K, a2, b2);
+            const u32 ma = L.m[a2], mb = L.m[b2];
+            const bool sb = mb < ma;
+            tp[j] = tp[j] | ((u32)a2 << 16) | ((u32)b2 << 22) | ((u32)sb << 28);
+            pmap[a2 * K + b2] = (unsigned short)(j + 1);
+            eacc[j] = 0;
+            xacc[j] = 0;
+            cp[j] = c;
+            c += ((sb ? mb : ma) + 63) / 64;
+        }
+        cp[L.ntp] = c;
+        L.nchunk = (int)c;
+        u32 s2 = 0;
+        for (int a3 = 0; a3 < K; ++a3) {
+            L.po[a3] = s2;
+            s2 += L.m[a3];
+        }
+        L.po[K] = s2;
+    }
+    __syncthreads();
+    const int ntp = L.ntp;
+    ISTAMP(1);
+    if (kmin == kmax) {
+        // one distinct value: every pair is a tie, no order needed
+        if (tid < K) {
+            const u64 c = L.m[tid];
+            if (c >= 2) atomicAdd((unsigned long long*)&A.accF[(size_t)tid * G + g], (unsigned long long)f_tie(c));
+        }
+        for (int j = tid; j < ntp; j += T) {
+            const u32 v = tp[j];
+            const u64 ca = L.m[tp_a(v)], cb = L.m[tp_b(v)];
+            if (ca && cb) {
+                atomicAdd((unsigned long long*)&A.accE[(size_t)tp_p(v) * G + g], (unsigned long long)(ca * cb));
+                atomicAdd((unsigned long long*)&A.accX[(size_t)tp_p(v) * G + g],
+                          (unsigned long long)(ca * cb * (ca + cb)));
+            }
+        }
+        return;
+    }
+    // ---- stable sort by (value, cluster) on the 32-bit window
+    for (int i = tid; i < n; i += T) ix0[i] = (IX)i;
+    __syncthreads();
     IX* in = ix0;
     IX* out = ix1;
-    for (int p = 0; sh + 8 * p < bits; ++p) {
-        radix_pass<T>(key, kmin, sh + 8 * p, in, out, n, L);
+    if (it.src != 0) {  // bucket input is not cluster-grouped: stable pass on the cluster first
+        radix_pass<W, 6>([&](IX id) { return (u32)code[id]; }, in, out, n, L.rx);
         IX* t = in;
         in = out;
         out = t;
     }
+    const int wbits = bits - sh;
+    for (int p = 0; 8 * p < wbits; ++p) {
+        const int s = 8 * p;
+        radix_pass<W, 8>([&](IX id) { return (win[id] >> s) & 255u; }, in, out, n, L.rx);
+        IX* t = in;
+        in = out;
+        out = t;
+    }
+    ISTAMP(2);
     if (sh > 0) {  // exact fix-up of windows that merged distinct doubles
         for (int i = tid; i + 1 < n; i += T) {
-            const u64 k0 = key[in[i]], k1 = key[in[i + 1]];
-            if (k0 != k1 && ((k0 - kmin) >> sh) == ((k1 - kmin) >> sh)) L.flag = 1;
+            const IX i0 = in[i], i1 = in[i + 1];
+            if (win[i0] == win[i1] && key[i0] != key[i1]) L.flag = 1;
         }
         __syncthreads();
         if (L.flag) {
             for (int i = tid; i < n; i += T) {
-                const u64 k0 = key[in[i]];
-                const u64 w0 = (k0 - kmin) >> sh;
-                const bool start = (i == 0 || ((key[in[i - 1]] - kmin) >> sh) != w0) && i + 1 < n &&
-                                   ((key[in[i + 1]] - kmin) >> sh) == w0;
+                const u32 w0 = win[in[i]];
+                const bool start = (i == 0 || win[in[i - 1]] != w0) && i + 1 < n && win[in[i + 1]] == w0;
                 if (!start) continue;
+                const u64 k0 = key[in[i]];
                 int e = i + 1;
                 bool mixed = false;
-                while (e < n) {
-                    const u64 ke = key[in[e]];
-                    if (((ke - kmin) >> sh) != w0) break;
-                    mixed |= ke != k0;
+                while (e < n && win[in[e]] == w0) {
+                    mixed |= key[in[e]] != k0;
                     ++e;
                 }
                 if (!mixed) continue;
@@ -373,208 +591,452 @@ __global__ void __launch_bounds__(T) k_gene_rank(RankArgs A, int cap)
                 }
             }
             __syncthreads();
-            if (L.redo) {  // pathological: exact sort on every bit
-                for (int i = tid; i < n; i += T) ix0[i] = (IX)i;
-                __syncthreads();
-                in = ix0;
-                out = ix1;
+            if (L.redo) {  // pathological: exact LSD sort on every key bit (equal keys keep their order)
                 for (int p = 0; 8 * p < bits; ++p) {
-                    radix_pass<T>(key, kmin, 8 * p, in, out, n, L);
+                    const int s = 8 * p;
+                    radix_pass<W, 8>([&](IX id) { return (u32)((key[id] - kmin) >> s) & 255u; }, in, out, n, L.rx);
                     IX* t = in;
                     in = out;
                     out = t;
                 }
             } else {
-                for (int r = w; r < L.nruns; r += W) wave_sort_run(key, in, L.run_s[r], L.run_l[r]);
+                // a mixed run holds one window: sort it exactly on (key, cluster, index)
+                for (int r = w; r < L.nruns; r += W) wave_sort_run(key, code, in, L.run_s[r], L.run_l[r]);
                 __syncthreads();
             }
         }
     }
-    // sorted codes; bit 7: equal to the next element (tie group continues)
+    // sorted codes; bit 7: equal to the next element (a tie group continues)
+    bool tie = false;
     for (int i = tid; i < n; i += T) {
         const IX id = in[i];
-        const u64 k0 = key[id];
-        const bool eqn = (i + 1 < n) && key[in[i + 1]] == k0;
-        sc[i] = (u8)(uc[id] | (eqn ? 128 : 0));
+        bool eqn = false;
+        if (i + 1 < n) {
+            const IX id1 = in[i + 1];
+            eqn = win[id1] == win[id] && (sh == 0 || key[id1] == key[id]);
+        }
+        tie |= eqn;
+        sc[i] = (u8)(code[id] | (eqn ? 128 : 0));
     }
+    if (__ballot(tie) && lane == 0) L.anytie = 1;
     __syncthreads();
-    STAMP(A, 6);
-    // ---- 3+4. sweep.  Wave w walks its chunk in order; lane b holds C_b = #b
-    // before the element and G_b = #b before it inside its tie group.  At an
-    // element of code a:  S[a][b] += C_b;  for b < a in the same group
-    // E[b][a] += G_b, X[b][a] += G_b (2 G_a + 1 + G_b);  F_a += 3 G_a (G_a + 1).
-    // Summed over a group these are c_a c_b, c_a c_b (c_a + c_b), c^3 - c.
-    const int ch = (n + W - 1) / W;
-    const int c0 = min(n, w * ch), c1 = min(n, c0 + ch);
-    for (int i = c0 + lane; i < c1; i += 64) atomicAdd(&L.whist[w * K + (sc[i] & 63)], 1u);
-    __syncthreads();
-    STAMP(A, 3);
+    ISTAMP(3);
+    // ---- positions partitioned by cluster (stable: ascending inside a cluster)
+    IX* pl = out;  // the free index buffer
     {
-        u32 C = 0, Gc = 0;
-        u64 Facc = 0;
-        if (lane < K)
-            for (int v = 0; v < w; ++v) C += L.whist[v * K + lane];
-        bool peq = false;
-        if (c0 < c1 && c0 > 0 && (sc[c0 - 1] & 128)) {  // a tie group runs into this chunk
-            peq = true;
-            for (int j = c0 - 1; j >= 0; --j) {
-                const int v = sc[j];
-                if (j < c0 - 1 && !(v & 128)) break;
-                Gc += ((v & 63) == lane);
+        const int R = (((n + W - 1) / W) + 63) & ~63;
+        const int lo = min(n, w * R), hi = min(n, lo + R);
+        u32* hw = L.rx.hist + w * 256;
+        for (int d = lane; d < 64; d += 64) hw[d] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (int i0 = lo; i0 < hi; i0 += 64) {
+            const int i = i0 + lane;
+            const bool ok = i < hi;
+            const u32 d = ok ? (sc[i] & 63u) : 0u;
+            const u64 peers = match_bits<6>(d, __ballot(ok));
+            if (ok && lanes_below(peers) == 0) hw[d] += (u32)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        if (tid < 64) {  // per-(wave, cluster) start offsets
+            u32 s = (tid < K) ? L.po[tid] : 0u;
+            for (int v = 0; v < W; ++v) {
+                const u32 c = L.rx.hist[v * 256 + tid];
+                L.rx.hist[v * 256 + tid] = s;
+                s += c;
             }
         }
-        u64* E = EX;
-        u64* X = EX + K * K;
-        if (K <= 32) {
-            u32 acc[32];
-#pragma unroll
-            for (int q = 0; q < 32; ++q) acc[q] = 0;
-            for (int i0 = c0; i0 < c1; i0 += 64) {
-                const int cv = (i0 + lane < c1) ? (int)sc[i0 + lane] : 0;
-                const int cnt = __builtin_amdgcn_readfirstlane(min(64, c1 - i0));
-                for (int j = 0; j < cnt; ++j) {
-                    const int v = __builtin_amdgcn_readlane(cv, j);
-                    const int a = v & 63;
-                    if (!peq) {
-                        Gc = 0;
-                    } else {
-                        const u32 Ga = __builtin_amdgcn_readlane(Gc, a);
-                        if (lane < a && Gc) {
-                            atomicAdd((unsigned long long*)&E[lane * K + a], (unsigned long long)Gc);
-                            atomicAdd((unsigned long long*)&X[lane * K + a],
-                                      (unsigned long long)Gc * (2ull * Ga + 1ull + Gc));
-                        }
-                    }
-                    const bool me = lane == a;
-                    Facc += me ? 3ull * Gc * (Gc + 1ull) : 0ull;
-                    acc[a & 31] += C;
-                    C += me;
-                    Gc += me;
-                    peq = (v & 128) != 0;
-                }
+        __syncthreads();
+        for (int i0 = lo; i0 < hi; i0 += 64) {
+            const int i = i0 + lane;
+            const bool ok = i < hi;
+            const u32 d = ok ? (sc[i] & 63u) : 0u;
+            const u64 peers = match_bits<6>(d, __ballot(ok));
+            if (ok) {
+                const u32 rank = lanes_below(peers);
+                const u32 b = hw[d];
+                pl[b + rank] = (IX)i;
+                if (rank == 0) hw[d] = b + (u32)__popcll(peers);
             }
-            if (lane < K)
-                for (int q = 0; q < lane; ++q) atomicAdd(&S[q * K + lane], (ST)acc[q]);
-        } else {
-            for (int i0 = c0; i0 < c1; i0 += 64) {
-                const int cv = (i0 + lane < c1) ? (int)sc[i0 + lane] : 0;
-                const int cnt = __builtin_amdgcn_readfirstlane(min(64, c1 - i0));
-                for (int j = 0; j < cnt; ++j) {
-                    const int v = __builtin_amdgcn_readlane(cv, j);
-                    const int a = v & 63;
-                    if (!peq) {
-                        Gc = 0;
-                    } else {
-                        const u32 Ga = __builtin_amdgcn_readlane(Gc, a);
-                        if (lane < a && Gc) {
-                            atomicAdd((unsigned long long*)&E[lane * K + a], (unsigned long long)Gc);
-                            atomicAdd((unsigned long long*)&X[lane * K + a],
-                                      (unsigned long long)Gc * (2ull * Ga + 1ull + Gc));
-                        }
-                    }
-                    const bool me = lane == a;
-                    Facc += me ? 3ull * Gc * (Gc + 1ull) : 0ull;
-                    if (lane > a && lane < K) atomicAdd(&S[a * K + lane], (ST)C);
-                    C += me;
-                    Gc += me;
-                    peq = (v & 128) != 0;
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+    }
+    ISTAMP(4);
+    // ---- within-item S_ab for every tested pair: the smaller cluster's
+    // positions binary-searched in the larger one's (positions are distinct)
+    {
+        const int nch = L.nchunk;
+        int cur = -1;
+        u64 acc = 0;
+        for (int c = w; c < nch; c += W) {
+            int lo = 0, hi = ntp;  // last j with cp[j] <= c (wave-uniform)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if ((int)cp[mid] <= c) lo = mid;
+                else hi = mid;
+            }
+            const int j = lo;
+            if (j != cur) {
+                if (cur >= 0) {
+                    const u64 s = u64_wave_sum(acc);
+                    if (lane == 0 && s)
+                        atomicAdd((unsigned long long*)&A.accS[(size_t)tp_p(tp[cur]) * G + g], (unsigned long long)s);
+                }
+                cur = j;
+                acc = 0;
+            }
+            const u32 v = tp[j];
+            const int a = tp_a(v), b = tp_b(v);
+            const bool sb = tp_sb(v);
+            const int s = sb ? b : a, lg = sb ? a : b;
+            const u32 ms = L.m[s];
+            const u32 e = (u32)(c - (int)cp[j]) * 64u + (u32)lane;
+            const u32 mlg = L.m[lg];
+            const IX* lst = pl + L.po[lg];
+            u32 x = 0;
+            if (e < ms) x = (u32)pl[L.po[s] + e];
+            const u32 lb = lower_bound_ix(lst, mlg, x);
+            if (e < ms) acc += sb ? (u64)(mlg - lb) : (u64)lb;
+        }
+        if (cur >= 0) {
+            const u64 s = u64_wave_sum(acc);
+            if (lane == 0 && s)
+                atomicAdd((unsigned long long*)&A.accS[(size_t)tp_p(tp[cur]) * G + g], (unsigned long long)s);
+        }
+    }
+    ISTAMP(5);
+    // ---- tie groups: runs of equal (value, cluster) inside groups of equal value
+    if (L.anytie) {
+        IX* rs = in;  // sorted order no longer needed: run starts
+        // run start flags -> exclusive scan (per-thread contiguous chunks)
+        const int chunk = (n + T - 1) / T;
+        const int c0 = min(n, tid * chunk), c1 = min(n, c0 + chunk);
+        u32 cnt = 0;
+        for (int i = c0; i < c1; ++i) {
+            const bool st = (i == 0) || !(sc[i - 1] & 128) || ((sc[i - 1] & 63) != (sc[i] & 63));
+            cnt += st;
+        }
+        u32 incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.redu[w] = incl;
+        __syncthreads();
+        u32 basev = incl - cnt;
+        for (int v = 0; v < w; ++v) basev += L.redu[v];
+        if (tid == T - 1) L.redu[W] = basev + cnt;  // number of runs
+        __syncthreads();
+        const u32 nr = L.redu[W];
+        // rs aliases the sorted-order buffer that is no longer read; the
+        // starts are written after every thread finished reading it above
+        for (int i = c0; i < c1; ++i) {
+            const bool st = (i == 0) || !(sc[i - 1] & 128) || ((sc[i - 1] & 63) != (sc[i] & 63));
+            if (st) rs[basev++] = (IX)i;
+        }
+        if (tid == 0) rs[nr] = (IX)n;
+        __syncthreads();
+        for (u32 r = tid; r < nr; r += T) {
+            const u32 s0 = rs[r], len = (u32)rs[r + 1] - s0;
+            const int a = sc[s0] & 63;
+            if (len >= 2) atomicAdd((unsigned long long*)&L.F[a], (unsigned long long)f_tie(len));
+            // earlier runs of the same value: their clusters are smaller (codes
+            // increase inside a group), each gives a cross-cluster tie block
+            u32 q = r;
+            while (q > 0 && (sc[(u32)rs[q] - 1] & 128)) {
+                --q;
+                const u32 ps = rs[q];
+                const u64 lb = (u32)rs[q + 1] - ps, la = len;
+                const int b = sc[ps] & 63;  // b < a
+                const int slot = pmap[b * K + a];
+                if (slot) {
+                    atomicAdd((unsigned long long*)&eacc[slot - 1], (unsigned long long)(la * lb));
+                    atomicAdd((unsigned long long*)&xacc[slot - 1], (unsigned long long)(la * lb * (la + lb)));
                 }
             }
         }
-        if (lane < K && Facc) atomicAdd((unsigned long long*)&L.F[lane], (unsigned long long)Facc);
+        __syncthreads();
+        if (tid < K && L.F[tid])
+            atomicAdd((unsigned long long*)&A.accF[(size_t)tid * G + g], (unsigned long long)L.F[tid]);
+        for (int j = tid; j < ntp; j += T) {
+            const int pp = tp_p(tp[j]);
+            if (eacc[j]) atomicAdd((unsigned long long*)&A.accE[(size_t)pp * G + g], (unsigned long long)eacc[j]);
+            if (xacc[j]) atomicAdd((unsigned long long*)&A.accX[(size_t)pp * G + g], (unsigned long long)xacc[j]);
+        }
+    }
+    ISTAMP(6);
+#undef ISTAMP
+}
+
+template <int T, bool GLOBALMEM, int KPT>
+__global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int cnt = A.counts[cls];
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const ScRankItem it = A.items[(size_t)cls * A.item_cap + i];
+        rank_one_item<T, GLOBALMEM, KPT>(A, it, i + A.stamp_base[cls], smem);
+        __syncthreads();
+    }
+}
+
+// ===================================================================== split
+#define SP_T 1024
+#define SP_W (SP_T / 64)
+#define SP_BINS 2048
+#define SP_BMAX 512
+
+struct SplitLds {
+    u32 hist[SP_BINS];
+    u32 excl[SP_BINS];
+    u32 bid[SP_BINS];   // bucket of each bin
+    u32 bcur[SP_BMAX];  // bucket cursors
+    u32 boff[SP_BMAX + 1];
+    u32 wsum[SP_W + 1];
+    u32 wsum2[SP_W + 1];
+    u64 rmn[SP_W], rmx[SP_W];
+    int off[65];
+    int nb;
+    u32 hb[1];  // [SP_BMAX][K] per-bucket cluster counts (dynamic)
+};
+
+__device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
+{
+    const int K = A.K, G = A.G;
+    const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    const i64 base = A.gstart[g];
+    const int n = (int)(A.gstart[g + 1] - base);
+    const u64* key = A.keys + base;
+    if (tid <= K) L.off[tid] = (int)A.coff[(size_t)A.cl_cc[tid] * G + g];
+    for (int i = tid; i < SP_BINS; i += SP_T) L.hist[i] = 0;
+    for (int i = tid; i < SP_BMAX * K; i += SP_T) L.hb[i] = 0;
+    // key range of the gene (min / max over its nonzeros)
+    u64 kmn = ~0ull, kmx = 0;
+    for (int i = tid; i < n; i += SP_T) {
+        const u64 k = key[i];
+        kmn = k < kmn ? k : kmn;
+        kmx = k > kmx ? k : kmx;
+    }
+    for (int m2 = 32; m2 >= 1; m2 >>= 1) {
+        const u64 o1 = shfl_xor_u64(kmn, m2), o2 = shfl_xor_u64(kmx, m2);
+        kmn = o1 < kmn ? o1 : kmn;
+        kmx = o2 > kmx ? o2 : kmx;
+    }
+    if (lane == 0) {
+        L.rmn[w] = kmn;
+        L.rmx[w] = kmx;
     }
     __syncthreads();
-    STAMP(A, 4);
-    // ---- 5. per pair outputs: exact 2U and tie term
-    for (int p = tid; p < A.P; p += T) {
-        int a, b;
-        pair_decode(p, K, a, b);
-        const u64 za = (u64)A.n_clu[a] - L.posc[a] - L.negc[a];
-        const u64 zb = (u64)A.n_clu[b] - L.posc[b] - L.negc[b];
-        const u64 s = (u64)S[a * K + b] + za * L.negc[b] + (u64)L.posc[a] * zb;  // S^pos + zero-group pairs
-        const u64 u2 = 2 * s + za * zb + EX[a * K + b];
-        const u64 t = L.F[a] + f_tie(za) + L.F[b] + f_tie(zb) + 3 * za * zb * (za + zb) + 3 * EX[K * K + a * K + b];
-        A.u2_base[(size_t)p * A.G + g] = (i64)u2;
-        A.t_base[(size_t)p * A.G + g] = (i64)t;
+    kmn = L.rmn[0];
+    kmx = L.rmx[0];
+    for (int v = 1; v < SP_W; ++v) {
+        kmn = L.rmn[v] < kmn ? L.rmn[v] : kmn;
+        kmx = L.rmx[v] > kmx ? L.rmx[v] : kmx;
     }
-    STAMP(A, 5);
+    const u64 range = kmx - kmn;
+    const int bits = range ? 64 - __clzll((long long)range) : 0;
+    const int sh = bits > 11 ? bits - 11 : 0;
+    // ---- 1. histogram of the top 11 bits of the key window
+    for (int i0 = 0; i0 < n; i0 += SP_T) {
+        const int i = i0 + tid;
+        const bool ok = i < n;
+        const u32 d = ok ? (u32)((key[i] - kmn) >> sh) : 0u;
+        const u64 peers = match_bits<11>(d, __ballot(ok));
+        if (ok && lanes_below(peers) == 0) atomicAdd(&L.hist[d], (u32)__popcll(peers));
+    }
+    __syncthreads();
+    // ---- 2. exclusive scan of the bins (2 per thread)
+    {
+        const u32 h0 = L.hist[2 * tid], h1 = L.hist[2 * tid + 1];
+        const u32 v = h0 + h1;
+        u32 incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.wsum[w] = incl;
+        __syncthreads();
+        u32 b = incl - v;
+        for (int q = 0; q < w; ++q) b += L.wsum[q];
+        L.excl[2 * tid] = b;
+        L.excl[2 * tid + 1] = b + h0;
+    }
+    __syncthreads();
+    // ---- 3. buckets: runs of bins with equal floor(excl / target); a bin of
+    // more than `target` elements is a bucket of its own.  Buckets hold at most
+    // 2 target elements (unless one bin alone is larger), and there are at most
+    // 1 + 3 n / target of them (<= SP_BMAX by the choice of target).
+    const u32 target = max((u32)A.bucket_target, (u32)((3 * (i64)n + SP_BMAX - 3) / (SP_BMAX - 2)));
+    {
+        u32 st[2];
+        for (int q = 0; q < 2; ++q) {
+            const int d = 2 * tid + q;
+            const bool fat = L.hist[d] > target;
+            const bool pfat = d > 0 && L.hist[d - 1] > target;
+            st[q] = (d == 0) || fat || pfat || (L.excl[d] / target != L.excl[d - 1] / target);
+        }
+        const u32 v = st[0] + st[1];
+        u32 incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.wsum2[w] = incl;
+        __syncthreads();
+        u32 b = incl - v;
+        for (int q = 0; q < w; ++q) b += L.wsum2[q];
+        // bucket id = number of starts up to and including this bin, minus 1
+        L.bid[2 * tid] = b + st[0] - 1;
+        L.bid[2 * tid + 1] = b + st[0] + st[1] - 1;
+        if (st[0]) L.boff[b] = L.excl[2 * tid];
+        if (st[1]) L.boff[b + st[0]] = L.excl[2 * tid + 1];
+        if (tid == SP_T - 1) {
+            L.nb = (int)(b + v);
+            L.boff[b + v] = (u32)n;
+        }
+    }
+    __syncthreads();
+    const int nb = L.nb;
+    for (int q = tid; q < nb; q += SP_T) L.bcur[q] = L.boff[q];
+    __syncthreads();
+    // ---- 4. scatter into bucket order (keys2 / codes2 over the gene's own
+    // range), per-bucket cluster counts
+    int a = 0;
+    for (int i0 = 0; i0 < n; i0 += SP_T) {
+        const int i = i0 + tid;
+        const bool ok = i < n;
+        u64 k = 0;
+        u32 d = 0;
+        if (ok) {
+            k = key[i];
+            d = (u32)((k - kmn) >> sh);
+            while (a + 1 < K && L.off[a + 1] <= i) ++a;
+        }
+        const u32 c = (u32)a;
+        const u64 peers = match_bits<11>(d, __ballot(ok));
+        const u32 bk = ok ? L.bid[d] : 0u;
+        const u32 rank = lanes_below(peers);
+        const int leader = __builtin_ctzll(peers ? peers : 1ull);
+        u32 basev = 0;
+        if (ok && rank == 0) basev = atomicAdd(&L.bcur[bk], (u32)__popcll(peers));
+        basev = __shfl(basev, leader, 64);
+        if (ok) {
+            A.keys2[base + basev + rank] = k;
+            A.codes2[base + basev + rank] = (u8)c;
+        }
+        const u64 pc = match_bits<6>(c, peers);  // same bucket and cluster
+        if (ok && lanes_below(pc) == 0) atomicAdd(&L.hb[(size_t)bk * K + c], (u32)__popcll(pc));
+    }
+    __syncthreads();
+    // ---- 5. cross-bucket rank sums of the tested pairs: sum over buckets of
+    // h_beta[a] * #(b-elements in lower buckets)
+    for (int p = tid; p < A.P; p += SP_T) {
+        if (!A.all_pairs && !(A.flags[(size_t)p * G + g] & 1)) continue;
+        int pa, pb;
+        pair_decode(p, K, pa, pb);
+        u64 s = 0, below = 0;
+        for (int q = 0; q < nb; ++q) {
+            s += (u64)L.hb[(size_t)q * K + pa] * below;
+            below += L.hb[(size_t)q * K + pb];
+        }
+        if (s) atomicAdd((unsigned long long*)&A.accS[(size_t)p * G + g], (unsigned long long)s);
+    }
+    // ---- 6. one work item per non-empty bucket
+    for (int q = tid; q < nb; q += SP_T) {
+        const int c = (int)(L.boff[q + 1] - L.boff[q]);
+        if (c <= 0) continue;
+        const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
+        const int s = atomicAdd(&A.counts[cls], 1);
+        A.items[(size_t)cls * A.item_cap + s] = ScRankItem{base + L.boff[q], c, g, 1};
+    }
+    __syncthreads();
 }
 
-// bytes of LDS for class cls at capacity cap (0: 256 threads, 1: 1024, 2: 1024 HBM-resident)
-__host__ inline size_t rank_lds_bytes(int cls, int cap, int K)
+__global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
 {
-    const size_t small = (cls == 0) ? sizeof(RankSmall<256>) : sizeof(RankSmall<1024>);
-    const size_t s = 16 * (size_t)K * K + (((size_t)K * K * (cls == 2 ? 8 : 4) + 15) & ~(size_t)15);
-    const size_t per = (cls == 2) ? 0 : (8 + 2 * 2 + 1 + 1);
-    return small + s + per * (size_t)cap;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    SplitLds& L = *(SplitLds*)smem;
+    const int cnt = A.counts[3];
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) split_one_gene(A, A.split_genes[i], L);
 }
 
-// Size classes: 0 small (n <= cap_s), 1 medium (n <= cap_m), 2 big.
-__global__ void k_classify(const i64* __restrict__ gstart, int G, int cap_s, int cap_m, int* lists, int* counts)
+// ===================================================================== host
+template <int W>
+static size_t item_lds_fixed(int ntp_max, int K)
 {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= G) return;
-    const i64 n = gstart[g + 1] - gstart[g];
-    const int cls = (n <= cap_s) ? 0 : ((n <= cap_m) ? 1 : 2);
-    const int slot = atomicAdd(&counts[cls], 1);
-    lists[(size_t)cls * G + slot] = g;
+    size_t s = sizeof(ItemLds<W>) + sizeof(u32) * (2 * (size_t)ntp_max + 1) + 8 + 16 * (size_t)ntp_max +
+               2 * (size_t)K * K;
+    return (s + 31) & ~(size_t)15;
 }
 
-extern "C" hipError_t scc_launch_classify(const i64* gstart, int G, int cap_s, int cap_m, int* lists, int* counts,
-                                          hipStream_t st)
+#define RK_T0 256   // small items
+#define RK_T1 512   // medium items (two workgroups per CU)
+#define RK_T1W 1024 // medium items, wide variant (one workgroup per CU)
+#define RK_T2 1024  // HBM-resident items
+
+extern "C" size_t scc_rank_item_lds(int cls, int cap, int ntp_max, int K)
 {
-    hipLaunchKernelGGL(k_classify, dim3((G + 255) / 256), dim3(256), 0, st, gstart, G, cap_s, cap_m, lists, counts);
-    return hipGetLastError();
+    if (cls == 0) return item_lds_fixed<RK_T0 / 64>(ntp_max, K) + (size_t)cap * (4 + 2 + 2 + 1 + 1);
+    if (cls == 1) return item_lds_fixed<RK_T1 / 64>(ntp_max, K) + (size_t)cap * (4 + 2 + 2 + 1 + 1);
+    if (cls == 3) return item_lds_fixed<RK_T1W / 64>(ntp_max, K) + (size_t)cap * (4 + 2 + 2 + 1 + 1);
+    return item_lds_fixed<RK_T2 / 64>(ntp_max, K);
 }
 
-// largest LDS-resident capacity of class cls (0, 1) that fits the CU
-extern "C" int scc_rank_cap(int cls, int want, int K)
+// largest LDS-resident item capacity (multiple of 64) of class cls within lim bytes
+#define RK_KPT0 8   // cap_s <= 8 * 256
+#define RK_KPT1 8  // cap_m <= 8 * 512
+
+extern "C" int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim)
 {
-    const size_t lim = 160 * 1024;
-    int cap = want;
-    while (cap > 64 && rank_lds_bytes(cls, cap, K) > lim) cap -= 64;
-    if (cap > 65535) cap = 65535;  // u16 indices
+    int cap = want & ~63;
+    if (cls == 0 && cap > RK_KPT0 * RK_T0) cap = RK_KPT0 * RK_T0;
+    if (cls == 1 && cap > RK_KPT1 * RK_T1) cap = RK_KPT1 * RK_T1;
+    if (cls == 3 && cap > RK_KPT1 * RK_T1W) cap = RK_KPT1 * RK_T1W;
+    while (cap > 64 && scc_rank_item_lds(cls, cap, ntp_max, K) > (size_t)lim) cap -= 64;
+    if (cap > 65535) cap = 65535 & ~63;
     return cap;
 }
 
-extern "C" size_t scc_rank_lds_bytes(int cls, int cap, int K) { return rank_lds_bytes(cls, cap, K); }
+extern "C" size_t scc_rank_split_lds(int K) { return sizeof(SplitLds) + sizeof(u32) * (size_t)SP_BMAX * K; }
 
-extern "C" hipError_t scc_launch_gene_rank(int cls, const ScRankLaunch* L, hipStream_t st)
+extern "C" hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st)
 {
-    RankArgs A;
-    A.gene_list = L->gene_list;
-    A.list_count = L->list_count;
-    A.gstart = L->gstart;
-    A.keys = L->keys;
-    A.G = L->G;
-    A.K = L->K;
-    A.P = L->K * (L->K - 1) / 2;
-    A.n_clu = L->n_clu;
-    A.coff = L->coff;
-    A.cl_cc = L->cl_cc;
-    A.mean_x = L->mean_x;
-    A.mean_e = L->mean_e;
-    A.cnt_pos = L->cnt_pos;
-    A.u2_base = L->u2_base;
-    A.t_base = L->t_base;
-    A.gix = L->gix;
-    A.guc = L->guc;
-    A.gsc = L->gsc;
-    A.nnz = L->nnz;
-    A.stamps = L->stamps;
-    const int grid = L->grid;
     if (grid <= 0) return hipSuccess;
-    const size_t lds = rank_lds_bytes(cls, L->cap, L->K);
+    const size_t lds = scc_rank_split_lds(L->K);
+    hipFuncSetAttribute((const void*)k_rank_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_rank_split, dim3(grid), dim3(SP_T), lds, st, *L);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st)
+{
+    if (grid <= 0) return hipSuccess;
+    ScRankLaunch A = *L;
     if (cls == 0) {
-        hipFuncSetAttribute((const void*)k_gene_rank<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_gene_rank<256, false>), dim3(grid), dim3(256), lds, st, A, L->cap);
-    } else if (cls == 1) {
-        hipFuncSetAttribute((const void*)k_gene_rank<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        A.cap_lds = L->cap_s;
+        const size_t lds = scc_rank_item_lds(0, L->cap_s, L->ntp_max, L->K);
+        hipFuncSetAttribute((const void*)k_rank_item<RK_T0, false, RK_KPT0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
-        hipLaunchKernelGGL((k_gene_rank<1024, false>), dim3(grid), dim3(1024), lds, st, A, L->cap);
+        hipLaunchKernelGGL((k_rank_item<RK_T0, false, RK_KPT0>), dim3(grid), dim3(RK_T0), lds, st, A, 0);
+    } else if (cls == 1 && L->med_wide) {
+        A.cap_lds = L->cap_m;
+        const size_t lds = scc_rank_item_lds(3, L->cap_m, L->ntp_max, L->K);
+        hipFuncSetAttribute((const void*)k_rank_item<RK_T1W, false, RK_KPT1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_rank_item<RK_T1W, false, RK_KPT1>), dim3(grid / 2), dim3(RK_T1W), lds, st, A, 1);
+    } else if (cls == 1) {
+        A.cap_lds = L->cap_m;
+        const size_t lds = scc_rank_item_lds(1, L->cap_m, L->ntp_max, L->K);
+        hipFuncSetAttribute((const void*)k_rank_item<RK_T1, false, RK_KPT1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        hipLaunchKernelGGL((k_rank_item<RK_T1, false, RK_KPT1>), dim3(grid), dim3(RK_T1), lds, st, A, 1);
     } else {
-        hipFuncSetAttribute((const void*)k_gene_rank<1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_gene_rank<1024, true>), dim3(grid), dim3(1024), lds, st, A, L->cap);
+        A.cap_lds = 0;
+        const size_t lds = scc_rank_item_lds(2, 0, L->ntp_max, L->K);
+        hipFuncSetAttribute((const void*)k_rank_item<RK_T2, true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+        hipLaunchKernelGGL((k_rank_item<RK_T2, true, 1>), dim3(grid), dim3(RK_T2), lds, st, A, 2);
     }
     return hipGetLastError();
 }

@@ -35,6 +35,10 @@ extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
         delete c;
         return SCC_ERR_HIP;
     }
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) {
+        hipGetLastError();
+        c->n_cu = 256;
+    }
     *out = c;
     return SCC_OK;
 }
@@ -257,15 +261,17 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     H.insert(H.end(), nclu.begin(), nclu.end());
 
     int rc;
-    int *d_tab, *d_nodg, *d_lists, *d_counts, *d_err, *d_tested, *d_union, *d_nu;
-    uint32_t *d_cnt, *d_cntpos, *d_gix;
+    int *d_tab, *d_nodg, *d_splitg, *d_counts, *d_err, *d_tested, *d_union, *d_nu;
+    uint32_t *d_cnt, *d_cntpos, *d_cntneg, *d_gix, *d_gwin;
     long long *d_gstart, *d_scan, *d_rowoff, *d_bnd;
     unsigned long long* d_keys;
-    uint8_t *d_guc, *d_gsc;
+    uint8_t *d_gcode, *d_gsc, *d_codes2;
+    unsigned long long *d_keys2, *d_acc;
+    ScRankItem* d_items;
     dd* d_wexp;
     dd* d_gexp;
     double *d_mx, *d_me;
-    long long *d_u2b, *d_tb, *d_u2, *d_t;
+    long long *d_u2, *d_t;
     unsigned long long* d_first;
     double *d_p, *d_lfc, *d_pct1, *d_pct2;
     uint8_t* d_flags;
@@ -283,22 +289,40 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     WS("scan", scc_scan_scratch_blocks(G) + 1, d_scan);
     WS("keys", nnz1, d_keys);
     WS("gix", 2 * (size_t)nnz1, d_gix);
-    WS("guc", nnz1, d_guc);
+    WS("gcode", nnz1, d_gcode);
+    WS("gwin", nnz1, d_gwin);
     WS("gsc", nnz1, d_gsc);
+    WS("keys2", nnz1, d_keys2);
+    WS("codes2", nnz1, d_codes2);
     {
         void* p;
         if ((rc = ws_get(c, "wexp", sizeof(double) * 2 * (nwaves + 1), &p))) return rc;
         d_wexp = (dd*)p;
         d_gexp = (dd*)((char*)p + sizeof(double) * 2 * nwaves);
     }
-    WS("lists", 3 * (size_t)G, d_lists);
+    WS("splitg", (size_t)G, d_splitg);
     WS("counts", 4, d_counts);
     WS("err", 4, d_err);
     WS("mx", GK, d_mx);
     WS("me", GK, d_me);
     WS("cntpos", GK, d_cntpos);
-    WS("u2b", PG, d_u2b);
-    WS("tb", PG, d_tb);
+    WS("cntneg", GK, d_cntneg);
+    // rank accumulators: S, E, X per (pair, gene), F per (cluster, gene)
+    const size_t acc_n = 3 * PG + (size_t)GK;
+    WS("acc", acc_n, d_acc);
+    // rank work items (LDS capacities depend on the tested-pair list size)
+    const bool all_pairs = !fast || prm->test_all;
+    const int ntp_max = P;
+    // small items: 4 workgroups per CU; medium: 2 per CU (LDS budget per workgroup)
+    const int cap_s = scc_rank_item_cap(0, env_int("SCC_CAP_SMALL", kCapSmall), ntp_max, K, 40 * 1024);
+    const int med_wide = env_int("SCC_RANK_WIDE", 0);
+    const int cap_m = std::max(cap_s, med_wide ? scc_rank_item_cap(3, env_int("SCC_CAP_MEDIUM", kCapMedium), ntp_max, K,
+                                                                   160 * 1024)
+                                               : scc_rank_item_cap(1, env_int("SCC_CAP_MEDIUM", kCapMedium), ntp_max, K,
+                                                                   80 * 1024));
+    const int bucket_target = std::max(64, cap_m / 2);
+    const int item_cap = G + (int)std::min<int64_t>(3 * nnz1 / bucket_target + 2 * (int64_t)G + 64, 1 << 28);
+    WS("items", 3 * (size_t)item_cap, d_items);
     WS("p", PG, d_p);
     WS("lfc", PG, d_lfc);
     WS("pct1", fast ? PG : 1, d_pct1);
@@ -336,84 +360,23 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         if (!fast) HIPCHK(c, scc_launch_reduce_dd(d_wexp, nwaves, d_gexp, s0));
     }
     {
-        Scope sc(c, "gene_rank", s0);
-        // size classes (env overrides exist to exercise the HBM-resident path on small test data)
-        const int cap_s = scc_rank_cap(0, env_int("SCC_CAP_SMALL", kCapSmall), K);
-        const int cap_m = std::max(cap_s, scc_rank_cap(1, env_int("SCC_CAP_MEDIUM", kCapMedium), K));
-        HIPCHK(c, scc_launch_classify(d_gstart, G, cap_s, cap_m, d_lists, d_counts, s0));
-        HIPCHK(c, hipEventRecord(c->ev_fork, s0));
-        HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
-        ScRankLaunch L{};
-        L.gstart = d_gstart;
-        L.keys = d_keys;
-        L.G = G;
-        L.K = K;
-        L.n_clu = d_nclu;
-        L.coff = d_cnt;
-        L.cl_cc = d_clcc;
-        L.gix = d_gix;
-        L.guc = d_guc;
-        L.gsc = d_gsc;
-        L.nnz = nnz1;
-        L.mean_x = d_mx;
-        L.mean_e = d_me;
-        L.cnt_pos = d_cntpos;
-        L.u2_base = d_u2b;
-        L.t_base = d_tb;
-        L.grid = G;
-        unsigned long long* st_buf = nullptr;
-        const bool stamps = env_int("SCC_STAMPS", 0) != 0;
-        if (stamps) {
-            WS("d_rstamps", (size_t)3 * G * 8, st_buf);
-            HIPCHK(c, hipMemsetAsync(st_buf, 0, sizeof(unsigned long long) * 3 * G * 8, s0));
-        }
-        // big genes first on the side stream
-        L.gene_list = d_lists + 2 * (size_t)G;
-        L.list_count = d_counts + 2;
-        L.cap = 0;
-        L.stamps = stamps ? st_buf + (size_t)2 * G * 8 : nullptr;
-        HIPCHK(c, scc_launch_gene_rank(2, &L, s1));
-        L.gene_list = d_lists + (size_t)G;
-        L.list_count = d_counts + 1;
-        L.cap = cap_m;
-        L.stamps = stamps ? st_buf + (size_t)G * 8 : nullptr;
-        HIPCHK(c, scc_launch_gene_rank(1, &L, s0));
-        L.gene_list = d_lists;
-        L.list_count = d_counts;
-        L.cap = cap_s;
-        L.stamps = stamps ? st_buf : nullptr;
-        HIPCHK(c, scc_launch_gene_rank(0, &L, s0));
-        HIPCHK(c, hipEventRecord(c->ev_join, s1));
-        HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
-        if (stamps) {
-            std::vector<unsigned long long> h((size_t)3 * G * 8);
-            int cnts[4];
-            HIPCHK(c, hipMemcpyAsync(h.data(), st_buf, h.size() * 8, hipMemcpyDeviceToHost, s0));
-            HIPCHK(c, hipMemcpyAsync(cnts, d_counts, sizeof(cnts), hipMemcpyDeviceToHost, s0));
-            HIPCHK(c, hipStreamSynchronize(s0));
-            const char* ph[] = {"load", "stats", "sort", "hist", "sweep+ties", "final"};
-            for (int cls = 0; cls < 3; ++cls) {
-                double acc[6] = {0, 0, 0, 0, 0, 0};
-                int nb = 0;
-                for (int b = 0; b < cnts[cls]; ++b) {
-                    const unsigned long long* t = &h[((size_t)cls * G + b) * 8];
-                    if (!t[0] || !t[5]) continue;
-                    acc[0] += (double)(t[1] - t[0]);
-                    acc[1] += (double)(t[2] - t[1]);
-                    acc[2] += (double)(t[6] - t[2]);
-                    acc[3] += (double)(t[3] - t[6]);
-                    acc[4] += (double)(t[4] - t[3]);
-                    acc[5] += (double)(t[5] - t[4]);
-                    ++nb;
-                }
-                fprintf(stderr, "[scc stamps] rank class %d: %d genes, mean cycles:", cls, nb);
-                for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.0f", ph[q], nb ? acc[q] / nb : 0.0);
-                fprintf(stderr, "\n");
-            }
-        }
+        Scope sc(c, "gene_stats", s0);
+        ScStatsLaunch S{};
+        S.gstart = d_gstart;
+        S.keys = d_keys;
+        S.G = G;
+        S.K = K;
+        S.n_clu = d_nclu;
+        S.coff = d_cnt;
+        S.cl_cc = d_clcc;
+        S.mean_x = d_mx;
+        S.mean_e = d_me;
+        S.cnt_pos = d_cntpos;
+        S.cnt_neg = d_cntneg;
+        HIPCHK(c, scc_launch_gene_stats(&S, s0));
     }
-    // SLOW: log(meanScalingFactor * mean(expm1(X))) on device would need one
-    // more kernel; it is a scalar, read back together with the union below.
+    // SLOW: log(meanScalingFactor * mean(expm1(X))) (slow:36) gates the pair
+    // filter; a scalar read back here.
     double log_thr = 0.0;
     if (!fast) {
         double gx[2];
@@ -426,31 +389,120 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         const double mean = q + r / tot;
         log_thr = std::log(prm->mean_scaling_factor * mean);
     }
+    unsigned long long* accS = d_acc;
+    unsigned long long* accE = d_acc + PG;
+    unsigned long long* accX = d_acc + 2 * PG;
+    unsigned long long* accF = d_acc + 3 * PG;
+    ScTestLaunch T{};
+    T.K = K;
+    T.G = G;
+    T.P = P;
+    T.mode = prm->mode;
+    T.min_pct = prm->min_per_cent;
+    T.lfc_thr = prm->log_fc_thrs;
+    T.log_thr = log_thr;
+    T.n_clu = d_nclu;
+    T.mean_x = d_mx;
+    T.mean_e = d_me;
+    T.cnt_pos = d_cntpos;
+    T.cnt_neg = d_cntneg;
+    T.accS = accS;
+    T.accE = accE;
+    T.accX = accX;
+    T.accF = accF;
+    T.all_pairs = all_pairs ? 1 : 0;
+    T.wtab = c->d_wtab;
+    T.woff = c->d_woff;
+    T.out_p = d_p;
+    T.out_lfc = d_lfc;
+    T.out_pct1 = d_pct1;
+    T.out_pct2 = d_pct2;
+    T.out_u2 = d_u2;
+    T.out_t = d_t;
+    T.out_flags = d_flags;
+    {
+        Scope sc(c, "pair_filter", s0);
+        HIPCHK(c, scc_launch_pair_filter(&T, s0));
+    }
+    {
+        Scope sc(c, "gene_rank", s0);
+        HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
+        ScRankLaunch L{};
+        L.gstart = d_gstart;
+        L.keys = d_keys;
+        L.G = G;
+        L.K = K;
+        L.P = P;
+        L.all_pairs = all_pairs ? 1 : 0;
+        L.coff = d_cnt;
+        L.cl_cc = d_clcc;
+        L.flags = d_flags;
+        L.cap_s = cap_s;
+        L.cap_m = cap_m;
+        L.med_wide = med_wide;
+        L.bucket_target = bucket_target;
+        L.ntp_max = ntp_max;
+        L.item_cap = item_cap;
+        L.items = d_items;
+        L.counts = d_counts;
+        L.split_genes = d_splitg;
+        L.keys2 = d_keys2;
+        L.codes2 = d_codes2;
+        L.gix = d_gix;
+        L.gwin = d_gwin;
+        L.gcode = d_gcode;
+        L.gsc = d_gsc;
+        L.nnz = nnz1;
+        L.accS = accS;
+        L.accE = accE;
+        L.accX = accX;
+        L.accF = accF;
+        unsigned long long* st_buf = nullptr;
+        const bool stamps = env_int("SCC_STAMPS", 0) != 0;
+        if (stamps) {
+            WS("d_rstamps", (size_t)3 * item_cap * 8, st_buf);
+            HIPCHK(c, hipMemsetAsync(st_buf, 0, sizeof(unsigned long long) * 3 * item_cap * 8, s0));
+            L.stamps = st_buf;
+            L.stamp_base[0] = 0;
+            L.stamp_base[1] = item_cap;
+            L.stamp_base[2] = 2 * item_cap;
+        }
+        HIPCHK(c, scc_launch_rank_classify(&L, s0));
+        const int ncu = c->n_cu > 0 ? c->n_cu : 256;
+        HIPCHK(c, scc_launch_rank_split(&L, ncu, s0));
+        // small and medium items share the CUs (two streams), HBM-resident ones last
+        HIPCHK(c, hipEventRecord(c->ev_fork, s0));
+        HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
+        HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, s0));
+        HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, s1));
+        HIPCHK(c, hipEventRecord(c->ev_join, s1));
+        HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
+        HIPCHK(c, scc_launch_rank_items(&L, 2, ncu, s0));
+        if (stamps) {
+            std::vector<unsigned long long> h((size_t)3 * item_cap * 8);
+            int cnts[4];
+            HIPCHK(c, hipMemcpyAsync(h.data(), st_buf, h.size() * 8, hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipMemcpyAsync(cnts, d_counts, sizeof(cnts), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            const char* ph[] = {"setup", "sort", "fixup+codes", "partition", "pairs", "ties"};
+            fprintf(stderr, "[scc stamps] split genes %d\n", cnts[3]);
+            for (int cls = 0; cls < 3; ++cls) {
+                double acc[6] = {0, 0, 0, 0, 0, 0};
+                int nb = 0;
+                for (int b = 0; b < cnts[cls]; ++b) {
+                    const unsigned long long* t = &h[((size_t)cls * item_cap + b) * 8];
+                    if (!t[0] || !t[6]) continue;
+                    for (int q = 0; q < 6; ++q) acc[q] += (double)(t[q + 1] - t[q]);
+                    ++nb;
+                }
+                fprintf(stderr, "[scc stamps] rank class %d: %d items (%d full), mean cycles:", cls, cnts[cls], nb);
+                for (int q = 0; q < 6; ++q) fprintf(stderr, " %s %.0f", ph[q], nb ? acc[q] / nb : 0.0);
+                fprintf(stderr, "\n");
+            }
+        }
+    }
     {
         Scope sc(c, "pair_test", s0);
-        ScTestLaunch T{};
-        T.K = K;
-        T.G = G;
-        T.P = P;
-        T.mode = prm->mode;
-        T.min_pct = prm->min_per_cent;
-        T.lfc_thr = prm->log_fc_thrs;
-        T.log_thr = log_thr;
-        T.n_clu = d_nclu;
-        T.mean_x = d_mx;
-        T.mean_e = d_me;
-        T.cnt_pos = d_cntpos;
-        T.u2_base = d_u2b;
-        T.t_base = d_tb;
-        T.wtab = c->d_wtab;
-        T.woff = c->d_woff;
-        T.out_p = d_p;
-        T.out_lfc = d_lfc;
-        T.out_pct1 = d_pct1;
-        T.out_pct2 = d_pct2;
-        T.out_u2 = d_u2;
-        T.out_t = d_t;
-        T.out_flags = d_flags;
         HIPCHK(c, scc_launch_pair_test(&T, s0));
     }
     // rows (FAST) / per-pair vectors (SLOW)

@@ -111,44 +111,30 @@ __device__ inline double wilcox_p(i64 u2, i64 tie, int nx, int ny, const double*
 }
 
 // -------------------------------------------------------- per (pair, gene)
-struct TestArgs {
-    int K, G, P, mode;
-    double min_pct, lfc_thr, log_thr;  // FAST: minPerCent, logFCThrs; SLOW: log(meanExprsThrs)
-    const int* n_clu;
-    const double* mean_x;
-    const double* mean_e;
-    const u32* cnt_pos;
-    const i64* u2_base;
-    const i64* t_base;
-    const double* wtab;
-    const int* woff;
-    double* out_p;     // [P][G]
-    double* out_lfc;   // [P][G]
-    double* out_pct1;  // [P][G] (FAST)
-    double* out_pct2;
-    i64* out_u2;       // [P][G]
-    i64* out_t;        // [P][G]
-    u8* out_flags;     // [P][G]: bit0 tested, bit1 gate (SLOW), bit2 exact test
-};
+__device__ inline u64 f_tie3(u64 c) { return c * c * c - c; }
 
-__global__ void __launch_bounds__(256) k_pair_test(TestArgs A)
+// Feature filters before the rank stage: FAST keeps only the features
+// ComputePairWiseDE tests (Fast:229-291), so the rank engine never sorts a
+// gene no pair tests; SLOW tests every gene (slow:90) and records the gate.
+// flags bit0 tested, bit1 expression gate (SLOW).
+__global__ void __launch_bounds__(256) k_pair_filter(ScTestLaunch A)
 {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     const int p = blockIdx.y;
     if (g >= A.G) return;
-    int a = 0, rem = p;
-    while (rem >= A.K - 1 - a) {
-        rem -= A.K - 1 - a;
-        ++a;
+    int a, b;
+    {
+        a = 0;
+        int rem = p;
+        while (rem >= A.K - 1 - a) {
+            rem -= A.K - 1 - a;
+            ++a;
+        }
+        b = a + 1 + rem;
     }
-    const int b = a + 1 + rem;
     const size_t pg = (size_t)p * A.G + g;
-    const i64 u2 = A.u2_base[pg];  // exact 2U and tie term from the rank kernel
-    const i64 t = A.t_base[pg];
     const int na = A.n_clu[a], nb = A.n_clu[b];
-    u8 ex = 0;
-    const double pv = wilcox_p(u2, t, na, nb, A.wtab, A.woff, &ex);
-    u8 fl = (u8)(ex << 2);
+    u8 fl = 0;
     double lfc;
     if (A.mode == SCC_DE_FAST) {
         // Fast:230-239  round(100 * rowSums(x > 0) / n, 16): the round is the identity here
@@ -171,11 +157,50 @@ __global__ void __launch_bounds__(256) k_pair_test(TestArgs A)
         fl |= 1;
         if (mi > A.log_thr || mj > A.log_thr) fl |= 2;  // slow:110-113
     }
-    A.out_p[pg] = pv;
     A.out_lfc[pg] = lfc;
-    A.out_u2[pg] = u2;
-    A.out_t[pg] = t;
     A.out_flags[pg] = fl;
+}
+
+// After the rank stage: exact 2U and tie term (the implicit zero group in
+// closed form) and the wilcox.test p-value of every tested (pair, gene).
+// Untested cells (FAST, not requested) carry u2 = t = -1 and p = NaN.
+__global__ void __launch_bounds__(256) k_pair_test(ScTestLaunch A)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = blockIdx.y;
+    if (g >= A.G) return;
+    int a, b;
+    {
+        a = 0;
+        int rem = p;
+        while (rem >= A.K - 1 - a) {
+            rem -= A.K - 1 - a;
+            ++a;
+        }
+        b = a + 1 + rem;
+    }
+    const size_t pg = (size_t)p * A.G + g;
+    u8 fl = A.out_flags[pg];
+    if (!(fl & 1) && !A.all_pairs) {
+        A.out_p[pg] = __longlong_as_double(0x7ff8000000000000ll);
+        A.out_u2[pg] = -1;
+        A.out_t[pg] = -1;
+        return;
+    }
+    const int na = A.n_clu[a], nb = A.n_clu[b];
+    const u64 pa = A.cnt_pos[(size_t)a * A.G + g], ga = A.cnt_neg[(size_t)a * A.G + g];
+    const u64 pb = A.cnt_pos[(size_t)b * A.G + g], gb = A.cnt_neg[(size_t)b * A.G + g];
+    const u64 za = (u64)na - pa - ga, zb = (u64)nb - pb - gb;
+    const u64 S = A.accS[pg] + za * gb + pa * zb;  // x > y, zeros included
+    const u64 u2 = 2 * S + za * zb + A.accE[pg];
+    const u64 t = A.accF[(size_t)a * A.G + g] + A.accF[(size_t)b * A.G + g] + f_tie3(za) + f_tie3(zb) +
+                  3 * za * zb * (za + zb) + 3 * A.accX[pg];
+    u8 ex = 0;
+    const double pv = wilcox_p((i64)u2, (i64)t, na, nb, A.wtab, A.woff, &ex);
+    A.out_p[pg] = pv;
+    A.out_u2[pg] = (i64)u2;
+    A.out_t[pg] = (i64)t;
+    A.out_flags[pg] = (u8)(fl | (ex << 2));
 }
 
 // -------------------------------------------------------- per pair counts
@@ -575,32 +600,15 @@ extern "C" int scc_wilcox_table_layout(int* woff /* WT_DIM*WT_DIM */)
     return o;
 }
 
+extern "C" hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_pair_filter, dim3((L->G + 255) / 256, L->P), dim3(256), 0, st, *L);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t scc_launch_pair_test(const ScTestLaunch* L, hipStream_t st)
 {
-    TestArgs A;
-    A.K = L->K;
-    A.G = L->G;
-    A.P = L->P;
-    A.mode = L->mode;
-    A.min_pct = L->min_pct;
-    A.lfc_thr = L->lfc_thr;
-    A.log_thr = L->log_thr;
-    A.n_clu = L->n_clu;
-    A.mean_x = L->mean_x;
-    A.mean_e = L->mean_e;
-    A.cnt_pos = L->cnt_pos;
-    A.u2_base = L->u2_base;
-    A.t_base = L->t_base;
-    A.wtab = L->wtab;
-    A.woff = L->woff;
-    A.out_p = L->out_p;
-    A.out_lfc = L->out_lfc;
-    A.out_pct1 = L->out_pct1;
-    A.out_pct2 = L->out_pct2;
-    A.out_u2 = L->out_u2;
-    A.out_t = L->out_t;
-    A.out_flags = L->out_flags;
-    hipLaunchKernelGGL(k_pair_test, dim3((L->G + 255) / 256, L->P), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(k_pair_test, dim3((L->G + 255) / 256, L->P), dim3(256), 0, st, *L);
     return hipGetLastError();
 }
 

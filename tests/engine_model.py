@@ -69,54 +69,83 @@ def gene_u2_ties(values, codes, n_clu):
     return u2, tt
 
 
-def gene_u2_ties_sweep(values, codes, n_clu, W=4):
-    """The kernel's actual sweep (scc_rank.hip step 3+4): the sorted array is
-    cut into W wave chunks; each chunk keeps C_b (count of b before) and G_b
-    (count of b before inside the current tie group, recovered by walking back
-    when a group runs into the chunk) and accumulates
-        S[a][b] += C_b, E[b][a] += G_b, X[b][a] += G_b (2 G_a + 1 + G_b)  (b < a),
-        F_a += 3 G_a (G_a + 1)
-    at every element of code a."""
+def _okey(v):
+    """orderable u64 key of a double (scc_common.hpp scc_key_of)."""
+    b = np.asarray(v, np.float64).view(np.uint64)
+    neg = (b >> np.uint64(63)) == 1
+    return np.where(neg, ~b, b | np.uint64(1 << 63))
+
+
+def gene_u2_ties_buckets(values, codes, n_clu, target=8, bins_bits=11):
+    """The kernel pipeline (scc_rank.hip): the nonzeros are cut into value
+    buckets (k_rank_split: 2^bins_bits-bin histogram of the key window, runs
+    of bins with equal floor(excl / target), fat bins alone); the
+    cross-bucket part of S comes from per-bucket cluster histograms; inside a
+    bucket (k_rank_item) the elements are sorted by (value, cluster), the
+    sorted positions are partitioned by cluster, S_ab is the sum of binary
+    searches of the smaller cluster's positions in the larger one's, and the
+    tie statistics come from runs of equal (value, cluster)."""
     values = np.asarray(values, np.float64)
     codes = np.asarray(codes, np.int64)
     K = len(n_clu)
     nz = values != 0
     v, c = values[nz], codes[nz]
-    order = np.lexsort((c, v))
-    v, c = v[order], c[order]
     n = len(v)
-    eqn = np.zeros(n, bool)
-    eqn[:-1] = v[1:] == v[:-1]
     S = np.zeros((K, K), np.int64)
     E = np.zeros((K, K), np.int64)
     X = np.zeros((K, K), np.int64)
     F = np.zeros(K, np.int64)
-    ch = (n + W - 1) // W if n else 0
-    for w in range(W):
-        c0, c1 = min(n, w * ch), min(n, w * ch + ch)
-        C = np.bincount(c[:c0], minlength=K).astype(np.int64)
-        G = np.zeros(K, np.int64)
-        peq = False
-        if c0 < c1 and c0 > 0 and eqn[c0 - 1]:
-            peq = True
-            j = c0 - 1
-            while j >= 0 and (j == c0 - 1 or eqn[j]):
-                G[c[j]] += 1
-                j -= 1
-        for i in range(c0, c1):
-            a = c[i]
-            if not peq:
-                G[:] = 0
-            else:
-                for b in range(a):
-                    if G[b]:
-                        E[b, a] += G[b]
-                        X[b, a] += G[b] * (2 * G[a] + 1 + G[b])
-            F[a] += 3 * G[a] * (G[a] + 1)
-            S[a] += C
-            C[a] += 1
-            G[a] += 1
-            peq = bool(eqn[i])
+    if n:
+        k = _okey(v)
+        kmn, kmx = k.min(), k.max()
+        rng = int(kmx - kmn)
+        bits = rng.bit_length()
+        sh = max(0, bits - bins_bits)
+        d = ((k - kmn) >> np.uint64(sh)).astype(np.int64)
+        nb = 1 << bins_bits
+        hist = np.bincount(d, minlength=nb)
+        excl = np.concatenate([[0], np.cumsum(hist)[:-1]])
+        fat = hist > target
+        start = np.zeros(nb, bool)
+        start[0] = True
+        start[1:] = fat[1:] | fat[:-1] | ((excl[1:] // target) != (excl[:-1] // target))
+        bid = np.cumsum(start) - 1
+        bk = bid[d]
+        nbk = bid[-1] + 1
+        hb = np.zeros((nbk, K), np.int64)
+        np.add.at(hb, (bk, c), 1)
+        for a in range(K):  # cross-bucket: x in a above every y of a lower bucket
+            for b in range(K):
+                below = np.concatenate([[0], np.cumsum(hb[:, b])[:-1]])
+                S[a, b] += int(np.sum(hb[:, a] * below))
+        for q in range(nbk):
+            sel = bk == q
+            vv, cc = v[sel], c[sel]
+            o = np.lexsort((cc, vv))
+            vv, cc = vv[o], cc[o]
+            pl = [np.nonzero(cc == a)[0] for a in range(K)]  # sorted positions by cluster
+            for a in range(K):
+                for b in range(K):
+                    if a == b:
+                        continue
+                    sm, lg = (pl[a], pl[b]) if len(pl[a]) <= len(pl[b]) else (pl[b], pl[a])
+                    lb = np.searchsorted(lg, sm, side="left")
+                    S[a, b] += int(lb.sum()) if sm is pl[a] else int((len(pl[a]) - lb).sum())
+            # runs of equal (value, cluster); groups of equal value
+            m = len(vv)
+            starts = [i for i in range(m) if i == 0 or vv[i] != vv[i - 1] or cc[i] != cc[i - 1]] + [m]
+            for r in range(len(starts) - 1):
+                s0, ln = starts[r], starts[r + 1] - starts[r]
+                a = cc[s0]
+                if ln >= 2:
+                    F[a] += f(ln)
+                q2 = r
+                while q2 > 0 and vv[starts[q2] - 1] == vv[starts[q2]]:
+                    q2 -= 1
+                    ps, lb2 = starts[q2], starts[q2 + 1] - starts[q2]
+                    b = cc[ps]
+                    E[b, a] += ln * lb2
+                    X[b, a] += ln * lb2 * (ln + lb2)
     pos = np.array([np.sum((values > 0) & (codes == a)) for a in range(K)], np.int64)
     neg = np.array([np.sum((values < 0) & (codes == a)) for a in range(K)], np.int64)
     z = np.asarray(n_clu, np.int64) - pos - neg

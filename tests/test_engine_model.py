@@ -46,19 +46,21 @@ def test_count_formula_continuous():
         _check(vals, codes, sizes)
 
 
-@pytest.mark.parametrize("seed", range(6))
-@pytest.mark.parametrize("W", [1, 3, 16])
-def test_sweep_tie_terms_match(seed, W):
-    """Chunked sweep with G-counts (the kernel's tie statistics, including
-    tie groups that straddle wave chunks) == explicit tie-group walk."""
-    from engine_model import gene_u2_ties, gene_u2_ties_sweep
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("target,bits", [(4, 11), (8, 3), (1000, 11), (3, 1)])
+def test_bucketed_engine_matches(seed, target, bits):
+    """Value buckets with cross-bucket histogram terms, per-bucket sorted
+    positions + binary searches, and run-based tie statistics (the kernel
+    pipeline) == the direct count formula, for many bucket shapes (fat bins,
+    single-bin genes, buckets of one distinct value)."""
+    from engine_model import gene_u2_ties, gene_u2_ties_buckets
     rng = np.random.default_rng(seed)
     K = int(rng.integers(2, 7))
-    N = int(rng.integers(5, 120))
+    N = int(rng.integers(5, 150))
     codes = rng.integers(0, K, N)
     codes[:K] = np.arange(K)
     vals = rng.choice([-2.0, -1.0, 0.0, 0.0, 1.0, 1.5, 2.0, 3.0], N) if seed % 2 else np.round(rng.normal(0, 1, N), 1)
     n_clu = np.bincount(codes, minlength=K)
     a = gene_u2_ties(vals, codes, n_clu)
-    b = gene_u2_ties_sweep(vals, codes, n_clu, W)
+    b = gene_u2_ties_buckets(vals, codes, n_clu, target, bits)
     assert a == b
