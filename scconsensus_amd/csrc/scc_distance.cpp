@@ -100,7 +100,17 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
                 for (auto& m : mk) m = ev_take(c);
                 marks = mk;
             }
-            HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, nullptr, marks, s0));
+            unsigned long long* st_buf = nullptr;
+            if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 8, st_buf);
+            int nwg_used = 0;
+            HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, marks, st_buf, s0));
+            if (st_buf) {
+                unsigned long long h[3];
+                HIPCHK(c, hipMemcpyAsync(h, st_buf, sizeof(h), hipMemcpyDeviceToHost, s0));
+                HIPCHK(c, hipStreamSynchronize(s0));
+                fprintf(stderr, "[scc stamps] tridiag n=%d nwg=%d: phase B %llu, hand-off wait %llu, phase C %llu cycles\n",
+                        nu, nwg_used, h[0], h[1], h[2]);
+            }
             if (marks) {
                 c->pending.push_back({"eig_tridiag", mk[0], mk[1]});
                 c->pending.push_back({"eig_vec", mk[2], mk[3]});

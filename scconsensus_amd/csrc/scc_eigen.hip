@@ -14,10 +14,11 @@
 //      so the matrix never goes back to L2/HBM.  One cross-workgroup hand-off
 //      per column: every workgroup publishes tau*A22*v for its rows (and the
 //      owner of the next column publishes that row), then all workgroups
-//      redundantly and deterministically form w and the next reflector.  The
-//      hand-off is write-through (`sc1`) stores + one agent-scope counter add
-//      per workgroup; readers poll the counter and read with `sc1` loads
-//      (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off row).
+//      redundantly and deterministically form w and the next reflector.  Every
+//      handed-off double travels as two 8-byte {half, step tag} granules, each
+//      written by one write-through (`sc1`) store and polled with `sc1` loads
+//      (MI355X_MICROARCH.md price list: data-tagged granules), so a hand-off
+//      costs one store-to-load trip and no counter or fence.
 //   2. k_tri_vectors — one workgroup per wanted eigenpair: multisection on
 //      Sturm counts (256 points per round), inverse iteration with the
 //      partially pivoted LU of T - lambda I (LAPACK dgttrf/dgttrs order),
@@ -33,6 +34,7 @@
 #define TRI_W (TRI_T / 64)
 #define VEC_T 256
 #define VEC_W (VEC_T / 64)
+#define VEC_NJ 8  // back-transform in registers up to n = 512
 #define FIN_T 1024
 #define FIN_W (FIN_T / 64)
 #define EIG_LDS_MAX (160 * 1024)
@@ -59,6 +61,19 @@ __device__ inline void st_sc1(double* p, double v)
     __hip_atomic_store((u64*)p, (u64)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 8-byte granules {32-bit half, 32-bit tag} written by ONE sc1 store each: a
+// double travels as two granules; a reader polls until both tags match
+// (MI355X_MICROARCH.md price list: data-tagged granules, handoff-1to1).
+__device__ inline void put_g(u64* g, double x, u32 tag)
+{
+    const u64 b = (u64)__double_as_longlong(x);
+    const u64 t = (u64)tag << 32;
+    __hip_atomic_store(g, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, t | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline u64 get_g(const u64* g) { return __hip_atomic_load((u64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline double g_val(u64 hi, u64 lo) { return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull))); }
+
 // deterministic block sum over W waves (every thread returns the same value)
 template <int W>
 __device__ inline double block_sum(double v, double* red)
@@ -83,11 +98,12 @@ struct TriArgs {
     double* e;        // [n] off-diagonal (e[i] = T[i+1][i])
     double* tau;      // [n]
     double* refl;     // reflector i in row i: refl[i*lda + j], j >= i+1 (refl[i][i+1] = 1)
-    double* pbuf;     // [2][lda] tau*A22*v of the current column (hand-off)
-    double* rowbuf;   // [2][lda] row i+1 of A^(i-1) (hand-off)
-    double* pdot;     // [2][EIG_MAX_WG] per-workgroup partial of p.v (hand-off)
+    u64* pg;          // [2][2 lda] granules of tau*A22*v of the current column (hand-off)
+    u64* rg;          // [2][2 lda] granules of row i+1 of A^(i-1) (hand-off)
+    u64* dg;          // [2][2 EIG_MAX_WG] granules of each workgroup's partial p.v
     double* work;     // own rows when they do not fit LDS: [nwg][R][n]
-    u32* counter;     // arrivals (monotonic, zeroed before the launch)
+    u32* counter;     // (unused)
+    u64* stamps;      // diagnostic: WG 0 per-phase cycle sums (nullptr normally)
     u32* err;         // 1: a hand-off timed out
 };
 
@@ -123,7 +139,8 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     double* vB = vA + n;       // v_{i-1}, then v_{i+1}
     double* wp = vB + n;       // w_{i-1}, then w_i
     double* y = wp + n;        // hand-off row / scratch
-    double* red = y + n;       // 64
+    double* pp = y + n;        // handed-off p of the current column
+    double* red = pp + n;      // 64
     double* part = red + 64;   // EIG_MAX_WG
     double* rows = a.rows_lds ? (part + EIG_MAX_WG) : (a.work + (size_t)me * R * n);
     const int nown = (me < n) ? (n - me + nwg - 1) / nwg : 0;
@@ -156,12 +173,18 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     }
     double tp = 0.0;  // tau_{i-1}
     __syncthreads();
+    u64 t_b = 0, t_w = 0, t_c = 0, t0 = 0;
+    const bool stmp = a.stamps && me == 0 && tid == 0;
     for (int i = 0; i <= n - 2; ++i) {
         const int par = i & 1;
-        double* pb = a.pbuf + (size_t)par * lda;
-        double* rb = a.rowbuf + (size_t)par * lda;
+        const u32 tag = (u32)(i + 1);
+        if (stmp) t0 = __builtin_amdgcn_s_memtime();
+        u64* pg = a.pg + (size_t)par * 2 * lda;
+        u64* rg = a.rg + (size_t)par * 2 * lda;
+        u64* dg = a.dg + (size_t)par * 2 * EIG_MAX_WG;
         const bool prev = (i >= 1) && (tp != 0.0);
-        // ---- phase B: own rows r >= i+1: apply update i-1, p_r = tau_i A_r. v_i
+        // ---- phase B: own rows r >= i+1: apply update i-1, p_r = tau_i A_r. v_i;
+        // publish p_r (and row i+1 by its owner) as tagged granules
         double pd = 0.0;
         const int l0 = (i + 1 > me) ? (i + 1 - me + nwg - 1) / nwg : 0;
         for (int l = l0 + wv; l < nown; l += TRI_W) {
@@ -176,79 +199,165 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                     x = x - vr * wp[j] - wr * vp[j];
                     row[j] = x;
                 }
-                if (pub) st_sc1(rb + j, x);
+                if (pub) put_g(rg + 2 * j, x, tag);
                 s += x * vc[j];
             }
             s = wave_sum_d(s);
             const double p = tc * s;
             if (lane == 0) {
-                st_sc1(pb + r, p);
+                put_g(pg + 2 * r, p, tag);
                 pd += p * vc[r];
             }
         }
-        if (lane == 0) red[wv] = pd;
+        if (lane == 0) red[32 + wv] = pd;  // (red[0..TRI_W) belongs to block_sum)
         __syncthreads();
         if (tid == 0) {
             double s = 0.0;
-            for (int q = 0; q < TRI_W; ++q) s += red[q];
-            st_sc1(a.pdot + (size_t)par * EIG_MAX_WG + me, s);
+            for (int q = 0; q < TRI_W; ++q) s += red[32 + q];
+            put_g(dg + 2 * me, s, tag);
         }
-        // ---- hand-off: every storing wave drains, one lane signals
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const u32 target = (u32)(i + 1) * (u32)nwg;
+        if (stmp) {
+            const u64 t1 = __builtin_amdgcn_s_memtime();
+            t_b += t1 - t0;
+            t0 = t1;
+        }
+        // ---- phase C (every workgroup, identical arithmetic): poll the granules
+        // of p, row i+1 and the partials, then w_i, row i+1 of A^(i), d[i+1]
+        // and reflector i+1 into the free v buffer
+        {
+            // every granule this thread needs is loaded at once and only the
+            // missing ones are polled again: one store-to-load trip per step
+            constexpr int GJ = 4;
             u32 spins = 0;
-            while (__hip_atomic_load(a.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > EIG_SPIN_LIMIT) {
-                    __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    s_abort = 1;
-                    break;
+            bool bad = false;
+            const bool hasd = tid < nwg;
+            for (int j0 = i + 1; j0 < n || (j0 == i + 1 && hasd); j0 += GJ * TRI_T) {
+                u64 g[GJ][4];
+                u64 gd[2] = {0, 0};
+                bool need[GJ];
+#pragma unroll
+                for (int u = 0; u < GJ; ++u) {
+                    const int j = j0 + u * TRI_T + tid;
+                    need[u] = j < n;
+                    if (need[u]) {
+                        g[u][0] = get_g(pg + 2 * j);
+                        g[u][1] = get_g(pg + 2 * j + 1);
+                        g[u][2] = get_g(rg + 2 * j);
+                        g[u][3] = get_g(rg + 2 * j + 1);
+                    }
                 }
+                const bool wantd = hasd && j0 == i + 1;
+                if (wantd) {
+                    gd[0] = get_g(dg + 2 * tid);
+                    gd[1] = get_g(dg + 2 * tid + 1);
+                }
+                for (;;) {
+                    bool ok = true;
+#pragma unroll
+                    for (int u = 0; u < GJ; ++u) {
+                        if (!need[u]) continue;
+                        const int j = j0 + u * TRI_T + tid;
+#pragma unroll
+                        for (int h = 0; h < 4; ++h) {
+                            if ((u32)(g[u][h] >> 32) != tag) {
+                                ok = false;
+                                g[u][h] = get_g((h < 2 ? pg : rg) + 2 * j + (h & 1));
+                            }
+                        }
+                    }
+                    if (wantd) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            if ((u32)(gd[h] >> 32) != tag) {
+                                ok = false;
+                                gd[h] = get_g(dg + 2 * tid + h);
+                            }
+                        }
+                    }
+                    if (ok) break;
+                    if (++spins > EIG_SPIN_LIMIT) {
+                        bad = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int u = 0; u < GJ; ++u) {
+                    if (!need[u]) continue;
+                    const int j = j0 + u * TRI_T + tid;
+                    pp[j] = g_val(g[u][0], g[u][1]);
+                    y[j] = g_val(g[u][2], g[u][3]);
+                }
+                if (wantd) part[tid] = g_val(gd[0], gd[1]);
+                if (bad) break;
+            }
+            if (bad) {
+                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_abort = 1;
             }
         }
         __syncthreads();
         if (s_abort) return;
-        // ---- phase C (every workgroup, identical arithmetic): w_i, row i+1 of
-        // A^(i), d[i+1], and reflector i+1 into the free v buffer
-        if (tid < nwg) part[tid] = ld_sc1(a.pdot + (size_t)par * EIG_MAX_WG + tid);
-        for (int j = i + 1 + tid; j < n; j += TRI_T) {
-            wp[j] = ld_sc1(pb + j);
-            y[j] = ld_sc1(rb + j);
+        if (stmp) {
+            const u64 t1 = __builtin_amdgcn_s_memtime();
+            t_w += t1 - t0;
+            t0 = t1;
         }
-        __syncthreads();
-        double pdt = 0.0;
-        for (int q = 0; q < nwg; ++q) pdt += part[q];
+        double pdt = 0.0;  // fixed-shape butterfly: identical in every wave of every workgroup
+        for (int q = lane; q < nwg; q += 64) pdt += part[q];
+        pdt = wave_sum_d(pdt);
         const double a2 = -0.5 * tc * pdt;
-        for (int j = i + 1 + tid; j < n; j += TRI_T) wp[j] = (tc != 0.0) ? wp[j] + a2 * vc[j] : 0.0;
-        __syncthreads();
-        const double v1 = vc[i + 1], w1 = wp[i + 1];
-        for (int j = i + 1 + tid; j < n; j += TRI_T) y[j] = y[j] - v1 * wp[j] - w1 * vc[j];
-        __syncthreads();
+        const double v1 = vc[i + 1];
+        const double w1 = (tc != 0.0) ? pp[i + 1] + a2 * v1 : 0.0;
+        double xp = 0.0;
+        for (int j = i + 1 + tid; j < n; j += TRI_T) {
+            const double vj = vc[j];
+            const double wj = (tc != 0.0) ? pp[j] + a2 * vj : 0.0;
+            const double yj = y[j] - v1 * wj - w1 * vj;
+            wp[j] = wj;
+            y[j] = yj;
+            if (j >= i + 3) xp += yj * yj;
+        }
         if (i + 1 <= n - 2) {
-            double bn, tn;
-            house<TRI_T>(y, i + 2, n, vp, red, bn, tn);
+            // Householder reflector from y[i+2..] (LAPACK dlarfg)
+            const double xn2 = block_sum<TRI_W>(xp, red);
+            const double alpha = y[i + 2];
+            double bn = alpha, tn = 0.0, scal = 0.0;
+            if (xn2 > 0.0) {
+                bn = -copysign(sqrt(alpha * alpha + xn2), alpha);
+                tn = (bn - alpha) / bn;
+                scal = 1.0 / (alpha - bn);
+            }
+            for (int j = i + 2 + tid; j < n; j += TRI_T) vp[j] = (j == i + 2) ? 1.0 : y[j] * scal;
             if (me == 0) {
                 if (tid == 0) {
                     a.d[i + 1] = y[i + 1];
                     a.e[i + 1] = bn;
                     a.tau[i + 1] = tn;
                 }
-                for (int j = i + 2 + tid; j < n; j += TRI_T) a.refl[(size_t)(i + 1) * lda + j] = vp[j];
+                for (int j = i + 2 + tid; j < n; j += TRI_T)
+                    a.refl[(size_t)(i + 1) * lda + j] = (j == i + 2) ? 1.0 : y[j] * scal;
             }
             tp = tc;
             tc = tn;
             double* t = vc;  // v_i becomes the previous reflector
             vc = vp;
             vp = t;
-        } else if (me == 0 && tid == 0) {
-            a.d[n - 1] = y[n - 1];
-            a.e[n - 1] = 0.0;
-            a.tau[n - 1] = 0.0;
+        } else {
+            __syncthreads();
+            if (me == 0 && tid == 0) {
+                a.d[n - 1] = y[n - 1];
+                a.e[n - 1] = 0.0;
+                a.tau[n - 1] = 0.0;
+            }
         }
         __syncthreads();
+        if (stmp) t_c += __builtin_amdgcn_s_memtime() - t0;
+    }
+    if (stmp) {
+        a.stamps[0] = t_b;
+        a.stamps[1] = t_w;
+        a.stamps[2] = t_c;
     }
 }
 
@@ -390,6 +499,7 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
             }
         }
         if (fd[n - 1] == 0.0) fd[n - 1] = tiny;
+        for (int i = 0; i < n; ++i) fd[i] = 1.0 / fd[i];  // the solves multiply by the pivots' reciprocals
     }
     for (int i = tid; i < n; i += VEC_T) {  // deterministic pseudo-random start
         unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)q * 40503u + 12345u);
@@ -399,7 +509,7 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
         y[i] = 0.5 + (double)(h & 0xffff) / 65536.0;
     }
     __syncthreads();
-    for (int iter = 0; iter < 3; ++iter) {
+    for (int iter = 0; iter < 2; ++iter) {
         if (tid == 0) {
             double bi = y[0];
             for (int i = 0; i < n - 1; ++i) {
@@ -413,15 +523,15 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
                 }
             }
             y[n - 1] = bi;
-            double z1 = y[n - 1] / fd[n - 1];
+            double z1 = y[n - 1] * fd[n - 1];
             y[n - 1] = z1;
             double z2 = 0.0;
             if (n >= 2) {
-                z2 = (y[n - 2] - fu[n - 2] * z1) / fd[n - 2];
+                z2 = (y[n - 2] - fu[n - 2] * z1) * fd[n - 2];
                 y[n - 2] = z2;
             }
             for (int i = n - 3; i >= 0; --i) {
-                const double z0 = (y[i] - fu[i] * z2 - fu2[i] * z1) / fd[i];
+                const double z0 = (y[i] - fu[i] * z2 - fu2[i] * z1) * fd[i];
                 y[i] = z0;
                 z1 = z2;
                 z2 = z0;
@@ -449,6 +559,54 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
         __syncthreads();
     }
     // ---- back-transformation: z = H_0 H_1 ... H_{n-3} y (last reflector first)
+    if (n <= 64 * VEC_NJ) {
+        // one wave, y in registers, next reflector prefetched: no barrier per reflector
+        if (wv == 0) {
+            double yr[VEC_NJ], vr[VEC_NJ], vn[VEC_NJ];
+#pragma unroll
+            for (int t = 0; t < VEC_NJ; ++t) {
+                const int j = lane + 64 * t;
+                yr[t] = (j < n) ? y[j] : 0.0;
+            }
+            int kk = n - 3;
+            if (kk >= 0) {
+                const double* v = a.refl + (size_t)kk * a.lda;
+#pragma unroll
+                for (int t = 0; t < VEC_NJ; ++t) {
+                    const int j = lane + 64 * t;
+                    vn[t] = (j > kk && j < n) ? v[j] : 0.0;
+                }
+            }
+            double tn = (kk >= 0) ? a.tau[kk] : 0.0;
+            for (; kk >= 0; --kk) {
+                const double tcur = tn;
+#pragma unroll
+                for (int t = 0; t < VEC_NJ; ++t) vr[t] = vn[t];
+                if (kk > 0) {  // prefetch reflector kk - 1
+                    const double* v = a.refl + (size_t)(kk - 1) * a.lda;
+#pragma unroll
+                    for (int t = 0; t < VEC_NJ; ++t) {
+                        const int j = lane + 64 * t;
+                        vn[t] = (j > kk - 1 && j < n) ? v[j] : 0.0;
+                    }
+                    tn = a.tau[kk - 1];
+                }
+                if (tcur == 0.0) continue;
+                double sd = 0.0;
+#pragma unroll
+                for (int t = 0; t < VEC_NJ; ++t) sd += vr[t] * yr[t];
+                sd = wave_sum_d(sd) * tcur;
+#pragma unroll
+                for (int t = 0; t < VEC_NJ; ++t) yr[t] -= sd * vr[t];
+            }
+#pragma unroll
+            for (int t = 0; t < VEC_NJ; ++t) {
+                const int j = lane + 64 * t;
+                if (j < n) a.Zq[(size_t)q * a.lda + j] = yr[t];
+            }
+        }
+        return;
+    }
     for (int kk = n - 3; kk >= 0; --kk) {
         const double t = a.tau[kk];
         if (t == 0.0) continue;
@@ -530,7 +688,7 @@ __global__ void __launch_bounds__(FIN_T) k_eig_finish(double* Zq, int n, int lda
 // ---------------------------------------------------------------------------
 // host side
 struct EigLayout {
-    size_t d, e, tau, tnorm, flags, pbuf, rowbuf, pdot, zq, refl, lu, work, total;
+    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, lu, work, total;
 };
 
 static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool lu_lds)
@@ -547,9 +705,9 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     L.tau = take(n);
     L.tnorm = take(1);
     L.flags = take(2);  // counter, err (u32 in doubles' space)
-    L.pbuf = take(2 * (size_t)lda);
-    L.rowbuf = take(2 * (size_t)lda);
-    L.pdot = take(2 * EIG_MAX_WG);
+    L.pg = take(4 * (size_t)lda);  // u64 granules occupy doubles' space
+    L.rg = take(4 * (size_t)lda);
+    L.dg = take(4 * EIG_MAX_WG);
     L.zq = take(16 * (size_t)lda);
     L.refl = take((size_t)n * lda);
     L.lu = lu_lds ? o : take((size_t)16 * 5 * n);
@@ -562,7 +720,7 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
 
 static size_t tri_lds_bytes(int n, int R, bool rows_lds)
 {
-    return sizeof(double) * (4 * (size_t)n + 64 + EIG_MAX_WG + (rows_lds ? (size_t)R * n : 0));
+    return sizeof(double) * (5 * (size_t)n + 64 + EIG_MAX_WG + (rows_lds ? (size_t)R * n : 0));
 }
 
 static int eig_nwg(int n)
@@ -606,7 +764,7 @@ extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 // marks (optional): 6 events recorded before/after each of the three launches.
 extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
                                             double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
-                                            hipStream_t st)
+                                            unsigned long long* stamps, hipStream_t st)
 {
     int nwg;
     bool rows_lds, lu_lds;
@@ -616,6 +774,9 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if (err_dev) *err_dev = flags + 1;
     if (nwg_out) *nwg_out = nwg;
     hipError_t e = hipMemsetAsync(flags, 0, 8, st);
+    if (e != hipSuccess) return e;
+    // granule tags restart at 1 every launch
+    e = hipMemsetAsync(scratch + L.pg, 0, sizeof(double) * (L.zq - L.pg), st);
     if (e != hipSuccess) return e;
     TriArgs t;
     t.A = A;
@@ -627,11 +788,12 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.e = scratch + L.e;
     t.tau = scratch + L.tau;
     t.refl = scratch + L.refl;
-    t.pbuf = scratch + L.pbuf;
-    t.rowbuf = scratch + L.rowbuf;
-    t.pdot = scratch + L.pdot;
+    t.pg = (u64*)(scratch + L.pg);
+    t.rg = (u64*)(scratch + L.rg);
+    t.dg = (u64*)(scratch + L.dg);
     t.work = scratch + L.work;
     t.counter = flags;
+    t.stamps = stamps;
     t.err = flags + 1;
     const int R = (n + nwg - 1) / nwg;
     // at least 82 KB so that every workgroup has a CU of its own

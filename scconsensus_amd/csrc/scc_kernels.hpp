@@ -137,7 +137,8 @@ hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipSt
 hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st);
 size_t scc_eigen_scratch_doubles(int n, int lda, int k);
 hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
-                                 unsigned int** err_dev, int* nwg_out, hipEvent_t* marks, hipStream_t st);
+                                 unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
+                                 unsigned long long* stamps, hipStream_t st);
 
 hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st);
 int scc_wilcox_table_layout(int* woff);

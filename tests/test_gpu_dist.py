@@ -125,3 +125,19 @@ def test_eigensolver_rows_beyond_lds(eng):
     dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+@pytest.mark.parametrize("n,nwg", [(700, 70), (700, 256), (1500, 40), (1500, 150), (2100, 210)])
+def test_eigensolver_workgroup_counts(eng, n, nwg, monkeypatch):
+    """Same eigenpairs for any number of tridiagonalisation workgroups (rows in
+    LDS or in HBM; up to one workgroup per CU)."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((n, 900)) * np.linspace(3.0, 0.5, n)[:, None]
+    X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 900)) * 4.0
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
