@@ -67,21 +67,40 @@ __global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indp
         cell_range<DENSE>(indptr, c, G, b, e);
         u32 pos = 0;
         i64* bp = bnd + (size_t)p * (ntile + 1);
-        for (i64 k = b + lane; k < e; k += 64) {
-            const double x = vals[k];
-            const int g = DENSE ? (int)(k - b) : rows[k];
-            const bool gok = (g >= 0) & (g < G);
-            bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
-            pos += (x > 0.0);
-            if (want_expm1) se = dd_add_d(se, expm1(x));
-            if (a >= 0 && x != 0.0 && gok) atomicAdd(&hist[g], 1u);
-            if (!DENSE && a >= 0) {
-                // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
-                const int gp = (k > b) ? rows[k - 1] : -1;
-                if (k > b && gp >= g) bad |= 4;
-                const int tp = (gp < 0) ? -1 : min(gp / gt, ntile - 1);
-                const int tg = gok ? g / gt : (g < 0 ? -1 : ntile - 1);
-                for (int t = tp + 1; t <= tg; ++t) bp[t] = k;
+        for (i64 k0 = b; k0 < e; k0 += 4 * 64) {  // four loads in flight per lane
+            double xs[4];
+            int gs[4], gps[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const i64 k = k0 + u * 64 + lane;
+                xs[u] = 0.0;
+                gs[u] = -1;
+                gps[u] = -1;
+                if (k < e) {
+                    xs[u] = vals[k];
+                    gs[u] = DENSE ? (int)(k - b) : rows[k];
+                    if (!DENSE && k > b) gps[u] = rows[k - 1];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const i64 k = k0 + u * 64 + lane;
+                if (k >= e) break;
+                const double x = xs[u];
+                const int g = gs[u];
+                const bool gok = (g >= 0) & (g < G);
+                bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
+                pos += (x > 0.0);
+                if (want_expm1) se = dd_add_d(se, expm1(x));
+                if (a >= 0 && x != 0.0 && gok) atomicAdd(&hist[g], 1u);
+                if (!DENSE && a >= 0) {
+                    // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
+                    const int gp = gps[u];
+                    if (k > b && gp >= g) bad |= 4;
+                    const int tp = (gp < 0) ? -1 : min(gp / gt, ntile - 1);
+                    const int tg = gok ? g / gt : (g < 0 ? -1 : ntile - 1);
+                    for (int t = tp + 1; t <= tg; ++t) bp[t] = k;
+                }
             }
         }
         if (!DENSE && a >= 0) {
@@ -104,22 +123,61 @@ __global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indp
     for (int g = threadIdx.x; g < G; g += ING_T) row[g] = hist[g];
 }
 
-// per gene: exclusive prefix over the nc count chunks; row nc = total
-__global__ void __launch_bounds__(256) k_ing_colscan(u32* __restrict__ cnt, int nc, int nc_kept, int G)
+// per gene: exclusive prefix over the count chunks (in place); rows >= nc_kept
+// (unkept cells) hold the total.  Three passes over [segment of CS_SEG
+// chunks] x [256 genes] blocks so the whole chip works on it.
+#define CS_SEG 32
+__global__ void __launch_bounds__(256) k_ing_colsum(const u32* __restrict__ cnt, int nc_kept, int G,
+                                                    u32* __restrict__ part)
+{
+    const int g = blockIdx.y * 256 + threadIdx.x;
+    if (g >= G) return;
+    const int w0 = blockIdx.x * CS_SEG, w1 = min(nc_kept, w0 + CS_SEG);
+    u32 s = 0;
+    for (int w = w0; w < w1; ++w) s += cnt[(size_t)w * G + g];
+    part[(size_t)blockIdx.x * G + g] = s;
+}
+
+__global__ void __launch_bounds__(256) k_ing_segscan(u32* __restrict__ part, int nseg, int G, u32* __restrict__ total)
 {
     const int g = blockIdx.x * 256 + threadIdx.x;
     if (g >= G) return;
     u32 run = 0;
-    for (int w = 0; w < nc_kept; ++w) {
+    for (int q = 0; q < nseg; ++q) {
+        const u32 v = part[(size_t)q * G + g];
+        part[(size_t)q * G + g] = run;
+        run += v;
+    }
+    total[g] = run;
+}
+
+__global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int nc, int nc_kept, int G,
+                                                      const u32* __restrict__ part, const u32* __restrict__ total)
+{
+    const int g = blockIdx.y * 256 + threadIdx.x;
+    if (g >= G) return;
+    const int w0 = blockIdx.x * CS_SEG;
+    if (w0 >= nc_kept) {  // unkept chunks (and the totals row nc) add nothing
+        const u32 tot = total[g];
+        for (int w = w0; w < min(nc + 1, w0 + CS_SEG); ++w) cnt[(size_t)w * G + g] = tot;
+        return;
+    }
+    u32 run = part[(size_t)blockIdx.x * G + g];
+    const int w1 = min(nc_kept, w0 + CS_SEG);
+    for (int w = w0; w < w1; ++w) {
         const u32 v = cnt[(size_t)w * G + g];
         cnt[(size_t)w * G + g] = run;
         run += v;
     }
-    for (int w = nc_kept; w <= nc; ++w) cnt[(size_t)w * G + g] = run;  // unkept chunks add nothing
+    if (w1 == nc_kept) {
+        const u32 tot = total[g];
+        for (int w = w1; w < min(nc + 1, w0 + CS_SEG); ++w) cnt[(size_t)w * G + g] = tot;
+    }
 }
 
-#define SC_GT 256       // genes per tile (== ING_T: one scan lane per gene)
-#define SC_CAP 6144     // staged entries per round (u64 key + u16 gene = 10 B each): 2 blocks per CU
+#define SC_GT 256       // genes per tile
+#define SC_CAP 7168     // staged entries per round (u64 key + u16 gene = 10 B each): 2 blocks per CU
+#define SC_CMAX 128     // cells per scatter chunk (kScatterCC * kCountChunk)
 
 template <bool DENSE>
 __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ indptr, const int* __restrict__ rows,
@@ -133,9 +191,12 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     __shared__ u32 cur[SC_GT];
     __shared__ u32 lcnt[SC_GT];
     __shared__ i64 gdst[SC_GT];
+    __shared__ i64 ckb[SC_CMAX];
+    __shared__ u32 cof[SC_CMAX + 1];
     __shared__ int rnd[SC_GT + 2];
     __shared__ int nrnd;
     __shared__ u32 wsum[ING_T / 64];
+    __shared__ u32 csum[ING_T / 64];
     extern __shared__ __attribute__((aligned(16))) u64 skey[];  // [SC_CAP]
     unsigned short* sg = (unsigned short*)(skey + SC_CAP);     // [SC_CAP]
     const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
@@ -143,28 +204,70 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     const int g0 = t * SC_GT, g1 = min(G, g0 + SC_GT), ng = g1 - g0;
     const int cc0 = sc_cc0[s], cc1 = sc_cc0[s + 1];
     const int p0 = cc_p0[cc0], p1 = cc_p0[cc1];
-    // local counts and destinations of this (chunk, tile) per gene
-    u32 myc = 0;
-    if (tid < ng) {
-        const int g = g0 + tid;
-        const u32 o0 = cnt[(size_t)cc0 * G + g];
-        myc = cnt[(size_t)cc1 * G + g] - o0;
-        lcnt[tid] = myc;
-        gdst[tid] = gstart[g] + o0;
+    const int ncell = p1 - p0;  // <= SC_CMAX
+    // ---- cell ranges inside this gene tile (all loads issued together)
+    u32 clen = 0;
+    if (tid < ncell) {
+        const int c = perm[p0 + tid];
+        i64 kb, ke;
+        if (DENSE) {
+            kb = (i64)c * G + g0;
+            ke = kb + ng;
+        } else {
+            // clamp: bnd is only trustworthy when the hist pass saw sorted
+            // rows (err bit 4 otherwise); reads must stay in bounds anyway
+            const i64* bp = bnd + (size_t)(p0 + tid) * (ntile + 1);
+            const i64 cb = indptr[c], ce = indptr[c + 1];
+            kb = min(max(bp[t], cb), ce);
+            ke = min(max(bp[t + 1], kb), ce);
+        }
+        ckb[tid] = kb;
+        clen = (u32)(ke - kb);
     }
-    // inclusive scan of the counts (ING_T == SC_GT)
-    u32 inc = myc;
+    // ---- per gene counts and destinations of this (chunk, tile): 2 genes per thread
+    u32 myc[2];
+    for (int h = 0; h < 2; ++h) {
+        const int gl = 2 * tid + h;
+        myc[h] = 0;
+        if (gl < ng) {
+            const int g = g0 + gl;
+            const u32 o0 = cnt[(size_t)cc0 * G + g];
+            myc[h] = cnt[(size_t)cc1 * G + g] - o0;
+            gdst[gl] = gstart[g] + o0;
+        }
+        if (gl < SC_GT) lcnt[gl] = myc[h];
+    }
+    // inclusive scans: gene counts (2 per thread) and cell lengths
+    u32 inc = myc[0] + myc[1], cinc = clen;
     for (int o = 1; o < 64; o <<= 1) {
-        const u32 y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
+        const u32 y = __shfl_up(inc, o, 64), z = __shfl_up(cinc, o, 64);
+        if (lane >= o) {
+            inc += y;
+            cinc += z;
+        }
     }
-    if (lane == 63) wsum[wv] = inc;
+    if (lane == 63) {
+        wsum[wv] = inc;
+        csum[wv] = cinc;
+    }
     __syncthreads();
-    for (int v = 0; v < wv; ++v) inc += wsum[v];
+    for (int v = 0; v < wv; ++v) {
+        inc += wsum[v];
+        cinc += csum[v];
+    }
+    if (2 * tid < SC_GT) {
+        loff[2 * tid + 1] = inc - myc[1];
+        loff[2 * tid + 2] = inc;
+    }
+    if (tid == 0) {
+        loff[0] = 0;
+        cof[0] = 0;
+    }
+    if (tid < ncell) cof[tid + 1] = cinc;
+    __syncthreads();
     // rounds of <= SC_CAP entries over consecutive genes
     if (tid == 0) {
-        u32 tot = 0;
-        for (int v = 0; v < ING_T / 64; ++v) tot += wsum[v];
+        const u32 tot = loff[ng];
         int nr = 0;
         rnd[0] = 0;
         if (tot <= SC_CAP) {
@@ -183,47 +286,57 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
         }
         nrnd = nr;
     }
-    if (tid < ng) loff[tid + 1] = inc;  // global-in-tile inclusive prefix
-    if (tid == 0) loff[0] = 0;
     __syncthreads();
     const int nr = nrnd;
+    const u32 E = cof[ncell];  // stored entries of the tile (zeros included for dense input)
     for (int r = 0; r < nr; ++r) {
         const int r0 = rnd[r], r1 = rnd[r + 1];
         const u32 base = loff[r0];
         for (int gl = tid; gl < SC_GT; gl += ING_T) cur[gl] = 0;
         __syncthreads();
-        for (int p = p0 + wv; p < p1; p += ING_T / 64) {
-            const int c = perm[p];
-            i64 kb, ke;
-            if (DENSE) {
-                kb = (i64)c * G + g0 + r0;
-                ke = (i64)c * G + g0 + r1;
-            } else {
-                // clamp: bnd is only trustworthy when the hist pass saw sorted
-                // rows (err bit 4 otherwise); reads must stay in bounds anyway
-                const i64* bp = bnd + (size_t)p * (ntile + 1);
-                const i64 cb = indptr[c], ce = indptr[c + 1];
-                kb = min(max(bp[t], cb), ce);
-                ke = min(max(bp[t + 1], kb), ce);
+        // each wave takes 4 cells at a time, lanes over a cell's entries in the
+        // tile (~60 at PBMC density); the 4 first chunks' loads are in flight together
+        auto put = [&](double x, int gq) {
+            if (x != 0.0 && gq >= r0 && gq < r1) {
+                const u32 o = atomicAdd(&cur[gq], 1u);
+                if (o < lcnt[gq]) {  // always, for valid input
+                    const u32 pos = loff[gq] - base + o;
+                    skey[pos] = scc_key_of(x);
+                    sg[pos] = (unsigned short)gq;
+                }
             }
-            for (i64 k = kb + lane; k < ke; k += 64) {
-                const double x = vals[k];
-                const int gl = DENSE ? (int)(k - (i64)c * G) - g0 : rows[k] - g0;
-                if (x != 0.0 && gl >= r0 && gl < r1) {
-                    const u32 o = atomicAdd(&cur[gl], 1u);
-                    if (o < lcnt[gl]) {  // always, for valid input
-                        const u32 pos = loff[gl] - base + o;
-                        skey[pos] = scc_key_of(x);
-                        sg[pos] = (unsigned short)gl;
-                    }
+        };
+        for (int cb = 4 * wv; cb < ncell; cb += 4 * (ING_T / 64)) {
+            double x[4];
+            int gq[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = cb + u;
+                x[u] = 0.0;
+                gq[u] = -1;
+                if (c < ncell && (u32)lane < cof[c + 1] - cof[c]) {
+                    const i64 k = ckb[c] + lane;
+                    x[u] = vals[k];
+                    gq[u] = DENSE ? lane : rows[k] - g0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) put(x[u], gq[u]);
+            for (int u = 0; u < 4; ++u) {  // cells with more than 64 entries in the tile
+                const int c = cb + u;
+                if (c >= ncell) break;
+                const u32 len = cof[c + 1] - cof[c];
+                for (u32 j = 64 + lane; j < len; j += 64) {
+                    const i64 k = ckb[c] + j;
+                    put(vals[k], DENSE ? (int)j : rows[k] - g0);
                 }
             }
         }
         __syncthreads();
-        const int E = (int)(loff[r1] - base);
-        for (int i = tid; i < E; i += ING_T) {
-            const int gl = sg[i];
-            keys[gdst[gl] + (i64)(i - (int)(loff[gl] - base))] = skey[i];
+        const int Er = (int)(loff[r1] - base);
+        for (int i = tid; i < Er; i += ING_T) {
+            const int gq = sg[i];
+            keys[gdst[gq] + (i64)(i - (int)(loff[gq] - base))] = skey[i];
         }
         __syncthreads();
     }
@@ -336,9 +449,18 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
     return hipGetLastError();
 }
 
-extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, int G, hipStream_t st)
+extern "C" int scc_ingest_colscan_scratch(int nc, int G) { return ((nc + 1 + CS_SEG - 1) / CS_SEG + 1) * G; }
+
+extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, int G, u32* scratch, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ing_colscan, dim3((G + 255) / 256), dim3(256), 0, st, cnt, nc, nc_kept, G);
+    const int nseg_k = (nc_kept + CS_SEG - 1) / CS_SEG;
+    const int nseg_all = (nc + 1 + CS_SEG - 1) / CS_SEG;
+    u32* part = scratch;
+    u32* total = scratch + (size_t)nseg_all * G;
+    const int gb = (G + 255) / 256;
+    if (nseg_k > 0) hipLaunchKernelGGL(k_ing_colsum, dim3(nseg_k, gb), dim3(256), 0, st, cnt, nc_kept, G, part);
+    hipLaunchKernelGGL(k_ing_segscan, dim3(gb), dim3(256), 0, st, part, nseg_k, G, total);
+    hipLaunchKernelGGL(k_ing_colapply, dim3(nseg_all, gb), dim3(256), 0, st, cnt, nc, nc_kept, G, part, total);
     return hipGetLastError();
 }
 

@@ -352,7 +352,9 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 4, s0));
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, d_err, s0));
-        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, s0));
+        uint32_t* d_cscr;
+        WS("colscan", scc_ingest_colscan_scratch(nc, G), d_cscr);
+        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, d_cscr, s0));
         const uint32_t* d_total = d_cnt + (size_t)nc * G;
         HIPCHK(c, scc_launch_scan(d_total, G, d_gstart, d_scan, d_gstart + G, s0));
         HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
