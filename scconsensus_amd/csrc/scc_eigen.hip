@@ -29,6 +29,8 @@
 // Output Z[u*16 + q] = q-th largest eigenvector (q < k), zero padded to 16;
 // W[q] the q-th largest eigenvalue.
 #include "scc_common.hpp"
+#include <algorithm>
+#include <cstdlib>
 
 #define TRI_T 256
 #define TRI_W (TRI_T / 64)
@@ -64,12 +66,18 @@ __device__ inline void st_sc1(double* p, double v)
 // 8-byte granules {32-bit half, 32-bit tag} written by ONE sc1 store each: a
 // double travels as two granules; a reader polls until both tags match
 // (MI355X_MICROARCH.md price list: data-tagged granules, handoff-1to1).
+template <bool LOCAL>
 __device__ inline void put_g(u64* g, double x, u32 tag)
 {
     const u64 b = (u64)__double_as_longlong(x);
     const u64 t = (u64)tag << 32;
-    __hip_atomic_store(g, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + 1, t | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (LOCAL) {  // one XCD: a plain 8-byte store lands in the shared L2, where the sc1 polls read
+        __hip_atomic_store(g, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(g + 1, t | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        __hip_atomic_store(g, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 1, t | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 __device__ inline u64 get_g(const u64* g) { return __hip_atomic_load((u64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ inline double g_val(u64 hi, u64 lo) { return __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull))); }
@@ -94,6 +102,10 @@ __device__ inline double block_sum(double v, double* red)
 struct TriArgs {
     const double* A;  // n x n symmetric, row-major, lda
     int n, lda, nwg, rows_lds;
+    int xcd_local;    // 1: the participating workgroups all run on one XCD (read from
+                      // HW_REG_XCC_ID at run time) and hand off through that XCD's L2
+    int lds_rows_cap; // rows per workgroup the dynamic LDS holds
+    u32* reg;         // [3] XCD pick (xcc + 1), registrations, check-ins (zeroed per launch)
     double* d;        // [n] diagonal of T
     double* e;        // [n] off-diagonal (e[i] = T[i+1][i])
     double* tau;      // [n]
@@ -128,13 +140,56 @@ __device__ inline void house(const double* y, int lo, int n, double* v, double* 
     for (int j = lo + tid; j < n; j += T) v[j] = (j == lo) ? 1.0 : y[j] * scal;
 }
 
+template <bool LOCAL>
 __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    __shared__ int s_abort;
-    const int n = a.n, nwg = a.nwg, me = blockIdx.x, lda = a.lda;
+    __shared__ int s_abort, s_rank, s_nwg;
+    const int n = a.n, lda = a.lda;
     const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    int me = blockIdx.x, nwg = a.nwg;
+    if (LOCAL) {
+        // the first workgroup to arrive picks its XCD; up to a.nwg workgroups
+        // found on that XCD take part, ranked by arrival; the others leave.
+        if (tid == 0) {
+            u32 x;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            x &= 0xfu;
+            const u32 old = atomicCAS(&a.reg[0], 0u, x + 1u);
+            const u32 target = old ? old - 1u : x;
+            int rank = -1;
+            if (x == target) {
+                const u32 r = atomicAdd(&a.reg[1], 1u);
+                if (r < (u32)a.nwg) rank = (int)r;
+            }
+            const u32 seen = atomicAdd(&a.reg[2], 1u) + 1u;  // after the registration returned
+            int nw = 0;
+            if (rank >= 0) {
+                u32 spins = 0, cur = seen;
+                while (cur < gridDim.x) {
+                    __builtin_amdgcn_s_sleep(2);
+                    cur = __hip_atomic_load(&a.reg[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (++spins > EIG_SPIN_LIMIT) {
+                        __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        rank = -1;
+                        break;
+                    }
+                }
+                const u32 reg = __hip_atomic_load(&a.reg[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                nw = (int)min(reg, (u32)a.nwg);
+                if (nw > n) nw = n;
+                if (rank >= nw) rank = -1;
+            }
+            s_rank = rank;
+            s_nwg = nw;
+        }
+        __syncthreads();
+        if (s_rank < 0) return;
+        me = s_rank;
+        nwg = s_nwg;
+    }
     const int R = (n + nwg - 1) / nwg;
+    const bool rows_lds = LOCAL ? (R <= a.lds_rows_cap) : (a.rows_lds != 0);
     double* vA = sm;           // v_i   (support i+1..n-1)
     double* vB = vA + n;       // v_{i-1}, then v_{i+1}
     double* wp = vB + n;       // w_{i-1}, then w_i
@@ -142,7 +197,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     double* pp = y + n;        // handed-off p of the current column
     double* red = pp + n;      // 64
     double* part = red + 64;   // EIG_MAX_WG
-    double* rows = a.rows_lds ? (part + EIG_MAX_WG) : (a.work + (size_t)me * R * n);
+    double* rows = rows_lds ? (part + EIG_MAX_WG) : (a.work + (size_t)me * R * n);
     const int nown = (me < n) ? (n - me + nwg - 1) / nwg : 0;
     if (tid == 0) s_abort = 0;
     for (int l = 0; l < nown; ++l) {
@@ -181,7 +236,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         if (stmp) t0 = __builtin_amdgcn_s_memtime();
         u64* pg = a.pg + (size_t)par * 2 * lda;
         u64* rg = a.rg + (size_t)par * 2 * lda;
-        u64* dg = a.dg + (size_t)par * 2 * EIG_MAX_WG;
+        u64* dg = a.dg + (size_t)par * 2 * EIG_MAX_WG * TRI_W;
         const bool prev = (i >= 1) && (tp != 0.0);
         // ---- phase B: own rows r >= i+1: apply update i-1, p_r = tau_i A_r. v_i;
         // publish p_r (and row i+1 by its owner) as tagged granules
@@ -199,13 +254,13 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                     x = x - vr * wp[j] - wr * vp[j];
                     row[j] = x;
                 }
-                if (pub) put_g(rg + 2 * j, x, tag);
+                if (pub) put_g<LOCAL>(rg + 2 * j, x, tag);
                 s += x * vc[j];
             }
             s = wave_sum_d(s);
             const double p = tc * s;
             if (lane == 0) {
-                put_g(pg + 2 * r, p, tag);
+                put_g<LOCAL>(pg + 2 * r, p, tag);
                 pd += p * vc[r];
             }
         }
@@ -214,7 +269,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         if (tid == 0) {
             double s = 0.0;
             for (int q = 0; q < TRI_W; ++q) s += red[32 + q];
-            put_g(dg + 2 * me, s, tag);
+            put_g<LOCAL>(dg + 2 * me, s, tag);
         }
         if (stmp) {
             const u64 t1 = __builtin_amdgcn_s_memtime();
@@ -352,6 +407,318 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
             }
         }
         __syncthreads();
+        if (stmp) t_c += __builtin_amdgcn_s_memtime() - t0;
+    }
+    if (stmp) {
+        a.stamps[0] = t_b;
+        a.stamps[1] = t_w;
+        a.stamps[2] = t_c;
+    }
+}
+
+// XCD registration shared by both tridiagonalisation kernels: the first
+// workgroup to arrive picks its XCD; up to a.nwg workgroups found on that XCD
+// take part, ranked by arrival; the others leave.  Returns the rank (-1: leave)
+// and the number of participants.
+__device__ inline void xcd_register(const TriArgs& a, int n, int* s_rank, int* s_nwg)
+{
+    if (threadIdx.x == 0) {
+        u32 x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        x &= 0xfu;
+        const u32 old = atomicCAS(&a.reg[0], 0u, x + 1u);
+        const u32 target = old ? old - 1u : x;
+        int rank = -1;
+        if (x == target) {
+            const u32 r = atomicAdd(&a.reg[1], 1u);
+            if (r < (u32)a.nwg) rank = (int)r;
+        }
+        const u32 seen = atomicAdd(&a.reg[2], 1u) + 1u;  // after the registration returned
+        int nw = 0;
+        if (rank >= 0) {
+            u32 spins = 0, cur = seen;
+            while (cur < gridDim.x) {
+                __builtin_amdgcn_s_sleep(2);
+                cur = __hip_atomic_load(&a.reg[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (++spins > EIG_SPIN_LIMIT) {
+                    __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    rank = -1;
+                    break;
+                }
+            }
+            const u32 reg = __hip_atomic_load(&a.reg[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            nw = (int)min(reg, (u32)a.nwg);
+            if (rank >= nw) rank = -1;
+        }
+        *s_rank = rank;
+        *s_nwg = nw;
+    }
+    __syncthreads();
+}
+
+// Wave-agent tridiagonalisation for n <= 64 * TW_NJ.  Every wave of every
+// participating workgroup is an independent agent: it owns rows r with
+// r % NA == agent, keeps v_i, v_{i-1}, w_{i-1} in registers (lane-strided,
+// j = lane + 64 t), polls every granule it needs itself and computes w_i,
+// row i+1 and the next reflector redundantly.  The main loop has no
+// workgroup barrier at all; agents only meet through the tagged granules.
+#define TW_NJ 8
+#define TW_MAXA 256  // agents (64 workgroups of 4 waves)
+template <bool LOCAL>
+__global__ void __launch_bounds__(TRI_T) k_tridiag_wa(TriArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ int s_rank, s_nwg;
+    const int n = a.n, lda = a.lda;
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    int me = blockIdx.x, nwg = a.nwg;
+    if (LOCAL) {
+        xcd_register(a, n, &s_rank, &s_nwg);
+        if (s_rank < 0) return;
+        me = s_rank;
+        nwg = s_nwg;
+    }
+    const int NA = nwg * TRI_W;         // agents
+    const int ag = me * TRI_W + wv;     // this wave's agent id
+    const int RA = (n + NA - 1) / NA;   // rows per agent
+    // rows in LDS when the participants' share fits (fewer workgroups than
+    // planned may register on the XCD: then the rows live in HBM scratch)
+    const bool in_lds = (size_t)TRI_W * RA * n <= (size_t)a.lds_rows_cap;
+    double* rows = in_lds ? sm + (size_t)wv * RA * n : a.work + (size_t)ag * RA * n;
+    const int nown = (ag < n) ? (n - ag + NA - 1) / NA : 0;
+    for (int l = 0; l < nown; ++l) {
+        const double* src = a.A + (size_t)(ag + NA * l) * lda;
+        for (int j = lane; j < n; j += 64) rows[(size_t)l * n + j] = src[j];
+    }
+    double vc[TW_NJ], vp[TW_NJ], wp[TW_NJ];
+    // row 0 -> reflector 0 (every agent)
+    double y[TW_NJ];
+#pragma unroll
+    for (int t = 0; t < TW_NJ; ++t) {
+        const int j = lane + 64 * t;
+        y[t] = (j < n) ? a.A[j] : 0.0;
+        vp[t] = 0.0;
+        wp[t] = 0.0;
+    }
+    auto bcast = [&](const double* r, int j) -> double {  // element j of a lane-strided register vector
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < TW_NJ; ++t)
+            if (t == (j >> 6)) v = r[t];
+        return __shfl(v, j & 63, 64);
+    };
+    const double d0 = bcast(y, 0);
+    if (n == 1) {
+        if (ag == 0 && lane == 0) {
+            a.d[0] = d0;
+            a.e[0] = 0.0;
+            a.tau[0] = 0.0;
+        }
+        return;
+    }
+    double tc, tp = 0.0;
+    {
+        double part = 0.0;
+#pragma unroll
+        for (int t = 0; t < TW_NJ; ++t) {
+            const int j = lane + 64 * t;
+            if (j >= 2 && j < n) part += y[t] * y[t];
+        }
+        const double xn2 = wave_sum_d(part);
+        const double alpha = bcast(y, 1);
+        double beta = alpha, scal = 0.0;
+        tc = 0.0;
+        if (xn2 > 0.0) {
+            beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+            tc = (beta - alpha) / beta;
+            scal = 1.0 / (alpha - beta);
+        }
+#pragma unroll
+        for (int t = 0; t < TW_NJ; ++t) {
+            const int j = lane + 64 * t;
+            vc[t] = (j == 1) ? 1.0 : ((j > 1 && j < n) ? y[t] * scal : 0.0);
+        }
+        if (ag == 0) {
+            if (lane == 0) {
+                a.d[0] = d0;
+                a.e[0] = beta;
+                a.tau[0] = tc;
+            }
+#pragma unroll
+            for (int t = 0; t < TW_NJ; ++t) {
+                const int j = lane + 64 * t;
+                if (j >= 1 && j < n) a.refl[j] = vc[t];
+            }
+        }
+    }
+    u64 t_b = 0, t_w = 0, t_c = 0, t0 = 0;
+    const bool stmp = a.stamps && ag == 0 && lane == 0;
+    for (int i = 0; i <= n - 2; ++i) {
+        const int par = i & 1;
+        const u32 tag = (u32)(i + 1);
+        u64* pg = a.pg + (size_t)par * 2 * lda;
+        u64* rg = a.rg + (size_t)par * 2 * lda;
+        u64* dg = a.dg + (size_t)par * 2 * EIG_MAX_WG * TRI_W;
+        const bool prev = (i >= 1) && (tp != 0.0);
+        if (stmp) t0 = __builtin_amdgcn_s_memtime();
+        // ---- phase B: own rows r >= i+1
+        double pd = 0.0;
+        const int l0 = (i + 1 > ag) ? (i + 1 - ag + NA - 1) / NA : 0;
+        for (int l = l0; l < nown; ++l) {
+            const int r = ag + NA * l;
+            double* row = rows + (size_t)l * n;
+            const double vr = prev ? bcast(vp, r) : 0.0, wr = prev ? bcast(wp, r) : 0.0;
+            const bool pub = (r == i + 1);
+            double s = 0.0;
+#pragma unroll
+            for (int t = 0; t < TW_NJ; ++t) {
+                const int j = lane + 64 * t;
+                if (j > i && j < n) {
+                    double x = row[j];
+                    if (prev) {
+                        x = x - vr * wp[t] - wr * vp[t];
+                        row[j] = x;
+                    }
+                    if (pub) put_g<LOCAL>(rg + 2 * j, x, tag);
+                    s += x * vc[t];
+                }
+            }
+            s = wave_sum_d(s);
+            const double p = tc * s;
+            if (lane == 0) put_g<LOCAL>(pg + 2 * r, p, tag);
+            pd += p * bcast(vc, r);
+        }
+        if (lane == 0) put_g<LOCAL>(dg + 2 * ag, pd, tag);
+        if (stmp) {
+            const u64 t1 = __builtin_amdgcn_s_memtime();
+            t_b += t1 - t0;
+            t0 = t1;
+        }
+        // ---- phase C: poll p, row i+1 and the agents' partials; all loads in flight
+        double pj[TW_NJ];
+        double pdt = 0.0;
+        {
+            u64 g[TW_NJ][4];
+            constexpr int DPL = TW_MAXA / 64;  // partial slots per lane
+            u64 gd[DPL][2];
+#pragma unroll
+            for (int t = 0; t < TW_NJ; ++t) {
+                const int j = lane + 64 * t;
+                if (j > i && j < n) {
+                    g[t][0] = get_g(pg + 2 * j);
+                    g[t][1] = get_g(pg + 2 * j + 1);
+                    g[t][2] = get_g(rg + 2 * j);
+                    g[t][3] = get_g(rg + 2 * j + 1);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < DPL; ++q) {
+                const int ax = lane + 64 * q;
+                if (ax < NA) {
+                    gd[q][0] = get_g(dg + 2 * ax);
+                    gd[q][1] = get_g(dg + 2 * ax + 1);
+                }
+            }
+            u32 spins = 0;
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int t = 0; t < TW_NJ; ++t) {
+                    const int j = lane + 64 * t;
+                    if (j > i && j < n) {
+#pragma unroll
+                        for (int h = 0; h < 4; ++h)
+                            if ((u32)(g[t][h] >> 32) != tag) {
+                                ok = false;
+                                g[t][h] = get_g((h < 2 ? pg : rg) + 2 * j + (h & 1));
+                            }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < DPL; ++q) {
+                    const int ax = lane + 64 * q;
+                    if (ax < NA) {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h)
+                            if ((u32)(gd[q][h] >> 32) != tag) {
+                                ok = false;
+                                gd[q][h] = get_g(dg + 2 * ax + h);
+                            }
+                    }
+                }
+                if (__all(ok)) break;
+                if (++spins > EIG_SPIN_LIMIT) {
+                    __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+#pragma unroll
+            for (int t = 0; t < TW_NJ; ++t) {
+                const int j = lane + 64 * t;
+                const bool act = j > i && j < n;
+                pj[t] = act ? g_val(g[t][0], g[t][1]) : 0.0;
+                y[t] = act ? g_val(g[t][2], g[t][3]) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < DPL; ++q)
+                if (lane + 64 * q < NA) pdt += g_val(gd[q][0], gd[q][1]);
+            pdt = wave_sum_d(pdt);
+        }
+        if (stmp) {
+            const u64 t1 = __builtin_amdgcn_s_memtime();
+            t_w += t1 - t0;
+            t0 = t1;
+        }
+        const double a2 = -0.5 * tc * pdt;
+        const double v1 = bcast(vc, i + 1);
+        const double w1 = (tc != 0.0) ? bcast(pj, i + 1) + a2 * v1 : 0.0;
+        double xp = 0.0;
+#pragma unroll
+        for (int t = 0; t < TW_NJ; ++t) {
+            const int j = lane + 64 * t;
+            const bool act = j > i && j < n;
+            const double wj = (act && tc != 0.0) ? pj[t] + a2 * vc[t] : 0.0;
+            const double yj = act ? y[t] - v1 * wj - w1 * vc[t] : 0.0;
+            wp[t] = wj;
+            y[t] = yj;
+            if (j >= i + 3 && j < n) xp += yj * yj;
+        }
+        const double dnext = bcast(y, i + 1);
+        if (i + 1 <= n - 2) {
+            const double xn2 = wave_sum_d(xp);
+            const double alpha = bcast(y, i + 2);
+            double bn = alpha, tn = 0.0, scal = 0.0;
+            if (xn2 > 0.0) {
+                bn = -copysign(sqrt(alpha * alpha + xn2), alpha);
+                tn = (bn - alpha) / bn;
+                scal = 1.0 / (alpha - bn);
+            }
+#pragma unroll
+            for (int t = 0; t < TW_NJ; ++t) {
+                const int j = lane + 64 * t;
+                vp[t] = vc[t];  // v_i becomes the previous reflector
+                vc[t] = (j == i + 2) ? 1.0 : ((j > i + 2 && j < n) ? y[t] * scal : 0.0);
+            }
+            if (ag == 0) {
+                if (lane == 0) {
+                    a.d[i + 1] = dnext;
+                    a.e[i + 1] = bn;
+                    a.tau[i + 1] = tn;
+                }
+#pragma unroll
+                for (int t = 0; t < TW_NJ; ++t) {
+                    const int j = lane + 64 * t;
+                    if (j >= i + 2 && j < n) a.refl[(size_t)(i + 1) * lda + j] = vc[t];
+                }
+            }
+            tp = tc;
+            tc = tn;
+        } else if (ag == 0 && lane == 0) {
+            a.d[n - 1] = dnext;
+            a.e[n - 1] = 0.0;
+            a.tau[n - 1] = 0.0;
+        }
         if (stmp) t_c += __builtin_amdgcn_s_memtime() - t0;
     }
     if (stmp) {
@@ -687,6 +1054,12 @@ __global__ void __launch_bounds__(FIN_T) k_eig_finish(double* Zq, int n, int lda
 
 // ---------------------------------------------------------------------------
 // host side
+static int eig_local()
+{
+    const char* env = getenv("SCC_EIG_XCD");
+    return (env && *env) ? atoi(env) : 1;
+}
+
 struct EigLayout {
     size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, lu, work, total;
 };
@@ -704,15 +1077,16 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     L.e = take(n);
     L.tau = take(n);
     L.tnorm = take(1);
-    L.flags = take(2);  // counter, err (u32 in doubles' space)
+    L.flags = take(4);  // counter, err, XCD registration [3] (u32 in doubles' space)
     L.pg = take(4 * (size_t)lda);  // u64 granules occupy doubles' space
     L.rg = take(4 * (size_t)lda);
-    L.dg = take(4 * EIG_MAX_WG);
+    L.dg = take(4 * EIG_MAX_WG * TRI_W);  // one partial per wave agent
     L.zq = take(16 * (size_t)lda);
     L.refl = take((size_t)n * lda);
     L.lu = lu_lds ? o : take((size_t)16 * 5 * n);
     const int R = (n + nwg - 1) / nwg;
-    L.work = rows_lds ? o : take((size_t)nwg * R * n);
+    // XCD-local mode: fewer workgroups may register than planned -> room for all rows
+    L.work = take(((size_t)n + 4 * 64) * n);  // row store of the HBM fall-backs (any participant count)
     L.total = o;
     (void)k;
     return L;
@@ -745,6 +1119,7 @@ static int eig_nwg(int n)
 static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
 {
     nwg = eig_nwg(n);
+    if (eig_local() && nwg > 32) nwg = 32;  // one XCD holds 32 CUs
     const int R = (n + nwg - 1) / nwg;
     rows_lds = tri_lds_bytes(n, R, true) <= EIG_LDS_MAX;
     lu_lds = sizeof(double) * 9 * (size_t)n <= EIG_LDS_MAX;
@@ -773,7 +1148,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     u32* flags = (u32*)(scratch + L.flags);
     if (err_dev) *err_dev = flags + 1;
     if (nwg_out) *nwg_out = nwg;
-    hipError_t e = hipMemsetAsync(flags, 0, 8, st);
+    hipError_t e = hipMemsetAsync(flags, 0, 32, st);
     if (e != hipSuccess) return e;
     // granule tags restart at 1 every launch
     e = hipMemsetAsync(scratch + L.pg, 0, sizeof(double) * (L.zq - L.pg), st);
@@ -793,15 +1168,46 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.dg = (u64*)(scratch + L.dg);
     t.work = scratch + L.work;
     t.counter = flags;
+    t.reg = flags + 2;
+    t.xcd_local = eig_local();
     t.stamps = stamps;
     t.err = flags + 1;
     const int R = (n + nwg - 1) / nwg;
     // at least 82 KB so that every workgroup has a CU of its own
     size_t lds = tri_lds_bytes(n, R, rows_lds);
     if (lds < 82 * 1024) lds = 82 * 1024;
-    hipFuncSetAttribute((const void*)k_tridiag, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    t.lds_rows_cap = rows_lds ? (int)((lds / sizeof(double) - (5 * (size_t)n + 64 + EIG_MAX_WG)) / n) : 0;
     if (marks) hipEventRecord(marks[0], st);
-    hipLaunchKernelGGL(k_tridiag, dim3(nwg), dim3(TRI_T), lds, st, t);
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 64;
+    }
+    const char* wa_env = getenv("SCC_EIG_WAVE");
+    const bool wave_agents = (wa_env && *wa_env) ? atoi(wa_env) != 0 : false;  // measured slower (polling load)
+    // wave agents: the planned participants' rows in LDS (HBM fall-back in the kernel)
+    const size_t wa_lds = sizeof(double) * (size_t)TRI_W * ((n + TRI_W * nwg - 1) / (TRI_W * nwg)) * n;
+    if (wave_agents && n <= 64 * TW_NJ && wa_lds <= EIG_LDS_MAX && nwg * TRI_W <= TW_MAXA) {
+        size_t l2 = wa_lds < 82 * 1024 ? 82 * 1024 : wa_lds;
+        t.lds_rows_cap = (int)(l2 / sizeof(double));
+        if (t.xcd_local) {
+            const int grid = std::min(8 * nwg, cus);
+            hipFuncSetAttribute((const void*)k_tridiag_wa<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
+            hipLaunchKernelGGL(k_tridiag_wa<true>, dim3(grid), dim3(TRI_T), l2, st, t);
+        } else {
+            hipFuncSetAttribute((const void*)k_tridiag_wa<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
+            hipLaunchKernelGGL(k_tridiag_wa<false>, dim3(nwg), dim3(TRI_T), l2, st, t);
+        }
+    } else if (t.xcd_local) {
+        const int grid = std::min(8 * nwg, cus);
+        hipFuncSetAttribute((const void*)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_tridiag<true>, dim3(grid), dim3(TRI_T), lds, st, t);
+    } else {
+        hipFuncSetAttribute((const void*)k_tridiag<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_tridiag<false>, dim3(nwg), dim3(TRI_T), lds, st, t);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (marks) hipEventRecord(marks[1], st);
     VecArgs v;

@@ -127,12 +127,18 @@ def test_eigensolver_rows_beyond_lds(eng):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
-@pytest.mark.parametrize("n,nwg", [(700, 70), (700, 256), (1500, 40), (1500, 150), (2100, 210)])
-def test_eigensolver_workgroup_counts(eng, n, nwg, monkeypatch):
-    """Same eigenpairs for any number of tridiagonalisation workgroups (rows in
-    LDS or in HBM; up to one workgroup per CU)."""
+@pytest.mark.parametrize("xcd", ["0", "1"])
+@pytest.mark.parametrize("wave", ["0", "1"])
+@pytest.mark.parametrize("n,nwg", [(323, 8), (323, 32), (323, 64), (500, 48), (700, 70), (700, 256), (1500, 40),
+                                   (1500, 150), (2100, 210)])
+def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, wave, monkeypatch):
+    """Same eigenpairs for any number of tridiagonalisation workgroups, either
+    hand-off (cross-XCD write-through or one-XCD L2), either kernel (wave
+    agents or workgroup barriers), rows in LDS or in HBM."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
+    monkeypatch.setenv("SCC_EIG_XCD", xcd)
+    monkeypatch.setenv("SCC_EIG_WAVE", wave)
     rng = np.random.default_rng(11)
     X = rng.standard_normal((n, 900)) * np.linspace(3.0, 0.5, n)[:, None]
     X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 900)) * 4.0
