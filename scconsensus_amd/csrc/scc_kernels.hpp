@@ -29,7 +29,7 @@ struct ScStatsLaunch {
 // segment) or one value bucket of a split gene (src 1: keys2 / codes2)
 struct ScRankItem {
     long long base;
-    int n, gene, src;
+    int n, gene, src, bucket;  // bucket: global bucket id (its cluster histogram row), -1 none
 };
 
 struct ScRankLaunch {
@@ -41,8 +41,13 @@ struct ScRankLaunch {
     const uint8_t* flags;  // [P][G] bit0: the pair tests the gene
     int cap_s, cap_m, cap_lds, bucket_target, ntp_max, item_cap;
     int med_wide;          // medium items: 1024 threads, one workgroup per CU
+    int wave_target;       // split: bins are packed into buckets of < 2 * wave_target elements
+    int bucket_cap;        // capacity of sbuckets / hbg rows
+    ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)
+    unsigned int* hbg;     // [bucket_cap][K] per-bucket cluster counts
+    int* gene_bk;          // [2 G] first bucket id and bucket count of each split gene
     ScRankItem* items;     // [3][item_cap]
-    int* counts;           // [0..2] items per class, [3] split genes
+    int* counts;           // [0..2] items per class, [3] split genes, [4] wave buckets, [5] bucket ids
     int* split_genes;      // [G]
     unsigned long long* keys2;  // [nnz] bucket-ordered keys of split genes
     uint8_t* codes2;            // [nnz]
@@ -135,6 +140,8 @@ int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim);
 size_t scc_rank_split_lds(int K);
 hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st);
+hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st);
+hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid_genes, hipStream_t st);
 hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st);
 size_t scc_eigen_scratch_doubles(int n, int lda, int k);
 hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,

@@ -166,14 +166,8 @@ __global__ void k_rank_classify(ScRankLaunch A)
         for (int p = 0; p < A.P && !any; ++p) any = (A.flags[(size_t)p * A.G + g] & 1) != 0;
         if (!any) return;
     }
-    if (n > A.cap_m) {
-        const int s = atomicAdd(&A.counts[3], 1);
-        A.split_genes[s] = g;
-        return;
-    }
-    const int cls = (n <= A.cap_s) ? 0 : 1;
-    const int s = atomicAdd(&A.counts[cls], 1);
-    A.items[(size_t)cls * A.item_cap + s] = ScRankItem{base, (int)n, g, 0};
+    const int s = atomicAdd(&A.counts[3], 1);  // every ranked gene is split into value buckets
+    A.split_genes[s] = g;
 }
 
 extern "C" hipError_t scc_launch_rank_classify(const ScRankLaunch* L, hipStream_t st)
@@ -521,6 +515,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
     }
     __syncthreads();
     const int ntp = L.ntp;
+    if (it.bucket >= 0 && tid < K) A.hbg[(size_t)it.bucket * K + tid] = L.m[tid];
     ISTAMP(1);
     if (kmin == kmax) {
         // one distinct value: every pair is a tie, no order needed
@@ -781,11 +776,13 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
     }
 }
 
+#define RW_SLOTS 4  // tested pairs per gene the wave kernel holds: 64 * RW_SLOTS
+
 // ===================================================================== split
 #define SP_T 1024
 #define SP_W (SP_T / 64)
 #define SP_BINS 2048
-#define SP_BMAX 512
+#define SP_BMAX (2 * SP_BINS + 1)  // a bucket starts at a bin, or right after a fat bin
 
 struct SplitLds {
     u32 hist[SP_BINS];
@@ -793,14 +790,21 @@ struct SplitLds {
     u32 bid[SP_BINS];   // bucket of each bin
     u32 bcur[SP_BMAX];  // bucket cursors
     u32 boff[SP_BMAX + 1];
+    u64 rep[SP_BINS];      // one key of each bin (any: the last leader's store wins)
+    u8 bdiff[SP_BMAX + 3]; // bucket holds two different keys
     u32 wsum[SP_W + 1];
     u32 wsum2[SP_W + 1];
     u64 rmn[SP_W], rmx[SP_W];
     int off[65];
-    int nb;
-    u32 hb[1];  // [SP_BMAX][K] per-bucket cluster counts (dynamic)
+    int nb, bk0;
 };
 
+// One ranked gene: 2048-bin histogram of its key window, bins packed into
+// value buckets of < 2 * target elements (a bin of more than `target` is a
+// bucket of its own), elements scattered into bucket order (keys2 / codes2
+// over the gene's own range).  Buckets of <= 64 elements go to the wave
+// kernel, larger ones (fat bins) to the LDS item kernel.  Every bucket gets a
+// global id: its cluster histogram row in hbg, written by whoever ranks it.
 __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
 {
     const int K = A.K, G = A.G;
@@ -810,7 +814,17 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     const u64* key = A.keys + base;
     if (tid <= K) L.off[tid] = (int)A.coff[(size_t)A.cl_cc[tid] * G + g];
     for (int i = tid; i < SP_BINS; i += SP_T) L.hist[i] = 0;
-    for (int i = tid; i < SP_BMAX * K; i += SP_T) L.hb[i] = 0;
+    // tested pairs of the gene (the wave kernel holds at most 64 * RW_SLOTS)
+    {
+        u32 t = 0;
+        for (int p = tid; p < A.P; p += SP_T) t += (A.all_pairs || (A.flags[(size_t)p * G + g] & 1)) ? 1u : 0u;
+        t = u32_wave_sum(t);
+        if (lane == 0) L.wsum2[w] = t;
+    }
+    __syncthreads();
+    u32 ntested = 0;
+    for (int v = 0; v < SP_W; ++v) ntested += L.wsum2[v];
+    const bool waves_ok = ntested <= 64 * RW_SLOTS;
     // key range of the gene (min / max over its nonzeros)
     u64 kmn = ~0ull, kmx = 0;
     for (int i = tid; i < n; i += SP_T) {
@@ -843,7 +857,10 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         const bool ok = i < n;
         const u32 d = ok ? (u32)((key[i] - kmn) >> sh) : 0u;
         const u64 peers = match_bits<11>(d, __ballot(ok));
-        if (ok && lanes_below(peers) == 0) atomicAdd(&L.hist[d], (u32)__popcll(peers));
+        if (ok && lanes_below(peers) == 0) {
+            atomicAdd(&L.hist[d], (u32)__popcll(peers));
+            L.rep[d] = key[i];
+        }
     }
     __syncthreads();
     // ---- 2. exclusive scan of the bins (2 per thread)
@@ -864,10 +881,8 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     }
     __syncthreads();
     // ---- 3. buckets: runs of bins with equal floor(excl / target); a bin of
-    // more than `target` elements is a bucket of its own.  Buckets hold at most
-    // 2 target elements (unless one bin alone is larger), and there are at most
-    // 1 + 3 n / target of them (<= SP_BMAX by the choice of target).
-    const u32 target = max((u32)A.bucket_target, (u32)((3 * (i64)n + SP_BMAX - 3) / (SP_BMAX - 2)));
+    // more than `target` elements is a bucket of its own
+    const u32 target = (u32)A.wave_target;
     {
         u32 st[2];
         for (int q = 0; q < 2; ++q) {
@@ -886,7 +901,6 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         __syncthreads();
         u32 b = incl - v;
         for (int q = 0; q < w; ++q) b += L.wsum2[q];
-        // bucket id = number of starts up to and including this bin, minus 1
         L.bid[2 * tid] = b + st[0] - 1;
         L.bid[2 * tid + 1] = b + st[0] + st[1] - 1;
         if (st[0]) L.boff[b] = L.excl[2 * tid];
@@ -894,14 +908,19 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         if (tid == SP_T - 1) {
             L.nb = (int)(b + v);
             L.boff[b + v] = (u32)n;
+            L.bk0 = atomicAdd(&A.counts[5], (int)(b + v));
+            A.gene_bk[2 * g] = L.bk0;
+            A.gene_bk[2 * g + 1] = (int)(b + v);
         }
     }
     __syncthreads();
-    const int nb = L.nb;
-    for (int q = tid; q < nb; q += SP_T) L.bcur[q] = L.boff[q];
+    const int nb = L.nb, bk0 = L.bk0;
+    for (int q = tid; q < nb; q += SP_T) {
+        L.bcur[q] = L.boff[q];
+        L.bdiff[q] = 0;
+    }
     __syncthreads();
-    // ---- 4. scatter into bucket order (keys2 / codes2 over the gene's own
-    // range), per-bucket cluster counts
+    // ---- 4. scatter into bucket order (keys2 / codes2 over the gene's own range)
     int a = 0;
     for (int i0 = 0; i0 < n; i0 += SP_T) {
         const int i = i0 + tid;
@@ -913,7 +932,6 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
             d = (u32)((k - kmn) >> sh);
             while (a + 1 < K && L.off[a + 1] <= i) ++a;
         }
-        const u32 c = (u32)a;
         const u64 peers = match_bits<11>(d, __ballot(ok));
         const u32 bk = ok ? L.bid[d] : 0u;
         const u32 rank = lanes_below(peers);
@@ -923,32 +941,28 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         basev = __shfl(basev, leader, 64);
         if (ok) {
             A.keys2[base + basev + rank] = k;
-            A.codes2[base + basev + rank] = (u8)c;
+            A.codes2[base + basev + rank] = (u8)a;
+            if (k != L.rep[d]) L.bdiff[bk] = 1;
         }
-        const u64 pc = match_bits<6>(c, peers);  // same bucket and cluster
-        if (ok && lanes_below(pc) == 0) atomicAdd(&L.hb[(size_t)bk * K + c], (u32)__popcll(pc));
     }
     __syncthreads();
-    // ---- 5. cross-bucket rank sums of the tested pairs: sum over buckets of
-    // h_beta[a] * #(b-elements in lower buckets)
-    for (int p = tid; p < A.P; p += SP_T) {
-        if (!A.all_pairs && !(A.flags[(size_t)p * G + g] & 1)) continue;
-        int pa, pb;
-        pair_decode(p, K, pa, pb);
-        u64 s = 0, below = 0;
-        for (int q = 0; q < nb; ++q) {
-            s += (u64)L.hb[(size_t)q * K + pa] * below;
-            below += L.hb[(size_t)q * K + pb];
-        }
-        if (s) atomicAdd((unsigned long long*)&A.accS[(size_t)p * G + g], (unsigned long long)s);
-    }
-    // ---- 6. one work item per non-empty bucket
+    // ---- 5. one work unit per bucket (empty buckets: a zero histogram row)
     for (int q = tid; q < nb; q += SP_T) {
         const int c = (int)(L.boff[q + 1] - L.boff[q]);
-        if (c <= 0) continue;
-        const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
-        const int s = atomicAdd(&A.counts[cls], 1);
-        A.items[(size_t)cls * A.item_cap + s] = ScRankItem{base + L.boff[q], c, g, 1};
+        const int bid = bk0 + q;
+        if (c <= 0) {
+            for (int k2 = 0; k2 < K; ++k2) A.hbg[(size_t)bid * K + k2] = 0;
+            continue;
+        }
+        // a bucket of one repeated key (a fat bin of ties): closed form in the wave kernel
+        const bool ties_only = c > 64 && !L.bdiff[q];
+        const ScRankItem itm{base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
+        if ((c <= 64 || ties_only) && waves_ok) {
+            A.sbuckets[atomicAdd(&A.counts[4], 1)] = itm;
+        } else {
+            const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
+            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+        }
     }
     __syncthreads();
 }
@@ -959,6 +973,305 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
     SplitLds& L = *(SplitLds*)smem;
     const int cnt = A.counts[3];
     for (int i = blockIdx.x; i < cnt; i += gridDim.x) split_one_gene(A, A.split_genes[i], L);
+}
+
+// ===================================================================== waves
+// One wave per bucket of <= 64 elements: bitonic sort of (key, cluster) across
+// the lanes (DPP / permlane swaps, no LDS), one ballot mask per cluster over
+// the sorted lanes, then every lane computes its own tested pair's S (and the
+// tie terms E, X) from the two masks (pair_counts).  Buckets of one repeated
+// key (fat bins of ties) need only their cluster histogram.  Consecutive
+// buckets of one gene accumulate in registers (lane j: tested pair j) and are
+// flushed with one integer atomic per pair when the gene changes.
+
+// Wave sum through DPP (no LDS round trip): quad butterflies, half-row and
+// row mirrors give every lane its 16-lane row total, row_bcast15 / row_bcast31
+// carry the totals up; lane 63 ends with the sum.
+__device__ inline u32 wave_sum_u32(u32 v)
+{
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, true);   // row_half_mirror
+    x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, true);   // row_mirror
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast31 -> rows 2, 3
+    return (u32)__builtin_amdgcn_readlane(x, 63);
+}
+
+// Value of lane (this lane ^ S) without LDS: DPP inside a 16-lane row,
+// v_permlane16/32_swap across rows (gfx950).
+template <int S>
+__device__ inline u32 xor_lane(u32 v)
+{
+    const int x = (int)v;
+    if constexpr (S == 1) {
+        return (u32)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    } else if constexpr (S == 2) {
+        return (u32)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    } else if constexpr (S == 4) {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xF, 0xF, true);  // row_shl:4
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+        return (u32)((__lane_id() & 4) ? dn : up);
+    } else if constexpr (S == 8) {
+        return (u32)__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, true);  // row_ror:8
+    } else if constexpr (S == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (__lane_id() & 16) ? r[0] : r[1];
+    } else {
+        static_assert(S == 32, "xor_lane: stride");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (__lane_id() & 32) ? r[0] : r[1];
+    }
+}
+
+__device__ inline u64 shfl_u64(u64 v, int src)
+{
+    const u32 lo = (u32)__shfl((int)(u32)v, src, 64), hi = (u32)__shfl((int)(u32)(v >> 32), src, 64);
+    return ((u64)hi << 32) | lo;
+}
+
+// One pair's counts over a sorted bucket from its cluster masks, walking the
+// set bits of the smaller one: S_ab = sum_{i in a} #b below i = sum_{j in b}
+// #a above j; with ties (gst: lanes starting a group of equal keys, n: valid
+// lanes) E_ab = sum over groups c_a c_b and X_ab = sum c_a c_b (c_a + c_b).
+__device__ inline void pair_counts(u64 ma, u64 mb, bool ties, u64 gst, int n, u32& S, u32& E, u32& X)
+{
+    const bool walk_a = __popcll(ma) <= __popcll(mb);
+    u64 m = walk_a ? ma : mb;
+    const u64 self = m, other = walk_a ? mb : ma;
+    S = E = X = 0;
+    while (m) {
+        const int i = __builtin_ctzll(m);
+        m &= m - 1;
+        const u64 le = (2ull << i) - 1;  // lanes <= i (all of them for i = 63)
+        S += (u32)__popcll(other & (walk_a ? (le >> 1) : ~le));
+        if (ties) {
+            const int gsl = 63 - __clzll((long long)(gst & le));
+            const u64 aft = gst & ~le;
+            const int ge = aft ? __builtin_ctzll(aft) : n;
+            const u64 grp = ((ge >= 64) ? ~0ull : ((1ull << ge) - 1)) & ~((1ull << gsl) - 1);
+            const u32 co = (u32)__popcll(other & grp), cs = (u32)__popcll(self & grp);
+            E += co;
+            X += co * (co + cs);
+        }
+    }
+}
+
+// One bitonic merge level of (key, code) across the lanes, strides ST .. 1.
+template <int ST>
+__device__ inline void bitonic_merge(u64& key, u32& code, bool up, int lane)
+{
+    const u64 ok = ((u64)xor_lane<ST>((u32)(key >> 32)) << 32) | (u64)xor_lane<ST>((u32)key);
+    const u32 oc = xor_lane<ST>(code);
+    const bool lower = (lane & ST) == 0;
+    const bool other_less = (ok < key) || (ok == key && oc < code);
+    if ((lower == up) ? other_less : !other_less) {
+        key = ok;
+        code = oc;
+    }
+    if constexpr (ST > 1) bitonic_merge<ST / 2>(key, code, up, lane);
+}
+
+__global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
+{
+    __shared__ u32 tpl[4][64 * RW_SLOTS];  // per-wave staging of the compacted pair list
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
+    const int cnt = A.counts[4];
+    const int K = A.K, G = A.G, P = A.P;
+    constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality)
+    int cur = -1, ntp = 0;
+    u32 pa[RW_SLOTS], pb[RW_SLOTS], pp[RW_SLOTS];
+    u64 aS[RW_SLOTS], aE[RW_SLOTS], aX[RW_SLOTS];
+#pragma unroll
+    for (int q = 0; q < RW_SLOTS; ++q) {
+        pa[q] = pb[q] = pp[q] = 0;
+        aS[q] = aE[q] = aX[q] = 0;
+    }
+    for (int c0 = W * CH; c0 < cnt; c0 += NW * CH) {
+        const int c1 = min(cnt, c0 + CH);
+        for (int bi = c0; bi < c1; ++bi) {
+            const ScRankItem B = A.sbuckets[bi];
+            const int g = __builtin_amdgcn_readfirstlane(B.gene);
+            const int n = __builtin_amdgcn_readfirstlane(B.n);
+            const int bucket = __builtin_amdgcn_readfirstlane(B.bucket);
+            if (g != cur) {
+                // flush the previous gene's sums: one integer atomic per pair
+                if (cur >= 0) {
+#pragma unroll
+                    for (int q = 0; q < RW_SLOTS; ++q) {
+                        if (q * 64 + lane < ntp) {
+                            const size_t o = (size_t)pp[q] * G + cur;
+                            if (aS[q]) atomicAdd((unsigned long long*)&A.accS[o], (unsigned long long)aS[q]);
+                            if (aE[q]) atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)aE[q]);
+                            if (aX[q]) atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)aX[q]);
+                        }
+                        aS[q] = aE[q] = aX[q] = 0;
+                    }
+                }
+                cur = g;
+                // tested pairs of g, compacted in pair order
+                int nt = 0;
+                for (int p0 = 0; p0 < P; p0 += 64) {
+                    const int p = p0 + lane;
+                    const bool t = p < P && (A.all_pairs || (A.flags[(size_t)p * G + g] & 1));
+                    const u64 bal = __ballot(t);
+                    const int r = nt + (int)lanes_below(bal);
+                    if (t && r < 64 * RW_SLOTS) tpl[wv][r] = (u32)p;
+                    nt += __popcll(bal);
+                }
+                ntp = min(nt, 64 * RW_SLOTS);  // the host never routes genes with more here
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+                for (int q = 0; q < RW_SLOTS; ++q) {
+                    const int j = q * 64 + lane;
+                    if (j < ntp) {
+                        const int pq = (int)tpl[wv][j];
+                        int a2, b2;
+                        pair_decode(pq, K, a2, b2);
+                        pp[q] = (u32)pq;
+                        pa[q] = (u32)a2;
+                        pb[q] = (u32)b2;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (__builtin_amdgcn_readfirstlane(B.src) == 2) {
+                // one repeated key: only the cluster histogram matters.  Inside
+                // the bucket S_ab = 0 (a < b: ties ordered by cluster),
+                // E_ab = c_a c_b, X_ab = c_a c_b (c_a + c_b), F_a = f(c_a).
+                u32 myc = 0;
+                for (int i0 = 0; i0 < n; i0 += 256) {
+                    u32 cd[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = i0 + u * 64 + lane;
+                        cd[u] = i < n ? (u32)A.codes2[B.base + i] : 255u;
+                    }
+                    for (int c = 0; c < K; ++c) {
+                        u32 t = 0;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) t += (u32)__popcll(__ballot(cd[u] == (u32)c));
+                        if (lane == c) myc += t;
+                    }
+                }
+                if (lane < K) {
+                    A.hbg[(size_t)bucket * K + lane] = myc;
+                    if (myc >= 2)
+                        atomicAdd((unsigned long long*)&A.accF[(size_t)lane * G + g], (unsigned long long)f_tie(myc));
+                }
+#pragma unroll
+                for (int q = 0; q < RW_SLOTS; ++q) {
+                    const u64 ca = (u32)__shfl((int)myc, (int)pa[q], 64);
+                    const u64 cb = (u32)__shfl((int)myc, (int)pb[q], 64);
+                    if (q * 64 + lane < ntp) {
+                        aE[q] += ca * cb;
+                        aX[q] += ca * cb * (ca + cb);
+                    }
+                }
+                continue;
+            }
+            // ---- load and bitonic sort by (key, code) across the lanes (invalid lanes last)
+            const bool vl = lane < n;
+            u64 key = vl ? A.keys2[B.base + lane] : ~0ull;
+            u32 code = vl ? (u32)A.codes2[B.base + lane] : 255u;
+            bitonic_merge<1>(key, code, (lane & 2) == 0, lane);
+            bitonic_merge<2>(key, code, (lane & 4) == 0, lane);
+            bitonic_merge<4>(key, code, (lane & 8) == 0, lane);
+            bitonic_merge<8>(key, code, (lane & 16) == 0, lane);
+            bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
+            bitonic_merge<32>(key, code, true, lane);
+            // ---- cluster masks over the sorted lanes (lane c holds cluster c's) and the hbg row
+            u64 cm = 0;
+            for (int c = 0; c < K; ++c) {
+                const u64 m = __ballot(code == (u32)c);
+                if (lane == c) cm = m;
+            }
+            if (lane < K) A.hbg[(size_t)bucket * K + lane] = (u32)__popcll(cm);
+            // ---- tie groups (equal keys) and runs (equal key and cluster)
+            const u64 kp = ((u64)(u32)__shfl_up((int)(u32)(key >> 32), 1, 64) << 32) |
+                           (u64)(u32)__shfl_up((int)(u32)key, 1, 64);
+            const u32 cpv = (u32)__shfl_up((int)code, 1, 64);
+            const u64 vmask = (n >= 64) ? ~0ull : ((1ull << n) - 1);
+            const bool gs_me = (lane == 0) || (kp != key);
+            const u64 gst = __ballot(gs_me && vl);
+            const bool anytie = ((~gst) & vmask & ~1ull) != 0;
+            if (anytie) {
+                // within-cluster runs: F_a += len^3 - len per run of >= 2
+                const u64 le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= me
+                const bool rs_me = (lane == 0) || (kp != key) || (cpv != code);
+                const u64 rst = __ballot(rs_me && vl);
+                if (rs_me && vl) {
+                    const u64 raft = rst & ~le;
+                    const int re = raft ? __builtin_ctzll(raft) : n;
+                    const u64 len = (u64)(re - lane);
+                    if (len >= 2)
+                        atomicAdd((unsigned long long*)&A.accF[(size_t)code * G + g], (unsigned long long)f_tie(len));
+                }
+            }
+            // ---- tested pairs: lane l of slot q owns pair q * 64 + l
+#pragma unroll
+            for (int q = 0; q < RW_SLOTS; ++q) {
+                if (q * 64 >= ntp) break;
+                const u64 ma = shfl_u64(cm, (int)pa[q]), mb = shfl_u64(cm, (int)pb[q]);
+                if (q * 64 + lane < ntp && ma && mb) {
+                    u32 S, E, X;
+                    pair_counts(ma, mb, anytie, gst, n, S, E, X);
+                    aS[q] += S;
+                    aE[q] += E;
+                    aX[q] += X;
+                }
+            }
+        }
+    }
+    if (cur >= 0) {
+#pragma unroll
+        for (int q = 0; q < RW_SLOTS; ++q) {
+            if (q * 64 + lane < ntp) {
+                const size_t o = (size_t)pp[q] * G + cur;
+                if (aS[q]) atomicAdd((unsigned long long*)&A.accS[o], (unsigned long long)aS[q]);
+                if (aE[q]) atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)aE[q]);
+                if (aX[q]) atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)aX[q]);
+            }
+        }
+    }
+}
+
+// ===================================================================== cross
+// Cross-bucket rank sums: for tested pair (a, b) of gene g,
+//   S_ab += sum over buckets beta of h_beta[a] * #(b-elements in buckets < beta)
+// one wave per (gene, pair), lanes over buckets (inclusive scan per 64).
+__global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
+{
+    const int lane = threadIdx.x & 63;
+    const int W = blockIdx.x * 4 + scc_wave_id(), NW = gridDim.x * 4;
+    const int ng = A.counts[3], P = A.P;
+    for (int f = W; f < ng * P; f += NW) {
+        const int gi = f / P, p = f - gi * P;
+        const int g = A.split_genes[gi];
+        if (!A.all_pairs && !(A.flags[(size_t)p * A.G + g] & 1)) continue;
+        int a, b;
+        pair_decode(p, A.K, a, b);
+        const int bk0 = A.gene_bk[2 * g], nb = A.gene_bk[2 * g + 1];
+        const unsigned int* h = A.hbg + (size_t)bk0 * A.K;
+        u64 s = 0, carry = 0;
+        for (int q0 = 0; q0 < nb; q0 += 64) {
+            const int q = q0 + lane;
+            const u32 ha = (q < nb) ? h[(size_t)q * A.K + a] : 0u;
+            const u32 hb = (q < nb) ? h[(size_t)q * A.K + b] : 0u;
+            u32 inc = hb;
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += y;
+            }
+            s += (u64)ha * (carry + inc - hb);
+            carry += (u32)__shfl((int)inc, 63, 64);
+        }
+        s = u64_wave_sum(s);
+        if (lane == 0 && s) atomicAdd((unsigned long long*)&A.accS[(size_t)p * A.G + g], (unsigned long long)s);
+    }
 }
 
 // ===================================================================== host
@@ -998,7 +1311,23 @@ extern "C" int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim)
     return cap;
 }
 
-extern "C" size_t scc_rank_split_lds(int K) { return sizeof(SplitLds) + sizeof(u32) * (size_t)SP_BMAX * K; }
+extern "C" size_t scc_rank_split_lds(int K)
+{
+    (void)K;
+    return sizeof(SplitLds);
+}
+
+extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_rank_waves, dim3(grid), dim3(256), 0, st, *L);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_rank_cross, dim3(grid), dim3(256), 0, st, *L);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st)
 {

@@ -301,7 +301,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         d_gexp = (dd*)((char*)p + sizeof(double) * 2 * nwaves);
     }
     WS("splitg", (size_t)G, d_splitg);
-    WS("counts", 4, d_counts);
+    WS("counts", 8, d_counts);
     WS("err", 4, d_err);
     WS("mx", GK, d_mx);
     WS("me", GK, d_me);
@@ -320,9 +320,17 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
                                                                    160 * 1024)
                                                : scc_rank_item_cap(1, env_int("SCC_CAP_MEDIUM", kCapMedium), ntp_max, K,
                                                                    80 * 1024));
+    const int wave_target = 32;  // value buckets of < 64 elements: one wave each
+    const int bucket_cap = (int)std::min<int64_t>(3 * nnz1 / wave_target + 2 * (int64_t)G + 64, 1 << 29);
+    const int item_cap = bucket_cap;
     const int bucket_target = std::max(64, cap_m / 2);
-    const int item_cap = G + (int)std::min<int64_t>(3 * nnz1 / bucket_target + 2 * (int64_t)G + 64, 1 << 28);
     WS("items", 3 * (size_t)item_cap, d_items);
+    ScRankItem* d_sbk;
+    unsigned int* d_hbg;
+    int* d_genebk;
+    WS("sbuckets", (size_t)bucket_cap, d_sbk);
+    WS("hbg", (size_t)bucket_cap * K, d_hbg);
+    WS("genebk", 2 * (size_t)G, d_genebk);
     WS("p", PG, d_p);
     WS("lfc", PG, d_lfc);
     WS("pct1", fast ? PG : 1, d_pct1);
@@ -349,7 +357,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     {
         Scope sc(c, "ingest", s0);
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
-        HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 4, s0));
+        HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 8, s0));
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, d_err, s0));
         uint32_t* d_cscr;
@@ -443,6 +451,11 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         L.cap_m = cap_m;
         L.med_wide = med_wide;
         L.bucket_target = bucket_target;
+        L.wave_target = wave_target;
+        L.bucket_cap = bucket_cap;
+        L.sbuckets = d_sbk;
+        L.hbg = d_hbg;
+        L.gene_bk = d_genebk;
         L.ntp_max = ntp_max;
         L.item_cap = item_cap;
         L.items = d_items;
@@ -471,15 +484,17 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         }
         HIPCHK(c, scc_launch_rank_classify(&L, s0));
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
-        HIPCHK(c, scc_launch_rank_split(&L, ncu, s0));
-        // small and medium items share the CUs (two streams), HBM-resident ones last
+        HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
+        // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS items)
         HIPCHK(c, hipEventRecord(c->ev_fork, s0));
         HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
-        HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, s0));
+        HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0));
+        HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, s1));
         HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, s1));
+        HIPCHK(c, scc_launch_rank_items(&L, 2, ncu, s1));
         HIPCHK(c, hipEventRecord(c->ev_join, s1));
         HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
-        HIPCHK(c, scc_launch_rank_items(&L, 2, ncu, s0));
+        HIPCHK(c, scc_launch_rank_cross(&L, 4 * ncu, s0));
         if (stamps) {
             std::vector<unsigned long long> h((size_t)3 * item_cap * 8);
             int cnts[4];
