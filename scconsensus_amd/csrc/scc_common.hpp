@@ -93,6 +93,64 @@ __device__ inline u32 u32_wave_sum(u32 x)
     return x;
 }
 
+// Value of lane (this lane ^ S) without an LDS round trip: DPP inside a
+// 16-lane row, v_permlane16/32_swap across rows (gfx950).  Whole-wave only:
+// every lane must be active.
+template <int S>
+__device__ inline u32 scc_xor_lane(u32 v)
+{
+    const int x = (int)v;
+    if constexpr (S == 1) {
+        return (u32)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    } else if constexpr (S == 2) {
+        return (u32)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+    } else if constexpr (S == 4) {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xF, 0xF, true);  // row_shl:4
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+        return (u32)((__lane_id() & 4) ? dn : up);
+    } else if constexpr (S == 8) {
+        return (u32)__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, true);  // row_ror:8
+    } else if constexpr (S == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (__lane_id() & 16) ? r[0] : r[1];
+    } else {
+        static_assert(S == 32, "scc_xor_lane: stride");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (__lane_id() & 32) ? r[0] : r[1];
+    }
+}
+template <int S>
+__device__ inline double scc_xor_lane_f64(double v)
+{
+    const u64 b = (u64)__double_as_longlong(v);
+    const u64 r = ((u64)scc_xor_lane<S>((u32)(b >> 32)) << 32) | scc_xor_lane<S>((u32)b);
+    return __longlong_as_double((long long)r);
+}
+template <int S>
+__device__ inline dd dd_xor_lane(dd x)
+{
+    return dd{scc_xor_lane_f64<S>(x.hi), scc_xor_lane_f64<S>(x.lo)};
+}
+// dd_wave_sum / u32_wave_sum without LDS (same butterfly order, whole wave only)
+__device__ inline dd dd_wave_sum_dpp(dd x)
+{
+    x = dd_add(x, dd_xor_lane<32>(x));
+    x = dd_add(x, dd_xor_lane<16>(x));
+    x = dd_add(x, dd_xor_lane<8>(x));
+    x = dd_add(x, dd_xor_lane<4>(x));
+    x = dd_add(x, dd_xor_lane<2>(x));
+    return dd_add(x, dd_xor_lane<1>(x));
+}
+__device__ inline u32 u32_wave_sum_dpp(u32 x)
+{
+    x += scc_xor_lane<32>(x);
+    x += scc_xor_lane<16>(x);
+    x += scc_xor_lane<8>(x);
+    x += scc_xor_lane<4>(x);
+    x += scc_xor_lane<2>(x);
+    return x + scc_xor_lane<1>(x);
+}
+
 // wave index inside the workgroup, as a wave-uniform (SGPR) value: loops
 // bounded by it stay scalar instead of being treated as divergent
 __device__ inline int scc_wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }

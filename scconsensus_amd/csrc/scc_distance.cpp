@@ -60,7 +60,7 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
     WS("d_umap", G, d_umap);
     WS("d_X", (size_t)Npad * ld, d_X);
     WS("d_mean", ld, d_mean);
-    const int nchunk_mean = 64;
+    const int nchunk_mean = 512;  // 2 x 512 workgroups over the column sums
     if ((rc = ws_get(c, "d_part", sizeof(double) * 2 * (size_t)nchunk_mean * ld, &d_part))) return rc;
     void* d_out = dist_out;
     if (out_kind == SCC_PTR_HOST || !dist_out) {  // NULL device output: keep it in the workspace

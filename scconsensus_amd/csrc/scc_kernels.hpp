@@ -42,10 +42,12 @@ struct ScRankLaunch {
     int cap_s, cap_m, cap_lds, bucket_target, ntp_max, item_cap;
     int med_wide;          // medium items: 1024 threads, one workgroup per CU
     int wave_target;       // split: bins are packed into buckets of < 2 * wave_target elements
+    int dbg;               // SCC_RW_DEBUG timing experiments (1: no pair counts, 2: no sort); results invalid
     int bucket_cap;        // capacity of sbuckets / hbg rows
     ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)
     unsigned int* hbg;     // [bucket_cap][K] per-bucket cluster counts
     int* gene_bk;          // [2 G] first bucket id and bucket count of each split gene
+    unsigned long long* gkmin;  // [G] key minimum of a split gene when its range fits 58 bits, else ~0
     ScRankItem* items;     // [3][item_cap]
     int* counts;           // [0..2] items per class, [3] split genes, [4] wave buckets, [5] bucket ids
     int* split_genes;      // [G]

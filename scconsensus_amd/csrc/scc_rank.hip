@@ -110,17 +110,22 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
         const int s0 = off[a] + (it - acc) * Lp, s1 = min(off[a + 1], s0 + Lp);
         dd sx{0.0, 0.0}, se{0.0, 0.0};
         u32 pos = 0, neg = 0;
-        for (int i = s0 + lane; i < s1; i += 64) {
-            const double x = scc_val_of(key[i]);
-            sx = dd_add_d(sx, x);
-            se = dd_add_d(se, expm1(x));
-            pos += (x > 0.0);
-            neg += (x < 0.0);
+        for (int i = s0 + lane; i < s1; i += 256) {
+            double x[4];  // 4 loads in flight; past the end adds +0 (exact no-op)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = (i + 64 * q < s1) ? scc_val_of(key[i + 64 * q]) : 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                sx = dd_add_d(sx, x[q]);
+                se = dd_add_d(se, expm1(x[q]));
+                pos += (x[q] > 0.0);
+                neg += (x[q] < 0.0);
+            }
         }
-        sx = dd_wave_sum(sx);
-        se = dd_wave_sum(se);
-        pos = u32_wave_sum(pos);
-        neg = u32_wave_sum(neg);
+        sx = dd_wave_sum_dpp(sx);
+        se = dd_wave_sum_dpp(se);
+        pos = u32_wave_sum_dpp(pos);
+        neg = u32_wave_sum_dpp(neg);
         if (lane == 0) item[it] = StatItem{sx.hi, sx.lo, se.hi, se.lo, pos, neg};
     }
     __syncthreads();
@@ -783,6 +788,8 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 #define SP_W (SP_T / 64)
 #define SP_BINS 2048
 #define SP_BMAX (2 * SP_BINS + 1)  // a bucket starts at a bin, or right after a fat bin
+#define SP_KPT 8                    // keys per thread held in registers across the passes
+#define SP_CHUNK (SP_T * SP_KPT)
 
 struct SplitLds {
     u32 hist[SP_BINS];
@@ -796,7 +803,7 @@ struct SplitLds {
     u32 wsum2[SP_W + 1];
     u64 rmn[SP_W], rmx[SP_W];
     int off[65];
-    int nb, bk0;
+    int nb, bk0, next;
 };
 
 // One ranked gene: 2048-bin histogram of its key window, bins packed into
@@ -825,12 +832,28 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     u32 ntested = 0;
     for (int v = 0; v < SP_W; ++v) ntested += L.wsum2[v];
     const bool waves_ok = ntested <= 64 * RW_SLOTS;
+    // the gene's keys stay in registers when they fit (SP_KPT per thread);
+    // larger genes re-read each chunk in every pass (from L2)
+    u64 kr[SP_KPT];
+    auto load_chunk = [&](int c0) {
+#pragma unroll
+        for (int q = 0; q < SP_KPT; ++q) {
+            const int i = c0 + q * SP_T + tid;
+            kr[q] = i < n ? key[i] : 0ull;
+        }
+    };
+    load_chunk(0);
     // key range of the gene (min / max over its nonzeros)
     u64 kmn = ~0ull, kmx = 0;
-    for (int i = tid; i < n; i += SP_T) {
-        const u64 k = key[i];
-        kmn = k < kmn ? k : kmn;
-        kmx = k > kmx ? k : kmx;
+    for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
+        if (c0) load_chunk(c0);
+#pragma unroll
+        for (int q = 0; q < SP_KPT; ++q) {
+            if (c0 + q * SP_T + tid < n) {
+                kmn = kr[q] < kmn ? kr[q] : kmn;
+                kmx = kr[q] > kmx ? kr[q] : kmx;
+            }
+        }
     }
     for (int m2 = 32; m2 >= 1; m2 >>= 1) {
         const u64 o1 = shfl_xor_u64(kmn, m2), o2 = shfl_xor_u64(kmx, m2);
@@ -851,15 +874,18 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     const u64 range = kmx - kmn;
     const int bits = range ? 64 - __clzll((long long)range) : 0;
     const int sh = bits > 11 ? bits - 11 : 0;
-    // ---- 1. histogram of the top 11 bits of the key window
-    for (int i0 = 0; i0 < n; i0 += SP_T) {
-        const int i = i0 + tid;
-        const bool ok = i < n;
-        const u32 d = ok ? (u32)((key[i] - kmn) >> sh) : 0u;
-        const u64 peers = match_bits<11>(d, __ballot(ok));
-        if (ok && lanes_below(peers) == 0) {
-            atomicAdd(&L.hist[d], (u32)__popcll(peers));
-            L.rep[d] = key[i];
+    if (tid == 0) A.gkmin[g] = bits <= 58 ? kmn : ~0ull;  // wave kernel: (key - kmin) << 6 | cluster
+    // ---- 1. histogram of the top 11 bits of the key window (one LDS atomic per
+    // element; any key of a bin is kept as its representative)
+    for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
+        if (n > SP_CHUNK) load_chunk(c0);
+#pragma unroll
+        for (int q = 0; q < SP_KPT; ++q) {
+            if (c0 + q * SP_T + tid < n) {
+                const u32 d = (u32)((kr[q] - kmn) >> sh);
+                atomicAdd(&L.hist[d], 1u);
+                L.rep[d] = kr[q];
+            }
         }
     }
     __syncthreads();
@@ -920,29 +946,24 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         L.bdiff[q] = 0;
     }
     __syncthreads();
-    // ---- 4. scatter into bucket order (keys2 / codes2 over the gene's own range)
-    int a = 0;
-    for (int i0 = 0; i0 < n; i0 += SP_T) {
-        const int i = i0 + tid;
-        const bool ok = i < n;
-        u64 k = 0;
-        u32 d = 0;
-        if (ok) {
-            k = key[i];
-            d = (u32)((k - kmn) >> sh);
-            while (a + 1 < K && L.off[a + 1] <= i) ++a;
-        }
-        const u64 peers = match_bits<11>(d, __ballot(ok));
-        const u32 bk = ok ? L.bid[d] : 0u;
-        const u32 rank = lanes_below(peers);
-        const int leader = __builtin_ctzll(peers ? peers : 1ull);
-        u32 basev = 0;
-        if (ok && rank == 0) basev = atomicAdd(&L.bcur[bk], (u32)__popcll(peers));
-        basev = __shfl(basev, leader, 64);
-        if (ok) {
-            A.keys2[base + basev + rank] = k;
-            A.codes2[base + basev + rank] = (u8)a;
-            if (k != L.rep[d]) L.bdiff[bk] = 1;
+    // ---- 4. scatter into bucket order (keys2 / codes2 over the gene's own range);
+    // the order inside a bucket is arbitrary (its ranker sorts by key and cluster)
+    for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
+        if (n > SP_CHUNK) load_chunk(c0);
+        int a = 0;
+#pragma unroll
+        for (int q = 0; q < SP_KPT; ++q) {
+            const int i = c0 + q * SP_T + tid;
+            if (i < n) {
+                while (a + 1 < K && L.off[a + 1] <= i) ++a;
+                const u64 k = kr[q];
+                const u32 d = (u32)((k - kmn) >> sh);
+                const u32 bk = L.bid[d];
+                const u32 pos = atomicAdd(&L.bcur[bk], 1u);
+                A.keys2[base + pos] = k;
+                A.codes2[base + pos] = (u8)a;
+                if (k != L.rep[d]) L.bdiff[bk] = 1;
+            }
         }
     }
     __syncthreads();
@@ -972,7 +993,13 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     SplitLds& L = *(SplitLds*)smem;
     const int cnt = A.counts[3];
-    for (int i = blockIdx.x; i < cnt; i += gridDim.x) split_one_gene(A, A.split_genes[i], L);
+    for (;;) {  // genes from a queue (their sizes vary by orders of magnitude)
+        if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[6], 1);
+        __syncthreads();
+        const int i = L.next;
+        if (i >= cnt) break;
+        split_one_gene(A, A.split_genes[i], L);
+    }
 }
 
 // ===================================================================== waves
@@ -999,30 +1026,14 @@ __device__ inline u32 wave_sum_u32(u32 v)
     return (u32)__builtin_amdgcn_readlane(x, 63);
 }
 
-// Value of lane (this lane ^ S) without LDS: DPP inside a 16-lane row,
-// v_permlane16/32_swap across rows (gfx950).
-template <int S>
-__device__ inline u32 xor_lane(u32 v)
+// The same merge on one combined key (key - gene minimum) << 6 | cluster.
+template <int ST>
+__device__ inline void bitonic_merge_ck(u64& ck, bool up, int lane)
 {
-    const int x = (int)v;
-    if constexpr (S == 1) {
-        return (u32)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
-    } else if constexpr (S == 2) {
-        return (u32)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
-    } else if constexpr (S == 4) {
-        const int up = __builtin_amdgcn_update_dpp(0, x, 0x104, 0xF, 0xF, true);  // row_shl:4
-        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
-        return (u32)((__lane_id() & 4) ? dn : up);
-    } else if constexpr (S == 8) {
-        return (u32)__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, true);  // row_ror:8
-    } else if constexpr (S == 16) {
-        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-        return (__lane_id() & 16) ? r[0] : r[1];
-    } else {
-        static_assert(S == 32, "xor_lane: stride");
-        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-        return (__lane_id() & 32) ? r[0] : r[1];
-    }
+    const u64 o = ((u64)scc_xor_lane<ST>((u32)(ck >> 32)) << 32) | (u64)scc_xor_lane<ST>((u32)ck);
+    const bool keep_min = ((lane & ST) == 0) == up;
+    ck = keep_min ? (o < ck ? o : ck) : (o < ck ? ck : o);
+    if constexpr (ST > 1) bitonic_merge_ck<ST / 2>(ck, up, lane);
 }
 
 __device__ inline u64 shfl_u64(u64 v, int src)
@@ -1062,8 +1073,8 @@ __device__ inline void pair_counts(u64 ma, u64 mb, bool ties, u64 gst, int n, u3
 template <int ST>
 __device__ inline void bitonic_merge(u64& key, u32& code, bool up, int lane)
 {
-    const u64 ok = ((u64)xor_lane<ST>((u32)(key >> 32)) << 32) | (u64)xor_lane<ST>((u32)key);
-    const u32 oc = xor_lane<ST>(code);
+    const u64 ok = ((u64)scc_xor_lane<ST>((u32)(key >> 32)) << 32) | (u64)scc_xor_lane<ST>((u32)key);
+    const u32 oc = scc_xor_lane<ST>(code);
     const bool lower = (lane & ST) == 0;
     const bool other_less = (ok < key) || (ok == key && oc < code);
     if ((lower == up) ? other_less : !other_less) {
@@ -1082,6 +1093,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
     const int K = A.K, G = A.G, P = A.P;
     constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality)
     int cur = -1, ntp = 0;
+    u64 gk = ~0ull;
     u32 pa[RW_SLOTS], pb[RW_SLOTS], pp[RW_SLOTS];
     u64 aS[RW_SLOTS], aE[RW_SLOTS], aX[RW_SLOTS];
 #pragma unroll
@@ -1091,11 +1103,38 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
     }
     for (int c0 = W * CH; c0 < cnt; c0 += NW * CH) {
         const int c1 = min(cnt, c0 + CH);
+        // the chunk's descriptors, one per lane, and the first bucket's elements:
+        // every bucket's loads are issued one bucket ahead
+        ScRankItem D{0, 0, 0, 0, 0};
+        if (lane < c1 - c0) D = A.sbuckets[c0 + lane];
+        const u32 dlo = (u32)(u64)D.base, dhi = (u32)((u64)D.base >> 32);
+        auto dbase = [&](int li) {
+            return (i64)(((u64)(u32)__builtin_amdgcn_readlane((int)dhi, li) << 32) |
+                         (u32)__builtin_amdgcn_readlane((int)dlo, li));
+        };
+        u64 nkey;
+        u32 ncode;
+        {
+            const i64 b0 = dbase(0);
+            const int n0 = __builtin_amdgcn_readlane(D.n, 0);
+            nkey = lane < n0 ? A.keys2[b0 + lane] : ~0ull;
+            ncode = lane < n0 ? (u32)A.codes2[b0 + lane] : 255u;
+        }
         for (int bi = c0; bi < c1; ++bi) {
-            const ScRankItem B = A.sbuckets[bi];
-            const int g = __builtin_amdgcn_readfirstlane(B.gene);
-            const int n = __builtin_amdgcn_readfirstlane(B.n);
-            const int bucket = __builtin_amdgcn_readfirstlane(B.bucket);
+            const int li = bi - c0;
+            const int g = __builtin_amdgcn_readlane(D.gene, li);
+            const int n = __builtin_amdgcn_readlane(D.n, li);
+            const int bucket = __builtin_amdgcn_readlane(D.bucket, li);
+            const int src = __builtin_amdgcn_readlane(D.src, li);
+            const i64 bbase = dbase(li);
+            u64 key = nkey;
+            u32 code = ncode;
+            if (bi + 1 < c1) {
+                const i64 b1 = dbase(li + 1);
+                const int n1 = __builtin_amdgcn_readlane(D.n, li + 1);
+                nkey = lane < n1 ? A.keys2[b1 + lane] : ~0ull;
+                ncode = lane < n1 ? (u32)A.codes2[b1 + lane] : 255u;
+            }
             if (g != cur) {
                 // flush the previous gene's sums: one integer atomic per pair
                 if (cur >= 0) {
@@ -1111,6 +1150,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                     }
                 }
                 cur = g;
+                gk = A.gkmin[g];
                 // tested pairs of g, compacted in pair order
                 int nt = 0;
                 for (int p0 = 0; p0 < P; p0 += 64) {
@@ -1138,7 +1178,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-            if (__builtin_amdgcn_readfirstlane(B.src) == 2) {
+            if (src == 2) {
                 // one repeated key: only the cluster histogram matters.  Inside
                 // the bucket S_ab = 0 (a < b: ties ordered by cluster),
                 // E_ab = c_a c_b, X_ab = c_a c_b (c_a + c_b), F_a = f(c_a).
@@ -1148,7 +1188,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int i = i0 + u * 64 + lane;
-                        cd[u] = i < n ? (u32)A.codes2[B.base + i] : 255u;
+                        cd[u] = i < n ? (u32)A.codes2[bbase + i] : 255u;
                     }
                     for (int c = 0; c < K; ++c) {
                         u32 t = 0;
@@ -1175,14 +1215,26 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             }
             // ---- load and bitonic sort by (key, code) across the lanes (invalid lanes last)
             const bool vl = lane < n;
-            u64 key = vl ? A.keys2[B.base + lane] : ~0ull;
-            u32 code = vl ? (u32)A.codes2[B.base + lane] : 255u;
-            bitonic_merge<1>(key, code, (lane & 2) == 0, lane);
-            bitonic_merge<2>(key, code, (lane & 4) == 0, lane);
-            bitonic_merge<4>(key, code, (lane & 8) == 0, lane);
-            bitonic_merge<8>(key, code, (lane & 16) == 0, lane);
-            bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
-            bitonic_merge<32>(key, code, true, lane);
+            if (A.dbg == 2) {
+            } else if (gk != ~0ull) {  // one 64-bit sort key: (key - gene minimum) << 6 | cluster
+                u64 ck = vl ? (((key - gk) << 6) | code) : ~0ull;
+                // levels up to the next power of two >= n (lanes past it hold only ~0)
+                if (n > 1) bitonic_merge_ck<1>(ck, (lane & 2) == 0, lane);
+                if (n > 2) bitonic_merge_ck<2>(ck, (lane & 4) == 0, lane);
+                if (n > 4) bitonic_merge_ck<4>(ck, (lane & 8) == 0, lane);
+                if (n > 8) bitonic_merge_ck<8>(ck, (lane & 16) == 0, lane);
+                if (n > 16) bitonic_merge_ck<16>(ck, (lane & 32) == 0, lane);
+                if (n > 32) bitonic_merge_ck<32>(ck, true, lane);
+                key = ck >> 6;  // order-equivalent for the tie tests below
+                code = vl ? (u32)(ck & 63u) : 255u;
+            } else {
+                if (n > 1) bitonic_merge<1>(key, code, (lane & 2) == 0, lane);
+                if (n > 2) bitonic_merge<2>(key, code, (lane & 4) == 0, lane);
+                if (n > 4) bitonic_merge<4>(key, code, (lane & 8) == 0, lane);
+                if (n > 8) bitonic_merge<8>(key, code, (lane & 16) == 0, lane);
+                if (n > 16) bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
+                if (n > 32) bitonic_merge<32>(key, code, true, lane);
+            }
             // ---- cluster masks over the sorted lanes (lane c holds cluster c's) and the hbg row
             u64 cm = 0;
             for (int c = 0; c < K; ++c) {
@@ -1214,7 +1266,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             // ---- tested pairs: lane l of slot q owns pair q * 64 + l
 #pragma unroll
             for (int q = 0; q < RW_SLOTS; ++q) {
-                if (q * 64 >= ntp) break;
+                if (q * 64 >= ntp || A.dbg == 1) break;
                 const u64 ma = shfl_u64(cm, (int)pa[q]), mb = shfl_u64(cm, (int)pb[q]);
                 if (q * 64 + lane < ntp && ma && mb) {
                     u32 S, E, X;

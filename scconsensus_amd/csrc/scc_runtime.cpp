@@ -331,6 +331,8 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     WS("sbuckets", (size_t)bucket_cap, d_sbk);
     WS("hbg", (size_t)bucket_cap * K, d_hbg);
     WS("genebk", 2 * (size_t)G, d_genebk);
+    unsigned long long* d_gkmin;
+    WS("gkmin", (size_t)G, d_gkmin);
     WS("p", PG, d_p);
     WS("lfc", PG, d_lfc);
     WS("pct1", fast ? PG : 1, d_pct1);
@@ -452,10 +454,12 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         L.med_wide = med_wide;
         L.bucket_target = bucket_target;
         L.wave_target = wave_target;
+        L.dbg = env_int("SCC_RW_DEBUG", 0);
         L.bucket_cap = bucket_cap;
         L.sbuckets = d_sbk;
         L.hbg = d_hbg;
         L.gene_bk = d_genebk;
+        L.gkmin = d_gkmin;
         L.ntp_max = ntp_max;
         L.item_cap = item_cap;
         L.items = d_items;
