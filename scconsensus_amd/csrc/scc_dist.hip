@@ -193,18 +193,19 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
 }
 
 // ------------------------------------------------------------------ Euclidean dist
-// Tile = DT_ROWS rows (2 per thread: i and i + 256) x DT_COLS columns (j); the
-// stores of one column are contiguous in the packed R order
-// out[j*(2N-j-1)/2 + i-j-1].  The tile's column scores sit in LDS and are read
-// as broadcasts; per element the sum of squared differences over the k <= 15
-// components (padding column 15 is zero), FMA-accumulated, and the hardware
-// sqrt: the distance contract is 1e-5 absolute (BASELINE north_star), and
-// the kernel is fp64-issue bound.  Only lower-triangle tiles are enumerated
-// (column blocks in order, row blocks rb >= cb / DT_RATIO), dealt to the XCDs
-// in runs of DT_RUN consecutive tiles: neighbouring row blocks of one column
-// block share a cache line at every column boundary, and a run keeps those
-// lines in one XCD's L2 instead of two partial write-backs.
-#define DT_ROWS 512
+// Tile = DT_ROWS rows (i, one per thread) x DT_COLS columns (j); the stores of
+// one column are contiguous in the packed R order out[j*(2N-j-1)/2 + i-j-1].
+// Column j's scores are uniform across the tile (scalar loads); per element
+// the sum of squared differences over the k <= 15 components (padding column
+// 15 is zero), FMA-accumulated, and the hardware sqrt: the distance contract
+// is 1e-5 absolute (BASELINE north_star).  The kernel is bound by the HBM
+// write stream (practical ceiling ~5.1 TB/s: scripts/write_bw.py).  Only
+// lower-triangle tiles are enumerated (column blocks in order, row blocks
+// rb >= cb / DT_RATIO), dealt to the XCDs in runs of DT_RUN consecutive tiles:
+// neighbouring row blocks of one column block share a cache line at every
+// column boundary, and a run keeps those lines in one XCD's L2 instead of two
+// partial write-backs.
+#define DT_ROWS 256
 #define DT_COLS 64
 #define DT_RATIO (DT_ROWS / DT_COLS)
 #define DT_RUN 8
@@ -223,56 +224,37 @@ __device__ inline void dist_tile_of(long long t, int nrb, int& cb, int& rb)
 }
 
 template <bool F32>
-__device__ inline void dist_store(void* out, size_t o, double d)
+__global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restrict__ P, int N, int nrb, long long ntiles,
+                                                         void* __restrict__ out)
 {
-    if (F32)
-        ((float*)out)[o] = (float)d;
-    else
-        ((double*)out)[o] = d;
-}
-
-template <bool F32>
-__global__ void __launch_bounds__(256) k_dist_euclid(const double* __restrict__ P, int N, int nrb, long long ntiles,
-                                                     void* __restrict__ out)
-{
-    __shared__ double2 sp[DT_COLS][8];
     // dispatch slot -> logical tile (slot x runs on XCD x % 8)
     const long long lin = blockIdx.x, k = lin >> 3, x = lin & 7;
     const long long t = ((k / DT_RUN) * 8 + x) * DT_RUN + k % DT_RUN;
     if (t >= ntiles) return;
     int cb, rb;
     dist_tile_of(t, nrb, cb, rb);
+    const int i = rb * DT_ROWS + (int)threadIdx.x;
     const int j0 = cb * DT_COLS, j1 = min(N, j0 + DT_COLS);
-    for (int e = threadIdx.x; e < DT_COLS * 8; e += 256) {
-        const int jj = e >> 3, q = e & 7;
-        sp[jj][q] = (j0 + jj < N) ? ((const double2*)(P + (size_t)(j0 + jj) * 16))[q] : double2{0.0, 0.0};
-    }
-    const int ia = rb * DT_ROWS + (int)threadIdx.x, ib = ia + 256;
-    double pa[15], pb[15];
+    if (i >= N) return;
+    double pi[15];
 #pragma unroll
-    for (int q = 0; q < 15; ++q) {
-        pa[q] = ia < N ? P[(size_t)ia * 16 + q] : 0.0;
-        pb[q] = ib < N ? P[(size_t)ib * 16 + q] : 0.0;
-    }
-    __syncthreads();
+    for (int q = 0; q < 15; ++q) pi[q] = P[(size_t)i * 16 + q];
+    const int jend = min(j1, i);  // columns j < i only
     // o(j, i) = B(j) + i with B(j) = j(2N - j - 1)/2 - j - 1, B(j + 1) = B(j) + N - j - 2
     long long B = (long long)j0 * (2LL * N - j0 - 1) / 2 - j0 - 1;
-    for (int j = j0; j < j1; ++j) {
-        double sa = 0.0, sb = 0.0;
+    for (int j = j0; j < jend; ++j) {
+        const double* pj = P + (size_t)j * 16;
+        double s = 0.0;
 #pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            const double2 v = sp[j - j0][h];
-            const double da0 = pa[2 * h] - v.x, db0 = pb[2 * h] - v.x;
-            sa = fma(da0, da0, sa);
-            sb = fma(db0, db0, sb);
-            if (h < 7) {
-                const double da1 = pa[2 * h + 1] - v.y, db1 = pb[2 * h + 1] - v.y;
-                sa = fma(da1, da1, sa);
-                sb = fma(db1, db1, sb);
-            }
+        for (int q = 0; q < 15; ++q) {
+            const double dv = pi[q] - pj[q];
+            s = fma(dv, dv, s);
         }
-        if (j < ia && ia < N) dist_store<F32>(out, (size_t)(B + ia), __builtin_amdgcn_sqrt(sa));
-        if (j < ib && ib < N) dist_store<F32>(out, (size_t)(B + ib), __builtin_amdgcn_sqrt(sb));
+        const double d = __builtin_amdgcn_sqrt(s);
+        if (F32)
+            ((float*)out)[B + i] = (float)d;
+        else
+            ((double*)out)[B + i] = d;
         B += N - j - 2;
     }
 }
@@ -433,9 +415,9 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, void* out, 
     const long long ngrp = (ntiles + DT_RUN - 1) / DT_RUN;
     const dim3 grid((unsigned)(((ngrp + 7) / 8) * 8 * DT_RUN));
     if (f32)
-        hipLaunchKernelGGL(k_dist_euclid<true>, grid, dim3(256), 0, st, P, N, nrb, ntiles, out);
+        hipLaunchKernelGGL(k_dist_euclid<true>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, out);
     else
-        hipLaunchKernelGGL(k_dist_euclid<false>, grid, dim3(256), 0, st, P, N, nrb, ntiles, out);
+        hipLaunchKernelGGL(k_dist_euclid<false>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, out);
     return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@
 #include "scc_kernels.hpp"
 
 #define ING_T 256
+#define IH_T (64 * SCC_ING_HIST_WAVES)  // k_ing_hist: one cell per wave at a time
 
 template <bool DENSE>
 __device__ inline void cell_range(const i64* indptr, int c, int G, i64& b, i64& e)
@@ -44,7 +45,7 @@ __device__ inline void cell_range(const i64* indptr, int c, int G, i64& b, i64& 
 
 // err bits: 1 non-finite value, 2 row index out of range, 4 rows not sorted
 template <bool DENSE>
-__global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
+__global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                     const double* __restrict__ vals, int G, const int* __restrict__ perm,
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
@@ -56,12 +57,12 @@ __global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indp
     const int ch = blockIdx.x;
     const int a = cc_code[ch];
     if (a >= 0)
-        for (int g = threadIdx.x; g < G; g += ING_T) hist[g] = 0;
+        for (int g = threadIdx.x; g < G; g += IH_T) hist[g] = 0;
     __syncthreads();
     const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
     dd se{0.0, 0.0};
     int bad = 0;
-    for (int p = p0 + wv; p < p1; p += ING_T / 64) {
+    for (int p = p0 + wv; p < p1; p += IH_T / 64) {
         const int c = perm[p];
         i64 b, e;
         cell_range<DENSE>(indptr, c, G, b, e);
@@ -114,13 +115,13 @@ __global__ void __launch_bounds__(ING_T) k_ing_hist(const i64* __restrict__ indp
     }
     if (want_expm1) {
         se = dd_wave_sum(se);
-        if (lane == 0) wave_expm1[blockIdx.x * (ING_T / 64) + wv] = se;
+        if (lane == 0) wave_expm1[blockIdx.x * (IH_T / 64) + wv] = se;
     }
     if (bad) atomicOr(err, bad);
     if (a < 0) return;
     __syncthreads();
     u32* row = cnt + (size_t)ch * G;
-    for (int g = threadIdx.x; g < G; g += ING_T) row[g] = hist[g];
+    for (int g = threadIdx.x; g < G; g += IH_T) row[g] = hist[g];
 }
 
 // per gene: exclusive prefix over the count chunks (in place); rows >= nc_kept
@@ -176,7 +177,7 @@ __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int
 }
 
 #define SC_GT 256       // genes per tile
-#define SC_CAP 7168     // staged entries per round (u64 key + u16 gene = 10 B each): 2 blocks per CU
+#define SC_CAP 4096     // default staged entries per round (u64 key + u16 gene = 10 B each): 3 blocks per CU
 #define SC_CMAX 128     // cells per scatter chunk (kScatterCC * kCountChunk)
 
 template <bool DENSE>
@@ -185,7 +186,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
                                                        const int* __restrict__ perm, const int* __restrict__ cc_p0,
                                                        const int* __restrict__ sc_cc0, const u32* __restrict__ cnt,
                                                        const i64* __restrict__ gstart, const i64* __restrict__ bnd,
-                                                       int ntile, u64* __restrict__ keys)
+                                                       int ntile, int cap, u64* __restrict__ keys)
 {
     __shared__ u32 loff[SC_GT + 1];
     __shared__ u32 cur[SC_GT];
@@ -198,7 +199,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     __shared__ u32 wsum[ING_T / 64];
     __shared__ u32 csum[ING_T / 64];
     extern __shared__ __attribute__((aligned(16))) u64 skey[];  // [SC_CAP]
-    unsigned short* sg = (unsigned short*)(skey + SC_CAP);     // [SC_CAP]
+    unsigned short* sg = (unsigned short*)(skey + cap);        // [cap]
     const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
     const int s = blockIdx.x, t = blockIdx.y;
     const int g0 = t * SC_GT, g1 = min(G, g0 + SC_GT), ng = g1 - g0;
@@ -265,18 +266,18 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     }
     if (tid < ncell) cof[tid + 1] = cinc;
     __syncthreads();
-    // rounds of <= SC_CAP entries over consecutive genes
+    // rounds of <= cap entries over consecutive genes
     if (tid == 0) {
         const u32 tot = loff[ng];
         int nr = 0;
         rnd[0] = 0;
-        if (tot <= SC_CAP) {
+        if (tot <= (u32)cap) {
             nr = 1;
             rnd[1] = ng;
         } else {
             u32 acc = 0;
             for (int gl = 0; gl < ng; ++gl) {
-                if (acc + lcnt[gl] > SC_CAP) {
+                if (acc + lcnt[gl] > (u32)cap) {
                     rnd[++nr] = gl;
                     acc = 0;
                 }
@@ -439,11 +440,11 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
     const size_t lds = sizeof(u32) * (size_t)G;
     if (dense) {
         hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
+        hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
                            cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, err);
     } else {
         hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+        hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
                            cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, err);
     }
     return hipGetLastError();
@@ -471,15 +472,19 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
 {
     if (ns <= 0) return hipSuccess;
     const dim3 grid(ns, ntile);
-    const size_t lds = (size_t)SC_CAP * (8 + 2);
+    static const int cap = [] {
+        const char* v = getenv("SCC_SC_CAP");
+        return (v && *v) ? std::max(SC_GT, atoi(v)) : SC_CAP;
+    }();
+    const size_t lds = (size_t)cap * (8 + 2);
     hipFuncSetAttribute((const void*)k_ing_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (dense)
         hipLaunchKernelGGL(k_ing_scatter<true>, grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, keys);
+                           sc_cc0, cnt, gstart, bnd, ntile, cap, keys);
     else
         hipLaunchKernelGGL(k_ing_scatter<false>, grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0, sc_cc0,
-                           cnt, gstart, bnd, ntile, keys);
+                           cnt, gstart, bnd, ntile, cap, keys);
     return hipGetLastError();
 }
 

@@ -10,6 +10,8 @@
 #define SCC_DE_SLOW 1
 #endif
 
+#define SCC_ING_HIST_WAVES 16  // waves per ingest histogram workgroup (one partial expm1 sum each)
+
 struct dd;
 
 struct ScStatsLaunch {
@@ -42,6 +44,7 @@ struct ScRankLaunch {
     int cap_s, cap_m, cap_lds, bucket_target, ntp_max, item_cap;
     int med_wide;          // medium items: 1024 threads, one workgroup per CU
     int wave_target;       // split: bins are packed into buckets of < 2 * wave_target elements
+    int rw_slots;          // wave kernel: tested pairs per gene held in registers, 64 * rw_slots (2 or 4)
     int dbg;               // SCC_RW_DEBUG timing experiments (1: no pair counts, 2: no sort); results invalid
     int bucket_cap;        // capacity of sbuckets / hbg rows
     ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)

@@ -781,7 +781,7 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
     }
 }
 
-#define RW_SLOTS 4  // tested pairs per gene the wave kernel holds: 64 * RW_SLOTS
+#define RW_SLOTS_MAX 4  // tested pairs per gene the wave kernel holds: 64 * slots (2 or 4)
 
 // ===================================================================== split
 #define SP_T 1024
@@ -821,7 +821,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     const u64* key = A.keys + base;
     if (tid <= K) L.off[tid] = (int)A.coff[(size_t)A.cl_cc[tid] * G + g];
     for (int i = tid; i < SP_BINS; i += SP_T) L.hist[i] = 0;
-    // tested pairs of the gene (the wave kernel holds at most 64 * RW_SLOTS)
+    // tested pairs of the gene (the wave kernel holds at most 64 * A.rw_slots)
     {
         u32 t = 0;
         for (int p = tid; p < A.P; p += SP_T) t += (A.all_pairs || (A.flags[(size_t)p * G + g] & 1)) ? 1u : 0u;
@@ -831,7 +831,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     __syncthreads();
     u32 ntested = 0;
     for (int v = 0; v < SP_W; ++v) ntested += L.wsum2[v];
-    const bool waves_ok = ntested <= 64 * RW_SLOTS;
+    const bool waves_ok = ntested <= 64u * (u32)A.rw_slots;
     // the gene's keys stay in registers when they fit (SP_KPT per thread);
     // larger genes re-read each chunk in every pass (from L2)
     u64 kr[SP_KPT];
@@ -1084,6 +1084,7 @@ __device__ inline void bitonic_merge(u64& key, u32& code, bool up, int lane)
     if constexpr (ST > 1) bitonic_merge<ST / 2>(key, code, up, lane);
 }
 
+template <int RW_SLOTS>
 __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 {
     __shared__ u32 tpl[4][64 * RW_SLOTS];  // per-wave staging of the compacted pair list
@@ -1371,7 +1372,10 @@ extern "C" size_t scc_rank_split_lds(int K)
 
 extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rank_waves, dim3(grid), dim3(256), 0, st, *L);
+    if (L->rw_slots <= 2)
+        hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, *L);
+    else
+        hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, *L);
     return hipGetLastError();
 }
 

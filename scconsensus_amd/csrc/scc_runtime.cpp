@@ -275,7 +275,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     unsigned long long* d_first;
     double *d_p, *d_lfc, *d_pct1, *d_pct2;
     uint8_t* d_flags;
-    const int nwaves = nc * 4;
+    const int nwaves = nc * SCC_ING_HIST_WAVES;
     const int64_t nnz1 = std::max<int64_t>(ds->nnz, 1);
 #define WS(name, n, ptr)                                  \
     do {                                                  \
@@ -454,6 +454,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         L.med_wide = med_wide;
         L.bucket_target = bucket_target;
         L.wave_target = wave_target;
+        L.rw_slots = P <= 128 ? 2 : 4;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
         L.bucket_cap = bucket_cap;
         L.sbuckets = d_sbk;

@@ -79,6 +79,17 @@ def test_fast_config_a_params(eng, cfg_a, kw):
     _fast_compare(eng, ds, X, code, len(names), **kw)
 
 
+@pytest.mark.parametrize("K", [18, 26])
+def test_fast_many_clusters(eng, K):
+    """More tested pairs per gene than the wave kernel's 2-slot variant holds
+    (P = 153: 4 slots; P = 325: genes past 256 tested pairs go to the LDS items)."""
+    d = synth.generate("A", G=400, N=4000, K=K, seed=7)
+    names, code = api.select_clusters(d.labels, 10)
+    assert len(names) * (len(names) - 1) // 2 > 128
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _fast_compare(eng, ds, d.dense(), code, len(names), min_per_cent=5.0, log_fc_thrs=0.1)
+
+
 def test_fast_edge_fixture(eng, edge):
     d, X, names, code = edge
     assert "grey" not in names and "grey60" not in names and "tiny" not in names
