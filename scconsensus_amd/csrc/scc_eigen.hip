@@ -36,7 +36,7 @@
 #define TRI_W (TRI_T / 64)
 #define VEC_T 256
 #define VEC_W (VEC_T / 64)
-#define VEC_NJ 8  // back-transform in registers up to n = 512
+#define BT_NB 32  // reflectors per compact-WY block of the back-transformation
 #define FIN_T 1024
 #define FIN_W (FIN_T / 64)
 #define EIG_LDS_MAX (160 * 1024)
@@ -45,11 +45,16 @@
 
 static constexpr double kEps = 2.220446049250313e-16;
 
+// butterfly 32, 16, ..., 1 through DPP / permlane swaps (whole wave only;
+// every lane ends with the same value)
 __device__ inline double wave_sum_d(double v)
 {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    return v;
+    v += scc_xor_lane_f64<32>(v);
+    v += scc_xor_lane_f64<16>(v);
+    v += scc_xor_lane_f64<8>(v);
+    v += scc_xor_lane_f64<4>(v);
+    v += scc_xor_lane_f64<2>(v);
+    return v + scc_xor_lane_f64<1>(v);
 }
 
 // write-through / L1-bypassing accessors for the cross-workgroup hand-off
@@ -140,9 +145,14 @@ __device__ inline void house(const double* y, int lo, int n, double* v, double* 
     for (int j = lo + tid; j < n; j += T) v[j] = (j == lo) ? 1.0 : y[j] * scal;
 }
 
-template <bool LOCAL>
+// REG: rows in registers when they fit (wave wv holds local rows wv + TRI_W m,
+// m < TRI_MR; lane holds columns lane + 64 t, t < NJ), so phase B is
+// register FMAs plus one DPP reduction per row instead of LDS round trips.
+#define TRI_MR 3
+template <bool LOCAL, int NJ>
 __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
 {
+    constexpr int NJA = NJ > 0 ? NJ : 1;  // register row slots per lane (NJ = 0: rows in LDS / HBM)
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ int s_abort, s_rank, s_nwg;
     const int n = a.n, lda = a.lda;
@@ -199,10 +209,25 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     double* part = red + 64;   // EIG_MAX_WG
     double* rows = rows_lds ? (part + EIG_MAX_WG) : (a.work + (size_t)me * R * n);
     const int nown = (me < n) ? (n - me + nwg - 1) / nwg : 0;
+    const bool in_regs = NJ > 0 && nown <= TRI_W * TRI_MR && n <= 64 * NJA;
+    double rr[TRI_MR][NJA];
     if (tid == 0) s_abort = 0;
-    for (int l = 0; l < nown; ++l) {
-        const double* src = a.A + (size_t)(me + nwg * l) * lda;
-        for (int j = tid; j < n; j += TRI_T) rows[(size_t)l * n + j] = src[j];
+    if (in_regs) {
+#pragma unroll
+        for (int m = 0; m < TRI_MR; ++m) {
+            const int l = wv + TRI_W * m;
+#pragma unroll
+            for (int t = 0; t < NJA; ++t) {
+                const int j = lane + 64 * t;
+                const double x = a.A[(size_t)(me + nwg * min(l, nown - 1)) * lda + min(j, n - 1)];
+                rr[m][t] = (l < nown && j < n) ? x : 0.0;
+            }
+        }
+    } else {
+        for (int l = 0; l < nown; ++l) {
+            const double* src = a.A + (size_t)(me + nwg * l) * lda;
+            for (int j = tid; j < n; j += TRI_T) rows[(size_t)l * n + j] = src[j];
+        }
     }
     for (int j = tid; j < n; j += TRI_T) y[j] = a.A[j];  // row 0
     __syncthreads();
@@ -228,7 +253,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     }
     double tp = 0.0;  // tau_{i-1}
     __syncthreads();
-    u64 t_b = 0, t_w = 0, t_c = 0, t0 = 0;
+    u64 t_b = 0, t_w = 0, t_c = 0, t_r = 0, t0 = 0;
     const bool stmp = a.stamps && me == 0 && tid == 0;
     for (int i = 0; i <= n - 2; ++i) {
         const int par = i & 1;
@@ -242,7 +267,48 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         // publish p_r (and row i+1 by its owner) as tagged granules
         double pd = 0.0;
         const int l0 = (i + 1 > me) ? (i + 1 - me + nwg - 1) / nwg : 0;
-        for (int l = l0 + wv; l < nown; l += TRI_W) {
+        if (in_regs) {
+            // this lane's columns of v_i, v_{i-1}, w_{i-1} (zero outside i+1..n-1, so
+            // the dead columns of a row stay untouched and add nothing)
+            double vcr[NJA], vpr[NJA], wpr[NJA];
+#pragma unroll
+            for (int t = 0; t < NJA; ++t) {  // unconditional (clamped) loads, then masks: no branch per load
+                const int j = lane + 64 * t, jc = min(j, n - 1);
+                const bool live = j > i && j < n;
+                const double c = vc[jc], pv = vp[jc], pw = wp[jc];
+                vcr[t] = live ? c : 0.0;
+                vpr[t] = (live && prev) ? pv : 0.0;
+                wpr[t] = (live && prev) ? pw : 0.0;
+            }
+#pragma unroll
+            for (int m = 0; m < TRI_MR; ++m) {
+                const int l = wv + TRI_W * m;
+                if (l >= nown || l < l0) continue;
+                const int r = me + nwg * l;
+                const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
+                double sd = 0.0;
+#pragma unroll
+                for (int t = 0; t < NJA; ++t) {
+                    const double x = rr[m][t] - vr * wpr[t] - wr * vpr[t];
+                    rr[m][t] = x;
+                    sd += x * vcr[t];
+                }
+                if (r == i + 1) {
+#pragma unroll
+                    for (int t = 0; t < NJA; ++t) {
+                        const int j = lane + 64 * t;
+                        if (j > i && j < n) put_g<LOCAL>(rg + 2 * j, rr[m][t], tag);
+                    }
+                }
+                sd = wave_sum_d(sd);
+                const double p = tc * sd;
+                if (lane == 0) {
+                    put_g<LOCAL>(pg + 2 * r, p, tag);
+                    pd += p * vc[r];
+                }
+            }
+        }
+        for (int l = l0 + wv; !in_regs && l < nown; l += TRI_W) {
             const int r = me + nwg * l;
             double* row = rows + (size_t)l * n;
             const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
@@ -265,6 +331,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
             }
         }
         if (lane == 0) red[32 + wv] = pd;  // (red[0..TRI_W) belongs to block_sum)
+        if (stmp) t_r += __builtin_amdgcn_s_memtime() - t0;
         __syncthreads();
         if (tid == 0) {
             double s = 0.0;
@@ -413,6 +480,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         a.stamps[0] = t_b;
         a.stamps[1] = t_w;
         a.stamps[2] = t_c;
+        a.stamps[7] = t_r;
     }
 }
 
@@ -740,6 +808,8 @@ struct VecArgs {
     double* Zq;     // [16][lda] back-transformed vectors (unnormalised sign)
     double* W;      // [k]
     double* tnorm;  // [1]
+    const double* tf;  // [ceil((n-2)/BT_NB)][BT_NB][BT_NB] compact-WY T factors
+    u64* stamps;    // diagnostic: workgroup 0's phase boundaries at [3..7] (nullptr normally)
 };
 
 // number of eigenvalues of T (d, e^2) strictly below x (Sturm sequence, dstebz)
@@ -763,11 +833,13 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
     __shared__ double red[16];
     __shared__ int ired[VEC_W];
     const int n = a.n, q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    const bool stmp = a.stamps && q == 0 && tid == 0;
+    const u64 t0 = stmp ? clock64() : 0;
     double* dl = sm;
     double* el = dl + n;
     double* e2l = el + n;
     double* y = e2l + n;
-    double* lu = a.lu_lds ? (y + n) : (a.lu + (size_t)q * 5 * n);
+    double* lu = a.lu_lds ? (y + n) : (a.lu + (size_t)q * 6 * n);
     for (int i = tid; i < n; i += VEC_T) {
         dl[i] = a.d[i];
         el[i] = a.e[i];
@@ -826,48 +898,61 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
         if (hi - lo <= 2.0 * kEps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
     }
     const double lam = 0.5 * (lo + hi);
+    const u64 t1 = stmp ? clock64() : 0;
     if (tid == 0) {
         a.W[q] = lam;
         if (q == 0) a.tnorm[0] = tnorm;
     }
-    // ---- inverse iteration (dgttrf / dgttrs), lane 0 of wave 0
-    double* fd = lu;
-    double* fu = fd + n;
+    // ---- inverse iteration (dgttrf / dgttrs) by thread 0: the factor's
+    // recurrence runs in registers (the next diagonal and super-diagonal are
+    // carried, the inputs are independent loads), pivots stored as reciprocals
+    double* fdr = lu;  // 1 / U diagonal
+    double* fu = fdr + n;
     double* fu2 = fu + n;
     double* fl = fu2 + n;
     double* fp = fl + n;
+    double* w = fp + n;  // forward-solve result
     const double tiny = kEps * tnorm + 1e-300;
     if (tid == 0) {
-        for (int i = 0; i < n; ++i) {
-            fd[i] = dl[i] - lam;
-            fu[i] = (i < n - 1) ? el[i] : 0.0;
-            fl[i] = (i < n - 1) ? el[i] : 0.0;
-            fu2[i] = 0.0;
-            fp[i] = 0.0;
-        }
-        for (int i = 0; i < n - 1; ++i) {
-            if (fabs(fd[i]) >= fabs(fl[i])) {
-                if (fd[i] == 0.0) fd[i] = tiny;
-                const double f = fl[i] / fd[i];
+        // inputs of LU_B steps are loaded together ahead of the dependent chain
+        constexpr int LU_B = 8;
+        double dcur = dl[0] - lam, ucur = (n > 1) ? el[0] : 0.0;
+        for (int i0 = 0; i0 < n - 1; i0 += LU_B) {
+            double li[LU_B], dn[LU_B], un[LU_B];
+#pragma unroll
+            for (int u = 0; u < LU_B; ++u) {  // clamped unconditional loads
+                const int i = i0 + u;
+                const double e0 = el[min(i, n - 1)], d1 = dl[min(i + 1, n - 1)], e1 = el[min(i + 1, n - 1)];
+                li[u] = e0;
+                dn[u] = d1 - lam;
+                un[u] = (i < n - 2) ? e1 : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < LU_B; ++u) {  // branch-free step: one division on the chain
+                const int i = i0 + u;
+                if (i >= n - 1) break;
+                const bool piv = fabs(dcur) < fabs(li[u]);  // LAPACK dgttrf: swap rows i, i+1
+                const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
+                const double den = piv ? li[u] : dc;
+                const double f = (piv ? dc : li[u]) / den;
                 fl[i] = f;
-                fd[i + 1] -= f * fu[i];
-            } else {
-                const double f = fd[i] / fl[i];
-                fd[i] = fl[i];
-                fl[i] = f;
-                const double tt = fu[i];
-                fu[i] = fd[i + 1];
-                fd[i + 1] = tt - f * fd[i + 1];
-                if (i < n - 2) {
-                    fu2[i] = fu[i + 1];
-                    fu[i + 1] = -f * fu[i + 1];
-                }
-                fp[i] = 1.0;
+                fdr[i] = den;  // the pivot; its reciprocal is taken below, off the chain
+                fu[i] = piv ? dn[u] : ucur;
+                fu2[i] = piv ? un[u] : 0.0;  // zero at i = n - 2
+                fp[i] = piv ? 1.0 : 0.0;
+                const double dnext = piv ? ucur - f * dn[u] : dn[u] - f * ucur;
+                ucur = piv ? -f * un[u] : un[u];
+                dcur = dnext;
             }
         }
-        if (fd[n - 1] == 0.0) fd[n - 1] = tiny;
-        for (int i = 0; i < n; ++i) fd[i] = 1.0 / fd[i];  // the solves multiply by the pivots' reciprocals
+        if (dcur == 0.0) dcur = tiny;
+        fdr[n - 1] = dcur;
+        fu[n - 1] = 0.0;
+        fu2[n - 1] = 0.0;
     }
+    __syncthreads();
+    for (int i = tid; i < n; i += VEC_T) fdr[i] = 1.0 / fdr[i];
+    const u64 t2 = stmp ? clock64() : 0;
     for (int i = tid; i < n; i += VEC_T) {  // deterministic pseudo-random start
         unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)q * 40503u + 12345u);
         h ^= h >> 13;
@@ -878,30 +963,46 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
     __syncthreads();
     for (int iter = 0; iter < 2; ++iter) {
         if (tid == 0) {
+            constexpr int SB = 8;  // inputs of SB steps loaded ahead of the dependent chain
             double bi = y[0];
-            for (int i = 0; i < n - 1; ++i) {
-                const double bn = y[i + 1];
-                if (fp[i] == 0.0) {
-                    y[i] = bi;
-                    bi = bn - fl[i] * bi;
-                } else {
-                    y[i] = bn;
-                    bi = bi - fl[i] * bn;
+            for (int i0 = 0; i0 < n - 1; i0 += SB) {  // w = L^-1 P y
+                double bn[SB], f[SB], pv[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int i = min(i0 + u, n - 2);
+                    bn[u] = y[i + 1];
+                    f[u] = fl[i];
+                    pv[u] = fp[i];
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    if (i0 + u >= n - 1) break;
+                    const bool piv = pv[u] != 0.0;
+                    w[i0 + u] = piv ? bn[u] : bi;
+                    bi = piv ? (bi - f[u] * bn[u]) : (bn[u] - f[u] * bi);
                 }
             }
-            y[n - 1] = bi;
-            double z1 = y[n - 1] * fd[n - 1];
-            y[n - 1] = z1;
-            double z2 = 0.0;
-            if (n >= 2) {
-                z2 = (y[n - 2] - fu[n - 2] * z1) * fd[n - 2];
-                y[n - 2] = z2;
-            }
-            for (int i = n - 3; i >= 0; --i) {
-                const double z0 = (y[i] - fu[i] * z2 - fu2[i] * z1) * fd[i];
-                y[i] = z0;
-                z1 = z2;
-                z2 = z0;
+            w[n - 1] = bi;
+            double z1 = 0.0, z2 = 0.0;  // y = U^-1 w, from the bottom
+            for (int i1 = n - 1; i1 >= 0; i1 -= SB) {
+                double wv8[SB], u1[SB], u2[SB], r[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int i = max(i1 - u, 0);
+                    wv8[u] = w[i];
+                    u1[u] = fu[i];
+                    u2[u] = fu2[i];
+                    r[u] = fdr[i];
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int i = i1 - u;
+                    if (i < 0) break;
+                    const double z0 = (wv8[u] - u1[u] * z2 - u2[u] * z1) * r[u];  // z2 = y[i+1], z1 = y[i+2]
+                    y[i] = z0;
+                    z1 = z2;
+                    z2 = z0;
+                }
             }
         }
         __syncthreads();
@@ -913,7 +1014,7 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
         if (lane == 0) red[8 + wv] = mx;
         __syncthreads();
         mx = red[8];
-        for (int w = 1; w < VEC_W; ++w) mx = fmax(mx, red[8 + w]);
+        for (int w2 = 1; w2 < VEC_W; ++w2) mx = fmax(mx, red[8 + w2]);
         const double sc = (mx > 0.0 && mx < INFINITY) ? 1.0 / mx : 1.0;
         double s = 0.0;
         for (int i = tid; i < n; i += VEC_T) {
@@ -925,66 +1026,107 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
         for (int i = tid; i < n; i += VEC_T) y[i] *= inv;
         __syncthreads();
     }
-    // ---- back-transformation: z = H_0 H_1 ... H_{n-3} y (last reflector first)
-    if (n <= 64 * VEC_NJ) {
-        // one wave, y in registers, next reflector prefetched: no barrier per reflector
-        if (wv == 0) {
-            double yr[VEC_NJ], vr[VEC_NJ], vn[VEC_NJ];
+    // ---- back-transformation z = H_0 H_1 ... H_{n-3} y in blocks of BT_NB
+    // reflectors, last block first: block b is I - V T V^T (compact WY, T from
+    // k_refl_T), three barrier-separated steps per block
+    const u64 t3 = stmp ? clock64() : 0;
+    __shared__ double bw[BT_NB], bt[BT_NB];
+    const int nr = n - 2;
+    for (int b = (nr > 0 ? (nr + BT_NB - 1) / BT_NB : 0) - 1; b >= 0; --b) {
+        const int kb = b * BT_NB, nb = min(BT_NB, nr - kb);
+        {  // bw = V^T y: wave wv takes i = wv + VEC_W t, all its loads in flight together
+            constexpr int NT = BT_NB / VEC_W;
+            double acc[NT];
 #pragma unroll
-            for (int t = 0; t < VEC_NJ; ++t) {
-                const int j = lane + 64 * t;
-                yr[t] = (j < n) ? y[j] : 0.0;
-            }
-            int kk = n - 3;
-            if (kk >= 0) {
-                const double* v = a.refl + (size_t)kk * a.lda;
+            for (int t = 0; t < NT; ++t) acc[t] = 0.0;
+            for (int j = kb + 1 + lane; j < n; j += 64) {
+                const double yj = y[j];
 #pragma unroll
-                for (int t = 0; t < VEC_NJ; ++t) {
-                    const int j = lane + 64 * t;
-                    vn[t] = (j > kk && j < n) ? v[j] : 0.0;
+                for (int t = 0; t < NT; ++t) {
+                    const int i = wv + VEC_W * t;  // v_i is zero at rows <= kb + i
+                    const double v = a.refl[(size_t)(kb + min(i, nb - 1)) * a.lda + j];  // unconditional load
+                    acc[t] += (i < nb && j > kb + i) ? v * yj : 0.0;
                 }
             }
-            double tn = (kk >= 0) ? a.tau[kk] : 0.0;
-            for (; kk >= 0; --kk) {
-                const double tcur = tn;
 #pragma unroll
-                for (int t = 0; t < VEC_NJ; ++t) vr[t] = vn[t];
-                if (kk > 0) {  // prefetch reflector kk - 1
-                    const double* v = a.refl + (size_t)(kk - 1) * a.lda;
-#pragma unroll
-                    for (int t = 0; t < VEC_NJ; ++t) {
-                        const int j = lane + 64 * t;
-                        vn[t] = (j > kk - 1 && j < n) ? v[j] : 0.0;
-                    }
-                    tn = a.tau[kk - 1];
-                }
-                if (tcur == 0.0) continue;
-                double sd = 0.0;
-#pragma unroll
-                for (int t = 0; t < VEC_NJ; ++t) sd += vr[t] * yr[t];
-                sd = wave_sum_d(sd) * tcur;
-#pragma unroll
-                for (int t = 0; t < VEC_NJ; ++t) yr[t] -= sd * vr[t];
-            }
-#pragma unroll
-            for (int t = 0; t < VEC_NJ; ++t) {
-                const int j = lane + 64 * t;
-                if (j < n) a.Zq[(size_t)q * a.lda + j] = yr[t];
+            for (int t = 0; t < NT; ++t) {
+                const double sd = wave_sum_d(acc[t]);
+                if (lane == 0 && wv + VEC_W * t < nb) bw[wv + VEC_W * t] = sd;
             }
         }
-        return;
-    }
-    for (int kk = n - 3; kk >= 0; --kk) {
-        const double t = a.tau[kk];
-        if (t == 0.0) continue;
-        const double* v = a.refl + (size_t)kk * a.lda;  // v[kk+1] = 1
-        double s = 0.0;
-        for (int j = kk + 1 + tid; j < n; j += VEC_T) s += v[j] * y[j];
-        s = block_sum<VEC_W>(s, red) * t;
-        for (int j = kk + 1 + tid; j < n; j += VEC_T) y[j] -= s * v[j];
+        __syncthreads();
+        if (tid < nb) {  // bt = T bw (upper triangular)
+            const double* T = a.tf + ((size_t)b * BT_NB + tid) * BT_NB;
+            double sd = 0.0;
+            for (int m = tid; m < nb; ++m) sd += T[m] * bw[m];
+            bt[tid] = sd;
+        }
+        __syncthreads();
+        for (int j = kb + 1 + tid; j < n; j += VEC_T) {  // y -= V bt
+            const int im = min(nb, j - kb);
+            double sd = 0.0;
+#pragma unroll 8
+            for (int i = 0; i < im; ++i) sd += a.refl[(size_t)(kb + i) * a.lda + j] * bt[i];
+            y[j] -= sd;
+        }
         __syncthreads();
     }
     for (int i = tid; i < n; i += VEC_T) a.Zq[(size_t)q * a.lda + i] = y[i];
+    if (stmp) {
+        a.stamps[3] = t1 - t0;
+        a.stamps[4] = t2 - t1;
+        a.stamps[5] = t3 - t2;
+        a.stamps[6] = clock64() - t3;
+    }
+}
+
+// T factors of the compact WY form of the reflectors, one workgroup per block
+// of BT_NB (LAPACK dlarft, forward / columnwise): T[i][i] = tau_i,
+// T[0:i, i] = -tau_i T[0:i, 0:i] (V[:, 0:i]^T v_i).
+__global__ void __launch_bounds__(1024) k_refl_T(const double* __restrict__ refl, const double* __restrict__ tau, int n,
+                                                 int lda, double* __restrict__ tf)
+{
+    __shared__ double G[BT_NB][BT_NB + 1];
+    __shared__ double T[BT_NB][BT_NB + 1];
+    const int b = blockIdx.x, kb = b * BT_NB, nb = min(BT_NB, n - 2 - kb), tid = threadIdx.x;
+    // G[i][j] = v_i . v_j for j < i (both nonzero from row kb + i + 1): wave wv
+    // takes rows i = wv and wv + 16, every j < i in registers
+    const int lane = tid & 63, wv = scc_wave_id();
+    for (int i = wv; i < BT_NB; i += 16) {
+        double acc[BT_NB];
+#pragma unroll
+        for (int j = 0; j < BT_NB; ++j) acc[j] = 0.0;
+        if (i < nb) {
+            const double* vi = refl + (size_t)(kb + i) * lda;
+            for (int r = kb + i + 1 + lane; r < n; r += 64) {
+                const double x = vi[r];
+#pragma unroll
+                for (int j = 0; j < BT_NB; ++j) {
+                    const double y = refl[(size_t)(kb + min(j, nb - 1)) * lda + r];  // unconditional load
+                    acc[j] += (j < i) ? x * y : 0.0;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < BT_NB; ++j) {
+            const double sj = wave_sum_d(acc[j]);
+            if (lane == 0) G[i][j] = sj;
+        }
+    }
+    for (int e = tid; e < BT_NB * (BT_NB + 1); e += 1024) (&T[0][0])[e] = 0.0;
+    __syncthreads();
+    for (int i = 0; i < nb; ++i) {
+        const double ti = tau[kb + i];
+        if (tid < i) {
+            double s = 0.0;
+            for (int m = tid; m < i; ++m) s += T[tid][m] * G[i][m];
+            T[tid][i] = -ti * s;
+        } else if (tid == i) {
+            T[i][i] = ti;
+        }
+        __syncthreads();
+    }
+    tf[(size_t)b * BT_NB * BT_NB + tid] = T[tid >> 5][tid & 31];
 }
 
 // ---------------------------------------------------------------------------
@@ -1061,7 +1203,7 @@ static int eig_local()
 }
 
 struct EigLayout {
-    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, lu, work, total;
+    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, tf, lu, work, total;
 };
 
 static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool lu_lds)
@@ -1083,7 +1225,8 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     L.dg = take(4 * EIG_MAX_WG * TRI_W);  // one partial per wave agent
     L.zq = take(16 * (size_t)lda);
     L.refl = take((size_t)n * lda);
-    L.lu = lu_lds ? o : take((size_t)16 * 5 * n);
+    L.tf = take((size_t)((n + BT_NB) / BT_NB) * BT_NB * BT_NB);
+    L.lu = lu_lds ? o : take((size_t)16 * 6 * n);
     const int R = (n + nwg - 1) / nwg;
     // XCD-local mode: fewer workgroups may register than planned -> room for all rows
     L.work = take(((size_t)n + 4 * 64) * n);  // row store of the HBM fall-backs (any participant count)
@@ -1122,7 +1265,7 @@ static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
     if (eig_local() && nwg > 32) nwg = 32;  // one XCD holds 32 CUs
     const int R = (n + nwg - 1) / nwg;
     rows_lds = tri_lds_bytes(n, R, true) <= EIG_LDS_MAX;
-    lu_lds = sizeof(double) * 9 * (size_t)n <= EIG_LDS_MAX;
+    lu_lds = sizeof(double) * 10 * (size_t)n <= EIG_LDS_MAX;
 }
 
 extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
@@ -1200,13 +1343,21 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
             hipFuncSetAttribute((const void*)k_tridiag_wa<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
             hipLaunchKernelGGL(k_tridiag_wa<false>, dim3(nwg), dim3(TRI_T), l2, st, t);
         }
-    } else if (t.xcd_local) {
-        const int grid = std::min(8 * nwg, cus);
-        hipFuncSetAttribute((const void*)k_tridiag<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_tridiag<true>, dim3(grid), dim3(TRI_T), lds, st, t);
     } else {
-        hipFuncSetAttribute((const void*)k_tridiag<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_tridiag<false>, dim3(nwg), dim3(TRI_T), lds, st, t);
+        // register rows for n <= 512 (6 or 8 column slots per lane), else LDS / HBM rows
+        const int nj = n <= 384 ? 6 : (n <= 512 ? 8 : 0);
+        const void* fn;
+        if (t.xcd_local)
+            fn = nj == 6 ? (const void*)(k_tridiag<true, 6>) : nj == 8 ? (const void*)(k_tridiag<true, 8>)
+                                                                      : (const void*)(k_tridiag<true, 0>);
+        else
+            fn = nj == 6 ? (const void*)(k_tridiag<false, 6>) : nj == 8 ? (const void*)(k_tridiag<false, 8>)
+                                                                       : (const void*)(k_tridiag<false, 0>);
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const dim3 grid(t.xcd_local ? std::min(8 * nwg, cus) : nwg);
+        void* args[] = {&t};
+        e = hipLaunchKernel(fn, grid, dim3(TRI_T), args, lds, st);
+        if (e != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (marks) hipEventRecord(marks[1], st);
@@ -1223,7 +1374,14 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     v.Zq = scratch + L.zq;
     v.W = W;
     v.tnorm = scratch + L.tnorm;
-    const size_t vlds = sizeof(double) * (lu_lds ? 9 : 4) * (size_t)n;
+    v.stamps = stamps;
+    v.tf = scratch + L.tf;
+    if (n > 2) {
+        hipLaunchKernelGGL(k_refl_T, dim3((n - 2 + BT_NB - 1) / BT_NB), dim3(1024), 0, st, t.refl, t.tau, n, lda,
+                           scratch + L.tf);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
     hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
     if (marks) hipEventRecord(marks[2], st);
     hipLaunchKernelGGL(k_tri_vectors, dim3(k), dim3(VEC_T), vlds, st, v);
