@@ -21,8 +21,9 @@ struct ScStatsLaunch {
     const int* n_clu;
     const uint32_t* coff;
     const int* cl_cc;
-    double* mean_x;     // [K][G]
-    double* mean_e;     // [K][G]
+    double* mean_x;     // [K][G] (slow mode only)
+    double* mean_e;     // [K][G] (fast mode only)
+    int mode;           // SCC_DE_FAST: mean of expm1(x); SCC_DE_SLOW: mean of x
     uint32_t* cnt_pos;  // [K][G]
     uint32_t* cnt_neg;  // [K][G]
 };

@@ -87,6 +87,9 @@ struct StatItem {
     u32 pos, neg;
 };
 
+// FAST needs the per-cluster mean of expm1(x) (Fast:259-272), SLOW the mean
+// of x (slow:105): each mode accumulates only its own double-double sum.
+template <bool EXPM1>
 __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 {
     __shared__ int off[65];
@@ -116,14 +119,18 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
             for (int q = 0; q < 4; ++q) x[q] = (i + 64 * q < s1) ? scc_val_of(key[i + 64 * q]) : 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                sx = dd_add_d(sx, x[q]);
-                se = dd_add_d(se, expm1(x[q]));
+                if (EXPM1)
+                    se = dd_add_d(se, expm1(x[q]));
+                else
+                    sx = dd_add_d(sx, x[q]);
                 pos += (x[q] > 0.0);
                 neg += (x[q] < 0.0);
             }
         }
-        sx = dd_wave_sum_dpp(sx);
-        se = dd_wave_sum_dpp(se);
+        if (EXPM1)
+            se = dd_wave_sum_dpp(se);
+        else
+            sx = dd_wave_sum_dpp(sx);
         pos = u32_wave_sum_dpp(pos);
         neg = u32_wave_sum_dpp(neg);
         if (lane == 0) item[it] = StatItem{sx.hi, sx.lo, se.hi, se.lo, pos, neg};
@@ -143,8 +150,10 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
             neg += item[q].neg;
         }
         const double na = (double)A.n_clu[a];
-        A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
-        A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
+        if (EXPM1)
+            A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
+        else
+            A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
         A.cnt_pos[(size_t)a * A.G + g] = pos;
         A.cnt_neg[(size_t)a * A.G + g] = neg;
     }
@@ -153,7 +162,10 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st)
 {
     if (L->G <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_gene_stats, dim3(L->G), dim3(ST_T), 0, st, *L);
+    if (L->mode == SCC_DE_FAST)
+        hipLaunchKernelGGL(k_gene_stats<true>, dim3(L->G), dim3(ST_T), 0, st, *L);
+    else
+        hipLaunchKernelGGL(k_gene_stats<false>, dim3(L->G), dim3(ST_T), 0, st, *L);
     return hipGetLastError();
 }
 

@@ -385,6 +385,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         S.mean_e = d_me;
         S.cnt_pos = d_cntpos;
         S.cnt_neg = d_cntneg;
+        S.mode = prm->mode;
         HIPCHK(c, scc_launch_gene_stats(&S, s0));
     }
     // SLOW: log(meanScalingFactor * mean(expm1(X))) (slow:36) gates the pair
