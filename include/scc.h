@@ -105,6 +105,22 @@ SCC_API void scc_dataset_destroy(scc_dataset* ds);
 SCC_API int scc_de_run(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
                const scc_de_params* params, scc_de_result** out);
 
+/* ---- the same DE sharded over gene row-blocks (one process per GPU) -------
+ * Replaces the reference's per-cluster foreach workers (Fast:61-65,359,384):
+ * every rank holds the whole dataset and runs scc_de_run_shard on its genes
+ * [gene_lo, gene_hi); `shard` (device, scc_de_shard_bytes) receives the
+ * per-(pair, gene) cells p, avg_logFC, pct1, pct2 (f64), 2U, ties (i64) and
+ * flags (u8), each [n_pairs][G], zero outside the shard.  The caller sums the
+ * shards of all ranks as int64 words (one all-reduce: the shards are
+ * disjoint, so the sum is the exact union) and calls scc_de_finish on the
+ * same context with the sum: per-pair BH, filters, top-N and the union, the
+ * same result scc_de_run gives. */
+SCC_API int64_t scc_de_shard_bytes(int32_t K, int64_t n_genes);
+SCC_API int scc_de_run_shard(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
+                     const scc_de_params* params, int64_t gene_lo, int64_t gene_hi, void* shard /* device */);
+SCC_API int scc_de_finish(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
+                  const scc_de_params* params, const void* shards_sum /* device */, scc_de_result** out);
+
 /* n_pairs = K(K-1)/2; n_rows = FAST tested rows over all pairs (0 for SLOW);
  * n_union = |deGeneUnion|. */
 SCC_API int scc_de_result_counts(const scc_de_result* r, int32_t* n_pairs, int64_t* n_rows, int32_t* n_union);

@@ -34,7 +34,7 @@ SCC_PTR_DEVICE = 1
 EXPORTS = [
     "scc_ctx_create", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_kernel_time",
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_dense", "scc_dataset_destroy",
-    "scc_de_run", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
+    "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
     "scc_distance", "scc_last_pca_scores",
 ]
@@ -96,6 +96,9 @@ def load():
         "scc_dataset_create_dense": (ctypes.c_int, [vp, vp, i64, i64, i32, P(vp)]),
         "scc_dataset_destroy": (None, [vp]),
         "scc_de_run": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), P(vp)]),
+        "scc_de_shard_bytes": (i64, [i32, i64]),
+        "scc_de_run_shard": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), i64, i64, vp]),
+        "scc_de_finish": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), vp, P(vp)]),
         "scc_de_result_counts": (ctypes.c_int, [vp, P(i32), P(i64), P(i32)]),
         "scc_de_result_union": (ctypes.c_int, [vp, vp]),
         "scc_de_result_rows": (ctypes.c_int, [vp] + [vp] * 10),
@@ -233,12 +236,44 @@ class Engine:
         feature filters drop; default: only when the full per-pair vectors are
         fetched (fetch="all")."""
         code = np.ascontiguousarray(code, np.int32)
-        if test_all is None:
-            test_all = fetch == "all"
-        prm = DeParams(mode, top_n, q_val_thrs, log_fc_thrs, min_per_cent, fc_thrs, mean_scaling_factor,
-                       1 if test_all else 0, 0)
+        prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
+                              fetch == "all" if test_all is None else test_all)
         r = ctypes.c_void_p()
         rc = self.lib.scc_de_run(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), ctypes.byref(r))
+        return self._collect(r, rc, ds, mode, K, fetch)
+
+    @staticmethod
+    def _de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor, test_all):
+        return DeParams(mode, top_n, q_val_thrs, log_fc_thrs, min_per_cent, fc_thrs, mean_scaling_factor,
+                        1 if test_all else 0, 0)
+
+    def de_shard_bytes(self, K, G) -> int:
+        return int(self.lib.scc_de_shard_bytes(K, G))
+
+    def de_run_shard(self, ds: Dataset, code, K, gene_lo, gene_hi, shard_ptr, mode=SCC_DE_FAST, q_val_thrs=0.1,
+                     log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0,
+                     test_all=False):
+        """Per-(pair, gene) DE cells of genes [gene_lo, gene_hi) into the device
+        buffer at shard_ptr (de_shard_bytes(K, G) bytes, zero outside the shard)."""
+        code = np.ascontiguousarray(code, np.int32)
+        prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
+                              test_all)
+        self._check(self.lib.scc_de_run_shard(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), gene_lo,
+                                              gene_hi, ctypes.c_void_p(shard_ptr)))
+
+    def de_finish(self, ds: Dataset, code, K, shards_sum_ptr, mode=SCC_DE_FAST, q_val_thrs=0.1, log_fc_thrs=0.5,
+                  min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all",
+                  test_all=False) -> DeResult:
+        """Selection and union from the summed shards of every rank (device)."""
+        code = np.ascontiguousarray(code, np.int32)
+        prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
+                              test_all)
+        r = ctypes.c_void_p()
+        rc = self.lib.scc_de_finish(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm),
+                                    ctypes.c_void_p(shards_sum_ptr), ctypes.byref(r))
+        return self._collect(r, rc, ds, mode, K, fetch)
+
+    def _collect(self, r, rc, ds, mode, K, fetch) -> DeResult:
         msg = ""
         if rc != SCC_OK:
             msg = self.lib.scc_ctx_last_error(self.ctx).decode()

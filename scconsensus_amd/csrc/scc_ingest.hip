@@ -50,8 +50,10 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
                                                     int* __restrict__ nodg, dd* __restrict__ wave_expm1,
-                                                    int want_expm1, int* __restrict__ err)
+                                                    int want_expm1, int glo, int ghi, int* __restrict__ err)
 {
+    // genes outside [glo, ghi) (a shard of the gene rows) are not counted; nodg
+    // and the expm1 sum still see every entry
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int ch = blockIdx.x;
@@ -93,7 +95,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                 bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
                 pos += (x > 0.0);
                 if (want_expm1) se = dd_add_d(se, expm1(x));
-                if (a >= 0 && x != 0.0 && gok) atomicAdd(&hist[g], 1u);
+                if (a >= 0 && x != 0.0 && g >= glo && g < ghi) atomicAdd(&hist[g], 1u);
                 if (!DENSE && a >= 0) {
                     // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
                     const int gp = gps[u];
@@ -186,7 +188,8 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
                                                        const int* __restrict__ perm, const int* __restrict__ cc_p0,
                                                        const int* __restrict__ sc_cc0, const u32* __restrict__ cnt,
                                                        const i64* __restrict__ gstart, const i64* __restrict__ bnd,
-                                                       int ntile, int cap, u64* __restrict__ keys)
+                                                       int ntile, int cap, int glo, int ghi, int t0,
+                                                       u64* __restrict__ keys)
 {
     __shared__ u32 loff[SC_GT + 1];
     __shared__ u32 cur[SC_GT];
@@ -201,7 +204,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     extern __shared__ __attribute__((aligned(16))) u64 skey[];  // [SC_CAP]
     unsigned short* sg = (unsigned short*)(skey + cap);        // [cap]
     const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
-    const int s = blockIdx.x, t = blockIdx.y;
+    const int s = blockIdx.x, t = t0 + (int)blockIdx.y;  // gene tiles from t0 (a gene shard's tiles)
     const int g0 = t * SC_GT, g1 = min(G, g0 + SC_GT), ng = g1 - g0;
     const int cc0 = sc_cc0[s], cc1 = sc_cc0[s + 1];
     const int p0 = cc_p0[cc0], p1 = cc_p0[cc1];
@@ -298,7 +301,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
         // each wave takes 4 cells at a time, lanes over a cell's entries in the
         // tile (~60 at PBMC density); the 4 first chunks' loads are in flight together
         auto put = [&](double x, int gq) {
-            if (x != 0.0 && gq >= r0 && gq < r1) {
+            if (x != 0.0 && gq >= r0 && gq < r1 && g0 + gq >= glo && g0 + gq < ghi) {
                 const u32 o = atomicAdd(&cur[gq], 1u);
                 if (o < lcnt[gq]) {  // always, for valid input
                     const u32 pos = loff[gq] - base + o;
@@ -435,17 +438,18 @@ extern "C" int scc_ingest_gene_tile(void) { return SC_GT; }
 extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows, const double* vals,
                                              const double* dense, int G, const int* perm, const int* cc_p0,
                                              const int* cc_code, int nc, int ntile, u32* cnt, i64* bnd, int* nodg,
-                                             dd* wave_expm1, int want_expm1, int* err, hipStream_t st)
+                                             dd* wave_expm1, int want_expm1, int glo, int ghi, int* err,
+                                             hipStream_t st)
 {
     const size_t lds = sizeof(u32) * (size_t)G;
     if (dense) {
         hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, err);
     } else {
         hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, err);
     }
     return hipGetLastError();
 }
@@ -468,10 +472,12 @@ extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, i
 extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* rows, const double* vals,
                                                 const double* dense, int G, const int* perm, const int* cc_p0,
                                                 const int* sc_cc0, int ns, const u32* cnt, const i64* gstart,
-                                                const i64* bnd, int ntile, u64* keys, hipStream_t st)
+                                                const i64* bnd, int ntile, int glo, int ghi, u64* keys,
+                                                hipStream_t st)
 {
-    if (ns <= 0) return hipSuccess;
-    const dim3 grid(ns, ntile);
+    if (ns <= 0 || ghi <= glo) return hipSuccess;
+    const int t0 = glo / SC_GT, t1 = (ghi + SC_GT - 1) / SC_GT;  // the gene tiles of [glo, ghi)
+    const dim3 grid(ns, t1 - t0);
     static const int cap = [] {
         const char* v = getenv("SCC_SC_CAP");
         return (v && *v) ? std::max(SC_GT, atoi(v)) : SC_CAP;
@@ -481,10 +487,10 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
     hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (dense)
         hipLaunchKernelGGL(k_ing_scatter<true>, grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, cap, keys);
+                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, keys);
     else
         hipLaunchKernelGGL(k_ing_scatter<false>, grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0, sc_cc0,
-                           cnt, gstart, bnd, ntile, cap, keys);
+                           cnt, gstart, bnd, ntile, cap, glo, ghi, t0, keys);
     return hipGetLastError();
 }
 

@@ -186,11 +186,21 @@ extern "C" void scc_dataset_destroy(scc_dataset* d)
 }
 
 // ====================================================================== DE
-extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
-                          const scc_de_params* prm, scc_de_result** out)
+// stage DE_FULL: the whole DE for genes [glo, ghi) (all genes: scc_de_run).
+// stage DE_SHARD: the per-(pair, gene) stage for the gene shard [glo, ghi),
+//   packed into `shard` (zero outside the shard, so the shards of all ranks
+//   combine by an integer sum: scc_de_shard_bytes layout) -- no selection.
+// stage DE_FINISH: `shard` holds every gene's (pair, gene) cells (the sum of
+//   all ranks' shards); per-pair BH, filters, top-N and the union, on the
+//   context that ran this rank's DE_SHARD for the same inputs.
+enum { DE_FULL = 0, DE_SHARD = 1, DE_FINISH = 2 };
+
+static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
+                       int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out)
 {
-    if (!c || !ds || !code || !prm || !out) return fail(c, SCC_ERR_INVALID, "scc_de_run: null argument");
-    *out = nullptr;
+    if (!c || !ds || !code || !prm || (stage != DE_SHARD && !out) || (stage != DE_FULL && !shard))
+        return fail(c, SCC_ERR_INVALID, "scc_de_run: null argument");
+    if (out) *out = nullptr;
     if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
     if (prm->mode != SCC_DE_FAST && prm->mode != SCC_DE_SLOW) return fail(c, SCC_ERR_INVALID, "bad mode");
     if (K < 2) return fail(c, SCC_ERR_INVALID, "need at least two clusters");
@@ -211,6 +221,8 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         if (fast && nclu[a] < 3) return fail(c, SCC_ERR_RSTOP, "cluster has fewer than 3 cells (R stop())");
     }
     if (G > kMaxGenesLds) return fail(c, SCC_ERR_UNSUPPORTED, "more than 40960 genes is not supported by this build");
+    if (glo64 < 0 || ghi64 > G || glo64 > ghi64) return fail(c, SCC_ERR_INVALID, "gene shard out of range");
+    const int glo = (int)glo64, ghi = (int)ghi64;
     const int64_t GK = (int64_t)G * K;
     const size_t PG = (size_t)P * G;
     // Cells in cluster order: kept cells by code, then unkept ones.  Count
@@ -355,20 +367,28 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     const int* d_clcc = d_tab + o_clcc;
     const int* d_nclu = d_tab + o_nclu;
 
+    const int64_t sig[6] = {G, N, K, prm->mode, ds->nnz, (int64_t)(intptr_t)ds};
+    double log_thr = 0.0;
+    if (stage == DE_FINISH) {
+        if (!std::equal(sig, sig + 6, c->shard_sig))
+            return fail(c, SCC_ERR_INVALID, "scc_de_finish: this context ran no scc_de_run_shard for these inputs");
+        log_thr = c->shard_log_thr;
+    } else {
     HIPCHK(c, hipMemcpyAsync(d_tab, H.data(), sizeof(int) * H.size(), hipMemcpyHostToDevice, s0));
     {
         Scope sc(c, "ingest", s0);
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
         HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 8, s0));
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
-                                         d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, d_err, s0));
+                                         d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
+                                         d_err, s0));
         uint32_t* d_cscr;
         WS("colscan", scc_ingest_colscan_scratch(nc, G), d_cscr);
         HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, d_cscr, s0));
         const uint32_t* d_total = d_cnt + (size_t)nc * G;
         HIPCHK(c, scc_launch_scan(d_total, G, d_gstart, d_scan, d_gstart + G, s0));
         HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
-                                            d_sccc0, ns, d_cnt, d_gstart, d_bnd, ntile, d_keys, s0));
+                                            d_sccc0, ns, d_cnt, d_gstart, d_bnd, ntile, glo, ghi, d_keys, s0));
         if (!fast) HIPCHK(c, scc_launch_reduce_dd(d_wexp, nwaves, d_gexp, s0));
     }
     {
@@ -390,7 +410,6 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     }
     // SLOW: log(meanScalingFactor * mean(expm1(X))) (slow:36) gates the pair
     // filter; a scalar read back here.
-    double log_thr = 0.0;
     if (!fast) {
         double gx[2];
         HIPCHK(c, hipMemcpyAsync(gx, d_gexp, sizeof(double) * 2, hipMemcpyDeviceToHost, s0));
@@ -528,6 +547,40 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
         Scope sc(c, "pair_test", s0);
         HIPCHK(c, scc_launch_pair_test(&T, s0));
     }
+    }  // compute stages
+    // the (pair, gene) fields a shard carries, in scc_de_shard_bytes order
+    struct Field {
+        void* p;
+        size_t es;
+    };
+    const Field fields[7] = {{d_p, 8}, {d_lfc, 8}, {fast ? (void*)d_pct1 : nullptr, 8}, {fast ? (void*)d_pct2 : nullptr, 8},
+                             {d_u2, 8}, {d_t, 8}, {d_flags, 1}};
+    if (stage == DE_SHARD) {
+        char* dst = (char*)shard;
+        HIPCHK(c, hipMemsetAsync(dst, 0, scc_de_shard_bytes(K, G), s0));
+        for (const Field& f : fields) {
+            if (f.p && ghi > glo)
+                HIPCHK(c, hipMemcpy2DAsync(dst + glo * f.es, G * f.es, (const char*)f.p + glo * f.es, G * f.es,
+                                           (size_t)(ghi - glo) * f.es, P, hipMemcpyDeviceToDevice, s0));
+            dst += PG * f.es;
+        }
+        std::copy(sig, sig + 6, c->shard_sig);
+        c->shard_log_thr = log_thr;
+        HIPCHK(c, hipStreamSynchronize(s0));
+        int e = 0;
+        HIPCHK(c, hipMemcpy(&e, d_err, sizeof(int), hipMemcpyDeviceToHost));
+        if (e & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
+        if (e & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
+        if (e & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
+        return SCC_OK;
+    }
+    if (stage == DE_FINISH) {
+        const char* src = (const char*)shard;
+        for (const Field& f : fields) {
+            if (f.p) HIPCHK(c, hipMemcpyAsync(f.p, src, PG * f.es, hipMemcpyDeviceToDevice, s0));
+            src += PG * f.es;
+        }
+    }
     // rows (FAST) / per-pair vectors (SLOW)
     int* d_row_gene = nullptr;
     double *d_row_p = nullptr, *d_row_q = nullptr, *d_row_lfc = nullptr, *d_row_pct1 = nullptr, *d_row_pct2 = nullptr;
@@ -635,6 +688,30 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     if (hdr[1] & 2) return fail(c, SCC_ERR_RSTOP, "NA adjusted p-value in a kept pair (R builds NA rows)");
     return SCC_OK;
 #undef WS
+}
+
+extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                          const scc_de_params* prm, scc_de_result** out)
+{
+    return de_run_impl(c, ds, code, K, prm, DE_FULL, 0, ds ? ds->G : 0, nullptr, out);
+}
+
+extern "C" int64_t scc_de_shard_bytes(int32_t K, int64_t n_genes)
+{
+    const int64_t PG = (int64_t)K * (K - 1) / 2 * n_genes;
+    return (PG * 49 + 7) / 8 * 8;  // p, lfc, pct1, pct2 (f64), u2, ties (i64), flags (u8); 8-byte multiple
+}
+
+extern "C" int scc_de_run_shard(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                                const scc_de_params* prm, int64_t gene_lo, int64_t gene_hi, void* shard)
+{
+    return de_run_impl(c, ds, code, K, prm, DE_SHARD, gene_lo, gene_hi, shard, nullptr);
+}
+
+extern "C" int scc_de_finish(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                             const scc_de_params* prm, const void* shards_sum, scc_de_result** out)
+{
+    return de_run_impl(c, ds, code, K, prm, DE_FINISH, 0, ds ? ds->G : 0, const_cast<void*>(shards_sum), out);
 }
 
 static int check_live(const scc_de_result* r)

@@ -44,6 +44,12 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def all_reduce_sum_(self, tensor):
+        """In-place sum over ranks (RCCL over xGMI on GPU tensors, gloo on CPU)."""
+        if self.active:
+            self.dist.all_reduce(tensor, op=self.dist.ReduceOp.SUM)
+        return tensor
+
     def close(self):
         if self.active:
             self.dist.destroy_process_group()
