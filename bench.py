@@ -11,9 +11,12 @@ One step = one pass of the hot path over one synthetic job resident in HBM:
   scc_distance       PCA(15) + packed Euclidean dist (N(N-1)/2 fp64, kept in HBM)
 value = cell-pairs / second = jobs * N(N-1)/2 / step time.
 
-Multi-GPU: one process per GPU (torchrun); every rank runs its own job (seed
-offset by rank) with no data-path collective ("scaling": "weak"); the step time
-is the max over ranks (RCCL all-reduce of the timer only).
+Multi-GPU: one process per GPU (torchrun); by default every rank runs its own
+job (seed offset by rank) with no data-path collective ("scaling": "weak").
+--mode shard runs ONE job over all ranks ("scaling": "strong"): DE on gene
+row-blocks combined by one RCCL all-reduce (scc_de_run_shard / scc_de_finish),
+then each rank's column slice of the packed distance (scc_distance_cols).  The
+step time is the max over ranks.
 """
 from __future__ import annotations
 
@@ -40,6 +43,9 @@ def _args():
     ap.add_argument("--config", default="B")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-genes", type=int, default=300)
+    ap.add_argument("--mode", choices=["jobs", "shard"], default="jobs",
+                    help="jobs: one job per rank (weak scaling); shard: ONE job over all ranks (strong scaling: "
+                         "DE gene row-blocks + one all-reduce, distance column slices)")
     return ap.parse_args()
 
 
@@ -75,23 +81,38 @@ def cpu_baseline(d, code, K, union, sample_genes, seed=0):
 
 def main():
     a = _args()
+    if a.mode == "shard":
+        import torch  # noqa: F401  (torch's HIP runtime first: the shard buffers are torch tensors)
     from scconsensus_amd import parallel
-    dist = parallel.init()  # RCCL ("nccl") when launched by torchrun with N > 1
+    # RCCL ("nccl") when launched by torchrun with N > 1.  SCC_SHARE_GPU=1 with
+    # SCC_DIST_BACKEND=gloo rehearses several ranks on one GPU (tests only).
+    dist = parallel.init(os.environ.get("SCC_DIST_BACKEND") or None)
     rank, world, local = dist.rank, dist.world, dist.local_rank
     from scconsensus_amd import _native as nat
     from scconsensus_amd import api, synth
     from scconsensus_amd.synth import CONFIGS
 
     cfg = CONFIGS[a.config]
-    d = synth.generate(a.config, seed=parallel.job_seed(cfg["seed"], rank))
+    shard = a.mode == "shard"
+    d = synth.generate(a.config, seed=cfg["seed"] if shard else parallel.job_seed(cfg["seed"], rank))
     names, code = api.select_clusters(d.labels, 10)
     K = len(names)
     P = K * (K - 1) // 2
-    eng = nat.Engine(local, profile=True)
+    gpu = 0 if os.environ.get("SCC_SHARE_GPU") else local
+    eng = nat.Engine(gpu, profile=True)
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)  # H2D before timing
     npairs_cells = d.N * (d.N - 1) / 2
 
+    if shard:
+        import torch
+        from scconsensus_amd import sharded
+        tdev = torch.device(f"cuda:{gpu}")
+
     def step():
+        if shard:  # one job: gene row-blocks + one RCCL all-reduce, then this rank's distance columns
+            r = sharded.de_sharded(eng, ds, code, K, dist, tdev, fetch="union")
+            sharded.distance_sharded(eng, ds, r.union, dist, device_out_ptr=0)
+            return r
         r = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")
         eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
         return r
@@ -159,7 +180,7 @@ def main():
         roof_dom["note"] = ("fp64 vector work on a one-stage Householder reduction: n-1 dependent "
                             "cross-workgroup hand-offs, latency-bound (no MFMA shape)")
     kernels = {f: roof(f) for f in alg if f in stage_ms and stage_ms[f] > 0}
-    value = world * npairs_cells / (ms / 1e3)
+    value = (1 if shard else world) * npairs_cells / (ms / 1e3)
     out = {
         "metric": "end-to-end DE+distance cell-pairs/sec at 26k PBMC shape",
         "value": value,
@@ -170,14 +191,14 @@ def main():
         "ms_per_step": ms,
         "end_to_end_s": ms / 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY §8d NB log1p generator, seed per rank)",
         "config": {"workload": f"config {a.config}: reclusterDEConsensusFast DE (all {P} pairs) + PCA15 "
                                f"Euclidean dist, {d.N} cells x {d.G} genes, K={K}",
                    "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": nnz, "union": nu,
-                   "parallelism": f"jobs{world}"},
+                   "parallelism": f"shard{world}" if shard else f"jobs{world}"},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "roofline": roof_dom,
         "kernels": kernels,

@@ -153,6 +153,15 @@ SCC_API void scc_de_result_destroy(scc_de_result* r);
  * float instead of double. */
 SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */, int32_t n_union,
                  int32_t metric, int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32);
+/* The same for the columns [col_lo, col_hi) only: entries
+ * [col_lo(2N-col_lo-1)/2, col_hi(2N-col_hi-1)/2) of the packed R `dist`
+ * vector, a contiguous slice.  Ranks that split [0, N) into column ranges of
+ * equal entry counts each compute and keep their slice (the
+ * distance tiles stay HBM-resident per GPU); the PCA is recomputed on every
+ * rank (deterministic, identical scores). */
+SCC_API int scc_distance_cols(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */,
+                      int32_t n_union, int32_t metric, int32_t ncomp, int64_t col_lo, int64_t col_hi,
+                      void* dist_out, int32_t out_kind, int32_t out_f32);
 /* PCA scores (N x ncomp, row-major) of the last PCA distance call. */
 SCC_API int scc_last_pca_scores(const scc_ctx* ctx, double* scores, int32_t* ncomp);
 

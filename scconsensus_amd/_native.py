@@ -36,7 +36,7 @@ EXPORTS = [
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_dense", "scc_dataset_destroy",
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
-    "scc_distance", "scc_last_pca_scores",
+    "scc_distance", "scc_distance_cols", "scc_last_pca_scores",
 ]
 
 
@@ -107,6 +107,7 @@ def load():
         "scc_de_result_nodg": (ctypes.c_int, [vp, vp]),
         "scc_de_result_destroy": (None, [vp]),
         "scc_distance": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp, i32, i32]),
+        "scc_distance_cols": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i64, i64, vp, i32, i32]),
         "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
     }
     for name, (res, args) in sig.items():
@@ -334,6 +335,23 @@ class Engine:
             out = np.empty(npairs, np.float32 if f32 else np.float64)
         self._check(self.lib.scc_distance(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, _ptr(out),
                                           SCC_PTR_HOST, 1 if f32 else 0))
+        return out
+
+    def distance_cols(self, ds: Dataset, genes, col_lo, col_hi, metric=SCC_DIST_PCA_EUCLID, ncomp=0, out=None,
+                      f32=False, device_out_ptr=None):
+        """Columns [col_lo, col_hi) of the packed distance vector (a contiguous slice)."""
+        genes = np.ascontiguousarray(genes, np.int32)
+        N = ds.N
+        n = col_hi * (2 * N - col_hi - 1) // 2 - col_lo * (2 * N - col_lo - 1) // 2
+        if device_out_ptr is not None:
+            self._check(self.lib.scc_distance_cols(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, col_lo,
+                                                   col_hi, ctypes.c_void_p(device_out_ptr or None), SCC_PTR_DEVICE,
+                                                   1 if f32 else 0))
+            return None
+        if out is None:
+            out = np.empty(n, np.float32 if f32 else np.float64)
+        self._check(self.lib.scc_distance_cols(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, col_lo,
+                                               col_hi, _ptr(out), SCC_PTR_HOST, 1 if f32 else 0))
         return out
 
     def last_pca_scores(self, N):

@@ -223,8 +223,11 @@ __device__ inline void dist_tile_of(long long t, int nrb, int& cb, int& rb)
     rb = (int)(Q + rem % per);
 }
 
+// Columns [c_lo, c_hi) only (a rank's slice of the packed output, which
+// starts at packed index obase); t0 = the tiles of the column blocks before.
 template <bool F32>
 __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restrict__ P, int N, int nrb, long long ntiles,
+                                                         long long t0, int c_lo, int c_hi, long long obase,
                                                          void* __restrict__ out)
 {
     // dispatch slot -> logical tile (slot x runs on XCD x % 8)
@@ -232,16 +235,16 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
     const long long t = ((k / DT_RUN) * 8 + x) * DT_RUN + k % DT_RUN;
     if (t >= ntiles) return;
     int cb, rb;
-    dist_tile_of(t, nrb, cb, rb);
+    dist_tile_of(t0 + t, nrb, cb, rb);
     const int i = rb * DT_ROWS + (int)threadIdx.x;
-    const int j0 = cb * DT_COLS, j1 = min(N, j0 + DT_COLS);
+    const int j0 = max(cb * DT_COLS, c_lo), j1 = min(min(N, cb * DT_COLS + DT_COLS), c_hi);
     if (i >= N) return;
     double pi[15];
 #pragma unroll
     for (int q = 0; q < 15; ++q) pi[q] = P[(size_t)i * 16 + q];
     const int jend = min(j1, i);  // columns j < i only
     // o(j, i) = B(j) + i with B(j) = j(2N - j - 1)/2 - j - 1, B(j + 1) = B(j) + N - j - 2
-    long long B = (long long)j0 * (2LL * N - j0 - 1) / 2 - j0 - 1;
+    long long B = (long long)j0 * (2LL * N - j0 - 1) / 2 - j0 - 1 - obase;
     for (int j = j0; j < jend; ++j) {
         const double* pj = P + (size_t)j * 16;
         double s = 0.0;
@@ -288,7 +291,7 @@ __global__ void __launch_bounds__(256) k_zscore(const double* __restrict__ Xc, i
 // C[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
 template <bool F32>
 __global__ void __launch_bounds__(256) k_pearson_f32(const float* __restrict__ Z, int N, int ldz, int ntile,
-                                                     void* __restrict__ out)
+                                                     int c_lo, int c_hi, long long obase, void* __restrict__ out)
 {
     // lower-triangular tile index (ti >= tj)
     int t = blockIdx.x, ti = 0;
@@ -298,6 +301,7 @@ __global__ void __launch_bounds__(256) k_pearson_f32(const float* __restrict__ Z
     }
     const int tj = t;
     (void)ntile;
+    if (tj * 128 + 128 <= c_lo || tj * 128 >= c_hi) return;  // no column of this rank's slice
     __shared__ float sa[16][128 + 4];
     __shared__ float sb[16][128 + 4];
     const int lane = threadIdx.x & 63, w = scc_wave_id();
@@ -339,8 +343,8 @@ __global__ void __launch_bounds__(256) k_pearson_f32(const float* __restrict__ Z
             for (int r = 0; r < 16; ++r) {
                 const int i = I0 + wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 const int j = J0 + wj + b * 32 + (lane & 31);
-                if (i < N && j < i) {
-                    const size_t o = (size_t)j * (2 * (size_t)N - j - 1) / 2 + (size_t)(i - j - 1);
+                if (i < N && j < i && j >= c_lo && j < c_hi) {
+                    const size_t o = (size_t)j * (2 * (size_t)N - j - 1) / 2 + (size_t)(i - j - 1) - obase;
                     const float d = 1.0f - acc[a][b][r];
                     if (F32)
                         ((float*)out)[o] = d;
@@ -406,30 +410,36 @@ extern "C" hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld,
     return hipGetLastError();
 }
 
-extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, void* out, int f32, hipStream_t st)
+extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32,
+                                             hipStream_t st)
 {
-    if (N < 2) return hipSuccess;
-    const int nrb = (N + DT_ROWS - 1) / DT_ROWS, ncb = (N + DT_COLS - 1) / DT_COLS;
-    long long ntiles = 0;
-    for (int cb = 0; cb < ncb; ++cb) ntiles += nrb - cb / DT_RATIO;
+    if (N < 2 || c_hi <= c_lo) return hipSuccess;
+    const int nrb = (N + DT_ROWS - 1) / DT_ROWS;
+    const int cb0 = c_lo / DT_COLS, cb1 = (c_hi + DT_COLS - 1) / DT_COLS;
+    long long t0 = 0, ntiles = 0;
+    for (int cb = 0; cb < cb1; ++cb) (cb < cb0 ? t0 : ntiles) += nrb - cb / DT_RATIO;
+    const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
     const long long ngrp = (ntiles + DT_RUN - 1) / DT_RUN;
     const dim3 grid((unsigned)(((ngrp + 7) / 8) * 8 * DT_RUN));
     if (f32)
-        hipLaunchKernelGGL(k_dist_euclid<true>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, out);
+        hipLaunchKernelGGL(k_dist_euclid<true>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo, c_hi, obase,
+                           out);
     else
-        hipLaunchKernelGGL(k_dist_euclid<false>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, out);
+        hipLaunchKernelGGL(k_dist_euclid<false>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo, c_hi, obase,
+                           out);
     return hipGetLastError();
 }
 
-extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, void* out,
-                                         int f32, hipStream_t st)
+extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, int c_lo,
+                                         int c_hi, void* out, int f32, hipStream_t st)
 {
     hipLaunchKernelGGL(k_zscore, dim3((N + 3) / 4), dim3(256), 0, st, Xc, N, nu, ld, ldz, Z);
     const int nt = (N + 127) / 128;
     const int ntri = nt * (nt + 1) / 2;
+    const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
     if (f32)
-        hipLaunchKernelGGL(k_pearson_f32<true>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, out);
+        hipLaunchKernelGGL(k_pearson_f32<true>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, c_lo, c_hi, obase, out);
     else
-        hipLaunchKernelGGL(k_pearson_f32<false>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, out);
+        hipLaunchKernelGGL(k_pearson_f32<false>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, c_lo, c_hi, obase, out);
     return hipGetLastError();
 }

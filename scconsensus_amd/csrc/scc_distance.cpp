@@ -22,15 +22,16 @@ hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nc
 hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C, hipStream_t st);
 hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
                              hipStream_t st);
-hipError_t scc_launch_dist_euclid(const double* P, int N, void* out, int f32, hipStream_t st);
-hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, void* out, int f32,
-                              hipStream_t st);
+hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st);
+hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, int c_lo, int c_hi,
+                              void* out, int f32, hipStream_t st);
 }
 
 extern "C" void scc_distance_release(scc_ctx*) {}
 
-extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
-                            int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32)
+// columns [col_lo, col_hi) of the packed output (the whole matrix: [0, N))
+static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
+                     int32_t ncomp, int64_t col_lo, int64_t col_hi, void* dist_out, int32_t out_kind, int32_t out_f32)
 {
     if (!c || !ds || !genes) return fail(c, SCC_ERR_INVALID, "scc_distance: null argument");
     if (!dist_out && out_kind != SCC_PTR_DEVICE) return fail(c, SCC_ERR_INVALID, "scc_distance: null output");
@@ -47,7 +48,9 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
     hipStream_t s0 = c->s0;
     const int ld = (nu + 63) & ~63;
     const int Npad = (N + 15) & ~15;
-    const size_t npairs = (size_t)N * (N - 1) / 2;
+    if (col_lo < 0 || col_hi > N || col_lo > col_hi) return fail(c, SCC_ERR_INVALID, "column slice out of range");
+    auto colbase = [&](int64_t j) { return (size_t)j * (2 * (size_t)N - j - 1) / 2; };
+    const size_t npairs = colbase(col_hi) - colbase(col_lo);  // the slice's packed entries
     int rc;
     int *d_genes, *d_umap;
     double *d_X, *d_mean;
@@ -140,7 +143,7 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         }
         {
             Scope sc(c, "dist", s0);
-            HIPCHK(c, scc_launch_dist_euclid(d_P, N, d_out, out_f32, s0));
+            HIPCHK(c, scc_launch_dist_euclid(d_P, N, (int)col_lo, (int)col_hi, d_out, out_f32, s0));
         }
         c->d_last_scores = d_P;
         c->last_n = N;
@@ -150,7 +153,7 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         const int ldz = (nu + 15) & ~15;
         WS("d_Zp", (size_t)N * ldz, d_Zp);
         Scope sc(c, "pearson", s0);
-        HIPCHK(c, scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, d_out, out_f32, s0));
+        HIPCHK(c, scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, (int)col_lo, (int)col_hi, d_out, out_f32, s0));
     }
     if (out_kind == SCC_PTR_HOST) {
         HIPCHK(c, hipMemcpyAsync(dist_out, d_out, npairs * (out_f32 ? 4 : 8), hipMemcpyDeviceToHost, s0));
@@ -160,6 +163,19 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
         return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
     return SCC_OK;
 #undef WS
+}
+
+extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
+                            int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32)
+{
+    return dist_impl(c, ds, genes, nu, metric, ncomp, 0, ds ? ds->N : 0, dist_out, out_kind, out_f32);
+}
+
+extern "C" int scc_distance_cols(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
+                                 int32_t ncomp, int64_t col_lo, int64_t col_hi, void* dist_out, int32_t out_kind,
+                                 int32_t out_f32)
+{
+    return dist_impl(c, ds, genes, nu, metric, ncomp, col_lo, col_hi, dist_out, out_kind, out_f32);
 }
 
 extern "C" int scc_last_pca_scores(const scc_ctx* c, double* scores, int32_t* ncomp)

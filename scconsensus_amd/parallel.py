@@ -72,6 +72,8 @@ def init(backend: str | None = None) -> Dist:
     if backend == "nccl":
         torch.cuda.set_device(local)
         device = torch.device(f"cuda:{local}")
+    elif os.environ.get("SCC_SHARE_GPU"):  # ranks rehearsed on one GPU over gloo
+        torch.cuda.set_device(0)
     tdist.init_process_group(backend)
     return Dist(rank, world, local, torch, tdist, device)
 

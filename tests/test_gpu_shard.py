@@ -91,3 +91,31 @@ def test_finish_requires_a_shard_run(cfg_a):
     buf = torch.zeros(e2.de_shard_bytes(len(names), d.G) // 8, dtype=torch.int64, device="cuda:0")
     with pytest.raises(nat.SccError):
         e2.de_finish(ds, code, len(names), buf.data_ptr())
+
+
+@pytest.mark.parametrize("metric,f32", [(nat.SCC_DIST_PCA_EUCLID, False), (nat.SCC_DIST_PCA_EUCLID, True),
+                                        (nat.SCC_DIST_PEARSON, False)])
+def test_distance_column_slices_match_full(eng, cfg_a, metric, f32):
+    d, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    union = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="union").union
+    full = eng.distance(ds, union, metric=metric, f32=f32)
+    for world in (2, 3, 8):
+        parts = [eng.distance_cols(ds, union, *sharded.column_shard(d.N, r, world), metric=metric, f32=f32)
+                 for r in range(world)]
+        np.testing.assert_array_equal(np.concatenate(parts), full)
+    # ragged slices: one column, the last column, an empty one, a block-unaligned middle
+    N = d.N
+    for lo, hi in [(0, 1), (N - 2, N), (5, 5), (63, 1000), (1000, N - 2)]:
+        s0 = lo * (2 * N - lo - 1) // 2
+        s1 = hi * (2 * N - hi - 1) // 2
+        np.testing.assert_array_equal(eng.distance_cols(ds, union, lo, hi, metric=metric, f32=f32), full[s0:s1])
+
+
+def test_distance_sharded_single_rank(eng, cfg_a):
+    d, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    union = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="union").union
+    lo, hi, out = sharded.distance_sharded(eng, ds, union, parallel.Dist(), device_out_ptr=None)
+    assert (lo, hi) == (0, d.N)
+    np.testing.assert_array_equal(out, eng.distance(ds, union))
