@@ -49,6 +49,8 @@ extern "C" {
 
 #define SCC_DE_FAST 0 /* reclusterDEConsensusFast(method = "wilcox") */
 #define SCC_DE_SLOW 1 /* reclusterDEConsensus(method = "Wilcoxon") */
+#define SCC_TEST_WILCOX 0 /* FAST test.use = "wilcox" (WilcoxDETest, Fast:78-91) */
+#define SCC_TEST_T 1      /* FAST test.use = "t" (DiffTTest: Welch t.test, Fast:185-196) */
 
 #define SCC_DIST_PCA_EUCLID 0 /* dist(prcomp_irlba(t(X[U,]), n=min(|U|,15))$x) */
 #define SCC_DIST_PEARSON 1    /* as.dist(1 - cor(X[U,], method = "pearson")) */
@@ -76,7 +78,7 @@ typedef struct {
     double mean_scaling_factor; /* SLOW: meanScalingFactor (slow:23) */
     int32_t test_all;           /* FAST: 1 = also compute U / p for the (pair, gene) cells the
                                    feature filters drop (diagnostics; R never tests them) */
-    int32_t reserved;
+    int32_t test;               /* FAST: SCC_TEST_WILCOX (default) | SCC_TEST_T; u2 / ties are 0 for t */
 } scc_de_params;
 
 /* ---- context ---------------------------------------------------------- */

@@ -53,14 +53,16 @@ reclusterDEConsensusFast <- function(dataMatrix, consensusClusterLabels, method 
                                      minClusterSize = 10, minPerCent = 20,
                                      filename = "de_gene_object.rds", plotName = "DE_Heatmap",
                                      NumbertopDEGenes = 30, nCores = 1) {
-  if (method != "wilcox") stop("Unknown test: ", method)
+  # test.use = method (Fast:372): "wilcox" and "t" run on the engine; "bimod" /
+  # "roc" need Seurat helpers the reference never loads
+  if (!(method %in% c("wilcox", "t"))) stop("Unknown test: ", method)
   if (is.null(names(consensusClusterLabels))) names(consensusClusterLabels) <- colnames(dataMatrix)
   labels <- consensusClusterLabels[colnames(dataMatrix)]
   sel <- .scc_codes(labels, minClusterSize)
   s <- .scc_slots(dataMatrix)
   res <- .Call("C_scc_de_fast", s$x, s$p, s$i, s$dim, sel$code, length(sel$clusters),
                as.double(qValThrs), as.double(logFCThrs), as.double(minPerCent),
-               as.integer(NumbertopDEGenes))
+               as.integer(NumbertopDEGenes), as.integer(method == "t"))
   deGeneUnion <- rownames(dataMatrix)[res[[1]]]
   print(str(deGeneUnion))
   d <- .scc_dist(s, res[[1]], ncol(dataMatrix))

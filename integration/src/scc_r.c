@@ -50,7 +50,8 @@ static scc_dataset* dataset_from(SEXP x, SEXP p, SEXP i, SEXP dim)
 }
 
 /* returns list(union = int (1-based gene rows), nodg = int[N]) */
-SEXP C_scc_de_fast(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qthr, SEXP lfc, SEXP minpct, SEXP topn)
+SEXP C_scc_de_fast(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qthr, SEXP lfc, SEXP minpct, SEXP topn,
+                   SEXP ttest)
 {
     ensure_ctx();
     scc_dataset* ds = dataset_from(x, p, i, dim);
@@ -61,6 +62,7 @@ SEXP C_scc_de_fast(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qth
     prm.log_fc_thrs = Rf_asReal(lfc);
     prm.min_per_cent = Rf_asReal(minpct);
     prm.top_n = Rf_asInteger(topn);
+    prm.test = Rf_asInteger(ttest) ? SCC_TEST_T : SCC_TEST_WILCOX; /* test.use = method (Fast:372) */
     scc_de_result* r = NULL;
     int rc = scc_de_run(g_ctx, ds, INTEGER(code), Rf_asInteger(K), &prm, &r);
     if (rc != SCC_OK && !r) {
@@ -154,7 +156,7 @@ SEXP C_scc_distance(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP genes, SEXP metric, S
 }
 
 static const R_CallMethodDef call_methods[] = {
-    {"C_scc_de_fast", (DL_FUNC)&C_scc_de_fast, 10},
+    {"C_scc_de_fast", (DL_FUNC)&C_scc_de_fast, 11},
     {"C_scc_de_slow", (DL_FUNC)&C_scc_de_slow, 9},
     {"C_scc_distance", (DL_FUNC)&C_scc_distance, 7},
     {NULL, NULL, 0}};

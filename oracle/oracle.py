@@ -117,6 +117,7 @@ class FastResult:
     row_de: np.ndarray        # q < qValThrs and pair kept (tested > 1)
     row_top: np.ndarray       # survived top_n
     union: np.ndarray         # deGeneUnion (gene indices, R order)
+    status: int = 0           # 5 (RSTOP): R's t.test stops on constant data
 
 
 def _check_dense(X, code, K):
@@ -128,17 +129,39 @@ def _check_dense(X, code, K):
     return X, code, G, N
 
 
-def de_fast(X, code, K, q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30) -> FastResult:
-    """reclusterDEConsensusFast DE stage. X is gene-major dense (G x N)."""
+def t_test_p(x, y):
+    """stats::t.test(x, y)$p.value (Welch); (p, constant) where constant means
+    R stops with "data are essentially constant"."""
+    L = lib()
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    f = L.orc_t_test_p
+    f.restype = ctypes.c_double
+    t = ctypes.c_double()
+    c = ctypes.c_int()
+    p = f(_dp(x), len(x), _dp(y), len(y), ctypes.byref(t), ctypes.byref(c))
+    return p, bool(c.value)
+
+
+def pt(x, n, lower_tail=True):
+    f = lib().orc_pt
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int]
+    return f(x, n, 1 if lower_tail else 0)
+
+
+def de_fast(X, code, K, q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, test="wilcox") -> FastResult:
+    """reclusterDEConsensusFast DE stage. X is gene-major dense (G x N).
+    test: "wilcox" (WilcoxDETest) or "t" (DiffTTest)."""
     L = lib()
     X, code, G, N = _check_dense(X, code, K)
     P = K * (K - 1) // 2
 
     class Prm(ctypes.Structure):
         _fields_ = [("q", ctypes.c_double), ("lfc", ctypes.c_double), ("mpc", ctypes.c_double),
-                    ("top", ctypes.c_int)]
+                    ("top", ctypes.c_int), ("test", ctypes.c_int), ("status", ctypes.c_int)]
 
-    prm = Prm(q_val_thrs, log_fc_thrs, min_per_cent, top_n)
+    prm = Prm(q_val_thrs, log_fc_thrs, min_per_cent, top_n, 1 if test == "t" else 0, 0)
     cap = max(1, P * G)
     tested = np.zeros(P, np.int32)
     gene = np.zeros(cap, np.int32)
@@ -155,7 +178,7 @@ def de_fast(X, code, K, q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_
     return FastResult(tested, pair, gene[:nrows].copy(), arr["p"][:nrows].copy(), arr["q"][:nrows].copy(),
                       arr["lfc"][:nrows].copy(), arr["pct1"][:nrows].copy(), arr["pct2"][:nrows].copy(),
                       arr["W"][:nrows].copy(), arr["T"][:nrows].copy(), (flags[:nrows] & 1) > 0,
-                      (flags[:nrows] & 2) > 0, uni[: nu.value].copy())
+                      (flags[:nrows] & 2) > 0, uni[: nu.value].copy(), prm.status)
 
 
 @dataclass

@@ -16,6 +16,7 @@
  *   R/reclusterDEConsensusFast.R:40-53   cluster selection (done by the caller; codes in)
  *   R/reclusterDEConsensusFast.R:229-291 pct / log-mean-expm1 / logFC feature filters
  *   R/reclusterDEConsensusFast.R:78-91   WilcoxDETest -> stats::wilcox.test(x ~ group)
+ *   R/reclusterDEConsensusFast.R:185-196 DiffTTest -> stats::t.test(x, y) (Welch), test.use = "t"
  *   R/reclusterDEConsensusFast.R:335-351 order(p, -avg_logFC); p.adjust(.,"BH")
  *   R/reclusterDEConsensusFast.R:359-392 pair loop, dim>1 rule, q filter, top_n, unique
  *   R/reclusterDEConsensus.R:32-36       global mean(expm1(X)) threshold
@@ -315,12 +316,130 @@ void orc_p_adjust_bh(const double *p, int len, long n, double *q)
     free(v);
 }
 
+/* ---------------------------------------------------------------- t test */
+/* R var() (src/library/stats/src/cov.c, one complete vector): long double
+ * mean, then the long double sum of squared deviations / (n - 1). */
+double orc_r_var(const double *x, long n, double mean)
+{
+    long double s = 0.0L;
+    for (long i = 0; i < n; ++i) s += ((long double)x[i] - mean) * ((long double)x[i] - mean);
+    return (double)(s / (long double)(n - 1));
+}
+
+/* Regularised incomplete beta I_x(a, b) by Lentz's continued fraction on the
+ * side where it converges fast (x < (a+1)/(a+b+2)), else 1 - I_{1-x}(b, a).
+ * DEVIATION: R's pbeta is TOMS 708 (bratio); Student t tails agree with scipy to ~1e-11
+ * relative here (checked against scipy in tests/test_oracle.py). */
+static double betacf(double a, double b, double x)
+{
+    const double tiny = 1e-300;
+    double qab = a + b, qap = a + 1.0, qam = a - 1.0, c = 1.0, d = 1.0 - qab * x / qap;
+    if (fabs(d) < tiny) d = tiny;
+    d = 1.0 / d;
+    double h = d;
+    for (int m = 1; m <= 10000; ++m) {
+        const int m2 = 2 * m;
+        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+        d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c; if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        h *= d * c;
+        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+        d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c; if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < 1e-16) break;
+    }
+    return h;
+}
+
+/* Stirling-series correction lgamma(x) - [(x - 1/2) log x - x + log sqrt(2 pi)], x >= 10 */
+static double lgammacor(double x)
+{
+    const double r = 1.0 / (x * x);
+    return (1.0 / 12 - r * (1.0 / 360 - r * (1.0 / 1260 - r * (1.0 / 1680 - r * (1.0 / 1188 -
+            r * (691.0 / 360360 - r / 156)))))) / x;
+}
+
+/* log B(a, b) in R nmath/lbeta.c's three regimes (no lgamma cancellation for
+ * large arguments) */
+static double orc_lbeta(double a, double b)
+{
+    const double p = fmin(a, b), q = fmax(a, b);
+    const double ln_sqrt_2pi = 0.918938533204672741780329736406;
+    if (p >= 10) {
+        const double corr = lgammacor(p) + lgammacor(q) - lgammacor(p + q);
+        return log(q) * -0.5 + ln_sqrt_2pi + corr + (p - 0.5) * log(p / (p + q)) + q * log1p(-p / (p + q));
+    }
+    if (q >= 10) {
+        const double corr = lgammacor(q) - lgammacor(p + q);
+        return lgamma(p) + corr + p - p * log(p + q) + (q - 0.5) * log1p(-p / (p + q));
+    }
+    return lgamma(p) + lgamma(q) - lgamma(p + q);
+}
+
+/* I_x(a, b) (lower = 1) or 1 - I_x(a, b) (lower = 0), x given with its
+ * complement y = 1 - x computed by the caller without cancellation. */
+static double orc_pbeta2(double x, double y, double a, double b, int lower)
+{
+    if (x <= 0.0) return lower ? 0.0 : 1.0;
+    if (y <= 0.0) return lower ? 1.0 : 0.0;
+    const double lx = x > 0.5 ? log1p(-y) : log(x), ly = y > 0.5 ? log1p(-x) : log(y);
+    const double lbt = a * lx + b * ly - orc_lbeta(a, b);
+    if (x < (a + 1.0) / (a + b + 2.0)) {
+        const double v = exp(lbt) * betacf(a, b, x) / a;
+        return lower ? v : 1.0 - v;
+    }
+    const double v = exp(lbt) * betacf(b, a, y) / b; /* = 1 - I_x(a, b) */
+    return lower ? 1.0 - v : v;
+}
+
+/* R nmath/pt.c, lower_tail, non-log */
+double orc_pt(double x, double n, int lower_tail)
+{
+    if (n > 4e5) {
+        const double val = 1.0 / (4.0 * n);
+        return orc_pnorm(x * (1.0 - val) / sqrt(1.0 + x * x * 2.0 * val), lower_tail);
+    }
+    const double nx = 1 + (x / n) * x;
+    double val;
+    if (nx > 1e100) {
+        const double lval = -0.5 * n * (2 * log(fabs(x)) - log(n)) - orc_lbeta(0.5 * n, 0.5) - log(0.5 * n);
+        val = exp(lval);
+    } else {
+        val = (n > x * x) ? orc_pbeta2(x * x / (n + x * x), n / (n + x * x), 0.5, n / 2.0, 0)
+                          : orc_pbeta2(1.0 / nx, (x / n) * x / nx, n / 2.0, 0.5, 1);
+    }
+    if (x <= 0.0) lower_tail = !lower_tail;
+    val /= 2.0;
+    return lower_tail ? (0.5 - val + 0.5) : val;
+}
+
+/* stats::t.test(x, y)$p.value (Welch, two-sided, mu = 0; R/t.test.R).
+ * *constant = 1 where R stops with "data are essentially constant". */
+double orc_t_test_p(const double *x, int nx, const double *y, int ny, double *tstat, int *constant)
+{
+    const double mx = orc_r_mean(x, nx), my = orc_r_mean(y, ny);
+    const double vx = orc_r_var(x, nx, mx), vy = orc_r_var(y, ny, my);
+    const double sx = sqrt(vx / nx), sy = sqrt(vy / ny);
+    const double se = sqrt(sx * sx + sy * sy);
+    const double df = pow(se, 4) / (pow(sx, 4) / (nx - 1) + pow(sy, 4) / (ny - 1));
+    *constant = se < 10 * DBL_EPSILON * fmax(fabs(mx), fabs(my));
+    const double t = (mx - my) / se;
+    if (tstat) *tstat = t;
+    return 2 * orc_pt(-fabs(t), df, 1);
+}
+
 /* ---------------------------------------------------------------- Fast driver */
 typedef struct {
     double q_val_thrs;   /* qValThrs */
     double log_fc_thrs;  /* logFCThrs (natural log) */
     double min_per_cent; /* minPerCent */
     int top_n;           /* NumbertopDEGenes */
+    int test;            /* 0: wilcox (Fast:78-91), 1: t (DiffTTest, Fast:185-196) */
+    int status;          /* out: ORC_ERR_RSTOP where R's t.test stops (constant data) */
 } orc_fast_params;
 
 typedef struct {
@@ -418,9 +537,16 @@ long orc_de_fast(const double *X, int G, int N, const int *code, int K, const or
                 const double *row = X + (size_t)g * N;
                 for (int k = 0; k < ni; ++k) xi[k] = row[ci[k]];
                 for (int k = 0; k < nj; ++k) yj[k] = row[cj[k]];
-                int meth;
-                pv[g] = orc_wilcox_p_scratch(xi, ni, yj, nj, &Wv[g], &Tv[g], &meth, tmp,
-                                             tmp + ni + nj, scr);
+                if (prm->test == 1) { /* DiffTTest: t.test(x = cells.1, y = cells.2)$p.value */
+                    int constant = 0;
+                    pv[g] = orc_t_test_p(xi, ni, yj, nj, NULL, &constant);
+                    if (constant) ((orc_fast_params *)prm)->status = ORC_ERR_RSTOP;
+                    Wv[g] = Tv[g] = 0.0;
+                } else {
+                    int meth;
+                    pv[g] = orc_wilcox_p_scratch(xi, ni, yj, nj, &Wv[g], &Tv[g], &meth, tmp,
+                                                 tmp + ni + nj, scr);
+                }
                 keys[f].gene = g;
                 keys[f].p = pv[g];
                 keys[f].nlfc = -(m1[g] - m2[g]);

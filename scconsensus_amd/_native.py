@@ -25,6 +25,8 @@ SCC_ERR_RSTOP = 5
 SCC_ERR_UNSUPPORTED = 6
 SCC_DE_FAST = 0
 SCC_DE_SLOW = 1
+SCC_TEST_WILCOX = 0
+SCC_TEST_T = 1
 SCC_DIST_PCA_EUCLID = 0
 SCC_DIST_PEARSON = 1
 SCC_PTR_HOST = 0
@@ -54,7 +56,7 @@ class DeParams(ctypes.Structure):
     _fields_ = [("mode", ctypes.c_int32), ("top_n", ctypes.c_int32), ("q_val_thrs", ctypes.c_double),
                 ("log_fc_thrs", ctypes.c_double), ("min_per_cent", ctypes.c_double), ("fc_thrs", ctypes.c_double),
                 ("mean_scaling_factor", ctypes.c_double), ("test_all", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("test", ctypes.c_int32)]
 
 
 _lib = None
@@ -232,43 +234,46 @@ class Engine:
 
     # -------------------------------------------------------------- DE
     def de_run(self, ds: Dataset, code, K, mode=SCC_DE_FAST, q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0,
-               top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all", test_all=None) -> DeResult:
+               top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all", test_all=None, test="wilcox") -> DeResult:
         """test_all (FAST): also compute U / p for the (pair, gene) cells the
         feature filters drop; default: only when the full per-pair vectors are
         fetched (fetch="all")."""
         code = np.ascontiguousarray(code, np.int32)
         prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
-                              fetch == "all" if test_all is None else test_all)
+                              fetch == "all" if test_all is None else test_all, test)
         r = ctypes.c_void_p()
         rc = self.lib.scc_de_run(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), ctypes.byref(r))
         return self._collect(r, rc, ds, mode, K, fetch)
 
     @staticmethod
-    def _de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor, test_all):
+    def _de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor, test_all,
+                   test="wilcox"):
+        if test not in ("wilcox", "t"):
+            raise ValueError(f"test must be 'wilcox' or 't', not {test!r}")
         return DeParams(mode, top_n, q_val_thrs, log_fc_thrs, min_per_cent, fc_thrs, mean_scaling_factor,
-                        1 if test_all else 0, 0)
+                        1 if test_all else 0, SCC_TEST_T if test == "t" else SCC_TEST_WILCOX)
 
     def de_shard_bytes(self, K, G) -> int:
         return int(self.lib.scc_de_shard_bytes(K, G))
 
     def de_run_shard(self, ds: Dataset, code, K, gene_lo, gene_hi, shard_ptr, mode=SCC_DE_FAST, q_val_thrs=0.1,
                      log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0,
-                     test_all=False):
+                     test_all=False, test="wilcox"):
         """Per-(pair, gene) DE cells of genes [gene_lo, gene_hi) into the device
         buffer at shard_ptr (de_shard_bytes(K, G) bytes, zero outside the shard)."""
         code = np.ascontiguousarray(code, np.int32)
         prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
-                              test_all)
+                              test_all, test)
         self._check(self.lib.scc_de_run_shard(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), gene_lo,
                                               gene_hi, ctypes.c_void_p(shard_ptr)))
 
     def de_finish(self, ds: Dataset, code, K, shards_sum_ptr, mode=SCC_DE_FAST, q_val_thrs=0.1, log_fc_thrs=0.5,
                   min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0, fetch="all",
-                  test_all=False) -> DeResult:
+                  test_all=False, test="wilcox") -> DeResult:
         """Selection and union from the summed shards of every rank (device)."""
         code = np.ascontiguousarray(code, np.int32)
         prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
-                              test_all)
+                              test_all, test)
         r = ctypes.c_void_p()
         rc = self.lib.scc_de_finish(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm),
                                     ctypes.c_void_p(shards_sum_ptr), ctypes.byref(r))

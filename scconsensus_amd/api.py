@@ -95,10 +95,9 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
                              deepSplitValues=(1, 2, 3, 4), minClusterSize=10, minPerCent=20,
                              filename="de_gene_object.rds", plotName="DE_Heatmap", NumbertopDEGenes=30, nCores=1,
                              *, gene_names=None, cluster_order=None, device=0, save=False, return_details=False):
-    if method != "wilcox":
-        # Fast:306-333: "bimod"/"roc" need Seurat helpers the reference never
-        # loads; "t" is SURVEY §8(f) "next".
-        raise NotImplementedError(f"Unknown test: {method} (this engine implements test.use = 'wilcox')")
+    if method not in ("wilcox", "t"):
+        # Fast:306-333: "bimod"/"roc" need Seurat helpers the reference never loads
+        raise NotImplementedError(f"Unknown test: {method} (this engine implements test.use = 'wilcox' and 't')")
     eng = _engine(device)
     m = _as_matrix(dataMatrix)
     N = m[-1] if m[0] == "csc" else m[1].shape[1]
@@ -109,7 +108,7 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
     ds = _upload(eng, m)
     res = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
                      min_per_cent=float(minPerCent), top_n=NumbertopDEGenes,
-                     fetch="rows" if return_details else "union")
+                     fetch="rows" if return_details else "union", test=method)
     if res.status == nat.SCC_ERR_RSTOP:
         raise RuntimeError(res.message)
     uni = res.union

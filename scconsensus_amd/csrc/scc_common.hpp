@@ -59,6 +59,18 @@ __device__ inline dd dd_add(dd x, dd y)
     s.lo += t.lo;
     return dd_fast_two_sum(s.hi, s.lo);
 }
+// exact product a * b as a double-double (FMA)
+__device__ inline dd dd_two_prod(double a, double b)
+{
+    const double p = a * b;
+    return dd{p, fma(a, b, -p)};
+}
+// x * y for a double-double x and a double y
+__device__ inline dd dd_mul_d(dd x, double y)
+{
+    const dd p = dd_two_prod(x.hi, y);
+    return dd_fast_two_sum(p.hi, fma(x.lo, y, p.lo));
+}
 // (hi + lo) / n rounded to double (one correction step; exact enough that the
 // result is the correctly rounded mean except in measure-zero cases).
 __device__ inline double dd_div_n(dd x, double n)

@@ -5,9 +5,13 @@
 #include <stdint.h>
 #include <stddef.h>
 
-#ifndef SCC_DE_FAST
+#ifndef SCC_DE_FAST  // (same values as include/scc.h)
 #define SCC_DE_FAST 0
 #define SCC_DE_SLOW 1
+#endif
+#ifndef SCC_TEST_T
+#define SCC_TEST_WILCOX 0
+#define SCC_TEST_T 1
 #endif
 
 #define SCC_ING_HIST_WAVES 16  // waves per ingest histogram workgroup (one partial expm1 sum each)
@@ -23,7 +27,9 @@ struct ScStatsLaunch {
     const int* cl_cc;
     double* mean_x;     // [K][G] (slow mode only)
     double* mean_e;     // [K][G] (fast mode only)
+    double* var_x;      // [K][G] (fast t test only)
     int mode;           // SCC_DE_FAST: mean of expm1(x); SCC_DE_SLOW: mean of x
+    int test;           // SCC_TEST_WILCOX | SCC_TEST_T (FAST)
     uint32_t* cnt_pos;  // [K][G]
     uint32_t* cnt_neg;  // [K][G]
 };
@@ -83,6 +89,9 @@ struct ScTestLaunch {
     const unsigned long long* accX;
     const unsigned long long* accF;
     int all_pairs;
+    int test;              // SCC_TEST_WILCOX | SCC_TEST_T
+    const double* var_x;   // [K][G] (t test)
+    int* err;              // bit 8: t.test would stop ("data are essentially constant")
     const double* wtab;
     const int* woff;
     double* out_p;

@@ -88,8 +88,11 @@ struct StatItem {
 };
 
 // FAST needs the per-cluster mean of expm1(x) (Fast:259-272), SLOW the mean
-// of x (slow:105): each mode accumulates only its own double-double sum.
-template <bool EXPM1>
+// of x (slow:105), the FAST t test (DiffTTest, Fast:185-196) both plus, in a
+// second pass (VAR), R's two-pass variance sum((x - mean)^2) / (n - 1) over
+// the cluster, zeros included.  Each pass accumulates only its own
+// double-double sums.
+template <bool EXPM1, bool SUMX, bool VAR>
 __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 {
     __shared__ int off[65];
@@ -111,6 +114,7 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
         }
         if (a == K) break;
         const int s0 = off[a] + (it - acc) * Lp, s1 = min(off[a + 1], s0 + Lp);
+        const double ma = VAR ? A.mean_x[(size_t)a * A.G + g] : 0.0;
         dd sx{0.0, 0.0}, se{0.0, 0.0};
         u32 pos = 0, neg = 0;
         for (int i = s0 + lane; i < s1; i += 256) {
@@ -119,18 +123,15 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
             for (int q = 0; q < 4; ++q) x[q] = (i + 64 * q < s1) ? scc_val_of(key[i + 64 * q]) : 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                if (EXPM1)
-                    se = dd_add_d(se, expm1(x[q]));
-                else
-                    sx = dd_add_d(sx, x[q]);
+                if (EXPM1) se = dd_add_d(se, expm1(x[q]));
+                if (SUMX) sx = dd_add_d(sx, x[q]);
+                if (VAR && i + 64 * q < s1) sx = dd_add(sx, dd_two_prod(x[q] - ma, x[q] - ma));
                 pos += (x[q] > 0.0);
                 neg += (x[q] < 0.0);
             }
         }
-        if (EXPM1)
-            se = dd_wave_sum_dpp(se);
-        else
-            sx = dd_wave_sum_dpp(sx);
+        if (EXPM1) se = dd_wave_sum_dpp(se);
+        if (SUMX || VAR) sx = dd_wave_sum_dpp(sx);
         pos = u32_wave_sum_dpp(pos);
         neg = u32_wave_sum_dpp(neg);
         if (lane == 0) item[it] = StatItem{sx.hi, sx.lo, se.hi, se.lo, pos, neg};
@@ -150,10 +151,15 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
             neg += item[q].neg;
         }
         const double na = (double)A.n_clu[a];
-        if (EXPM1)
-            A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
-        else
-            A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
+        if (VAR) {  // + the zeros' (0 - mean)^2, then / (n - 1)
+            const double m = A.mean_x[(size_t)a * A.G + g];
+            const double z = na - (double)A.cnt_pos[(size_t)a * A.G + g] - (double)A.cnt_neg[(size_t)a * A.G + g];
+            sx = dd_add(sx, dd_mul_d(dd_two_prod(m, m), z));
+            A.var_x[(size_t)a * A.G + g] = dd_div_n(sx, na - 1.0);
+            return;
+        }
+        if (EXPM1) A.mean_e[(size_t)a * A.G + g] = dd_div_n(se, na);
+        if (SUMX) A.mean_x[(size_t)a * A.G + g] = dd_div_n(sx, na);
         A.cnt_pos[(size_t)a * A.G + g] = pos;
         A.cnt_neg[(size_t)a * A.G + g] = neg;
     }
@@ -162,10 +168,14 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st)
 {
     if (L->G <= 0) return hipSuccess;
-    if (L->mode == SCC_DE_FAST)
-        hipLaunchKernelGGL(k_gene_stats<true>, dim3(L->G), dim3(ST_T), 0, st, *L);
-    else
-        hipLaunchKernelGGL(k_gene_stats<false>, dim3(L->G), dim3(ST_T), 0, st, *L);
+    if (L->mode == SCC_DE_FAST && L->test == SCC_TEST_T) {
+        hipLaunchKernelGGL((k_gene_stats<true, true, false>), dim3(L->G), dim3(ST_T), 0, st, *L);
+        hipLaunchKernelGGL((k_gene_stats<false, false, true>), dim3(L->G), dim3(ST_T), 0, st, *L);
+    } else if (L->mode == SCC_DE_FAST) {
+        hipLaunchKernelGGL((k_gene_stats<true, false, false>), dim3(L->G), dim3(ST_T), 0, st, *L);
+    } else {
+        hipLaunchKernelGGL((k_gene_stats<false, true, false>), dim3(L->G), dim3(ST_T), 0, st, *L);
+    }
     return hipGetLastError();
 }
 

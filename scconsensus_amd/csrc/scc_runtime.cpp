@@ -203,6 +203,8 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (out) *out = nullptr;
     if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
     if (prm->mode != SCC_DE_FAST && prm->mode != SCC_DE_SLOW) return fail(c, SCC_ERR_INVALID, "bad mode");
+    if (prm->test != SCC_TEST_WILCOX && (prm->test != SCC_TEST_T || prm->mode != SCC_DE_FAST))
+        return fail(c, SCC_ERR_INVALID, "test: SCC_TEST_WILCOX, or SCC_TEST_T with SCC_DE_FAST");
     if (K < 2) return fail(c, SCC_ERR_INVALID, "need at least two clusters");
     if (K > kMaxK) return fail(c, SCC_ERR_UNSUPPORTED, "K > 64 clusters is not supported by this build");
     hipSetDevice(c->device);
@@ -319,6 +321,9 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     WS("me", GK, d_me);
     WS("cntpos", GK, d_cntpos);
     WS("cntneg", GK, d_cntneg);
+    const bool ttest = fast && prm->test == SCC_TEST_T;  // DiffTTest (Fast:185-196): no rank stage
+    double* d_vx;
+    WS("vx", ttest ? GK : 1, d_vx);
     // rank accumulators: S, E, X per (pair, gene), F per (cluster, gene)
     const size_t acc_n = 3 * PG + (size_t)GK;
     WS("acc", acc_n, d_acc);
@@ -406,6 +411,8 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         S.cnt_pos = d_cntpos;
         S.cnt_neg = d_cntneg;
         S.mode = prm->mode;
+        S.test = ttest ? SCC_TEST_T : SCC_TEST_WILCOX;
+        S.var_x = d_vx;
         HIPCHK(c, scc_launch_gene_stats(&S, s0));
     }
     // SLOW: log(meanScalingFactor * mean(expm1(X))) (slow:36) gates the pair
@@ -443,6 +450,9 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     T.accX = accX;
     T.accF = accF;
     T.all_pairs = all_pairs ? 1 : 0;
+    T.test = ttest ? SCC_TEST_T : SCC_TEST_WILCOX;
+    T.var_x = d_vx;
+    T.err = d_err;
     T.wtab = c->d_wtab;
     T.woff = c->d_woff;
     T.out_p = d_p;
@@ -456,7 +466,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         Scope sc(c, "pair_filter", s0);
         HIPCHK(c, scc_launch_pair_filter(&T, s0));
     }
-    {
+    if (!ttest) {
         Scope sc(c, "gene_rank", s0);
         HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
         ScRankLaunch L{};
@@ -572,6 +582,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         if (e & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
         if (e & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
         if (e & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
+        if (e & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
         return SCC_OK;
     }
     if (stage == DE_FINISH) {
@@ -649,6 +660,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
     if (hdr[1] & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
+    if (hdr[1] & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
     scc_de_result* r = new scc_de_result();
     r->ctx = c;
     r->generation = c->generation;

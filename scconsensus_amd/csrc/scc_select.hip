@@ -110,6 +110,96 @@ __device__ inline double wilcox_p(i64 u2, i64 tie, int nx, int ny, const double*
     return 2 * scc_pnorm_small_tail(z);
 }
 
+// -------------------------------------------------------- Welch t test
+// stats::t.test(x, y)$p.value (R/t.test.R, two-sided, var.equal = FALSE) for
+// the DiffTTest path (Fast:185-196): 2 * pt(-|t|, df) with R nmath/pt.c's
+// regimes; pbeta by Lentz's continued fraction with R's lbeta (the oracle's
+// restatement, oracle/scc_oracle.c; TOMS 708 in R agrees to ~1e-11).
+__device__ inline double t_lgammacor(double x)
+{
+    const double r = 1.0 / (x * x);
+    return (1.0 / 12 - r * (1.0 / 360 - r * (1.0 / 1260 - r * (1.0 / 1680 - r * (1.0 / 1188 -
+            r * (691.0 / 360360 - r / 156)))))) / x;
+}
+
+__device__ inline double t_lbeta(double a, double b)
+{
+    const double p = fmin(a, b), q = fmax(a, b);
+    const double ln_sqrt_2pi = 0.918938533204672741780329736406;
+    if (p >= 10) {
+        const double corr = t_lgammacor(p) + t_lgammacor(q) - t_lgammacor(p + q);
+        return log(q) * -0.5 + ln_sqrt_2pi + corr + (p - 0.5) * log(p / (p + q)) + q * log1p(-p / (p + q));
+    }
+    if (q >= 10) {
+        const double corr = t_lgammacor(q) - t_lgammacor(p + q);
+        return lgamma(p) + corr + p - p * log(p + q) + (q - 0.5) * log1p(-p / (p + q));
+    }
+    return lgamma(p) + lgamma(q) - lgamma(p + q);
+}
+
+__device__ inline double t_betacf(double a, double b, double x)
+{
+    const double tiny = 1e-300;
+    const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
+    double c = 1.0, d = 1.0 - qab * x / qap;
+    if (fabs(d) < tiny) d = tiny;
+    d = 1.0 / d;
+    double h = d;
+    for (int m = 1; m <= 10000; ++m) {
+        const int m2 = 2 * m;
+        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        h *= d * c;
+        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < tiny) d = tiny;
+        c = 1.0 + aa / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < 1e-16) break;
+    }
+    return h;
+}
+
+// I_x(a, b) (lower) or 1 - I_x(a, b), with y = 1 - x from the caller
+__device__ inline double t_pbeta2(double x, double y, double a, double b, bool lower)
+{
+    if (x <= 0.0) return lower ? 0.0 : 1.0;
+    if (y <= 0.0) return lower ? 1.0 : 0.0;
+    const double lx = x > 0.5 ? log1p(-y) : log(x), ly = y > 0.5 ? log1p(-x) : log(y);
+    const double lbt = a * lx + b * ly - t_lbeta(a, b);
+    if (x < (a + 1.0) / (a + b + 2.0)) {
+        const double v = exp(lbt) * t_betacf(a, b, x) / a;
+        return lower ? v : 1.0 - v;
+    }
+    const double v = exp(lbt) * t_betacf(b, a, y) / b;
+    return lower ? 1.0 - v : v;
+}
+
+// 2 * pt(-|t|, n): the upper tail beyond |t| twice (R nmath/pt.c)
+__device__ inline double t_two_sided(double t, double n)
+{
+    const double x = -fabs(t);
+    if (n > 4e5) {
+        const double val = 1.0 / (4.0 * n);
+        return 2 * scc_pnorm_small_tail(x * (1.0 - val) / sqrt(1.0 + x * x * 2.0 * val));
+    }
+    const double nx = 1 + (x / n) * x;
+    double val;
+    if (nx > 1e100)
+        val = exp(-0.5 * n * (2 * log(fabs(x)) - log(n)) - t_lbeta(0.5 * n, 0.5) - log(0.5 * n));
+    else
+        val = (n > x * x) ? t_pbeta2(x * x / (n + x * x), n / (n + x * x), 0.5, n / 2.0, false)
+                          : t_pbeta2(1.0 / nx, (x / n) * x / nx, n / 2.0, 0.5, true);
+    return 2 * (val / 2.0);  // x <= 0: pt(x, lower) = val / 2
+}
+
 // -------------------------------------------------------- per (pair, gene)
 __device__ inline u64 f_tie3(u64 c) { return c * c * c - c; }
 
@@ -188,6 +278,22 @@ __global__ void __launch_bounds__(256) k_pair_test(ScTestLaunch A)
         return;
     }
     const int na = A.n_clu[a], nb = A.n_clu[b];
+    if (A.test == SCC_TEST_T) {  // DiffTTest: t.test(x = cluster a, y = cluster b)
+        const double mx = A.mean_x[(size_t)a * A.G + g], my = A.mean_x[(size_t)b * A.G + g];
+        const double vx = A.var_x[(size_t)a * A.G + g], vy = A.var_x[(size_t)b * A.G + g];
+        const double sx = sqrt(vx / na), sy = sqrt(vy / nb);
+        const double se = sqrt(sx * sx + sy * sy);
+        const double df = pow(se, 4.0) / (pow(sx, 4.0) / (na - 1) + pow(sy, 4.0) / (nb - 1));
+        double pv = __longlong_as_double(0x7ff8000000000000ll);
+        if (se < 10 * 2.220446049250313e-16 * fmax(fabs(mx), fabs(my)))
+            atomicOr(A.err, 8);  // R: stop("data are essentially constant")
+        else
+            pv = t_two_sided((mx - my) / se, df);
+        A.out_p[pg] = pv;
+        A.out_u2[pg] = 0;
+        A.out_t[pg] = 0;
+        return;
+    }
     const u64 pa = A.cnt_pos[(size_t)a * A.G + g], ga = A.cnt_neg[(size_t)a * A.G + g];
     const u64 pb = A.cnt_pos[(size_t)b * A.G + g], gb = A.cnt_neg[(size_t)b * A.G + g];
     const u64 za = (u64)na - pa - ga, zb = (u64)nb - pb - gb;

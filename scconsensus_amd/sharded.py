@@ -18,7 +18,7 @@ from __future__ import annotations
 from . import parallel
 
 _SHARD_KEYS = ("mode", "q_val_thrs", "log_fc_thrs", "min_per_cent", "top_n", "fc_thrs", "mean_scaling_factor",
-               "test_all")
+               "test_all", "test")
 
 
 def gene_shard(G: int, rank: int, world: int) -> tuple[int, int]:

@@ -79,6 +79,35 @@ def test_fast_config_a_params(eng, cfg_a, kw):
     _fast_compare(eng, ds, X, code, len(names), **kw)
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(min_per_cent=5.0, log_fc_thrs=0.1, top_n=10)])
+def test_fast_t_test_config_a(eng, cfg_a, kw):
+    """test.use = "t" (DiffTTest, Fast:185-196): Welch t.test p per tested
+    feature, then the same BH / filters / union as the Wilcoxon path."""
+    d, X, names, code = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g, o = _fast_compare(eng, ds, X, code, len(names), test="t", **kw)
+    assert o.status == 0 and len(o.union) > 20
+    assert np.max(np.abs(g.rows.p - o.row_p) / np.maximum(o.row_p, 1e-300)) < 1e-9
+    assert (g.rows.u2 == 0).all()
+
+
+def test_fast_t_test_constant_data_stops(eng):
+    """R's t.test stops on "data are essentially constant": a tested gene
+    constant within both clusters (different levels) makes the engine return
+    SCC_ERR_RSTOP, like the oracle's status."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(5)
+    N, G = 60, 5
+    code = np.repeat(np.arange(3), 20).astype(np.int32)
+    X = rng.gamma(1.0, 1.0, (G, N)) * (rng.random((G, N)) < 0.7)
+    X[2] = np.where(code == 0, 1.0, 3.0)
+    assert O.de_fast(X, code, 3, test="t").status == nat.SCC_ERR_RSTOP
+    ds = eng.dataset_dense(X)
+    with pytest.raises(nat.SccError) as e:
+        eng.de_run(ds, code, 3, nat.SCC_DE_FAST, test="t", fetch="rows")
+    assert e.value.code == nat.SCC_ERR_RSTOP
+
+
 @pytest.mark.parametrize("K", [18, 26])
 def test_fast_many_clusters(eng, K):
     """More tested pairs per gene than the wave kernel's 2-slot variant holds

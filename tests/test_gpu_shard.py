@@ -62,6 +62,15 @@ def test_fast_shards_match_unsharded(eng, cfg_a, bounds):
     assert len(got.union) > 50
 
 
+def test_fast_t_shards_match_unsharded(eng, cfg_a):
+    d, names, code = cfg_a
+    K = len(names)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    ref = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows", test="t")
+    tot = _run_shards(eng, ds, code, K, [(0, 900), (900, 2000)], test="t")
+    _same(ref, eng.de_finish(ds, code, K, tot.data_ptr(), fetch="rows", test="t"))
+
+
 def test_slow_shards_match_unsharded(eng, cfg_a):
     d, names, code = cfg_a
     K = len(names)

@@ -119,3 +119,51 @@ def test_r_mean_long_double():
     v = rng.gamma(0.5, 3, 5000)
     exact = math.fsum(v) / len(v)
     assert O.r_mean(v) == pytest.approx(exact, rel=2e-16)
+
+
+# ------------------------------------------------------------------ t test (DiffTTest, Fast:185-196)
+@pytest.mark.parametrize("seed", range(6))
+def test_t_test_vs_scipy(seed):
+    from scipy import stats
+    rng = np.random.default_rng(seed)
+    for _ in range(40):
+        nx, ny = rng.integers(3, 400, 2)
+        x = rng.gamma(rng.uniform(0.2, 3), 1.0, nx) * (rng.random(nx) < 0.6)
+        y = rng.gamma(rng.uniform(0.2, 3), 1.0, ny) * (rng.random(ny) < 0.6) + rng.uniform(0, 2)
+        p, const = O.t_test_p(x, y)
+        ref = stats.ttest_ind(x, y, equal_var=False).pvalue
+        assert not const
+        assert abs(p - ref) <= 1e-12 * max(ref, 1e-300) + 1e-300, (p, ref)
+
+
+def test_t_test_tails_and_constant():
+    from scipy import stats
+    x = np.r_[np.zeros(50), 10.0 + np.arange(5) * 1e-3]
+    y = np.r_[np.full(60, 20.0), 20.001, 19.999]
+    p, const = O.t_test_p(x, y)
+    assert p == pytest.approx(stats.ttest_ind(x, y, equal_var=False).pvalue, rel=1e-10)
+    _, const = O.t_test_p(np.full(5, 2.0), np.full(7, 2.0))
+    assert const                                      # R: "data are essentially constant"
+
+
+@pytest.mark.parametrize("df", [1.0, 2.5, 7.0, 30.0, 1e3, 1e5])
+def test_pt_vs_scipy(df):
+    from scipy import stats
+    for t in [-40.0, -8.0, -3.0, -1.0, -0.1, 0.0, 0.5, 2.0, 6.0]:
+        assert O.pt(t, df) == pytest.approx(stats.t.cdf(t, df), rel=1e-10, abs=1e-300)  # CF vs cephes
+
+
+def test_de_fast_t_matches_scipy_per_row():
+    from scipy import stats
+    from scconsensus_amd import synth, api
+    d = synth.generate("A", G=150, N=600, K=4, seed=3)
+    names, code = api.select_clusters(d.labels, 10)
+    X = d.dense()
+    o = O.de_fast(X, code, len(names), test="t", log_fc_thrs=0.1, min_per_cent=10.0)
+    assert o.status == 0 and len(o.row_gene) > 20
+    pairs = [(i, j) for i in range(len(names)) for j in range(i + 1, len(names))]
+    for r in range(len(o.row_gene)):
+        i, j = pairs[o.row_pair[r]]
+        x, y = X[o.row_gene[r], code == i], X[o.row_gene[r], code == j]
+        assert o.row_p[r] == pytest.approx(stats.ttest_ind(x, y, equal_var=False).pvalue, rel=1e-10)
+    assert (o.row_W == 0).all()
