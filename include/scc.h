@@ -164,6 +164,17 @@ SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* gen
 SCC_API int scc_distance_cols(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */,
                       int32_t n_union, int32_t metric, int32_t ncomp, int64_t col_lo, int64_t col_hi,
                       void* dist_out, int32_t out_kind, int32_t out_f32);
+/* ---- silhouette on the distance vector (Fast:433) ---------
+ * cluster::silhouette(groups, dmatrix = as.matrix(d)) without the N x N
+ * matrix: widths[i] = s(i) (0 for a singleton cluster), clus_avg[k] = mean
+ * width of the k-th cluster in increasing group-id order (summary(.)$
+ * clus.avg.widths; the reference averages them into "SI").  dist: device
+ * pointer to the full packed vector (f64, or f32 if dist_f32), or NULL for
+ * the engine-kept output of the last full scc_distance call.  Needs
+ * 2 <= n_groups < n_cells (R returns NA otherwise).  Any output may be NULL. */
+SCC_API int scc_silhouette(scc_ctx* ctx, int64_t n_cells, const int32_t* groups /* host [N] */, const void* dist,
+                   int32_t dist_f32, double* widths /* host [N] */, double* clus_avg /* host [n_groups] */,
+                   int32_t* n_groups);
 /* PCA scores (N x ncomp, row-major) of the last PCA distance call. */
 SCC_API int scc_last_pca_scores(const scc_ctx* ctx, double* scores, int32_t* ncomp);
 

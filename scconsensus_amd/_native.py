@@ -38,7 +38,7 @@ EXPORTS = [
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_dense", "scc_dataset_destroy",
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
-    "scc_distance", "scc_distance_cols", "scc_last_pca_scores",
+    "scc_distance", "scc_distance_cols", "scc_silhouette", "scc_last_pca_scores",
 ]
 
 
@@ -110,6 +110,7 @@ def load():
         "scc_de_result_destroy": (None, [vp]),
         "scc_distance": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp, i32, i32]),
         "scc_distance_cols": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i64, i64, vp, i32, i32]),
+        "scc_silhouette": (ctypes.c_int, [vp, i64, vp, vp, i32, vp, vp, P(i32)]),
         "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
     }
     for name, (res, args) in sig.items():
@@ -358,6 +359,17 @@ class Engine:
         self._check(self.lib.scc_distance_cols(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, col_lo,
                                                col_hi, _ptr(out), SCC_PTR_HOST, 1 if f32 else 0))
         return out
+
+    def silhouette(self, N, groups, dist_device_ptr=None, f32=False):
+        """(widths [N], per-cluster average widths in sorted group order) of
+        cluster::silhouette(groups, as.matrix(d)); d = the engine-kept output
+        of the last full distance() call unless a device pointer is given."""
+        groups = np.ascontiguousarray(groups, np.int32)
+        C = len(np.unique(groups))
+        w, ca, k = np.zeros(N), np.zeros(max(C, 1)), ctypes.c_int32()
+        self._check(self.lib.scc_silhouette(self.ctx, N, _ptr(groups), ctypes.c_void_p(dist_device_ptr or None),
+                                            1 if f32 else 0, _ptr(w), _ptr(ca), ctypes.byref(k)))
+        return w, ca[:k.value]
 
     def last_pca_scores(self, N):
         k = ctypes.c_int32()

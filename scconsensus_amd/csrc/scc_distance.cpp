@@ -22,6 +22,9 @@ hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nc
 hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C, hipStream_t st);
 hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
                              hipStream_t st);
+size_t scc_sil_scratch_doubles(int N, int C);
+hipError_t scc_launch_silhouette(const void* D, int f32, int N, const int* lab, const int* cnt, int C, double* part,
+                                 double* width, hipStream_t st);
 hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st);
 hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, int c_lo, int c_hi,
                               void* out, int f32, hipStream_t st);
@@ -158,6 +161,9 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     if (out_kind == SCC_PTR_HOST) {
         HIPCHK(c, hipMemcpyAsync(dist_out, d_out, npairs * (out_f32 ? 4 : 8), hipMemcpyDeviceToHost, s0));
     }
+    c->d_last_dist = (col_lo == 0 && col_hi == N) ? d_out : nullptr;  // what scc_silhouette(dist = NULL) reads
+    c->last_dist_n = N;
+    c->last_dist_f32 = out_f32 ? 1 : 0;
     HIPCHK(c, hipStreamSynchronize(s0));
     if (metric == SCC_DIST_PCA_EUCLID && c->eig_err)
         return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
@@ -176,6 +182,59 @@ extern "C" int scc_distance_cols(scc_ctx* c, const scc_dataset* ds, const int32_
                                  int32_t out_f32)
 {
     return dist_impl(c, ds, genes, nu, metric, ncomp, col_lo, col_hi, dist_out, out_kind, out_f32);
+}
+
+extern "C" int scc_silhouette(scc_ctx* c, int64_t n_cells, const int32_t* groups, const void* dist, int32_t dist_f32,
+                              double* widths, double* clus_avg, int32_t* n_groups)
+{
+    if (!c || !groups) return fail(c, SCC_ERR_INVALID, "scc_silhouette: null argument");
+    const int N = (int)n_cells;
+    if (N < 2) return fail(c, SCC_ERR_INVALID, "scc_silhouette: need at least two cells");
+    const void* D = dist;
+    int f32 = dist_f32 ? 1 : 0;
+    if (!D) {
+        if (!c->d_last_dist || c->last_dist_n != N)
+            return fail(c, SCC_ERR_INVALID, "scc_silhouette: no full scc_distance output of this size is kept");
+        D = c->d_last_dist;
+        f32 = c->last_dist_f32;
+    }
+    // cluster codes in increasing id order (silhouette's sorted clusters)
+    std::vector<int32_t> ids(groups, groups + N);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    const int C = (int)ids.size();
+    if (n_groups) *n_groups = C;
+    if (C < 2 || C >= N) return fail(c, SCC_ERR_INVALID, "silhouette needs 2 <= clusters < cells (R returns NA)");
+    std::vector<int> lab(N), cnt(C, 0);
+    for (int i = 0; i < N; ++i) {
+        lab[i] = (int)(std::lower_bound(ids.begin(), ids.end(), groups[i]) - ids.begin());
+        cnt[lab[i]]++;
+    }
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    int rc;
+    int *d_lab, *d_cnt;
+    double *d_part, *d_w;
+    if ((rc = ws(c, "sil_lab", N, &d_lab))) return rc;
+    if ((rc = ws(c, "sil_cnt", C, &d_cnt))) return rc;
+    if ((rc = ws(c, "sil_part", scc_sil_scratch_doubles(N, C), &d_part))) return rc;
+    if ((rc = ws(c, "sil_w", N, &d_w))) return rc;
+    HIPCHK(c, hipMemcpyAsync(d_lab, lab.data(), sizeof(int) * N, hipMemcpyHostToDevice, s0));
+    HIPCHK(c, hipMemcpyAsync(d_cnt, cnt.data(), sizeof(int) * C, hipMemcpyHostToDevice, s0));
+    {
+        Scope sc(c, "silhouette", s0);
+        HIPCHK(c, scc_launch_silhouette(D, f32, N, d_lab, d_cnt, C, d_part, d_w, s0));
+    }
+    std::vector<double> w(N);
+    HIPCHK(c, hipMemcpyAsync(w.data(), d_w, sizeof(double) * N, hipMemcpyDeviceToHost, s0));
+    HIPCHK(c, hipStreamSynchronize(s0));
+    if (widths) std::copy(w.begin(), w.end(), widths);
+    if (clus_avg) {  // summary(.)$clus.avg.widths: mean width per cluster (long double sums, R mean)
+        std::vector<long double> sum(C, 0.0L);
+        for (int i = 0; i < N; ++i) sum[lab[i]] += w[i];
+        for (int k = 0; k < C; ++k) clus_avg[k] = (double)(sum[k] / cnt[k]);
+    }
+    return SCC_OK;
 }
 
 extern "C" int scc_last_pca_scores(const scc_ctx* c, double* scores, int32_t* ncomp)

@@ -63,6 +63,9 @@ struct scc_ctx {
     int last_n = 0;
     int last_ncomp = 0;
     unsigned int eig_err = 0;  // hand-off timeout flag of the last eigensolve (host copy)
+    const void* d_last_dist = nullptr;  // device copy of the last full scc_distance output
+    int64_t last_dist_n = 0;
+    int last_dist_f32 = 0;
     int64_t shard_sig[6] = {-1, -1, -1, -1, -1, -1};  // inputs of the last scc_de_run_shard
     double shard_log_thr = 0.0;
 };
