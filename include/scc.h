@@ -178,6 +178,21 @@ SCC_API int scc_silhouette(scc_ctx* ctx, int64_t n_cells, const int32_t* groups 
 /* PCA scores (N x ncomp, row-major) of the last PCA distance call. */
 SCC_API int scc_last_pca_scores(const scc_ctx* ctx, double* scores, int32_t* ncomp);
 
+/* ---- host clustering on the packed distance --------------
+ * Host code (no device needed), restating the packages the reference calls:
+ *   fastcluster::hclust(d, method = "ward.D2")            Fast:406-411
+ *     merge: [2 (n-1)] int32, R's column-major (n-1) x 2 merge matrix
+ *     (-i = observation i, +k = merge k, 1-based); height [n-1]; order [n]
+ *     (1-based leaf order, may be NULL).  dist: host packed R `dist` vector.
+ *   dynamicTreeCut::cutreeDynamic(dendro, distM = as.matrix(d), deepSplit,
+ *     pamStage = FALSE, minClusterSize) (method "hybrid", default cut height)
+ *                                                         Fast:421-427
+ *     labels [n]: 0 = unassigned, 1.. by decreasing cluster size; cut_height
+ *     (may be NULL) receives the default cut height used. */
+SCC_API int scc_hclust_ward_d2(const double* dist, int64_t n, int32_t* merge, double* height, int32_t* order);
+SCC_API int scc_cutree_hybrid(const int32_t* merge, const double* height, int64_t n, const double* dist,
+                              int32_t deep_split, int32_t min_cluster_size, int32_t* labels, double* cut_height);
+
 #ifdef __cplusplus
 }
 #endif

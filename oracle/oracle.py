@@ -255,3 +255,167 @@ def dist_pearson(X, genes):
     D = 1.0 - C
     np.fill_diagonal(D, 0.0)
     return squareform(D, checks=False)
+
+
+# ---------------------------------------------------------------------------
+# Host clustering restatements, checkers for libscc's
+# scc_hclust_ward_d2 / scc_cutree_hybrid.  Pure Python, small N only.
+#
+# hclust(ward.D2) (fastcluster, Fast:406-411) is pinned to scipy's Ward
+# linkage, which fastcluster's documentation names as the same method
+# ("ward.D2" in R == "ward" in Python): ward_d2_r converts scipy's linkage to
+# R's hclust merge / height convention.  cutreeDynamic(hybrid, pamStage =
+# FALSE) (dynamicTreeCut, Fast:421-427) has no independent implementation in
+# this image: cutree_hybrid below restates the package's published
+# cutreeHybrid line by line on a full distM (R vectors, 1-based branch ids),
+# and is itself "parity unpinned" — it cross-checks the C++ restatement and
+# is checked against hand-worked dendrograms in tests/test_cluster.py.
+
+def ward_d2_r(dist_packed, n):
+    """R hclust(d, "ward.D2") merge (n-1 x 2, R convention), height via scipy."""
+    from scipy.cluster.hierarchy import linkage
+    Z = linkage(np.asarray(dist_packed, np.float64), method="ward")
+    merge = np.zeros((n - 1, 2), np.int64)
+    for k in range(n - 1):
+        a, b = sorted((int(Z[k, 0]), int(Z[k, 1])))
+        merge[k] = [-(a + 1) if a < n else a - n + 1, -(b + 1) if b < n else b - n + 1]
+    return merge, Z[:, 2].copy()
+
+
+def _interpolate(data, index):
+    i = round(index)  # Python round == R round (half to even)
+    n = len(data)
+    if i < 1:
+        return data[0]
+    if i >= n:
+        return data[n - 1]
+    r = index - i
+    return data[i - 1] * (1 - r) + data[i] * r
+
+
+def _core_size(branch_size, min_cluster_size):
+    base = min_cluster_size / 2 + 1
+    return int(base + np.sqrt(branch_size - base)) if base < branch_size else branch_size
+
+
+def cutree_hybrid(merge, height, distM, deepSplit=1, minClusterSize=20):
+    """dynamicTreeCut::cutreeHybrid(..., pamStage = FALSE)$labels."""
+    merge = np.asarray(merge)
+    height = np.asarray(height, np.float64)
+    nMerge = len(height)
+    nPoints = nMerge + 1
+    refMerge = max(int(round(nMerge * 0.05)), 1)
+    refHeight = height[refMerge - 1]
+    cutHeight = 0.99 * (height.max() - refHeight) + refHeight
+    nMergeBelowCut = int((height <= cutHeight).sum())
+    if nMergeBelowCut < minClusterSize:
+        return np.zeros(nPoints, np.int64)
+    defMCS = [0.64, 0.73, 0.82, 0.91, 0.95]
+    defMG = [(1 - x) * 3 / 4 for x in defMCS]
+    ds = deepSplit + 1
+    maxCoreScatter = _interpolate(defMCS, ds)
+    minGap = _interpolate(defMG, ds)
+    maxAbsCoreScatter = refHeight + maxCoreScatter * (cutHeight - refHeight)
+    minAbsGap = minGap * (cutHeight - refHeight)
+    minAbsSplitHeight = refHeight + 0 * (cutHeight - refHeight)
+
+    isBasic, isTopBasic, failSize, attachHeight = {}, {}, {}, {}
+    size, singletons, basicClusters, mergedInto = {}, {}, {}, {}
+    IndMergeToBranch = [0] * nMerge
+    nBranches = 0
+
+    def scatter(b):
+        cs = _core_size(len(singletons[b]), minClusterSize)
+        core = np.array(singletons[b][:cs]) - 1
+        sub = distM[np.ix_(core, core)]
+        return float(np.mean(sub.sum(axis=0) / (cs - 1)))
+
+    for m in range(nMerge):
+        if not height[m] <= cutHeight:
+            continue
+        a, b = int(merge[m, 0]), int(merge[m, 1])
+        h = height[m]
+        if a < 0 and b < 0:
+            nBranches += 1
+            isBasic[nBranches] = isTopBasic[nBranches] = True
+            failSize[nBranches] = False
+            attachHeight[nBranches] = None
+            size[nBranches] = 2
+            singletons[nBranches] = [-a, -b]
+            basicClusters[nBranches] = []
+            IndMergeToBranch[m] = nBranches
+        elif (a < 0) != (b < 0):
+            clust = IndMergeToBranch[max(a, b) - 1]
+            gene = -min(a, b)
+            if isBasic[clust]:
+                singletons[clust].append(gene)
+            size[clust] += 1
+            IndMergeToBranch[m] = clust
+        else:
+            clusts = [IndMergeToBranch[a - 1], IndMergeToBranch[b - 1]]
+            sizes = [size[c] for c in clusts]
+            small, large = (clusts[1], clusts[0]) if sizes[0] > sizes[1] else (clusts[0], clusts[1])
+            SmAveDist = scatter(small) if isBasic[small] else 0.0
+            LgAveDist = scatter(large) if isBasic[large] else 0.0
+            Sm = [isBasic[small], size[small] < minClusterSize, SmAveDist > maxAbsCoreScatter,
+                  h - SmAveDist < minAbsGap, h < minAbsSplitHeight]
+            if Sm[0] and sum(Sm[1:]) > 0:
+                DoMerge, SmallerFailSize = True, not (Sm[2] or Sm[3])
+            else:
+                Lg = [isBasic[large], size[large] < minClusterSize, LgAveDist > maxAbsCoreScatter,
+                      h - LgAveDist < minAbsGap, h < minAbsSplitHeight]
+                if Lg[0] and sum(Lg[1:]) > 0:
+                    DoMerge, SmallerFailSize = True, not (Lg[2] or Lg[3])
+                    small, large = large, small
+                else:
+                    DoMerge = False
+            if DoMerge:
+                failSize[small] = SmallerFailSize
+                mergedInto[small] = large
+                attachHeight[small] = h
+                isTopBasic[small] = False
+                if isBasic[large]:
+                    singletons[large] = singletons[large] + singletons[small]
+                size[large] += size[small]
+                IndMergeToBranch[m] = large
+            else:
+                if isBasic[large] and not isBasic[small]:
+                    small, large = large, small
+                if isBasic[large]:
+                    nBranches += 1
+                    attachHeight[large] = attachHeight[small] = h
+                    mergedInto[large] = mergedInto[small] = nBranches
+                    add = [small] if isBasic[small] else list(basicClusters[small])
+                    add += [large] if isBasic[large] else list(basicClusters[large])
+                    isBasic[nBranches] = isTopBasic[nBranches] = False
+                    failSize[nBranches] = False
+                    attachHeight[nBranches] = None
+                    basicClusters[nBranches] = add
+                    singletons[nBranches] = []
+                    size[nBranches] = size[small] + size[large]
+                    IndMergeToBranch[m] = nBranches
+                else:
+                    add = [small] if isBasic[small] else list(basicClusters[small])
+                    basicClusters[large] = basicClusters[large] + add
+                    size[large] += size[small]
+                    attachHeight[small] = h
+                    mergedInto[small] = large
+                    IndMergeToBranch[m] = large
+
+    Colors = np.zeros(nPoints, np.int64)
+    color = 0
+    for clust in range(1, nBranches + 1):
+        if attachHeight[clust] is None:
+            attachHeight[clust] = cutHeight
+        if isTopBasic[clust]:
+            cs = scatter(clust)
+            if size[clust] >= minClusterSize and cs < maxAbsCoreScatter and attachHeight[clust] - cs > minAbsGap:
+                color += 1
+                Colors[np.array(singletons[clust]) - 1] = color
+    # relabel by decreasing size, 0 (unlabeled) kept
+    counts = np.bincount(Colors, minlength=color + 1)
+    order = sorted(range(1, color + 1), key=lambda c: (-counts[c], c))
+    rel = np.zeros(color + 1, np.int64)
+    for r, c in enumerate(order):
+        rel[c] = r + 1
+    return rel[Colors]

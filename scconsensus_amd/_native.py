@@ -39,6 +39,7 @@ EXPORTS = [
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
     "scc_distance", "scc_distance_cols", "scc_silhouette", "scc_last_pca_scores",
+    "scc_hclust_ward_d2", "scc_cutree_hybrid",
 ]
 
 
@@ -112,6 +113,8 @@ def load():
         "scc_distance_cols": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i64, i64, vp, i32, i32]),
         "scc_silhouette": (ctypes.c_int, [vp, i64, vp, vp, i32, vp, vp, P(i32)]),
         "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
+        "scc_hclust_ward_d2": (ctypes.c_int, [vp, i64, vp, vp, vp]),
+        "scc_cutree_hybrid": (ctypes.c_int, [vp, vp, i64, vp, i32, i32, vp, P(dbl)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -389,3 +392,41 @@ class Engine:
 
     def synchronize(self):
         self._check(self.lib.scc_ctx_synchronize(self.ctx))
+
+
+# ---------------------------------------------------------------- host clustering
+# Host functions of libscc (no device, no Engine): the reference keeps tree
+# building and tree cutting on the host (Fast:406-427).
+
+def hclust_ward_d2(dist_packed, n):
+    """fastcluster::hclust(d, "ward.D2") -> (merge (n-1, 2) int32 in R's
+    convention, height (n-1,), order (n,) 1-based)."""
+    d = np.ascontiguousarray(dist_packed, np.float64)
+    if d.shape != (n * (n - 1) // 2,):
+        raise ValueError("dist_packed must hold n(n-1)/2 entries")
+    merge = np.zeros(2 * (n - 1), np.int32)
+    height = np.zeros(n - 1)
+    order = np.zeros(n, np.int32)
+    rc = load().scc_hclust_ward_d2(_ptr(d), n, _ptr(merge), _ptr(height), _ptr(order))
+    if rc != SCC_OK:
+        raise SccError(rc, "scc_hclust_ward_d2 failed")
+    return merge.reshape(2, n - 1).T.copy(), height, order
+
+
+def cutree_hybrid(merge, height, dist_packed, deep_split=1, min_cluster_size=20):
+    """dynamicTreeCut::cutreeDynamic(method = "hybrid", pamStage = FALSE)
+    labels (0 = unassigned) and the default cut height used."""
+    merge = np.asarray(merge)
+    n = merge.shape[0] + 1
+    m = np.ascontiguousarray(merge.T.reshape(-1), np.int32)
+    h = np.ascontiguousarray(height, np.float64)
+    d = np.ascontiguousarray(dist_packed, np.float64)
+    if d.shape != (n * (n - 1) // 2,) or h.shape != (n - 1,):
+        raise ValueError("shape mismatch between merge, height and dist_packed")
+    lab = np.zeros(n, np.int32)
+    cut = ctypes.c_double()
+    rc = load().scc_cutree_hybrid(_ptr(m), _ptr(h), n, _ptr(d), int(deep_split), int(min_cluster_size), _ptr(lab),
+                                  ctypes.byref(cut))
+    if rc != SCC_OK:
+        raise SccError(rc, "scc_cutree_hybrid failed (deepSplit must be 0..4)")
+    return lab, cut.value

@@ -13,11 +13,11 @@ Reference signatures:
 
 What runs where: cluster selection (A0), printing and the
 saved object stay on the host like in R; the pairwise DE, BH/filters/union and
-the distance matrix run in libscc on the GPU; hclust(ward.D2) runs on the host
-(scipy's Ward linkage == R's "ward.D2") as the reference keeps it on the host.
-dynamicTreeCut::cutreeDynamic / WGCNA::labels2colors and the ComplexHeatmap
-plot are not part of this engine; ``dynamicColors`` is returned
-as ``None`` and ``plotName`` is ignored.
+the distance matrix run in libscc on the GPU; hclust(ward.D2), cutreeDynamic
+(hybrid, pamStage = FALSE) and labels2colors run on the host as the reference
+keeps them there (libscc's host functions scc_hclust_ward_d2 /
+scc_cutree_hybrid).  The ComplexHeatmap plot is not part of
+this engine; ``plotName`` is ignored.
 """
 from __future__ import annotations
 
@@ -78,9 +78,46 @@ def _upload(eng, m):
     return eng.dataset_dense(m[1])
 
 
+# WGCNA standardColors(): the 34 base colours (labels2colors' palette for
+# labels 1..34).  WGCNA extends the list with the rest of R's colors() in a
+# fixed pseudo-random order; R is absent here, so labels above 34 use the
+# first entries of that extension as recalled (unpinned) and then "colorK".
+STANDARD_COLORS = [
+    "turquoise", "blue", "brown", "yellow", "green", "red", "black", "pink", "magenta", "purple", "greenyellow",
+    "tan", "salmon", "cyan", "midnightblue", "lightcyan", "grey60", "lightgreen", "lightyellow", "royalblue",
+    "darkred", "darkgreen", "darkturquoise", "darkgrey", "orange", "darkorange", "white", "skyblue", "saddlebrown",
+    "steelblue", "paleturquoise", "violet", "darkolivegreen", "darkmagenta",
+    "sienna3", "yellowgreen", "skyblue3", "plum1", "orangered4", "mediumpurple3", "lightsteelblue1", "lightcyan1",
+    "ivory", "floralwhite", "darkorange2", "brown4", "bisque4", "darkslateblue", "plum2", "thistle2", "thistle1",
+    "salmon4", "palevioletred3", "navajowhite2", "maroon", "lightpink4", "lavenderblush3", "honeydew1",
+    "darkseagreen4", "coral1", "antiquewhite4", "coral2", "mediumorchid", "skyblue2", "yellow4", "skyblue1", "plum",
+    "orangered3", "mediumpurple2", "lightsteelblue", "lightcoral", "indianred4", "firebrick4", "darkolivegreen4",
+    "brown2", "blue2", "darkviolet", "plum3", "thistle3", "thistle",
+]
+
+
+def labels2colors(labels):
+    """WGCNA::labels2colors(labels) for numeric labels (Fast:428): 0 -> "grey",
+    k -> standardColors()[k]."""
+    lab = np.asarray(labels)
+    return [("grey" if v == 0 else STANDARD_COLORS[v - 1] if v <= len(STANDARD_COLORS) else f"color{v}")
+            for v in lab.tolist()]
+
+
 def _hclust_ward_d2(dist_packed, N):
-    from scipy.cluster.hierarchy import linkage
-    return linkage(dist_packed, method="ward", preserve_input=True) if N > 1 else None
+    """fastcluster::hclust(d, "ward.D2") (Fast:406-411) -> R hclust fields."""
+    merge, height, order = nat.hclust_ward_d2(dist_packed, N)
+    return {"merge": merge, "height": height, "order": order, "method": "ward.D2", "dist.method": "euclidean"}
+
+
+def _dynamic_colors(tree, dist_packed, deepSplitValues, minClusterSize):
+    """Fast:418-431: cutreeDynamic(dendro, distM = as.matrix(d), deepSplit = dsv,
+    pamStage = FALSE, minClusterSize) -> labels2colors, named "deepsplit: dsv"."""
+    out = {}
+    for dsv in deepSplitValues:
+        lab, _ = nat.cutree_hybrid(tree["merge"], tree["height"], dist_packed, int(dsv), int(minClusterSize))
+        out[f"deepsplit: {dsv}"] = labels2colors(lab)
+    return out
 
 
 def _save(obj, filename):
@@ -118,7 +155,8 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
         raise RuntimeError("no DE genes (R fails on an empty deGenes data frame, Fast:386)")
     d = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
     tree = _hclust_ward_d2(d, N)
-    ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree, "dynamicColors": None}
+    ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree,
+           "dynamicColors": _dynamic_colors(tree, d, deepSplitValues, minClusterSize)}
     if save:
         _save(ret, filename)
     if return_details:
@@ -167,7 +205,8 @@ def reclusterDEConsensus(dataMatrix, consensusClusterLabels, method="Wilcoxon", 
         raise RuntimeError("empty DE gene union")
     d = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
     tree = _hclust_ward_d2(d, N)
-    ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree, "dynamicColors": None}
+    ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree,
+           "dynamicColors": _dynamic_colors(tree, d, deepSplitValues, minClusterSize)}
     if save:
         _save({"qValueList": qlist, "logFCList": lflist, "deGeneList": delist}, "de_lists")
         _save(ret, filename)

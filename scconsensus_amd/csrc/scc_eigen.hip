@@ -524,6 +524,75 @@ __device__ inline void xcd_register(const TriArgs& a, int n, int* s_rank, int* s
     __syncthreads();
 }
 
+// Work items of a follow-up kernel pinned to the XCD the tridiagonalisation ran
+// on (its reflectors sit in that XCD's L2): grid = 8 x items; workgroups on
+// that XCD claim items from a counter until none are left, the others leave at
+// once.  The workgroup that arrives last claims items too, so every item is
+// done whatever the dispatch placement, and nothing waits on another
+// workgroup (no co-residency assumption).  vc: 2 zeroed counters; *role:
+// thread 0's state across calls (0 on entry).  Returns the next item or -1.
+__device__ inline int xcd_next(const u32* xcd_pick, u32* vc, int items, int* role)
+{
+    __shared__ int s_item;
+    __syncthreads();  // every thread has read the previous item
+    if (threadIdx.x == 0) {
+        if (*role == 0) {
+            u32 x;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+            x &= 0xfu;
+            const u32 want = __hip_atomic_load(xcd_pick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
+            const u32 arrived = atomicAdd(&vc[1], 1u);
+            *role = (x == want || arrived == gridDim.x - 1) ? 1 : 2;
+        }
+        int r = -1;
+        if (*role == 1) {
+            const u32 t = atomicAdd(&vc[0], 1u);
+            if (t < (u32)items) r = (int)t;
+        }
+        s_item = r;
+    }
+    __syncthreads();
+    return s_item;
+}
+
+// Variant of xcd_next for grids that are co-resident (8 x items workgroups
+// all fit on the chip at once): one item per workgroup; workgroups off the
+// XCD wait until every workgroup has arrived and then take what is left.
+__device__ inline int xcd_item_wait(const u32* xcd_pick, u32* vc, int items, u32* err)
+{
+    __shared__ int s_item;
+    if (threadIdx.x == 0) {
+        u32 x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        x &= 0xfu;
+        const u32 want = __hip_atomic_load(xcd_pick, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;
+        int r = -1;
+        if (x == want) {
+            const u32 t = atomicAdd(&vc[0], 1u);
+            if (t < (u32)items) r = (int)t;
+        }
+        atomicAdd(&vc[1], 1u);
+        if (r < 0) {
+            u32 spins = 0;
+            while (__hip_atomic_load(&vc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > EIG_SPIN_LIMIT) {
+                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            const u32 on = min(__hip_atomic_load(&vc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (u32)items);
+            if (on < (u32)items) {
+                const u32 t = on + atomicAdd(&vc[2], 1u);
+                if (t < (u32)items) r = (int)t;
+            }
+        }
+        s_item = r;
+    }
+    __syncthreads();
+    return s_item;
+}
+
 // Wave-agent tridiagonalisation for n <= 64 * TW_NJ.  Every wave of every
 // participating workgroup is an independent agent: it owns rows r with
 // r % NA == agent, keeps v_i, v_{i-1}, w_{i-1} in registers (lane-strided,
@@ -809,6 +878,10 @@ struct VecArgs {
     double* W;      // [k]
     double* tnorm;  // [1]
     const double* tf;  // [ceil((n-2)/BT_NB)][BT_NB][BT_NB] compact-WY T factors
+    const u32* xcd;    // the tridiagonalisation's XCD pick (x + 1), or nullptr: run anywhere
+    u32* vcount;       // [3] xcd_next / xcd_item_wait counters (zeroed per launch)
+    u32* err;
+    int wait;          // 1: xcd_item_wait (grid co-resident), 0: xcd_next
     u64* stamps;    // diagnostic: workgroup 0's phase boundaries at [3..7] (nullptr normally)
 };
 
@@ -817,22 +890,26 @@ __device__ inline int sturm_count(const double* d, const double* e2, int n, doub
 {
     int c = 0;
     double q = d[0] - x;
-    if (fabs(q) < pivmin) q = -pivmin;
+    q = fabs(q) < pivmin ? -pivmin : q;
     c += (q < 0.0);
     for (int i = 1; i < n; ++i) {
-        q = d[i] - x - e2[i - 1] / q;
-        if (fabs(q) < pivmin) q = -pivmin;
+        // e2 / q as the hardware reciprocal refined by one Newton step (a few
+        // ulp from the IEEE quotient; the count is insensitive to that)
+        const double r0 = __builtin_amdgcn_rcp(q);
+        const double r = fma(fma(-q, r0, 1.0), r0, r0);
+        q = fma(-e2[i - 1], r, d[i] - x);
+        q = fabs(q) < pivmin ? -pivmin : q;
         c += (q < 0.0);
     }
     return c;
 }
 
-__global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
+__device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ double red[16];
     __shared__ int ired[VEC_W];
-    const int n = a.n, q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    const int n = a.n, tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
     const bool stmp = a.stamps && q == 0 && tid == 0;
     const u64 t0 = stmp ? clock64() : 0;
     double* dl = sm;
@@ -937,12 +1014,13 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
                 const double f = (piv ? dc : li[u]) / den;
                 fl[i] = f;
                 fdr[i] = den;  // the pivot; its reciprocal is taken below, off the chain
-                fu[i] = piv ? dn[u] : ucur;
+                // operands selected first, one FMA each on the chain (no branch)
+                const double ua = piv ? dn[u] : ucur, ub = piv ? ucur : dn[u];
+                fu[i] = ua;
                 fu2[i] = piv ? un[u] : 0.0;  // zero at i = n - 2
                 fp[i] = piv ? 1.0 : 0.0;
-                const double dnext = piv ? ucur - f * dn[u] : dn[u] - f * ucur;
+                dcur = fma(-f, ua, ub);
                 ucur = piv ? -f * un[u] : un[u];
-                dcur = dnext;
             }
         }
         if (dcur == 0.0) dcur = tiny;
@@ -977,9 +1055,11 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
 #pragma unroll
                 for (int u = 0; u < SB; ++u) {
                     if (i0 + u >= n - 1) break;
+                    // operands selected first, one FMA on the chain (no branch)
                     const bool piv = pv[u] != 0.0;
-                    w[i0 + u] = piv ? bn[u] : bi;
-                    bi = piv ? (bi - f[u] * bn[u]) : (bn[u] - f[u] * bi);
+                    const double xa = piv ? bn[u] : bi, xb = piv ? bi : bn[u];
+                    w[i0 + u] = xa;
+                    bi = fma(-f[u], xa, xb);
                 }
             }
             w[n - 1] = bi;
@@ -998,7 +1078,7 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
                 for (int u = 0; u < SB; ++u) {
                     const int i = i1 - u;
                     if (i < 0) break;
-                    const double z0 = (wv8[u] - u1[u] * z2 - u2[u] * z1) * r[u];  // z2 = y[i+1], z1 = y[i+2]
+                    const double z0 = fma(-u1[u], z2, fma(-u2[u], z1, wv8[u])) * r[u];  // z2 = y[i+1], z1 = y[i+2]
                     y[i] = z0;
                     z1 = z2;
                     z2 = z0;
@@ -1080,15 +1160,30 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
     }
 }
 
+__global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
+{
+    if (!a.xcd) {
+        tri_vector_item(a, (int)blockIdx.x);
+        return;
+    }
+    if (a.wait) {
+        const int q = xcd_item_wait(a.xcd, a.vcount, a.k, a.err);
+        if (q >= 0) tri_vector_item(a, q);
+        return;
+    }
+    int role = 0;
+    for (int q; (q = xcd_next(a.xcd, a.vcount, a.k, &role)) >= 0;) tri_vector_item(a, q);
+}
+
 // T factors of the compact WY form of the reflectors, one workgroup per block
 // of BT_NB (LAPACK dlarft, forward / columnwise): T[i][i] = tau_i,
 // T[0:i, i] = -tau_i T[0:i, 0:i] (V[:, 0:i]^T v_i).
-__global__ void __launch_bounds__(1024) k_refl_T(const double* __restrict__ refl, const double* __restrict__ tau, int n,
-                                                 int lda, double* __restrict__ tf)
+__device__ __forceinline__ void refl_T_item(const double* __restrict__ refl, const double* __restrict__ tau, int n,
+                                            int lda, double* __restrict__ tf, const int b)
 {
     __shared__ double G[BT_NB][BT_NB + 1];
     __shared__ double T[BT_NB][BT_NB + 1];
-    const int b = blockIdx.x, kb = b * BT_NB, nb = min(BT_NB, n - 2 - kb), tid = threadIdx.x;
+    const int kb = b * BT_NB, nb = min(BT_NB, n - 2 - kb), tid = threadIdx.x;
     // G[i][j] = v_i . v_j for j < i (both nonzero from row kb + i + 1): wave wv
     // takes rows i = wv and wv + 16, every j < i in registers
     const int lane = tid & 63, wv = scc_wave_id();
@@ -1127,6 +1222,18 @@ __global__ void __launch_bounds__(1024) k_refl_T(const double* __restrict__ refl
         __syncthreads();
     }
     tf[(size_t)b * BT_NB * BT_NB + tid] = T[tid >> 5][tid & 31];
+}
+
+__global__ void __launch_bounds__(1024) k_refl_T(const double* __restrict__ refl, const double* __restrict__ tau, int n,
+                                                 int lda, double* __restrict__ tf, const u32* xcd, u32* vcount)
+{
+    if (!xcd) {
+        refl_T_item(refl, tau, n, lda, tf, (int)blockIdx.x);
+        return;
+    }
+    const int nblk = (n - 2 + BT_NB - 1) / BT_NB;
+    int role = 0;
+    for (int b; (b = xcd_next(xcd, vcount, nblk, &role)) >= 0;) refl_T_item(refl, tau, n, lda, tf, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -1219,7 +1326,7 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     L.e = take(n);
     L.tau = take(n);
     L.tnorm = take(1);
-    L.flags = take(4);  // counter, err, XCD registration [3] (u32 in doubles' space)
+    L.flags = take(8);  // counter, err, XCD registration [3], follow-up counters [6] (u32 in doubles' space)
     L.pg = take(4 * (size_t)lda);  // u64 granules occupy doubles' space
     L.rg = take(4 * (size_t)lda);
     L.dg = take(4 * EIG_MAX_WG * TRI_W);  // one partial per wave agent
@@ -1291,7 +1398,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     u32* flags = (u32*)(scratch + L.flags);
     if (err_dev) *err_dev = flags + 1;
     if (nwg_out) *nwg_out = nwg;
-    hipError_t e = hipMemsetAsync(flags, 0, 32, st);
+    hipError_t e = hipMemsetAsync(flags, 0, 64, st);  // counter, err, XCD pick [3], follow-up counters [6]
     if (e != hipSuccess) return e;
     // granule tags restart at 1 every launch
     e = hipMemsetAsync(scratch + L.pg, 0, sizeof(double) * (L.zq - L.pg), st);
@@ -1376,15 +1483,27 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     v.tnorm = scratch + L.tnorm;
     v.stamps = stamps;
     v.tf = scratch + L.tf;
+    // follow-up kernels on the tridiagonalisation's XCD (its reflectors are in that L2)
+    // SCC_EIG_PIN: 0 = anywhere, 1 = claim loop (xcd_next), 2 (default) = one
+    // item per workgroup with a co-resident wait when 8 x k workgroups fit
+    const char* pin_env = getenv("SCC_EIG_PIN");
+    const int pin_mode = pin_env ? atoi(pin_env) : 2;
+    // (measured at config B: eig_vec 0.37 ms anywhere, 0.42 claim loop, 0.32 wait)
+    const bool pin = t.xcd_local != 0 && pin_mode != 0;
+    v.wait = pin_mode == 2;
+    v.xcd = pin && (pin_mode == 1 || 8 * k <= 256) ? t.reg : nullptr;  // wait needs co-residency
+    v.vcount = flags + 5;
+    v.err = flags + 1;
     if (n > 2) {
-        hipLaunchKernelGGL(k_refl_T, dim3((n - 2 + BT_NB - 1) / BT_NB), dim3(1024), 0, st, t.refl, t.tau, n, lda,
-                           scratch + L.tf);
+        const int nblk = (n - 2 + BT_NB - 1) / BT_NB;
+        hipLaunchKernelGGL(k_refl_T, dim3(pin ? 8 * nblk : nblk), dim3(1024), 0, st, t.refl, t.tau, n, lda,
+                           scratch + L.tf, pin ? t.reg : nullptr, flags + 9);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
     hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
     if (marks) hipEventRecord(marks[2], st);
-    hipLaunchKernelGGL(k_tri_vectors, dim3(k), dim3(VEC_T), vlds, st, v);
+    hipLaunchKernelGGL(k_tri_vectors, dim3(v.xcd ? 8 * k : k), dim3(VEC_T), vlds, st, v);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (marks) hipEventRecord(marks[3], st);
     if (marks) hipEventRecord(marks[4], st);
