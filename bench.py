@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_FP64_TFS = 78.6     # MI355X FP64 matrix (spec)
+PEAK_FP32_TFS = 157.3    # MI355X FP32 matrix (v_mfma_f32_32x32x2_f32; MI355X_MICROARCH.md)
 
 
 def _args():
@@ -42,6 +43,7 @@ def _args():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="B")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pearson", action="store_true", help="skip the side measurement of the Pearson kernel")
     ap.add_argument("--cpu-sample-genes", type=int, default=300)
     ap.add_argument("--mode", choices=["jobs", "shard"], default="jobs",
                     help="jobs: one job per rank (weak scaling); shard: ONE job over all ranks (strong scaling: "
@@ -169,8 +171,26 @@ def main():
             return {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
                     "kernel": kname, "bytes_per_launch": work, "avg_launch_ms": stage_ms[f]}
         ach = work / t_s / 1e12
+        if bound == "mfma32":
+            return {"bound": "mfma", "dtype": "f32", "achieved": ach, "peak": PEAK_FP32_TFS, "unit": "TFLOP/s",
+                    "frac": ach / PEAK_FP32_TFS, "kernel": kname, "flops_per_launch": work,
+                    "avg_launch_ms": stage_ms[f], "output_bytes_per_launch": 8.0 * npairs_cells}
         return {"bound": "mfma", "achieved": ach, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP64_TFS, "kernel": kname, "flops_per_launch": work, "avg_launch_ms": stage_ms[f]}
+
+    # north_star's MFMA kernel: the Pearson 1 - cor distance (Fast:403) on the
+    # same union, measured beside the step (not part of the reference's path)
+    if not a.no_pearson:
+        eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)  # warm-up (first launch, buffers)
+        eng.synchronize()
+        eng.reset_timers()
+        for _ in range(5):
+            eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)
+        eng.synchronize()
+        for f in ("zscore", "pearson"):
+            t = eng.kernel_time(f)
+            stage_ms[f] = t[0] / max(t[1], 1)
+        alg["pearson"] = ("mfma32", float(d.N) * (d.N - 1) * nu, "k_pearson_mfma")
 
     roof_dom = roof(dom)
     roof_dom["traffic"] = traffic

@@ -13,9 +13,9 @@
 //   k_scores        P = Xc V_k (N x 16, zero padded components)
 //   k_dist_euclid   packed lower triangle in R `dist` order; per element the
 //                   sum of squared differences (FMA) + hardware sqrt
-//   k_zscore / k_pearson_f32   Pearson: per-cell centring/scaling, then an
-//                   LDS-tiled FP32 MFMA (v_mfma_f32_32x32x2_f32) Gram with the
-//                   1 - r epilogue fused into the packed-triangle store.
+//   k_zscore / k_pearson_mfma  Pearson: per-cell centring/scaling, then an
+//                   LDS-pipelined FP32 MFMA (v_mfma_f32_32x32x2_f32) Gram with the
+//                   1 - r epilogue fused into coalesced packed-column stores.
 #include "scc_common.hpp"
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -285,73 +285,221 @@ __global__ void __launch_bounds__(256) k_zscore(const double* __restrict__ Xc, i
     for (int u = lane; u < ldz; u += 64) Z[(size_t)c * ldz + u] = (u < nu) ? (float)((row[u] - mean) * inv) : 0.0f;
 }
 
-// 128 x 128 output tile per WG (4 waves, 64x64 each = 2x2 tiles of 32x32),
-// K staged through LDS in 16-wide steps.  v_mfma_f32_32x32x2_f32: lane l holds
-// A[i = l&31][k = l>>5], B[k = l>>5][j = l&31]; accumulator reg r is
-// C[row = (r&3) + 8*(r>>2) + 4*(l>>5)][col = l&31].
-template <bool F32>
-__global__ void __launch_bounds__(256) k_pearson_f32(const float* __restrict__ Z, int N, int ldz, int ntile,
-                                                     int c_lo, int c_hi, long long obase, void* __restrict__ out)
+// 1 - r on FP32 MFMA (v_mfma_f32_32x32x2_f32), one 128 x 128 tile of the
+// lower triangle per workgroup (4 waves, 64 x 64 each = 2 x 2 blocks of 32 x 32).
+//   * Operand roles: A = the tile's column cells j, B = its row cells i, so an
+//     accumulator register holds D[j][i] with i = lane & 31: the epilogue's 32
+//     lanes of a half-wave store 32 consecutive entries of one packed column
+//     (R `dist` order is column-major, i contiguous) — two 256-byte runs per
+//     store instruction instead of 32 scattered 8-byte writes.
+//   * K (the union genes, zero padded to PK) streams in chunks of PK = 32
+//     floats through two LDS buffers; chunk c + 1 is loaded from global into
+//     registers while chunk c feeds the MFMAs, then written to the other buffer
+//     (one barrier per chunk).  Rows past N are clamped to row N - 1 (their
+//     results are never stored), so the loads carry no conditions.
+//   * Fragments: lane half h reads the float4 at k = 8g + 4h of its row (LDS
+//     row stride 36 floats: the 16-lane groups of a ds_read_b128 hit disjoint
+//     banks), i.e. MFMA step s of group g pairs k = 8g + s (half 0) with
+//     8g + 4 + s (half 1) — the same pairing for A and B, so the sum over k is
+//     unchanged.
+//   * Tiles are dealt to XCDs in contiguous runs of the row-major lower-
+//     triangle enumeration (workgroup b runs on XCD b % 8), so an XCD's tiles
+//     share their row blocks in its L2.
+constexpr int PT = 128, PK = 32, PLD = PK + 4;
+
+// Tile t of the lower triangle (ti >= tj, nt tile rows) in banded order: tile
+// rows come in bands of PB; a band's rectangle left of its diagonal block is
+// walked column by column (the PB row panels stay in L2 while the column
+// panels stream), then its diagonal triangle row by row.  At ~32 resident
+// workgroups per XCD the live tiles touch ~4 column panels + PB row panels.
+constexpr int PB = 8;
+__device__ __forceinline__ int2 pearson_tile(long long t, int nt)
 {
-    // lower-triangular tile index (ti >= tj)
-    int t = blockIdx.x, ti = 0;
-    while (t > ti) {
-        t -= ti + 1;
-        ++ti;
-    }
-    const int tj = t;
-    (void)ntile;
-    if (tj * 128 + 128 <= c_lo || tj * 128 >= c_hi) return;  // no column of this rank's slice
-    __shared__ float sa[16][128 + 4];
-    __shared__ float sb[16][128 + 4];
-    const int lane = threadIdx.x & 63, w = scc_wave_id();
-    const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
-    const int I0 = ti * 128, J0 = tj * 128;
-    f16v acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
-    for (int k0 = 0; k0 < ldz; k0 += 16) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < 16 * 128; e += 256) {
-            const int rr = e >> 4, kk = e & 15;  // row within tile, k within step
-            const int gi = I0 + rr, gj = J0 + rr;
-            sa[kk][rr] = (gi < N) ? Z[(size_t)gi * ldz + k0 + kk] : 0.0f;
-            sb[kk][rr] = (gj < N) ? Z[(size_t)gj * ldz + k0 + kk] : 0.0f;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int kk = 0; kk < 16; kk += 2) {
-            const int kq = kk + (lane >> 5);
-            const float a0 = sa[kq][wi + (lane & 31)], a1 = sa[kq][wi + 32 + (lane & 31)];
-            const float b0 = sb[kq][wj + (lane & 31)], b1 = sb[kq][wj + 32 + (lane & 31)];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    // band = (row-major tile row of t) / PB: bands are contiguous row ranges
+    int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((long long)r * (r + 1) / 2 > t) --r;
+    while ((long long)(r + 1) * (r + 2) / 2 <= t) ++r;
+    const int b0 = (r / PB) * PB, R = min(PB, nt - b0);
+    long long l = t - (long long)b0 * (b0 + 1) / 2;
+    const long long rect = (long long)R * b0;
+    // the diagonal triangle: row q with q(q+1)/2 <= l - rect
+    const long long l2 = l - rect;
+    int q = 0;
+    while ((long long)(q + 1) * (q + 2) / 2 <= l2) ++q;
+    const int ti = l < rect ? b0 + (int)(l % R) : b0 + q;
+    const int tj = l < rect ? (int)(l / R) : b0 + (int)(l2 - (long long)q * (q + 1) / 2);
+    return make_int2(ti, tj);
+}
+
+// the first tile at or after t (stepping by stride, below tend) that has a
+// column in [c_lo, c_hi); returns tend if none
+__device__ __forceinline__ long long pearson_next(long long t, long long tend, long long stride, int nt, int c_lo, int c_hi,
+                                         int2& tile)
+{
+    for (; t < tend; t += stride) {
+        const int2 tt = pearson_tile(t, nt);
+        if (tt.y * PT + PT > c_lo && tt.y * PT < c_hi) {
+            tile = tt;
+            return t;
         }
     }
-    // epilogue: 1 - r for i > j, packed R order
+    return tend;
+}
+
+// Persistent: gridDim.x = 8 x (workgroups per XCD); the workgroups of XCD x
+// stride through its contiguous run [x per, (x + 1) per) of the banded tile
+// order.  The last K chunk of a tile prefetches chunk 0 of the workgroup's
+// next tile, so the epilogue's stores and the next tile's first loads overlap
+// instead of paying a workgroup launch and a cold first chunk per tile.
+template <bool F32>
+__global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict__ Z, int N, int ldz, int nt, long long ntri,
+                                                         long long per_xcd, int c_lo, int c_hi, long long obase,
+                                                         void* __restrict__ out, int diag_nostore)
+{
+    const long long tbeg = (long long)(blockIdx.x & 7) * per_xcd;
+    const long long tend = min(tbeg + per_xcd, ntri);
+    const long long tstride = gridDim.x >> 3;
+    int2 tt;
+    long long t = pearson_next(tbeg + (blockIdx.x >> 3), tend, tstride, nt, c_lo, c_hi, tt);
+    int ti = tt.x, tj = tt.y;
+    if (t >= tend) return;
+
+    __shared__ __attribute__((aligned(16))) float sA[2][PT * PLD];
+    __shared__ __attribute__((aligned(16))) float sB[2][PT * PLD];
+    const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    const int h = lane >> 5, r32 = lane & 31;
+    const int wj = (w >> 1) * 64, wi = (w & 1) * 64;
+
+    // staging: thread tid moves float4 (tid & 7) of rows (tid >> 3) + 32 q;
+    // offsets (floats) of the 4 staged rows of each panel, clamped to N - 1
+    const int srow = tid >> 3, sc4 = (tid & 7) * 4;
+    size_t oA0, oA1, oA2, oA3, oB0, oB1, oB2, oB3;
+#define PEARSON_OFFSETS(I0_, J0_)                                                                             \
+    do {                                                                                                      \
+        oA0 = (size_t)min((J0_) + srow, N - 1) * ldz + sc4;                                                   \
+        oA1 = (size_t)min((J0_) + srow + 32, N - 1) * ldz + sc4;                                              \
+        oA2 = (size_t)min((J0_) + srow + 64, N - 1) * ldz + sc4;                                              \
+        oA3 = (size_t)min((J0_) + srow + 96, N - 1) * ldz + sc4;                                              \
+        oB0 = (size_t)min((I0_) + srow, N - 1) * ldz + sc4;                                                   \
+        oB1 = (size_t)min((I0_) + srow + 32, N - 1) * ldz + sc4;                                              \
+        oB2 = (size_t)min((I0_) + srow + 64, N - 1) * ldz + sc4;                                              \
+        oB3 = (size_t)min((I0_) + srow + 96, N - 1) * ldz + sc4;                                              \
+    } while (0)
+    float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+#define PEARSON_GLOAD(k0)                              \
+    do {                                               \
+        ra0 = *(const float4*)(Z + oA0 + (k0));        \
+        ra1 = *(const float4*)(Z + oA1 + (k0));        \
+        ra2 = *(const float4*)(Z + oA2 + (k0));        \
+        ra3 = *(const float4*)(Z + oA3 + (k0));        \
+        rb0 = *(const float4*)(Z + oB0 + (k0));        \
+        rb1 = *(const float4*)(Z + oB1 + (k0));        \
+        rb2 = *(const float4*)(Z + oB2 + (k0));        \
+        rb3 = *(const float4*)(Z + oB3 + (k0));        \
+    } while (0)
+#define PEARSON_LSTORE(buf)                                          \
+    do {                                                             \
+        *(float4*)&sA[buf][(srow) * PLD + sc4] = ra0;                \
+        *(float4*)&sA[buf][(srow + 32) * PLD + sc4] = ra1;           \
+        *(float4*)&sA[buf][(srow + 64) * PLD + sc4] = ra2;           \
+        *(float4*)&sA[buf][(srow + 96) * PLD + sc4] = ra3;           \
+        *(float4*)&sB[buf][(srow) * PLD + sc4] = rb0;                \
+        *(float4*)&sB[buf][(srow + 32) * PLD + sc4] = rb1;           \
+        *(float4*)&sB[buf][(srow + 64) * PLD + sc4] = rb2;           \
+        *(float4*)&sB[buf][(srow + 96) * PLD + sc4] = rb3;           \
+    } while (0)
+
+    const int nchunk = (ldz + PK - 1) / PK;
+    PEARSON_OFFSETS(ti * PT, tj * PT);
+    PEARSON_GLOAD(0);
+    PEARSON_LSTORE(0);
+    __syncthreads();
+    int buf = 0;
+    const long long twoN = 2LL * N;
+    for (;;) {
+        const int I0 = ti * PT, J0 = tj * PT;
+        int2 nn = make_int2(0, 0);
+        const long long tn = pearson_next(t + tstride, tend, tstride, nt, c_lo, c_hi, nn);
+        const int tin = nn.x, tjn = nn.y;
+        f16v acc[2][2];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = I0 + wi + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                const int j = J0 + wj + b * 32 + (lane & 31);
-                if (i < N && j < i && j >= c_lo && j < c_hi) {
-                    const size_t o = (size_t)j * (2 * (size_t)N - j - 1) / 2 + (size_t)(i - j - 1) - obase;
-                    const float d = 1.0f - acc[a][b][r];
-                    if (F32)
-                        ((float*)out)[o] = d;
-                    else
-                        ((double*)out)[o] = (double)d;
-                }
+                for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+        for (int c = 0; c < nchunk; ++c) {
+            bool more = true;
+            if (c + 1 < nchunk) {
+                PEARSON_GLOAD((c + 1) * PK);
+            } else if (tn < tend) {
+                PEARSON_OFFSETS(tin * PT, tjn * PT);  // the next tile's chunk 0
+                PEARSON_GLOAD(0);
+            } else {
+                more = false;
             }
+            const float* A = sA[buf];
+            const float* B = sB[buf];
+            const int ng = min(PK, ldz - c * PK) / 8;  // 8-float groups of this chunk (the last may be short)
+#pragma unroll
+            for (int g = 0; g < PK / 8; ++g) {
+                if (g >= ng) break;
+                const int ko = 8 * g + 4 * h;
+                const float4 a0 = *(const float4*)&A[(wj + r32) * PLD + ko];
+                const float4 a1 = *(const float4*)&A[(wj + 32 + r32) * PLD + ko];
+                const float4 b0 = *(const float4*)&B[(wi + r32) * PLD + ko];
+                const float4 b1 = *(const float4*)&B[(wi + 32 + r32) * PLD + ko];
+#define PEARSON_STEP(SEL)                                                                       \
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.SEL, b0.SEL, acc[0][0], 0, 0, 0);          \
+    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.SEL, b1.SEL, acc[0][1], 0, 0, 0);          \
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.SEL, b0.SEL, acc[1][0], 0, 0, 0);          \
+    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.SEL, b1.SEL, acc[1][1], 0, 0, 0)
+                PEARSON_STEP(x);
+                PEARSON_STEP(y);
+                PEARSON_STEP(z);
+                PEARSON_STEP(w);
+#undef PEARSON_STEP
+            }
+            if (more) PEARSON_LSTORE(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+
+        if (diag_nostore) {  // diagnostic (SCC_PEARSON_NOSTORE=1): keep the result live, store nothing
+            float x = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) x += acc[0][0][r] + acc[0][1][r] + acc[1][0][r] + acc[1][1][r];
+            if (x == 12345.678f) ((float*)out)[0] = x;
+        } else {
+            // epilogue: D[j][i] -> 1 - r at packed (i, j), i > j, columns of this slice
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int j = J0 + wj + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (j < c_lo || j >= c_hi) continue;
+                    const long long col = (long long)j * (twoN - j - 1) / 2 - j - 1 - obase;
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) {
+                        const int i = I0 + wi + 32 * b + r32;
+                        if (i < N && j < i) {
+                            const float d = 1.0f - acc[a][b][r];
+                            if (F32)
+                                __builtin_nontemporal_store(d, (float*)out + (col + i));
+                            else
+                                __builtin_nontemporal_store((double)d, (double*)out + (col + i));
+                        }
+                    }
+                }
+        }
+        if (tn >= tend) break;
+        t = tn;
+        ti = tin;
+        tj = tjn;
+    }
+#undef PEARSON_OFFSETS
+#undef PEARSON_GLOAD
+#undef PEARSON_LSTORE
 }
 
 // ------------------------------------------------------------------ launchers
@@ -430,16 +578,32 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     return hipGetLastError();
 }
 
+extern "C" hipError_t scc_launch_zscore(const double* Xc, int N, int nu, int ld, float* Z, int ldz, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_zscore, dim3((N + 3) / 4), dim3(256), 0, st, Xc, N, nu, ld, ldz, Z);
+    return hipGetLastError();
+}
+
+// Z holds the z-scores (scc_launch_zscore); Xc / ld are not read
 extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, int c_lo,
                                          int c_hi, void* out, int f32, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_zscore, dim3((N + 3) / 4), dim3(256), 0, st, Xc, N, nu, ld, ldz, Z);
-    const int nt = (N + 127) / 128;
-    const int ntri = nt * (nt + 1) / 2;
+    if (ldz % 8 != 0 || ldz < nu || N < 2) return hipErrorInvalidValue;  // Z: N * ldz + 32 floats
+    (void)Xc;
+    (void)ld;
+    const int nt = (N + PT - 1) / PT;
+    const long long ntri = (long long)nt * (nt + 1) / 2;
+    const long long per = (ntri + 7) / 8;
+    // persistent grid: 2 workgroups per CU (LDS: 72 KB each), at most one per tile
+    const long long nwg_xcd = per < 64 ? per : 64;
     const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
+    const char* ns = getenv("SCC_PEARSON_NOSTORE");
+    const int nostore = ns && ns[0] == '1';
     if (f32)
-        hipLaunchKernelGGL(k_pearson_f32<true>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, c_lo, c_hi, obase, out);
+        hipLaunchKernelGGL(k_pearson_mfma<true>, dim3((unsigned)(8 * nwg_xcd)), dim3(256), 0, st, Z, N, ldz, nt, ntri, per,
+                           c_lo, c_hi, obase, out, nostore);
     else
-        hipLaunchKernelGGL(k_pearson_f32<false>, dim3(ntri), dim3(256), 0, st, Z, N, ldz, nt, c_lo, c_hi, obase, out);
+        hipLaunchKernelGGL(k_pearson_mfma<false>, dim3((unsigned)(8 * nwg_xcd)), dim3(256), 0, st, Z, N, ldz, nt, ntri, per,
+                           c_lo, c_hi, obase, out, nostore);
     return hipGetLastError();
 }

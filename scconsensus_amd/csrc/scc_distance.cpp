@@ -26,6 +26,7 @@ size_t scc_sil_scratch_doubles(int N, int C);
 hipError_t scc_launch_silhouette(const void* D, int f32, int N, const int* lab, const int* cnt, int C, double* part,
                                  double* width, hipStream_t st);
 hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st);
+hipError_t scc_launch_zscore(const double* Xc, int N, int nu, int ld, float* Z, int ldz, hipStream_t st);
 hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, int c_lo, int c_hi,
                               void* out, int f32, hipStream_t st);
 }
@@ -153,8 +154,14 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         c->last_ncomp = k;
     } else {
         float* d_Zp;
-        const int ldz = (nu + 15) & ~15;
-        WS("d_Zp", (size_t)N * ldz, d_Zp);
+        // rows padded to 8 floats (k_pearson_mfma's fragment group); its 32-float
+        // staging reads run up to 24 floats past a row, so the last row has slack
+        const int ldz = (nu + 7) & ~7;
+        WS("d_Zp", (size_t)N * ldz + 32, d_Zp);
+        {
+            Scope sz(c, "zscore", s0);
+            HIPCHK(c, scc_launch_zscore(d_X, N, nu, ld, d_Zp, ldz, s0));
+        }
         Scope sc(c, "pearson", s0);
         HIPCHK(c, scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, (int)col_lo, (int)col_hi, d_out, out_f32, s0));
     }
