@@ -51,6 +51,9 @@ def _args():
     return ap.parse_args()
 
 
+DEVICE_GEN = ("C", "D", "E")
+
+
 def cpu_baseline(d, code, K, union, sample_genes, seed=0):
     """The oracle (C restatement of the R algorithm, 1 thread) on a bounded
     sample of the same workload, scaled linearly: DE on a seeded gene sample
@@ -59,6 +62,8 @@ def cpu_baseline(d, code, K, union, sample_genes, seed=0):
     import oracle as O
     from scipy.spatial.distance import cdist
     rng = np.random.default_rng(seed)
+    if not hasattr(d, "scipy_csc"):
+        d = d.to_host()
     genes = np.sort(rng.choice(d.G, min(sample_genes, d.G), replace=False))
     csr = d.scipy_csc().tocsr()
     Xs = np.asarray(csr[genes].todense())
@@ -96,13 +101,22 @@ def main():
 
     cfg = CONFIGS[a.config]
     shard = a.mode == "shard"
-    d = synth.generate(a.config, seed=cfg["seed"] if shard else parallel.job_seed(cfg["seed"], rank))
+    seed = cfg["seed"] if shard else parallel.job_seed(cfg["seed"], rank)
+    gpu = 0 if os.environ.get("SCC_SHARE_GPU") else local
+    if a.config in DEVICE_GEN:  # C/D/E: generated in HBM (host generation takes minutes)
+        import torch
+        d = synth.generate_device(a.config, f"cuda:{gpu}", seed=seed)
+        torch.cuda.synchronize()
+    else:
+        d = synth.generate(a.config, seed=seed)
     names, code = api.select_clusters(d.labels, 10)
     K = len(names)
     P = K * (K - 1) // 2
-    gpu = 0 if os.environ.get("SCC_SHARE_GPU") else local
     eng = nat.Engine(gpu, profile=True)
-    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)  # H2D before timing
+    if a.config in DEVICE_GEN:
+        ds = eng.dataset_csc_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
+    else:
+        ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)  # H2D before timing
     npairs_cells = d.N * (d.N - 1) / 2
 
     if shard:
@@ -224,7 +238,8 @@ def main():
         "kernels": kernels,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(d, code, K, r.union, a.cpu_sample_genes)
+        ng = a.cpu_sample_genes if a.config in ("A", "B") else max(16, int(300 * 66 * 26000 / (P * d.N)))
+        out["cpu_baseline"] = cpu_baseline(d, code, K, r.union, ng)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.close()

@@ -51,7 +51,7 @@ struct ScRankLaunch {
     int cap_s, cap_m, cap_lds, bucket_target, ntp_max, item_cap;
     int med_wide;          // medium items: 1024 threads, one workgroup per CU
     int wave_target;       // split: bins are packed into buckets of < 2 * wave_target elements
-    int rw_slots;          // wave kernel: tested pairs per gene held in registers, 64 * rw_slots (2 or 4)
+    int rw_slots;          // wave kernel: tested pairs per gene held in registers, 64 * rw_slots (2, 4, 8 or 16)
     int dbg;               // SCC_RW_DEBUG timing experiments (1: no pair counts, 2: no sort); results invalid
     int bucket_cap;        // capacity of sbuckets / hbg rows
     ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)
@@ -59,7 +59,13 @@ struct ScRankLaunch {
     int* gene_bk;          // [2 G] first bucket id and bucket count of each split gene
     unsigned long long* gkmin;  // [G] key minimum of a split gene when its range fits 58 bits, else ~0
     ScRankItem* items;     // [3][item_cap]
-    int* counts;           // [0..2] items per class, [3] split genes, [4] wave buckets, [5] bucket ids
+    int* counts;           // [0..2] items per class, [3] split genes, [4] wave buckets, [5] bucket ids,
+                           // [8] fat buckets, [9] re-split queue, [10] re-split segments
+    uint32_t* gene_tp;     // [G][P] tested pairs of each split gene, p | a << 16 | b << 24 (pair order)
+    int* gene_nt;          // [G] their number
+    ScRankItem* fatbk;     // [fat_cap] buckets of > 64 distinct values (re-split into sub-buckets)
+    int4* rsseg;           // [fat_cap] {gene, first sub-bucket id, sub-buckets}: in-parent cross terms
+    int fat_cap;
     int* split_genes;      // [G]
     unsigned long long* keys2;  // [nnz] bucket-ordered keys of split genes
     uint8_t* codes2;            // [nnz]
@@ -157,6 +163,8 @@ hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st
 hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st);
 hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid_genes, hipStream_t st);
+hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st);
+hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st);
 size_t scc_eigen_scratch_doubles(int n, int lda, int k);
 hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,

@@ -516,29 +516,48 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
         }
     }
     __syncthreads();
-    if (tid == 0) {
-        // pack (pair, a, b, smaller side) and chunk the smaller side by 64
-        u32 c = 0;
-        for (int j = 0; j < L.ntp; ++j) {
-            int a2, b2;
-            pair_decode((int)tp[j], K, a2, b2);
-            const u32 ma = L.m[a2], mb = L.m[b2];
-            const bool sb = mb < ma;
-            tp[j] = tp[j] | ((u32)a2 << 16) | ((u32)b2 << 22) | ((u32)sb << 28);
-            pmap[a2 * K + b2] = (unsigned short)(j + 1);
-            eacc[j] = 0;
-            xacc[j] = 0;
-            cp[j] = c;
-            c += ((sb ? mb : ma) + 63) / 64;
+    {
+        // pack (pair, a, b, smaller side), one tested pair per thread, and chunk
+        // the smaller side by 64 (chunk offsets: a workgroup exclusive scan)
+        const int ntp0 = L.ntp;
+        u32 basec = 0;
+        for (int j0 = 0; j0 < ntp0; j0 += T) {
+            const int j = j0 + tid;
+            u32 nchk = 0;
+            if (j < ntp0) {
+                int a2, b2;
+                pair_decode((int)tp[j], K, a2, b2);
+                const u32 ma = L.m[a2], mb = L.m[b2];
+                const bool sb = mb < ma;
+                tp[j] = tp[j] | ((u32)a2 << 16) | ((u32)b2 << 22) | ((u32)sb << 28);
+                pmap[a2 * K + b2] = (unsigned short)(j + 1);
+                eacc[j] = 0;
+                xacc[j] = 0;
+                nchk = ((sb ? mb : ma) + 63) / 64;
+            }
+            u32 inc = nchk;
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += y;
+            }
+            if (lane == 63) L.redu[w] = inc;
+            __syncthreads();
+            u32 pre = basec;
+            for (int v = 0; v < w; ++v) pre += L.redu[v];
+            if (j < ntp0) cp[j] = pre + inc - nchk;
+            for (int v = 0; v < W; ++v) basec += L.redu[v];
+            __syncthreads();
         }
-        cp[L.ntp] = c;
-        L.nchunk = (int)c;
+        if (tid == 0) {
+        cp[ntp0] = basec;
+        L.nchunk = (int)basec;
         u32 s2 = 0;
         for (int a3 = 0; a3 < K; ++a3) {
             L.po[a3] = s2;
             s2 += L.m[a3];
         }
         L.po[K] = s2;
+        }
     }
     __syncthreads();
     const int ntp = L.ntp;
@@ -803,7 +822,13 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
     }
 }
 
-#define RW_SLOTS_MAX 4  // tested pairs per gene the wave kernel holds: 64 * slots (2 or 4)
+#define RW_SLOTS_MAX 16  // tested pairs per gene the wave kernel holds: 64 * slots (2, 4, 8 or 16)
+#define RS_T 256          // re-split: threads per workgroup
+#define RS_KPT 16         // keys per thread (held in registers: the scatter is in place)
+#define RS_CAP (RS_T * RS_KPT)
+#define RS_BINS 1024
+#define RS_BMAX (2 * RS_BINS + 1)
+#define RS_HCAP 4096      // sub-bucket x cluster histogram entries held in LDS
 
 // ===================================================================== split
 #define SP_T 1024
@@ -843,16 +868,26 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     const u64* key = A.keys + base;
     if (tid <= K) L.off[tid] = (int)A.coff[(size_t)A.cl_cc[tid] * G + g];
     for (int i = tid; i < SP_BINS; i += SP_T) L.hist[i] = 0;
-    // tested pairs of the gene (the wave kernel holds at most 64 * A.rw_slots)
-    {
-        u32 t = 0;
-        for (int p = tid; p < A.P; p += SP_T) t += (A.all_pairs || (A.flags[(size_t)p * G + g] & 1)) ? 1u : 0u;
-        t = u32_wave_sum(t);
-        if (lane == 0) L.wsum2[w] = t;
-    }
-    __syncthreads();
+    // tested pairs of the gene (the wave kernel holds at most 64 * A.rw_slots),
+    // compacted in pair order into gene_tp[g] as p | a << 16 | b << 24
     u32 ntested = 0;
-    for (int v = 0; v < SP_W; ++v) ntested += L.wsum2[v];
+    for (int p0 = 0; p0 < A.P; p0 += SP_T) {
+        const int p = p0 + tid;
+        const bool t = p < A.P && (A.all_pairs || (A.flags[(size_t)p * G + g] & 1));
+        const u64 bal = __ballot(t);
+        if (lane == 0) L.wsum2[w] = (u32)__popcll(bal);
+        __syncthreads();
+        u32 o = ntested;
+        for (int v = 0; v < w; ++v) o += L.wsum2[v];
+        if (t) {
+            int a2, b2;
+            pair_decode(p, K, a2, b2);
+            A.gene_tp[(size_t)g * A.P + o + lanes_below(bal)] = (u32)p | ((u32)a2 << 16) | ((u32)b2 << 24);
+        }
+        for (int v = 0; v < SP_W; ++v) ntested += L.wsum2[v];
+        __syncthreads();
+    }
+    if (tid == 0) A.gene_nt[g] = (int)ntested;
     const bool waves_ok = ntested <= 64u * (u32)A.rw_slots;
     // the gene's keys stay in registers when they fit (SP_KPT per thread);
     // larger genes re-read each chunk in every pass (from L2)
@@ -1002,6 +1037,15 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         const ScRankItem itm{base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
         if ((c <= 64 || ties_only) && waves_ok) {
             A.sbuckets[atomicAdd(&A.counts[4], 1)] = itm;
+        } else if (waves_ok && c <= RS_CAP && A.fatbk) {
+            // > 64 distinct values in one bin: re-split on a finer window (k_rank_resplit)
+            const int f = atomicAdd(&A.counts[8], 1);
+            if (f < A.fat_cap) {
+                A.fatbk[f] = itm;
+            } else {
+                const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
+                A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+            }
         } else {
             const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
             A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
@@ -1021,6 +1065,254 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
         const int i = L.next;
         if (i >= cnt) break;
         split_one_gene(A, A.split_genes[i], L);
+    }
+}
+
+// ===================================================================== re-split
+// A bucket the split left with > 64 distinct values (a dense stretch of the
+// value axis: at 100k+ cells a 2048-bin window over the gene's whole range
+// puts hundreds of values in one bin) is split again on its own key window:
+// 1024 bins, the same packing rule, elements scattered in place (all of them
+// are in registers first).  The sub-buckets go to the wave kernel; the
+// parent keeps its cluster histogram row (the gene-level cross term of
+// k_rank_cross) and records its sub-bucket range, whose in-parent cross term
+// k_rank_cross_seg adds from the sub-buckets' rows.
+struct ResplitLds {
+    u32 hist[RS_BINS];
+    u32 excl[RS_BINS];
+    u32 bid[RS_BINS];
+    u64 rep[RS_BINS];
+    u32 bcur[RS_BMAX];
+    u32 boff[RS_BMAX + 1];
+    u8 bdiff[RS_BMAX + 3];
+    u32 m[64];
+    u32 wsum[RS_T / 64 + 1];
+    u32 wsum2[RS_T / 64 + 1];
+    u64 rmn[RS_T / 64], rmx[RS_T / 64];
+    u32 hs[RS_HCAP];  // [sub-bucket][cluster] counts (in-parent cross term), when nb * K fits
+    int nb, bk0, next, ovf, nw, w0;
+};
+
+__device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitLds& L)
+{
+    constexpr int W = RS_T / 64, BPT = RS_BINS / RS_T;
+    const int K = A.K, g = it.gene, n = it.n;
+    const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    u64 kr[RS_KPT];
+    u8 cd[RS_KPT];
+#pragma unroll
+    for (int q = 0; q < RS_KPT; ++q) {
+        const int i = q * RS_T + tid;
+        kr[q] = i < n ? A.keys2[it.base + i] : 0ull;
+        cd[q] = i < n ? A.codes2[it.base + i] : (u8)0;
+    }
+    for (int d = tid; d < RS_BINS; d += RS_T) L.hist[d] = 0;
+    if (tid < 64) L.m[tid] = 0;
+    u64 kmn = ~0ull, kmx = 0;
+#pragma unroll
+    for (int q = 0; q < RS_KPT; ++q) {
+        if (q * RS_T + tid < n) {
+            kmn = kr[q] < kmn ? kr[q] : kmn;
+            kmx = kr[q] > kmx ? kr[q] : kmx;
+        }
+    }
+    for (int m2 = 32; m2 >= 1; m2 >>= 1) {
+        const u64 o1 = shfl_xor_u64(kmn, m2), o2 = shfl_xor_u64(kmx, m2);
+        kmn = o1 < kmn ? o1 : kmn;
+        kmx = o2 > kmx ? o2 : kmx;
+    }
+    if (lane == 0) {
+        L.rmn[w] = kmn;
+        L.rmx[w] = kmx;
+    }
+    __syncthreads();
+    kmn = L.rmn[0];
+    kmx = L.rmx[0];
+    for (int v = 1; v < W; ++v) {
+        kmn = L.rmn[v] < kmn ? L.rmn[v] : kmn;
+        kmx = L.rmx[v] > kmx ? L.rmx[v] : kmx;
+    }
+    const u64 range = kmx - kmn;
+    const int bits = range ? 64 - __clzll((long long)range) : 0;
+    const int sh = bits > 10 ? bits - 10 : 0;
+#pragma unroll
+    for (int q = 0; q < RS_KPT; ++q) {
+        if (q * RS_T + tid < n) {
+            const u32 d = (u32)((kr[q] - kmn) >> sh);
+            atomicAdd(&L.hist[d], 1u);
+            L.rep[d] = kr[q];
+            atomicAdd(&L.m[cd[q]], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the bins (BPT consecutive bins per thread)
+    {
+        u32 h[BPT], v = 0;
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            h[q] = L.hist[BPT * tid + q];
+            v += h[q];
+        }
+        u32 incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.wsum[w] = incl;
+        __syncthreads();
+        u32 b = incl - v;
+        for (int q = 0; q < w; ++q) b += L.wsum[q];
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            L.excl[BPT * tid + q] = b;
+            b += h[q];
+        }
+    }
+    __syncthreads();
+    // buckets: runs of bins with equal floor(excl / target); a bin of more
+    // than `target` elements is a bucket of its own (the split's rule)
+    const u32 target = (u32)A.wave_target;
+    {
+        u32 st[BPT], v = 0;
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            const int d = BPT * tid + q;
+            const bool fat = L.hist[d] > target;
+            const bool pfat = d > 0 && L.hist[d - 1] > target;
+            st[q] = (d == 0) || fat || pfat || (L.excl[d] / target != L.excl[d - 1] / target);
+            v += st[q];
+        }
+        u32 incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.wsum2[w] = incl;
+        __syncthreads();
+        u32 b = incl - v;
+        for (int q = 0; q < w; ++q) b += L.wsum2[q];
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            const int d = BPT * tid + q;
+            if (st[q]) L.boff[b] = L.excl[d];
+            b += st[q];
+            L.bid[d] = b - 1;
+        }
+        if (tid == RS_T - 1) {
+            L.nb = (int)b;
+            L.boff[b] = (u32)n;
+            const int bk0 = atomicAdd(&A.counts[5], (int)b);
+            L.ovf = bk0 + (int)b > A.bucket_cap;
+            L.bk0 = bk0;
+        }
+    }
+    __syncthreads();
+    const int nb = L.nb, bk0 = L.bk0;
+    if (L.ovf) {  // out of bucket ids: rank the parent as one LDS item
+        if (tid == 0) {
+            const int cls = (n <= A.cap_s) ? 0 : ((n <= A.cap_m) ? 1 : 2);
+            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = it;
+        }
+        return;
+    }
+    const bool hist_lds = nb * K <= RS_HCAP;
+    for (int q = tid; q < nb; q += RS_T) {
+        L.bcur[q] = L.boff[q];
+        L.bdiff[q] = 0;
+    }
+    if (hist_lds)
+        for (int e = tid; e < nb * K; e += RS_T) L.hs[e] = 0;
+    __syncthreads();
+    // in-place scatter into sub-bucket order (every element is in registers)
+#pragma unroll
+    for (int q = 0; q < RS_KPT; ++q) {
+        if (q * RS_T + tid < n) {
+            const u32 d = (u32)((kr[q] - kmn) >> sh);
+            const u32 bk = L.bid[d];
+            const u32 pos = atomicAdd(&L.bcur[bk], 1u);
+            A.keys2[it.base + pos] = kr[q];
+            A.codes2[it.base + pos] = cd[q];
+            if (kr[q] != L.rep[d]) L.bdiff[bk] = 1;
+            if (hist_lds) atomicAdd(&L.hs[bk * K + cd[q]], 1u);
+        }
+    }
+    __syncthreads();
+    if (tid < K) A.hbg[(size_t)it.bucket * K + tid] = L.m[tid];  // the parent's row (gene-level cross)
+    // sub-buckets for the wave kernel: one list reservation per parent
+    {
+        u32 wv[(RS_BMAX + RS_T - 1) / RS_T];
+        u32 cntw = 0;
+        for (int q0 = 0, r = 0; q0 < nb; q0 += RS_T, ++r) {
+            const int q = q0 + tid;
+            const int c = q < nb ? (int)(L.boff[q + 1] - L.boff[q]) : 0;
+            const bool tw = c > 0 && (c <= 64 || !L.bdiff[q]);
+            wv[r] = tw;
+            cntw += tw;
+        }
+        cntw = u32_wave_sum(cntw);
+        if (lane == 0) L.wsum[w] = cntw;
+        __syncthreads();
+        if (tid == 0) {
+            u32 t = 0;
+            for (int v = 0; v < W; ++v) t += L.wsum[v];
+            L.nw = (int)t;
+            L.w0 = t ? atomicAdd(&A.counts[4], (int)t) : 0;
+        }
+        __syncthreads();
+        u32 o = (u32)L.w0;
+        for (int q0 = 0, r = 0; q0 < nb; q0 += RS_T, ++r) {  // ordered slots: wave prefix per round
+            const int q = q0 + tid;
+            const u64 bal = __ballot(wv[r] != 0);
+            if (lane == 0) L.wsum2[w] = (u32)__popcll(bal);
+            __syncthreads();
+            u32 ow = o;
+            for (int v = 0; v < w; ++v) ow += L.wsum2[v];
+            if (q < nb) {
+                const int c = (int)(L.boff[q + 1] - L.boff[q]);
+                const int bid = bk0 + q;
+                if (c <= 0) {
+                    for (int k2 = 0; k2 < K; ++k2) A.hbg[(size_t)bid * K + k2] = 0;
+                } else {
+                    const bool ties_only = c > 64 && !L.bdiff[q];
+                    const ScRankItem itm{it.base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
+                    if (wv[r]) {
+                        A.sbuckets[ow + lanes_below(bal)] = itm;
+                    } else {
+                        const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
+                        A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+                    }
+                }
+            }
+            for (int v = 0; v < W; ++v) o += L.wsum2[v];
+            __syncthreads();
+        }
+    }
+    if (!hist_lds) {  // many sub-buckets: k_rank_cross_seg adds the in-parent cross term
+        if (tid == 0) A.rsseg[atomicAdd(&A.counts[10], 1)] = int4{g, bk0, nb, 0};
+        return;
+    }
+    // in-parent cross term: S_ab += sum_s hs[s][a] * #(b in sub-buckets < s)
+    const int ntp = min(A.gene_nt[g], A.P);
+    for (int j = tid; j < ntp; j += RS_T) {
+        const u32 v = A.gene_tp[(size_t)g * A.P + j];
+        const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+        u64 sacc = 0;
+        u32 below = 0;
+        for (int q = 0; q < nb; ++q) {
+            sacc += (u64)L.hs[q * K + a] * below;
+            below += L.hs[q * K + b];
+        }
+        if (sacc) atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
+    }
+}
+
+__global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
+{
+    __shared__ ResplitLds L;
+    const int cnt = min(A.counts[8], A.fat_cap);
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {  // parents are <= RS_CAP elements: a static deal
+        resplit_one(A, A.fatbk[i], L);
+        __syncthreads();
     }
 }
 
@@ -1109,7 +1401,6 @@ __device__ inline void bitonic_merge(u64& key, u32& code, bool up, int lane)
 template <int RW_SLOTS>
 __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 {
-    __shared__ u32 tpl[4][64 * RW_SLOTS];  // per-wave staging of the compacted pair list
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
     const int cnt = A.counts[4];
@@ -1174,32 +1465,19 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 }
                 cur = g;
                 gk = A.gkmin[g];
-                // tested pairs of g, compacted in pair order
-                int nt = 0;
-                for (int p0 = 0; p0 < P; p0 += 64) {
-                    const int p = p0 + lane;
-                    const bool t = p < P && (A.all_pairs || (A.flags[(size_t)p * G + g] & 1));
-                    const u64 bal = __ballot(t);
-                    const int r = nt + (int)lanes_below(bal);
-                    if (t && r < 64 * RW_SLOTS) tpl[wv][r] = (u32)p;
-                    nt += __popcll(bal);
-                }
-                ntp = min(nt, 64 * RW_SLOTS);  // the host never routes genes with more here
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                // tested pairs of g in pair order (compacted by the split)
+                ntp = min(A.gene_nt[g], 64 * RW_SLOTS);  // the host never routes genes with more here
+                const u32* tl = A.gene_tp + (size_t)g * P;
 #pragma unroll
                 for (int q = 0; q < RW_SLOTS; ++q) {
                     const int j = q * 64 + lane;
+                    const u32 v = tl[j < ntp ? j : 0];
                     if (j < ntp) {
-                        const int pq = (int)tpl[wv][j];
-                        int a2, b2;
-                        pair_decode(pq, K, a2, b2);
-                        pp[q] = (u32)pq;
-                        pa[q] = (u32)a2;
-                        pb[q] = (u32)b2;
+                        pp[q] = v & 0xffffu;
+                        pa[q] = (v >> 16) & 0xffu;
+                        pb[q] = v >> 24;
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
             }
             if (src == 2) {
                 // one repeated key: only the cluster histogram matters.  Inside
@@ -1318,18 +1596,29 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 // Cross-bucket rank sums: for tested pair (a, b) of gene g,
 //   S_ab += sum over buckets beta of h_beta[a] * #(b-elements in buckets < beta)
 // one wave per (gene, pair), lanes over buckets (inclusive scan per 64).
+// SEG: the same over the sub-buckets of each re-split parent (k_rank_resplit).
+template <bool SEG>
 __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 {
     const int lane = threadIdx.x & 63;
     const int W = blockIdx.x * 4 + scc_wave_id(), NW = gridDim.x * 4;
-    const int ng = A.counts[3], P = A.P;
+    const int ng = SEG ? A.counts[10] : A.counts[3], P = A.P;
     for (int f = W; f < ng * P; f += NW) {
         const int gi = f / P, p = f - gi * P;
-        const int g = A.split_genes[gi];
+        int g, bk0, nb;
+        if (SEG) {
+            const int4 sg = A.rsseg[gi];
+            g = sg.x;
+            bk0 = sg.y;
+            nb = sg.z;
+        } else {
+            g = A.split_genes[gi];
+            bk0 = A.gene_bk[2 * g];
+            nb = A.gene_bk[2 * g + 1];
+        }
         if (!A.all_pairs && !(A.flags[(size_t)p * A.G + g] & 1)) continue;
         int a, b;
         pair_decode(p, A.K, a, b);
-        const int bk0 = A.gene_bk[2 * g], nb = A.gene_bk[2 * g + 1];
         const unsigned int* h = A.hbg + (size_t)bk0 * A.K;
         u64 s = 0, carry = 0;
         for (int q0 = 0; q0 < nb; q0 += 64) {
@@ -1396,6 +1685,10 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
 {
     if (L->rw_slots <= 2)
         hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, *L);
+    else if (L->rw_slots <= 4)
+        hipLaunchKernelGGL(k_rank_waves<4>, dim3(grid), dim3(256), 0, st, *L);
+    else if (L->rw_slots <= 8)
+        hipLaunchKernelGGL(k_rank_waves<8>, dim3(grid), dim3(256), 0, st, *L);
     else
         hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, *L);
     return hipGetLastError();
@@ -1403,7 +1696,21 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
 
 extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rank_cross, dim3(grid), dim3(256), 0, st, *L);
+    hipLaunchKernelGGL(k_rank_cross<false>, dim3(grid), dim3(256), 0, st, *L);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid, hipStream_t st)
+{
+    if (!L->fatbk) return hipSuccess;
+    hipLaunchKernelGGL(k_rank_cross<true>, dim3(grid), dim3(256), 0, st, *L);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st)
+{
+    if (!L->fatbk || grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), 0, st, *L);
     return hipGetLastError();
 }
 

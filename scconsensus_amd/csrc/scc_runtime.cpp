@@ -315,7 +315,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         d_gexp = (dd*)((char*)p + sizeof(double) * 2 * nwaves);
     }
     WS("splitg", (size_t)G, d_splitg);
-    WS("counts", 8, d_counts);
+    WS("counts", 16, d_counts);
     WS("err", 4, d_err);
     WS("mx", GK, d_mx);
     WS("me", GK, d_me);
@@ -383,7 +383,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     {
         Scope sc(c, "ingest", s0);
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
-        HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 8, s0));
+        HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 16, s0));
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
                                          d_err, s0));
@@ -484,7 +484,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.med_wide = med_wide;
         L.bucket_target = bucket_target;
         L.wave_target = wave_target;
-        L.rw_slots = P <= 128 ? 2 : 4;
+        L.rw_slots = P <= 128 ? 2 : P <= 256 ? 4 : P <= 512 ? 8 : 16;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
         L.bucket_cap = bucket_cap;
         L.sbuckets = d_sbk;
@@ -507,6 +507,13 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.accE = accE;
         L.accX = accX;
         L.accF = accF;
+        WS("gene_tp", (size_t)G * P, L.gene_tp);
+        WS("gene_nt", (size_t)G, L.gene_nt);
+        if (env_int("SCC_RESPLIT", 1)) {
+            L.fat_cap = (int)std::min<int64_t>(nnz1 / 64 + 64, 1 << 28);
+            WS("fatbk", (size_t)L.fat_cap, L.fatbk);
+            WS("rsseg", (size_t)L.fat_cap, L.rsseg);
+        }
         unsigned long long* st_buf = nullptr;
         const bool stamps = env_int("SCC_STAMPS", 0) != 0;
         if (stamps) {
@@ -520,6 +527,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_rank_classify(&L, s0));
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
         HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
+        HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0));
         // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS items)
         HIPCHK(c, hipEventRecord(c->ev_fork, s0));
         HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
@@ -530,6 +538,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, hipEventRecord(c->ev_join, s1));
         HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
         HIPCHK(c, scc_launch_rank_cross(&L, 4 * ncu, s0));
+        HIPCHK(c, scc_launch_rank_cross_seg(&L, 4 * ncu, s0));
         if (stamps) {
             std::vector<unsigned long long> h((size_t)3 * item_cap * 8);
             int cnts[4];

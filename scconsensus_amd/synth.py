@@ -192,3 +192,112 @@ def edge_fixture(seed: int = 11) -> Dataset:
     X[45, :] = rng.normal(0.0, 1.0, N)
     X[46, :] = np.where(rng.random(N) < 0.5, -rng.gamma(2.0, 1.0, N), 0.0)
     return from_dense(X, labels)
+
+
+# ---------------------------------------------------------------- on the GPU
+@dataclass
+class DeviceDataset:
+    """The same generator's matrix built in HBM with torch (synthetic-data
+    plumbing for the large configs C/D/E, whose host generation would take
+    minutes).  ``layout`` "csc": per cell, ascending gene rows (dgCMatrix);
+    "csr": per gene, ascending cells (a gene-major CSR).  The arrays are torch
+    tensors on the device; ``labels`` is a host array."""
+    G: int
+    N: int
+    layout: str
+    indptr: object   # torch int64 [N+1] (csc) or [G+1] (csr)
+    indices: object  # torch int32 [nnz]: gene row (csc) or cell column (csr)
+    data: object     # torch float64 [nnz]
+    labels: np.ndarray
+
+    @property
+    def nnz(self) -> int:
+        return int(self.data.numel())
+
+    def to_host(self) -> Dataset:
+        """Host CSC copy (the CPU baseline's sample reads it)."""
+        import torch
+        if self.layout == "csc":
+            ip, ix, x = self.indptr.cpu().numpy(), self.indices.cpu().numpy(), self.data.cpu().numpy()
+        else:
+            rows = torch.repeat_interleave(torch.arange(self.G, device=self.data.device, dtype=torch.int32),
+                                           torch.diff(self.indptr))
+            key = self.indices.to(torch.int64) * self.G + rows
+            order = torch.argsort(key)
+            ix = rows[order].cpu().numpy()
+            x = self.data[order].cpu().numpy()
+            ip = np.zeros(self.N + 1, np.int64)
+            np.cumsum(np.bincount(self.indices.cpu().numpy(), minlength=self.N), out=ip[1:])
+        return Dataset(self.G, self.N, ip, ix.astype(np.int32), x, self.labels,
+                       [f"gene{g:05d}" for g in range(self.G)], [f"cell{c:07d}" for c in range(self.N)])
+
+
+# Mean-expression scale per config: E's 1M-cell CSR is generated at the
+# SURVEY §8(d) E density (~5 %, about 1e9 stored values); the others at the
+# generator's natural ~11 %.
+DEVICE_BASE_SCALE = {"E": 0.2}
+
+
+def generate_device(name: str, device, *, seed=None, layout: str = "csc", block_genes: int = 0) -> DeviceDataset:
+    """SURVEY §8(d) generator on the GPU: cluster sizes, labels, base, marker
+    multipliers and size factors from the host numpy stream (as `generate`);
+    the NB(r=2) counts as Poisson(mu/2 * (E1 + E2)) (a shape-2 gamma is the
+    sum of two unit exponentials) from a seeded torch generator, gene block
+    by gene block; X = log1p(count / lib * 1e4)."""
+    import torch
+    cfg = dict(CONFIGS[name])
+    G, N, K = cfg["G"], cfg["N"], cfg["K"]
+    seed = cfg["seed"] if seed is None else seed
+    rng = np.random.default_rng(seed)
+    sz = cluster_sizes(cfg["sizes"], N, K, rng)
+    lab_idx = np.repeat(np.arange(K), sz)
+    rng.shuffle(lab_idx)
+    names = np.array(label_names(K), dtype=object)
+    base = rng.gamma(0.3, 1.0, G) * 0.5 * DEVICE_BASE_SCALE.get(name, 1.0)
+    mult = np.ones((K, G))
+    nmark = max(1, int(0.05 * G))
+    for a in range(K):
+        idx = rng.choice(G, nmark, replace=False)
+        mult[a, idx] = rng.uniform(2.0, 8.0, nmark)
+    s = rng.lognormal(0.0, 0.3, N)
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(int(seed) * 7919 + 17)
+    t_base = torch.tensor(base, dtype=torch.float32, device=dev)
+    t_multT = torch.tensor(mult.T.copy(), dtype=torch.float32, device=dev)  # [G, K]
+    t_lab = torch.tensor(lab_idx, dtype=torch.int64, device=dev)
+    t_s = torch.tensor(s, dtype=torch.float32, device=dev)
+    if block_genes <= 0:
+        block_genes = max(1, min(G, (1 << 28) // N))
+    rows, cols, cnts = [], [], []
+    for g0 in range(0, G, block_genes):
+        g1 = min(G, g0 + block_genes)
+        mu = t_base[g0:g1, None] * t_multT[g0:g1][:, t_lab] * t_s[None, :]
+        u = torch.rand((2, g1 - g0, N), generator=gen, device=dev, dtype=torch.float32).clamp_(min=1e-30)
+        lam = mu.mul_(-0.5).mul_(torch.log(u[0] * u[1]))
+        del u
+        cnt = torch.poisson(lam, generator=gen)
+        del lam
+        nz = torch.nonzero(cnt)  # row-major: gene-major, ascending cells
+        rows.append((nz[:, 0] + g0).to(torch.int32))
+        cols.append(nz[:, 1].to(torch.int32))
+        cnts.append(cnt[nz[:, 0], nz[:, 1]])
+        del cnt, nz
+    rows = torch.cat(rows)
+    cols = torch.cat(cols)
+    v = torch.cat(cnts).to(torch.float64)
+    del cnts
+    lib = torch.zeros(N, dtype=torch.float64, device=dev).index_add_(0, cols.to(torch.int64), v)
+    lib[lib == 0] = 1.0
+    x = torch.log1p(v / lib[cols.to(torch.int64)] * 1e4)
+    del v, lib
+    if layout == "csr":
+        indptr = torch.zeros(G + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(torch.bincount(rows.to(torch.int64), minlength=G), 0)
+        return DeviceDataset(G, N, "csr", indptr, cols, x, names[lab_idx])
+    key = cols.to(torch.int64) * G + rows.to(torch.int64)
+    order = torch.argsort(key)
+    del key
+    indptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    indptr[1:] = torch.cumsum(torch.bincount(cols.to(torch.int64), minlength=N), 0)
+    return DeviceDataset(G, N, "csc", indptr, rows[order].contiguous(), x[order].contiguous(), names[lab_idx])

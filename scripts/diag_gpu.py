@@ -1,7 +1,7 @@
 """GPU diagnostics (not a test): run one DE configuration with stage-level
 synchronisation (SCC_DEBUG_SYNC=1) and compare with the oracle.
 
-usage: python scripts/diag_gpu.py {forced|B}"""
+usage: python scripts/diag_gpu.py {forced|B|C|D|E}"""
 import os
 import sys
 import time
@@ -20,6 +20,9 @@ def log(*a):
 
 
 def main(which):
+    if which in ("C", "D", "E"):
+        import torch  # torch's HIP runtime first (the synthetic matrix is generated with it)
+        torch.zeros(1, device="cuda:0")
     eng = nat.Engine(0)
     if which == "forced":
         d = synth.generate("A")
@@ -42,6 +45,18 @@ def main(which):
         log("DE done: union", len(g.union), "rows", len(g.rows.gene), "tested/pair max", g.rows.pair_tested.max())
         dist = eng.distance(ds, g.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
         log("dist done")
+    elif which in ("C", "D", "E"):
+        import torch
+        d = synth.generate_device(which, "cuda:0")
+        torch.cuda.synchronize()
+        log("generated", which, "nnz", d.nnz)
+        names, code = api.select_clusters(d.labels, 10)
+        ds = eng.dataset_csc_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
+        for rep in range(2):
+            t0 = time.perf_counter()
+            g = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="rows")
+            log("DE done in", round(time.perf_counter() - t0, 4), "s: union", len(g.union), "rows", len(g.rows.gene),
+                "tested/pair max", g.rows.pair_tested.max())
     else:
         raise SystemExit(2)
 

@@ -108,10 +108,10 @@ def test_fast_t_test_constant_data_stops(eng):
     assert e.value.code == nat.SCC_ERR_RSTOP
 
 
-@pytest.mark.parametrize("K", [18, 26])
+@pytest.mark.parametrize("K", [18, 26, 40])
 def test_fast_many_clusters(eng, K):
     """More tested pairs per gene than the wave kernel's 2-slot variant holds
-    (P = 153: 4 slots; P = 325: genes past 256 tested pairs go to the LDS items)."""
+    (P = 153: 4 slots; P = 325: 8 slots; P = 780: 16 slots, config C/D-like)."""
     d = synth.generate("A", G=400, N=4000, K=K, seed=7)
     names, code = api.select_clusters(d.labels, 10)
     assert len(names) * (len(names) - 1) // 2 > 128
@@ -168,6 +168,16 @@ def test_slow_config_a_subset(eng, cfg_a):
     ds = eng.dataset_csc(sub.indptr, sub.indices, sub.data, sub.G, sub.N)
     g, o = _slow_compare(eng, ds, Xs, code, len(names))
     assert len(o.union) > 0
+
+
+def test_slow_many_clusters(eng):
+    """SLOW tests every pair: P = 1225 (config D's K = 50) is past the wave
+    kernel's 1024 tested pairs, so every bucket goes to the LDS items."""
+    d = synth.generate("A", G=120, N=3000, K=50, seed=9)
+    names, code = api.select_clusters(d.labels, 10)
+    assert len(names) == 50
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _slow_compare(eng, ds, d.dense(), code, len(names))
 
 
 def test_slow_edge_fixture(eng, edge):
@@ -292,3 +302,35 @@ def test_rank_size_classes(eng, cfg_a, caps, monkeypatch):
     d, X, names, code = cfg_a
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     _fast_compare(eng, ds, X, code, len(names))
+
+
+def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6):
+    """Genes whose nonzeros crowd a narrow stretch of the value axis (relative
+    width 1e-7) next to a few large outliers: the split's 2048-bin window puts
+    the whole stretch in one bin of > 64 distinct values, which k_rank_resplit
+    splits again.  Some genes are rounded to a grid (ties inside the stretch)."""
+    rng = np.random.default_rng(seed)
+    lab = rng.integers(0, K, N)
+    names = np.array(synth.label_names(K), dtype=object)
+    X = np.zeros((G, N))
+    for g in range(G):
+        m = rng.random(N) < 0.9
+        v = 1.0 + rng.random(N) * 1e-7 * (1 + g % 5) + lab * 2e-8 * (g % 3)
+        if g % 4 == 3:
+            v = np.round(v, 9)
+        X[g, m] = v[m]
+        out = rng.random(N) < 0.01
+        X[g, out] = 50.0 + rng.random(out.sum())
+    return synth.from_dense(X, names[lab]), X
+
+
+@pytest.mark.parametrize("resplit", ["1", "0"])
+def test_resplit_dense_value_stretch(eng, resplit, monkeypatch):
+    """Exact U / ties with and without the re-split route (SCC_RESPLIT=0: the
+    fat buckets go to the LDS items as before)."""
+    monkeypatch.setenv("SCC_RESPLIT", resplit)
+    d, X = _dense_stretch_matrix()
+    names, code = api.select_clusters(d.labels, 10)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _slow_compare(eng, ds, X, code, len(names))
+    _fast_compare(eng, ds, X, code, len(names), min_per_cent=5.0, log_fc_thrs=0.0)
