@@ -60,10 +60,12 @@ struct ScRankLaunch {
     unsigned long long* gkmin;  // [G] key minimum of a split gene when its range fits 58 bits, else ~0
     ScRankItem* items;     // [3][item_cap]
     int* counts;           // [0..2] items per class, [3] split genes, [4] wave buckets, [5] bucket ids,
-                           // [8] fat buckets, [9] re-split queue, [10] re-split segments
+                           // [8] fat buckets, [9] re-split queue, [10] re-split segments, [11] re-split genes
     uint32_t* gene_tp;     // [G][P] tested pairs of each split gene, p | a << 16 | b << 24 (pair order)
     int* gene_nt;          // [G] their number
+    int wv_lo, wv_hi;      // wave kernel launch: genes with wv_lo < tested pairs <= wv_hi
     ScRankItem* fatbk;     // [fat_cap] buckets of > 64 distinct values (re-split into sub-buckets)
+    int4* fatg;            // [G] {gene, first fatbk entry, parents}: the re-split work units
     int4* rsseg;           // [fat_cap] {gene, first sub-bucket id, sub-buckets}: in-parent cross terms
     int fat_cap;
     int* split_genes;      // [G]

@@ -824,11 +824,12 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 
 #define RW_SLOTS_MAX 16  // tested pairs per gene the wave kernel holds: 64 * slots (2, 4, 8 or 16)
 #define RS_T 256          // re-split: threads per workgroup
-#define RS_KPT 16         // keys per thread (held in registers: the scatter is in place)
+#define RS_KPT 8          // keys per thread (held in registers: the scatter is in place)
 #define RS_CAP (RS_T * RS_KPT)
-#define RS_BINS 1024
+#define RS_LOG2B 9
+#define RS_BINS (1 << RS_LOG2B)
 #define RS_BMAX (2 * RS_BINS + 1)
-#define RS_HCAP 4096      // sub-bucket x cluster histogram entries held in LDS
+#define RS_HCAP 2048      // sub-bucket x cluster histogram entries held in LDS
 
 // ===================================================================== split
 #define SP_T 1024
@@ -851,6 +852,7 @@ struct SplitLds {
     u64 rmn[SP_W], rmx[SP_W];
     int off[65];
     int nb, bk0, next;
+    int nfat, fat0, nwav, wav0;
 };
 
 // One ranked gene: 2048-bin histogram of its key window, bins packed into
@@ -1024,28 +1026,58 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         }
     }
     __syncthreads();
-    // ---- 5. one work unit per bucket (empty buckets: a zero histogram row)
+    // ---- 5. one work unit per bucket (empty buckets: a zero histogram row).
+    // Wave buckets and re-split parents are reserved once per gene (one global
+    // atomic each, not one per bucket) and placed with LDS cursors.
+    auto kind = [&](int q) {  // 0 none, 1 wave bucket, 2 re-split parent, 3 LDS item
+        const int c = (int)(L.boff[q + 1] - L.boff[q]);
+        if (c <= 0) return 0;
+        const bool ties_only = c > 64 && !L.bdiff[q];
+        if ((c <= 64 || ties_only) && waves_ok) return 1;
+        if (waves_ok && c <= RS_CAP && A.fatbk) return 2;
+        return 3;
+    };
+    if (tid == 0) {
+        L.nfat = 0;
+        L.nwav = 0;
+    }
+    __syncthreads();
+    for (int q = tid; q < nb; q += SP_T) {
+        const int k = kind(q);
+        if (k == 1) atomicAdd(&L.nwav, 1);
+        if (k == 2) atomicAdd(&L.nfat, 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        L.wav0 = L.nwav ? atomicAdd(&A.counts[4], L.nwav) : 0;
+        L.fat0 = -1;
+        if (L.nfat) {
+            const int f0 = atomicAdd(&A.counts[8], L.nfat);
+            if (f0 + L.nfat <= A.fat_cap) {
+                L.fat0 = f0;
+                A.fatg[atomicAdd(&A.counts[11], 1)] = int4{g, f0, L.nfat, 0};
+            }
+        }
+        L.nfat = 0;
+        L.nwav = 0;
+    }
+    __syncthreads();
     for (int q = tid; q < nb; q += SP_T) {
         const int c = (int)(L.boff[q + 1] - L.boff[q]);
         const int bid = bk0 + q;
-        if (c <= 0) {
+        const int k = kind(q);
+        if (k == 0) {
             for (int k2 = 0; k2 < K; ++k2) A.hbg[(size_t)bid * K + k2] = 0;
             continue;
         }
         // a bucket of one repeated key (a fat bin of ties): closed form in the wave kernel
         const bool ties_only = c > 64 && !L.bdiff[q];
         const ScRankItem itm{base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
-        if ((c <= 64 || ties_only) && waves_ok) {
-            A.sbuckets[atomicAdd(&A.counts[4], 1)] = itm;
-        } else if (waves_ok && c <= RS_CAP && A.fatbk) {
+        if (k == 1) {
+            A.sbuckets[L.wav0 + atomicAdd(&L.nwav, 1)] = itm;
+        } else if (k == 2 && L.fat0 >= 0) {
             // > 64 distinct values in one bin: re-split on a finer window (k_rank_resplit)
-            const int f = atomicAdd(&A.counts[8], 1);
-            if (f < A.fat_cap) {
-                A.fatbk[f] = itm;
-            } else {
-                const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
-                A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
-            }
+            A.fatbk[L.fat0 + atomicAdd(&L.nfat, 1)] = itm;
         } else {
             const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
             A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
@@ -1072,7 +1104,7 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
 // A bucket the split left with > 64 distinct values (a dense stretch of the
 // value axis: at 100k+ cells a 2048-bin window over the gene's whole range
 // puts hundreds of values in one bin) is split again on its own key window:
-// 1024 bins, the same packing rule, elements scattered in place (all of them
+// 512 bins, the same packing rule, elements scattered in place (all of them
 // are in registers first).  The sub-buckets go to the wave kernel; the
 // parent keeps its cluster histogram row (the gene-level cross term of
 // k_rank_cross) and records its sub-bucket range, whose in-parent cross term
@@ -1090,6 +1122,8 @@ struct ResplitLds {
     u32 wsum2[RS_T / 64 + 1];
     u64 rmn[RS_T / 64], rmx[RS_T / 64];
     u32 hs[RS_HCAP];  // [sub-bucket][cluster] counts (in-parent cross term), when nb * K fits
+    u32 bs[RS_HCAP];  // [sub-bucket][cluster] elements of the cluster in lower sub-buckets
+    u64 acc[64 * RW_SLOTS_MAX];  // the gene's in-parent cross terms per tested pair
     int nb, bk0, next, ovf, nw, w0;
 };
 
@@ -1098,6 +1132,15 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
     constexpr int W = RS_T / 64, BPT = RS_BINS / RS_T;
     const int K = A.K, g = it.gene, n = it.n;
     const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    u64 t_prev = A.stamps ? __builtin_amdgcn_s_memtime() : 0;
+#define RSTAMP(ph)                                                                         \
+    do {                                                                                   \
+        if (A.stamps && tid == 0) {                                                        \
+            const u64 t_now = __builtin_amdgcn_s_memtime();                               \
+            atomicAdd((unsigned long long*)&A.stamps[ph], (unsigned long long)(t_now - t_prev)); \
+            t_prev = t_now;                                                                \
+        }                                                                                  \
+    } while (0)
     u64 kr[RS_KPT];
     u8 cd[RS_KPT];
 #pragma unroll
@@ -1132,9 +1175,10 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         kmn = L.rmn[v] < kmn ? L.rmn[v] : kmn;
         kmx = L.rmx[v] > kmx ? L.rmx[v] : kmx;
     }
+    RSTAMP(0);
     const u64 range = kmx - kmn;
     const int bits = range ? 64 - __clzll((long long)range) : 0;
-    const int sh = bits > 10 ? bits - 10 : 0;
+    const int sh = bits > RS_LOG2B ? bits - RS_LOG2B : 0;
 #pragma unroll
     for (int q = 0; q < RS_KPT; ++q) {
         if (q * RS_T + tid < n) {
@@ -1208,6 +1252,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
     }
     __syncthreads();
     const int nb = L.nb, bk0 = L.bk0;
+    RSTAMP(1);
     if (L.ovf) {  // out of bucket ids: rank the parent as one LDS item
         if (tid == 0) {
             const int cls = (n <= A.cap_s) ? 0 : ((n <= A.cap_m) ? 1 : 2);
@@ -1237,6 +1282,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         }
     }
     __syncthreads();
+    RSTAMP(2);
     if (tid < K) A.hbg[(size_t)it.bucket * K + tid] = L.m[tid];  // the parent's row (gene-level cross)
     // sub-buckets for the wave kernel: one list reservation per parent
     {
@@ -1287,31 +1333,61 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
             __syncthreads();
         }
     }
+    RSTAMP(3);
     if (!hist_lds) {  // many sub-buckets: k_rank_cross_seg adds the in-parent cross term
         if (tid == 0) A.rsseg[atomicAdd(&A.counts[10], 1)] = int4{g, bk0, nb, 0};
         return;
     }
-    // in-parent cross term: S_ab += sum_s hs[s][a] * #(b in sub-buckets < s)
-    const int ntp = min(A.gene_nt[g], A.P);
+    // in-parent cross term: S_ab += sum_s hs[s][a] * bs[s][b], bs = #(b in
+    // sub-buckets < s) (a column scan per cluster first: the pair sums are
+    // then independent loads, not a dependent chain)
+    for (int c = tid; c < K; c += RS_T) {
+        u32 run = 0;
+        for (int q = 0; q < nb; ++q) {
+            L.bs[q * K + c] = run;
+            run += L.hs[q * K + c];
+        }
+    }
+    __syncthreads();
+    const int ntp = min(A.gene_nt[g], 64 * RW_SLOTS_MAX);
     for (int j = tid; j < ntp; j += RS_T) {
         const u32 v = A.gene_tp[(size_t)g * A.P + j];
         const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+        if (!L.m[a] || !L.m[b]) continue;
         u64 sacc = 0;
-        u32 below = 0;
-        for (int q = 0; q < nb; ++q) {
-            sacc += (u64)L.hs[q * K + a] * below;
-            below += L.hs[q * K + b];
-        }
-        if (sacc) atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
+#pragma unroll 4
+        for (int q = 0; q < nb; ++q) sacc += (u64)L.hs[q * K + a] * L.bs[q * K + b];
+        L.acc[j] += sacc;  // thread j owns tested pair j for the whole gene
     }
+    RSTAMP(4);
+    if (A.stamps && tid == 0) atomicAdd((unsigned long long*)&A.stamps[7], 1ull);
+#undef RSTAMP
 }
 
 __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
 {
     __shared__ ResplitLds L;
-    const int cnt = min(A.counts[8], A.fat_cap);
-    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {  // parents are <= RS_CAP elements: a static deal
-        resplit_one(A, A.fatbk[i], L);
+    const int ng = A.counts[11];
+    for (;;) {  // one gene (all its parents, a contiguous run of fatbk) at a time, from a queue
+        if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[9], 1);
+        __syncthreads();
+        const int i = L.next;
+        if (i >= ng) break;
+        const int4 ge = A.fatg[i];
+        const int g = ge.x;
+        const int ntp = min(A.gene_nt[g], 64 * RW_SLOTS_MAX);
+        for (int j = threadIdx.x; j < ntp; j += RS_T) L.acc[j] = 0;
+        __syncthreads();
+        for (int f = ge.y; f < ge.y + ge.z; ++f) {
+            resplit_one(A, A.fatbk[f], L);
+            __syncthreads();
+        }
+        for (int j = threadIdx.x; j < ntp; j += RS_T) {
+            if (L.acc[j]) {
+                const u32 v = A.gene_tp[(size_t)g * A.P + j];
+                atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)L.acc[j]);
+            }
+        }
         __syncthreads();
     }
 }
@@ -1421,6 +1497,11 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
         // every bucket's loads are issued one bucket ahead
         ScRankItem D{0, 0, 0, 0, 0};
         if (lane < c1 - c0) D = A.sbuckets[c0 + lane];
+        // this launch ranks the buckets of genes with wv_lo < tested pairs <= wv_hi
+        // (the slot count of each launch fits its genes: fewer registers, more waves)
+        const int ntg = (lane < c1 - c0) ? A.gene_nt[D.gene] : -1;
+        u64 rem = __ballot(ntg > A.wv_lo && ntg <= A.wv_hi);
+        if (!rem) continue;
         const u32 dlo = (u32)(u64)D.base, dhi = (u32)((u64)D.base >> 32);
         auto dbase = [&](int li) {
             return (i64)(((u64)(u32)__builtin_amdgcn_readlane((int)dhi, li) << 32) |
@@ -1429,13 +1510,15 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
         u64 nkey;
         u32 ncode;
         {
-            const i64 b0 = dbase(0);
-            const int n0 = __builtin_amdgcn_readlane(D.n, 0);
+            const int l0 = __builtin_ctzll(rem);
+            const i64 b0 = dbase(l0);
+            const int n0 = __builtin_amdgcn_readlane(D.n, l0);
             nkey = lane < n0 ? A.keys2[b0 + lane] : ~0ull;
             ncode = lane < n0 ? (u32)A.codes2[b0 + lane] : 255u;
         }
-        for (int bi = c0; bi < c1; ++bi) {
-            const int li = bi - c0;
+        while (rem) {
+            const int li = __builtin_ctzll(rem);
+            rem &= rem - 1;
             const int g = __builtin_amdgcn_readlane(D.gene, li);
             const int n = __builtin_amdgcn_readlane(D.n, li);
             const int bucket = __builtin_amdgcn_readlane(D.bucket, li);
@@ -1443,9 +1526,10 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             const i64 bbase = dbase(li);
             u64 key = nkey;
             u32 code = ncode;
-            if (bi + 1 < c1) {
-                const i64 b1 = dbase(li + 1);
-                const int n1 = __builtin_amdgcn_readlane(D.n, li + 1);
+            if (rem) {
+                const int l1 = __builtin_ctzll(rem);
+                const i64 b1 = dbase(l1);
+                const int n1 = __builtin_amdgcn_readlane(D.n, l1);
                 nkey = lane < n1 ? A.keys2[b1 + lane] : ~0ull;
                 ncode = lane < n1 ? (u32)A.codes2[b1 + lane] : 255u;
             }
@@ -1683,15 +1767,26 @@ extern "C" size_t scc_rank_split_lds(int K)
 
 extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st)
 {
-    if (L->rw_slots <= 2)
-        hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, *L);
-    else if (L->rw_slots <= 4)
-        hipLaunchKernelGGL(k_rank_waves<4>, dim3(grid), dim3(256), 0, st, *L);
-    else if (L->rw_slots <= 8)
-        hipLaunchKernelGGL(k_rank_waves<8>, dim3(grid), dim3(256), 0, st, *L);
-    else
-        hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, *L);
-    return hipGetLastError();
+    // one launch per slot class present: genes with <= 128 tested pairs on the
+    // 2-slot kernel, <= 256 on 4, <= 512 on 8, <= 1024 on 16
+    ScRankLaunch A = *L;
+    const int hi[4] = {128, 256, 512, 1024};
+    for (int c = 0; c < 4; ++c) {
+        if (64 * L->rw_slots < hi[c] && c > 0) break;
+        A.wv_lo = c ? hi[c - 1] : -1;
+        A.wv_hi = hi[c];
+        if (c == 0)
+            hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, A);
+        else if (c == 1)
+            hipLaunchKernelGGL(k_rank_waves<4>, dim3(grid), dim3(256), 0, st, A);
+        else if (c == 2)
+            hipLaunchKernelGGL(k_rank_waves<8>, dim3(grid), dim3(256), 0, st, A);
+        else
+            hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, A);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hipStream_t st)

@@ -513,6 +513,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             L.fat_cap = (int)std::min<int64_t>(nnz1 / 64 + 64, 1 << 28);
             WS("fatbk", (size_t)L.fat_cap, L.fatbk);
             WS("rsseg", (size_t)L.fat_cap, L.rsseg);
+            WS("fatg", (size_t)G, L.fatg);
         }
         unsigned long long* st_buf = nullptr;
         const bool stamps = env_int("SCC_STAMPS", 0) != 0;
@@ -527,7 +528,22 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_rank_classify(&L, s0));
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
         HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
-        HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0));
+        if (stamps) {  // re-split phase clocks (summed over parents): 8 u64 after the item stamps
+            ScRankLaunch R = L;
+            R.stamps = st_buf + (size_t)3 * item_cap * 8 - 8;
+            HIPCHK(c, hipMemsetAsync(R.stamps, 0, 64, s0));
+            HIPCHK(c, scc_launch_rank_resplit(&R, 4 * ncu, s0));
+            unsigned long long h[8];
+            HIPCHK(c, hipMemcpyAsync(h, R.stamps, 64, hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            fprintf(stderr, "[scc stamps] resplit parents %llu, mean cycles: load %.0f bins %.0f scatter %.0f list %.0f cross %.0f\n",
+                    h[7], h[0] / (double)std::max(1ull, h[7]), h[1] / (double)std::max(1ull, h[7]),
+                    h[2] / (double)std::max(1ull, h[7]), h[3] / (double)std::max(1ull, h[7]),
+                    h[4] / (double)std::max(1ull, h[7]));
+            HIPCHK(c, hipMemsetAsync(R.stamps, 0, 64, s0));
+        } else {
+            HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0));
+        }
         // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS items)
         HIPCHK(c, hipEventRecord(c->ev_fork, s0));
         HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
