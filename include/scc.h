@@ -97,6 +97,18 @@ SCC_API void scc_ctx_reset_timers(scc_ctx* ctx);
 SCC_API int scc_dataset_create_csc(scc_ctx* ctx, const int64_t* indptr, const int32_t* rows, const double* vals,
                            int64_t n_genes, int64_t n_cells, int64_t nnz, int32_t ptr_kind,
                            scc_dataset** out);
+/* Gene-major CSR (genes x cells; per gene ascending cell columns, e.g. a
+ * scipy csr_matrix or an AnnData .X transposed; BASELINE config E's CSR
+ * input): indptr[G+1], cols[nnz] (0-based cells), vals[nnz].  Transposed once
+ * on the device into the resident CSC over cells above (the dgCMatrix R
+ * would hold for the same matrix), so every result equals the CSC path's.
+ * Column indices outside [0, N) fail with SCC_ERR_INVALID; a repeated
+ * (gene, cell) fails like unsorted dgCMatrix rows at scc_de_run.  No
+ * reference interface: the reference takes dataMatrix as an R matrix
+ * (Fast:22, :368); this is the R-free caller's equivalent. */
+SCC_API int scc_dataset_create_csr(scc_ctx* ctx, const int64_t* indptr, const int32_t* cols, const double* vals,
+                           int64_t n_genes, int64_t n_cells, int64_t nnz, int32_t ptr_kind,
+                           scc_dataset** out);
 /* base R matrix: G x N column-major doubles (slow:32 as.matrix). */
 SCC_API int scc_dataset_create_dense(scc_ctx* ctx, const double* x_colmajor, int64_t n_genes, int64_t n_cells,
                              int32_t ptr_kind, scc_dataset** out);

@@ -35,7 +35,7 @@ SCC_PTR_DEVICE = 1
 # every symbol include/scc.h declares (tests check the library exports them all)
 EXPORTS = [
     "scc_ctx_create", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_kernel_time",
-    "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_dense", "scc_dataset_destroy",
+    "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_csr", "scc_dataset_create_dense", "scc_dataset_destroy",
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
     "scc_distance", "scc_distance_cols", "scc_silhouette", "scc_last_pca_scores",
@@ -96,6 +96,7 @@ def load():
         "scc_ctx_kernel_time": (ctypes.c_int, [vp, ctypes.c_char_p, P(dbl), P(i64)]),
         "scc_ctx_reset_timers": (None, [vp]),
         "scc_dataset_create_csc": (ctypes.c_int, [vp, vp, vp, vp, i64, i64, i64, i32, P(vp)]),
+        "scc_dataset_create_csr": (ctypes.c_int, [vp, vp, vp, vp, i64, i64, i64, i32, P(vp)]),
         "scc_dataset_create_dense": (ctypes.c_int, [vp, vp, i64, i64, i32, P(vp)]),
         "scc_dataset_destroy": (None, [vp]),
         "scc_de_run": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), P(vp)]),
@@ -223,6 +224,24 @@ class Engine:
     def dataset_csc_device(self, indptr_ptr, rows_ptr, vals_ptr, G, N, nnz) -> Dataset:
         h = ctypes.c_void_p()
         self._check(self.lib.scc_dataset_create_csc(self.ctx, ctypes.c_void_p(indptr_ptr), ctypes.c_void_p(rows_ptr),
+                                                    ctypes.c_void_p(vals_ptr), G, N, nnz, SCC_PTR_DEVICE,
+                                                    ctypes.byref(h)))
+        return Dataset(self, h, G, N)
+
+    def dataset_csr(self, indptr, cols, vals, G, N) -> Dataset:
+        """Gene-major CSR (genes x cells: indptr[G+1], cell columns, values),
+        transposed on the device into the resident dgCMatrix layout."""
+        indptr = np.ascontiguousarray(indptr, np.int64)
+        cols = np.ascontiguousarray(cols, np.int32)
+        vals = np.ascontiguousarray(vals, np.float64)
+        h = ctypes.c_void_p()
+        self._check(self.lib.scc_dataset_create_csr(self.ctx, _ptr(indptr), _ptr(cols), _ptr(vals), G, N, len(vals),
+                                                    SCC_PTR_HOST, ctypes.byref(h)))
+        return Dataset(self, h, G, N)
+
+    def dataset_csr_device(self, indptr_ptr, cols_ptr, vals_ptr, G, N, nnz) -> Dataset:
+        h = ctypes.c_void_p()
+        self._check(self.lib.scc_dataset_create_csr(self.ctx, ctypes.c_void_p(indptr_ptr), ctypes.c_void_p(cols_ptr),
                                                     ctypes.c_void_p(vals_ptr), G, N, nnz, SCC_PTR_DEVICE,
                                                     ctypes.byref(h)))
         return Dataset(self, h, G, N)

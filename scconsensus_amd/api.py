@@ -54,9 +54,14 @@ def select_clusters(labels, min_cluster_size: int, cluster_order=None):
 
 def _as_matrix(dataMatrix):
     """Accept scipy.sparse (genes x cells), numpy dense (genes x cells) or a
-    synth.Dataset; return ('csc', indptr, rows, vals, G, N) or ('dense', X)."""
+    synth.Dataset; return ('csc' | 'csr', indptr, idx, vals, G, N) or ('dense', X)."""
     try:
         import scipy.sparse as sp
+        if sp.issparse(dataMatrix) and dataMatrix.format == "csr":  # gene-major: transposed on the device
+            m = dataMatrix.copy() if not dataMatrix.has_sorted_indices else dataMatrix
+            m.sort_indices()
+            return "csr", m.indptr.astype(np.int64), m.indices.astype(np.int32), m.data.astype(np.float64), \
+                m.shape[0], m.shape[1]
         if sp.issparse(dataMatrix):
             m = dataMatrix.tocsc()
             m.sort_indices()
@@ -75,6 +80,9 @@ def _upload(eng, m):
     if m[0] == "csc":
         _, indptr, rows, vals, G, N = m
         return eng.dataset_csc(indptr, rows, vals, G, N)
+    if m[0] == "csr":
+        _, indptr, cols, vals, G, N = m
+        return eng.dataset_csr(indptr, cols, vals, G, N)
     return eng.dataset_dense(m[1])
 
 
@@ -137,8 +145,8 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
         raise NotImplementedError(f"Unknown test: {method} (this engine implements test.use = 'wilcox' and 't')")
     eng = _engine(device)
     m = _as_matrix(dataMatrix)
-    N = m[-1] if m[0] == "csc" else m[1].shape[1]
-    G = m[-2] if m[0] == "csc" else m[1].shape[0]
+    N = m[-1] if m[0] in ("csc", "csr") else m[1].shape[1]
+    G = m[-2] if m[0] in ("csc", "csr") else m[1].shape[0]
     names, code = select_clusters(consensusClusterLabels, minClusterSize, cluster_order)
     if len(names) < 2:
         raise ValueError("need at least two clusters with > minClusterSize cells")
@@ -178,8 +186,8 @@ def reclusterDEConsensus(dataMatrix, consensusClusterLabels, method="Wilcoxon", 
         return None
     eng = _engine(device)
     m = _as_matrix(dataMatrix)
-    N = m[-1] if m[0] == "csc" else m[1].shape[1]
-    G = m[-2] if m[0] == "csc" else m[1].shape[0]
+    N = m[-1] if m[0] in ("csc", "csr") else m[1].shape[1]
+    G = m[-2] if m[0] in ("csc", "csr") else m[1].shape[0]
     names, code = select_clusters(consensusClusterLabels, minClusterSize, cluster_order)
     if len(names) < 2:
         raise ValueError("need at least two clusters with > minClusterSize cells")

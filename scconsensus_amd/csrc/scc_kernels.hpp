@@ -154,6 +154,11 @@ hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, c
 hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
                            long long* total, hipStream_t st);
 int scc_scan_scratch_blocks(long long n);
+#define SCC_CSR_TG 32  // genes per tile of the CSR -> CSC transpose
+size_t scc_csr_scratch_words(long long G, long long N);
+hipError_t scc_launch_csr_to_csc(const long long* indptr, const int* cols, const double* vals, int G, int N,
+                                 uint32_t* scratch, long long* scan_scratch, long long* csc_indptr, int* csc_rows,
+                                 double* csc_vals, int* err, int check_only, hipStream_t st);
 hipError_t scc_launch_reduce_dd(const dd* parts, int n, dd* out, hipStream_t st);
 
 hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st);

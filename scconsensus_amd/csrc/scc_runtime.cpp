@@ -139,6 +139,116 @@ extern "C" int scc_dataset_create_csc(scc_ctx* c, const int64_t* indptr, const i
     return SCC_OK;
 }
 
+extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const int32_t* cols, const double* vals,
+                                      int64_t G, int64_t N, int64_t nnz, int32_t kind, scc_dataset** out)
+{
+    if (!c || !out || !indptr || G <= 0 || N <= 0 || nnz < 0 || (nnz > 0 && (!cols || !vals)))
+        return fail(c, SCC_ERR_INVALID, "scc_dataset_create_csr: bad arguments");
+    if (G > INT32_MAX || N > INT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "dimensions exceed int32");
+    if (nnz > UINT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "more than 2^32 stored values");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    // the CSR on the device (borrowed, or a temporary upload)
+    long long* d_ip = nullptr;
+    int* d_cols = nullptr;
+    double* d_vals = nullptr;
+    std::vector<void*> tmp;
+    auto cleanup = [&]() {
+        hipStreamSynchronize(s0);
+        for (void* p : tmp) hipFree(p);
+    };
+    auto dalloc = [&](void** p, size_t bytes) {
+        if (hipMalloc(p, std::max<size_t>(bytes, 8)) != hipSuccess) {
+            hipGetLastError();
+            *p = nullptr;
+            return false;
+        }
+        tmp.push_back(*p);
+        return true;
+    };
+    if (kind == SCC_PTR_DEVICE) {
+        d_ip = (long long*)indptr;
+        d_cols = (int*)cols;
+        d_vals = (double*)vals;
+    } else {
+        if (!dalloc((void**)&d_ip, sizeof(long long) * (G + 1)) || !dalloc((void**)&d_cols, sizeof(int) * nnz) ||
+            !dalloc((void**)&d_vals, sizeof(double) * nnz)) {
+            cleanup();
+            return fail(c, SCC_ERR_OOM, "CSR upload allocation failed");
+        }
+        hipMemcpyAsync(d_ip, indptr, sizeof(long long) * (G + 1), hipMemcpyHostToDevice, s0);
+        if (nnz > 0) {
+            hipMemcpyAsync(d_cols, cols, sizeof(int) * nnz, hipMemcpyHostToDevice, s0);
+            hipMemcpyAsync(d_vals, vals, sizeof(double) * nnz, hipMemcpyHostToDevice, s0);
+        }
+    }
+    // host-side shape checks on the row pointer (G+1 words)
+    std::vector<long long> hip_(G + 1);
+    if (hipMemcpyAsync(hip_.data(), d_ip, sizeof(long long) * (G + 1), hipMemcpyDeviceToHost, s0) != hipSuccess ||
+        hipStreamSynchronize(s0) != hipSuccess) {
+        hipGetLastError();
+        cleanup();
+        return fail(c, SCC_ERR_HIP, "CSR upload failed");
+    }
+    if (hip_[0] != 0 || hip_[G] != nnz) {
+        cleanup();
+        return fail(c, SCC_ERR_INVALID, "CSR indptr must start at 0 and end at nnz");
+    }
+    for (int64_t g = 0; g < G; ++g)
+        if (hip_[g + 1] < hip_[g]) {
+            cleanup();
+            return fail(c, SCC_ERR_INVALID, "CSR indptr is not non-decreasing");
+        }
+    uint32_t* scratch = nullptr;
+    long long* scan_scr = nullptr;
+    int* d_err = nullptr;
+    if (!dalloc((void**)&scratch, sizeof(uint32_t) * scc_csr_scratch_words(G, N)) ||
+        !dalloc((void**)&scan_scr, sizeof(long long) * (scc_scan_scratch_blocks(N) + 1)) ||
+        !dalloc((void**)&d_err, sizeof(int))) {
+        cleanup();
+        return fail(c, SCC_ERR_OOM, "CSR transpose scratch allocation failed");
+    }
+    scc_dataset* d = new scc_dataset();
+    d->ctx = c;
+    d->device = c->device;
+    d->G = G;
+    d->N = N;
+    d->nnz = nnz;
+    d->owned = true;
+    if (hipMalloc(&d->d_indptr, sizeof(long long) * (N + 1)) != hipSuccess ||
+        hipMalloc(&d->d_rows, sizeof(int) * std::max<int64_t>(nnz, 1)) != hipSuccess ||
+        hipMalloc(&d->d_vals, sizeof(double) * std::max<int64_t>(nnz, 1)) != hipSuccess) {
+        hipGetLastError();
+        cleanup();
+        scc_dataset_destroy(d);
+        return fail(c, SCC_ERR_OOM, "dataset allocation failed");
+    }
+    int herr = 0;
+    hipError_t e = hipMemsetAsync(d_err, 0, sizeof(int), s0);
+    if (e == hipSuccess)
+        e = scc_launch_csr_to_csc(d_ip, d_cols, d_vals, (int)G, (int)N, scratch, scan_scr, d->d_indptr, d->d_rows,
+                                  d->d_vals, d_err, 1, s0);
+    if (e == hipSuccess) e = hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess) e = hipStreamSynchronize(s0);
+    if (e == hipSuccess && herr) {
+        cleanup();
+        scc_dataset_destroy(d);
+        return fail(c, SCC_ERR_INVALID, "CSR column index out of range");
+    }
+    if (e == hipSuccess)
+        e = scc_launch_csr_to_csc(d_ip, d_cols, d_vals, (int)G, (int)N, scratch, scan_scr, d->d_indptr, d->d_rows,
+                                  d->d_vals, d_err, 0, s0);
+    if (e == hipSuccess) e = hipStreamSynchronize(s0);
+    cleanup();
+    if (e != hipSuccess) {
+        hipGetLastError();
+        scc_dataset_destroy(d);
+        return fail(c, SCC_ERR_HIP, std::string("CSR transpose failed: ") + hipGetErrorString(e));
+    }
+    *out = d;
+    return SCC_OK;
+}
+
 extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, int64_t N, int32_t kind,
                                         scc_dataset** out)
 {
