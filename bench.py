@@ -86,6 +86,47 @@ def cpu_baseline(d, code, K, union, sample_genes, seed=0):
             "end_to_end_s": t}
 
 
+def de_only(a, eng, ds, d, code, K, dist, world):
+    """Config E (BASELINE: "1M-cell sparse CSR input, 100 clusters (4950
+    pairs), DE-only"): the FAST DE over all pairs, K > 64 through the grouped
+    orchestration (scconsensus_amd/grouped.py), rows fetched to the host."""
+    from scconsensus_amd import grouped
+
+    def step():
+        return grouped.de_fast_grouped(eng, ds, code, K)
+
+    for _ in range(a.warmup):
+        r = step()
+    eng.synchronize()
+    eng.reset_timers()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        r = step()
+    eng.synchronize()
+    dist.barrier()
+    dt = dist.max_over_ranks(time.perf_counter() - t0)
+    s_step = dt / a.steps
+    fams = ["ingest", "gene_stats", "pair_filter", "gene_rank", "pair_test", "pair_select"]
+    stage_ms = {}
+    for f in fams:
+        t, n = eng.kernel_time(f)
+        stage_ms[f] = round(t / max(a.steps, 1), 3)  # per step (several engine runs per step)
+    P = K * (K - 1) // 2
+    out = {"metric": "DE-only seconds per reclusterDEConsensusFast DE at config E", "value": s_step, "unit": "s",
+           "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": s_step * 1e3,
+           "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (SURVEY §8d generator on the GPU, gene-major CSR)",
+           "config": {"workload": f"config E: FAST DE (all {P} pairs, Wilcoxon), {d.N} cells x {d.G} genes CSR, K={K}",
+                      "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": d.nnz,
+                      "union": len(r.union), "rows": int(len(r.rows.gene)), "engine_runs_per_step": max(1, -(-K // grouped.GROUP) * (-(-K // grouped.GROUP) - 1) // 2),
+                      "parallelism": f"jobs{world}"},
+           "stage_ms_per_step": stage_ms}
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.close()
+
+
 def main():
     a = _args()
     if a.mode == "shard":
@@ -105,7 +146,7 @@ def main():
     gpu = 0 if os.environ.get("SCC_SHARE_GPU") else local
     if a.config in DEVICE_GEN:  # C/D/E: generated in HBM (host generation takes minutes)
         import torch
-        d = synth.generate_device(a.config, f"cuda:{gpu}", seed=seed)
+        d = synth.generate_device(a.config, f"cuda:{gpu}", seed=seed, layout="csr" if a.config == "E" else "csc")
         torch.cuda.synchronize()
     else:
         d = synth.generate(a.config, seed=seed)
@@ -113,6 +154,9 @@ def main():
     K = len(names)
     P = K * (K - 1) // 2
     eng = nat.Engine(gpu, profile=True)
+    if a.config == "E":
+        ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
+        return de_only(a, eng, ds, d, code, K, dist, world)
     if a.config in DEVICE_GEN:
         ds = eng.dataset_csc_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
     else:
