@@ -151,9 +151,14 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
     if len(names) < 2:
         raise ValueError("need at least two clusters with > minClusterSize cells")
     ds = _upload(eng, m)
-    res = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
-                     min_per_cent=float(minPerCent), top_n=NumbertopDEGenes,
-                     fetch="rows" if return_details else "union", test=method)
+    if len(names) > 64:  # one engine run holds <= 64 clusters: group-pair runs (grouped.py)
+        from . import grouped
+        res = grouped.de_fast_grouped(eng, ds, code, len(names), q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
+                                      min_per_cent=float(minPerCent), top_n=NumbertopDEGenes, test=method)
+    else:
+        res = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
+                         min_per_cent=float(minPerCent), top_n=NumbertopDEGenes,
+                         fetch="rows" if return_details else "union", test=method)
     if res.status == nat.SCC_ERR_RSTOP:
         raise RuntimeError(res.message)
     uni = res.union
