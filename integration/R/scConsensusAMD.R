@@ -20,6 +20,9 @@
 .scc_slots <- function(m) {
   if (inherits(m, "dgCMatrix")) {
     list(x = m@x, p = m@p, i = m@i, dim = dim(m))
+  } else if (inherits(m, "dgRMatrix")) {
+    # gene-major CSR: a third dim entry 1L selects scc_dataset_create_csr
+    list(x = m@x, p = m@p, i = m@j, dim = c(dim(m), 1L))
   } else {
     m <- as.matrix(m)
     storage.mode(m) <- "double"

@@ -33,13 +33,19 @@ static void check(int rc)
     if (rc != SCC_OK) Rf_error("scConsensus engine error %d: %s", rc, scc_ctx_last_error(g_ctx));
 }
 
-/* dgCMatrix slots (@p int, @i int, @x double) or a base double matrix */
+/* dgCMatrix slots (@p int, @i int, @x double), dgRMatrix slots (@p, @j, @x;
+ * dim has a third entry 1) or a base double matrix */
 static scc_dataset* dataset_from(SEXP x, SEXP p, SEXP i, SEXP dim)
 {
     scc_dataset* ds = NULL;
     const int G = INTEGER(dim)[0], N = INTEGER(dim)[1];
     if (Rf_isNull(p)) {
         check(scc_dataset_create_dense(g_ctx, REAL(x), G, N, SCC_PTR_HOST, &ds));
+    } else if (XLENGTH(dim) > 2 && INTEGER(dim)[2] == 1) {
+        /* dgRMatrix @p is int[G+1] over genes, @j the cell columns */
+        int64_t* p64 = (int64_t*)R_alloc((size_t)G + 1, sizeof(int64_t));
+        for (int g = 0; g <= G; ++g) p64[g] = INTEGER(p)[g];
+        check(scc_dataset_create_csr(g_ctx, p64, INTEGER(i), REAL(x), G, N, (int64_t)XLENGTH(x), SCC_PTR_HOST, &ds));
     } else {
         /* dgCMatrix @p is int[N+1]: widen to int64 once */
         int64_t* p64 = (int64_t*)R_alloc((size_t)N + 1, sizeof(int64_t));
