@@ -830,6 +830,10 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 #define RS_BINS (1 << RS_LOG2B)
 #define RS_BMAX (2 * RS_BINS + 1)
 #define RS_HCAP 2048      // sub-bucket x cluster histogram entries held in LDS
+#define RSW_LOG2B 8       // wave re-split: parents of <= RSW_CAP elements, 256 bins
+#define RSW_BINS (1 << RSW_LOG2B)
+#define RSW_CAP 256
+#define RSW_HCAP 512
 
 // ===================================================================== split
 #define SP_T 1024
@@ -1379,7 +1383,9 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
         for (int j = threadIdx.x; j < ntp; j += RS_T) L.acc[j] = 0;
         __syncthreads();
         for (int f = ge.y; f < ge.y + ge.z; ++f) {
-            resplit_one(A, A.fatbk[f], L);
+            const ScRankItem it = A.fatbk[f];
+            if (it.n <= RSW_CAP) continue;  // k_rank_resplit_w (one wave per parent)
+            resplit_one(A, it, L);
             __syncthreads();
         }
         for (int j = threadIdx.x; j < ntp; j += RS_T) {
@@ -1390,6 +1396,258 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
         }
         __syncthreads();
     }
+}
+
+// One wave per re-split parent of <= RSW_CAP elements (most of them): the
+// same binning, packing, in-place scatter and in-parent cross term as
+// resplit_one, with wave-level ordering only (no workgroup barriers) and four
+// parents per workgroup in flight.
+struct ResplitWLds {
+    u32 hist[RSW_BINS];
+    u32 excl[RSW_BINS];
+    u32 bid[RSW_BINS];
+    u64 rep[RSW_BINS];
+    u32 bcur[2 * RSW_BINS + 1];
+    u32 boff[2 * RSW_BINS + 2];
+    u8 bdiff[2 * RSW_BINS + 4];
+    u32 m[64];
+    u32 hs[RSW_HCAP];
+    u32 bs[RSW_HCAP];
+};
+
+__device__ inline void wsync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
+{
+    __shared__ ResplitWLds Ls[4];
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    ResplitWLds& L = Ls[wv];
+    const int K = A.K;
+    const int cnt = min(A.counts[8], A.fat_cap);
+    constexpr int EPL = RSW_CAP / 64, BPL = RSW_BINS / 64;
+    // Bucket ids and wave-list slots come from wave-private chunks: one global
+    // atomic per chunk, not per parent (same-address atomics serialise in L2:
+    // two per parent cost 48 of this kernel's 54 ms at config D).  Unused
+    // list slots are filled with empty descriptors the wave kernel skips.
+    const ScRankItem nullit{0, 0, 0, 1, -1};
+    const int chunk = A.rsw_chunk;
+    int id_cur = 0, id_end = 0, sl_cur = 0, sl_end = 0;
+    auto fill_null = [&](int a, int b) {
+        for (int q = a + lane; q < b; q += 64) A.sbuckets[q] = nullit;
+    };
+    for (int f = blockIdx.x * 4 + wv; f < cnt; f += gridDim.x * 4) {
+        const ScRankItem it = A.fatbk[f];
+        const int n = it.n, g = it.gene;
+        if (n > RSW_CAP) continue;  // k_rank_resplit (a workgroup per parent)
+        u64 kr[EPL];
+        u32 cd[EPL];
+        u64 kmn = ~0ull, kmx = 0;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            const int i = q * 64 + lane;
+            kr[q] = i < n ? A.keys2[it.base + i] : 0ull;
+            cd[q] = i < n ? (u32)A.codes2[it.base + i] : 0u;
+            if (i < n) {
+                kmn = kr[q] < kmn ? kr[q] : kmn;
+                kmx = kr[q] > kmx ? kr[q] : kmx;
+            }
+        }
+        for (int m2 = 32; m2 >= 1; m2 >>= 1) {
+            const u64 o1 = shfl_xor_u64(kmn, m2), o2 = shfl_xor_u64(kmx, m2);
+            kmn = o1 < kmn ? o1 : kmn;
+            kmx = o2 > kmx ? o2 : kmx;
+        }
+        const u64 range = kmx - kmn;
+        const int bits = range ? 64 - __clzll((long long)range) : 0;
+        const int sh = bits > RSW_LOG2B ? bits - RSW_LOG2B : 0;
+#pragma unroll
+        for (int q = 0; q < BPL; ++q) L.hist[q * 64 + lane] = 0;
+        L.m[lane] = 0;
+        wsync();
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            if (q * 64 + lane < n) {
+                const u32 d = (u32)((kr[q] - kmn) >> sh);
+                atomicAdd(&L.hist[d], 1u);
+                L.rep[d] = kr[q];
+                atomicAdd(&L.m[cd[q]], 1u);
+            }
+        }
+        wsync();
+        // exclusive scan of the bins, BPL consecutive bins per lane
+        {
+            u32 h[BPL], v = 0;
+#pragma unroll
+            for (int q = 0; q < BPL; ++q) {
+                h[q] = L.hist[BPL * lane + q];
+                v += h[q];
+            }
+            u32 incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            u32 b = incl - v;
+#pragma unroll
+            for (int q = 0; q < BPL; ++q) {
+                L.excl[BPL * lane + q] = b;
+                b += h[q];
+            }
+        }
+        wsync();
+        const u32 target = (u32)A.wave_target;
+        int nb;
+        {
+            u32 st[BPL], v = 0;
+#pragma unroll
+            for (int q = 0; q < BPL; ++q) {
+                const int d = BPL * lane + q;
+                const bool fat = L.hist[d] > target;
+                const bool pfat = d > 0 && L.hist[d - 1] > target;
+                st[q] = (d == 0) || fat || pfat || (L.excl[d] / target != L.excl[d - 1] / target);
+                v += st[q];
+            }
+            u32 incl = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const u32 y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            u32 b = incl - v;
+#pragma unroll
+            for (int q = 0; q < BPL; ++q) {
+                const int d = BPL * lane + q;
+                if (st[q]) L.boff[b] = L.excl[d];
+                b += st[q];
+                L.bid[d] = b - 1;
+            }
+            nb = __shfl((int)incl, 63, 64);
+            if (lane == 0) L.boff[nb] = (u32)n;
+        }
+        bool ovf = false;
+        if (nb > id_end - id_cur) {
+            const int grab = max(nb, 2 * chunk);
+            int b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&A.counts[5], grab);
+            b0 = __shfl(b0, 0, 64);
+            ovf = b0 + grab > A.bucket_cap;
+            id_cur = b0;
+            id_end = ovf ? b0 : b0 + grab;
+        }
+        const int bk0 = id_cur;
+        if (!ovf) id_cur += nb;
+        if (ovf) {  // out of bucket ids: rank the parent as one LDS item
+            if (lane == 0) {
+                const int cls = (n <= A.cap_s) ? 0 : ((n <= A.cap_m) ? 1 : 2);
+                A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = it;
+            }
+            continue;
+        }
+        const bool hist_lds = nb * K <= RSW_HCAP;
+        wsync();
+        for (int q = lane; q < nb; q += 64) {
+            L.bcur[q] = L.boff[q];
+            L.bdiff[q] = 0;
+        }
+        if (hist_lds)
+            for (int e = lane; e < nb * K; e += 64) L.hs[e] = 0;
+        wsync();
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+            if (q * 64 + lane < n) {
+                const u32 d = (u32)((kr[q] - kmn) >> sh);
+                const u32 bk = L.bid[d];
+                const u32 pos = atomicAdd(&L.bcur[bk], 1u);
+                A.keys2[it.base + pos] = kr[q];
+                A.codes2[it.base + pos] = (u8)cd[q];
+                if (kr[q] != L.rep[d]) L.bdiff[bk] = 1;
+                if (hist_lds) atomicAdd(&L.hs[bk * K + cd[q]], 1u);
+            }
+        }
+        wsync();
+        if (lane < K) A.hbg[(size_t)it.bucket * K + lane] = L.m[lane];  // the parent's row (gene-level cross)
+        // sub-buckets: one list reservation per parent, slots in sub-bucket order
+        {
+            u32 cw = 0;
+            for (int q = lane; q < nb; q += 64) {
+                const int c = (int)(L.boff[q + 1] - L.boff[q]);
+                cw += (c > 0 && (c <= 64 || !L.bdiff[q])) ? 1u : 0u;
+            }
+            cw = u32_wave_sum(cw);
+            bool to_items = false;
+            if ((int)cw > sl_end - sl_cur) {
+                fill_null(sl_cur, sl_end);
+                const int grab = max((int)cw, chunk);
+                int s0 = 0;
+                if (lane == 0) s0 = atomicAdd(&A.counts[4], grab);
+                s0 = __shfl(s0, 0, 64);
+                if (s0 + grab > A.bucket_cap) {  // list full: these sub-buckets go to the LDS items
+                    fill_null(min(s0, A.bucket_cap), A.bucket_cap);
+                    to_items = true;
+                    sl_cur = sl_end = 0;
+                } else {
+                    sl_cur = s0;
+                    sl_end = s0 + grab;
+                }
+            }
+            u32 o = (u32)sl_cur;
+            if (!to_items) sl_cur += (int)cw;
+            for (int q0 = 0; q0 < nb; q0 += 64) {
+                const int q = q0 + lane;
+                int c = 0;
+                bool tw = false;
+                if (q < nb) {
+                    c = (int)(L.boff[q + 1] - L.boff[q]);
+                    tw = c > 0 && (c <= 64 || !L.bdiff[q]);
+                }
+                if (to_items) tw = false;
+                const u64 bal = __ballot(tw);
+                if (q < nb) {
+                    const int bid = bk0 + q;
+                    if (c <= 0) {
+                        for (int k2 = 0; k2 < K; ++k2) A.hbg[(size_t)bid * K + k2] = 0;
+                    } else {
+                        const bool ties_only = c > 64 && !L.bdiff[q];
+                        const ScRankItem itm{it.base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
+                        if (tw) {
+                            A.sbuckets[o + lanes_below(bal)] = itm;
+                        } else {
+                            const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
+                            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+                        }
+                    }
+                }
+                o += (u32)__popcll(bal);
+            }
+        }
+        if (!hist_lds) {  // many sub-buckets: k_rank_cross_seg adds the in-parent cross term
+            if (lane == 0) A.rsseg[atomicAdd(&A.counts[10], 1)] = int4{g, bk0, nb, 0};
+            continue;
+        }
+        for (int c = lane; c < K; c += 64) {
+            u32 run = 0;
+            for (int q = 0; q < nb; ++q) {
+                L.bs[q * K + c] = run;
+                run += L.hs[q * K + c];
+            }
+        }
+        wsync();
+        const int ntp = min(A.gene_nt[g], 64 * RW_SLOTS_MAX);
+        const u32* tl = A.gene_tp + (size_t)g * A.P;
+        for (int j = lane; j < ntp; j += 64) {
+            const u32 v = tl[j];
+            const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+            if (!L.m[a] || !L.m[b]) continue;
+            u64 sacc = 0;
+            for (int q = 0; q < nb; ++q) sacc += (u64)L.hs[q * K + a] * L.bs[q * K + b];
+            if (sacc) atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
+        }
+        wsync();
+    }
+    fill_null(sl_cur, sl_end);
 }
 
 // ===================================================================== waves
@@ -1479,7 +1737,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 {
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
-    const int cnt = A.counts[4];
+    const int cnt = min(A.counts[4], A.bucket_cap);
     const int K = A.K, G = A.G, P = A.P;
     constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality)
     int cur = -1, ntp = 0;
@@ -1499,7 +1757,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
         if (lane < c1 - c0) D = A.sbuckets[c0 + lane];
         // this launch ranks the buckets of genes with wv_lo < tested pairs <= wv_hi
         // (the slot count of each launch fits its genes: fewer registers, more waves)
-        const int ntg = (lane < c1 - c0) ? A.gene_nt[D.gene] : -1;
+        const int ntg = (lane < c1 - c0 && D.n > 0) ? A.gene_nt[D.gene] : -1;  // n = 0: an unused re-split slot
         u64 rem = __ballot(ntg > A.wv_lo && ntg <= A.wv_hi);
         if (!rem) continue;
         const u32 dlo = (u32)(u64)D.base, dhi = (u32)((u64)D.base >> 32);
@@ -1805,6 +2063,12 @@ extern "C" hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid,
 extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st)
 {
     if (!L->fatbk || grid <= 0) return hipSuccess;
+    // wave-private allocation chunks sized so that the unused tails of all
+    // waves stay a small part of the bucket capacity
+    ScRankLaunch W = *L;
+    const long long waves = 2LL * grid * 4;
+    W.rsw_chunk = (int)std::max(8LL, std::min(128LL, (long long)L->bucket_cap / (16 * waves)));
+    hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
     hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), 0, st, *L);
     return hipGetLastError();
 }

@@ -304,7 +304,7 @@ def test_rank_size_classes(eng, cfg_a, caps, monkeypatch):
     _fast_compare(eng, ds, X, code, len(names))
 
 
-def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6):
+def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6, frac=0.9):
     """Genes whose nonzeros crowd a narrow stretch of the value axis (relative
     width 1e-7) next to a few large outliers: the split's 2048-bin window puts
     the whole stretch in one bin of > 64 distinct values, which k_rank_resplit
@@ -314,7 +314,7 @@ def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6):
     names = np.array(synth.label_names(K), dtype=object)
     X = np.zeros((G, N))
     for g in range(G):
-        m = rng.random(N) < 0.9
+        m = rng.random(N) < frac
         v = 1.0 + rng.random(N) * 1e-7 * (1 + g % 5) + lab * 2e-8 * (g % 3)
         if g % 4 == 3:
             v = np.round(v, 9)
@@ -324,12 +324,14 @@ def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6):
     return synth.from_dense(X, names[lab]), X
 
 
+@pytest.mark.parametrize("frac", [0.9, 0.07])
 @pytest.mark.parametrize("resplit", ["1", "0"])
-def test_resplit_dense_value_stretch(eng, resplit, monkeypatch):
+def test_resplit_dense_value_stretch(eng, resplit, frac, monkeypatch):
     """Exact U / ties with and without the re-split route (SCC_RESPLIT=0: the
-    fat buckets go to the LDS items as before)."""
+    fat buckets go to the LDS items as before); stretches of ~2700 elements
+    (workgroup re-split) and ~210 (one wave per parent)."""
     monkeypatch.setenv("SCC_RESPLIT", resplit)
-    d, X = _dense_stretch_matrix()
+    d, X = _dense_stretch_matrix(frac=frac)
     names, code = api.select_clusters(d.labels, 10)
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     _slow_compare(eng, ds, X, code, len(names))
