@@ -68,7 +68,8 @@ struct ScRankLaunch {
     int4* fatg;            // [G] {gene, first fatbk entry, parents}: the re-split work units
     int4* rsseg;           // [fat_cap] {gene, first sub-bucket id, sub-buckets}: in-parent cross terms
     int fat_cap;
-    int rsw_chunk;         // wave re-split: bucket ids / list slots taken per global atomic
+    int rsw_chunk;
+    int cross_wave;        // 1: gene-level cross terms by the per-(gene, pair) wave kernel         // wave re-split: bucket ids / list slots taken per global atomic
     int* split_genes;      // [G]
     unsigned long long* keys2;  // [nnz] bucket-ordered keys of split genes
     uint8_t* codes2;            // [nnz]

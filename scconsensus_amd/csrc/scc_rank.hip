@@ -1980,6 +1980,83 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
     }
 }
 
+// Gene-level cross terms, one workgroup per split gene:
+//   S_ab += sum_q H[q][a] * C[q][b],  C[q][b] = #(b-elements in buckets < q)
+// over the gene's buckets q in value order.  The gene's histogram rows are
+// read once, 64 buckets at a time, into LDS (coalesced: rows are [bucket][K]),
+// C comes from a column scan with a carry, and each thread accumulates its
+// tested pairs (<= XC_J per thread) in registers: one atomic per (gene, pair).
+// (The per-(gene, pair) wave version re-read the rows once per pair.)
+#define XC_T 256
+#define XC_Q 64
+#define XC_J 8  // tested pairs per thread: <= 2048 per gene (K <= 64: P <= 2016)
+__global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
+{
+    __shared__ u32 Hs[XC_Q][65];
+    __shared__ u32 Cs[XC_Q][65];
+    __shared__ u32 seg[4][64];
+    __shared__ u32 carry[64];
+    const int tid = threadIdx.x, K = A.K, G = A.G, P = A.P;
+    const int ng = A.counts[3];
+    for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
+        const int g = A.split_genes[gi];
+        const int bk0 = A.gene_bk[2 * g], nb = A.gene_bk[2 * g + 1];
+        const int ntp = min(A.gene_nt[g], P);
+        const u32* tl = A.gene_tp + (size_t)g * P;
+        u32 pv[XC_J];
+        u64 acc[XC_J];
+#pragma unroll
+        for (int u = 0; u < XC_J; ++u) {
+            const int j = u * XC_T + tid;
+            pv[u] = j < ntp ? tl[j] : 0u;
+            acc[u] = 0;
+        }
+        if (tid < 64) carry[tid] = 0;
+        for (int q0 = 0; q0 < nb; q0 += XC_Q) {
+            const int nq = min(XC_Q, nb - q0);
+            __syncthreads();
+            const unsigned int* h = A.hbg + (size_t)(bk0 + q0) * K;
+            for (int e = tid; e < XC_Q * K; e += XC_T) {
+                const int q = e / K, c = e - q * K;
+                Hs[q][c] = q < nq ? h[e] : 0u;
+            }
+            __syncthreads();
+            // column scan: thread (c, part) sums 16 rows, parts combined through LDS
+            const int c = tid & 63, part = tid >> 6;
+            u32 ssum = 0;
+            if (c < K)
+                for (int q = part * 16; q < part * 16 + 16; ++q) ssum += Hs[q][c];
+            seg[part][c] = ssum;
+            __syncthreads();
+            if (c < K) {
+                u32 run = carry[c];
+                for (int v = 0; v < part; ++v) run += seg[v][c];
+                for (int q = part * 16; q < part * 16 + 16; ++q) {
+                    Cs[q][c] = run;
+                    run += Hs[q][c];
+                }
+            }
+            __syncthreads();
+            if (tid < K) carry[tid] += seg[0][tid] + seg[1][tid] + seg[2][tid] + seg[3][tid];
+#pragma unroll
+            for (int u = 0; u < XC_J; ++u) {
+                if (u * XC_T + tid < ntp) {
+                    const int a = (int)((pv[u] >> 16) & 0xffu), b = (int)(pv[u] >> 24);
+                    u64 sacc = 0;
+                    for (int q = 0; q < nq; ++q) sacc += (u64)Hs[q][a] * Cs[q][b];
+                    acc[u] += sacc;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < XC_J; ++u) {
+            if (u * XC_T + tid < ntp && acc[u])
+                atomicAdd((unsigned long long*)&A.accS[(size_t)(pv[u] & 0xffffu) * G + g], (unsigned long long)acc[u]);
+        }
+        __syncthreads();
+    }
+}
+
 // ===================================================================== host
 template <int W>
 static size_t item_lds_fixed(int ntp_max, int K)
@@ -2049,7 +2126,10 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
 
 extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_rank_cross<false>, dim3(grid), dim3(256), 0, st, *L);
+    if (L->P <= XC_J * XC_T && !L->cross_wave)
+        hipLaunchKernelGGL(k_rank_cross_gene, dim3(grid), dim3(XC_T), 0, st, *L);
+    else  // one wave per (gene, pair) (SCC_CROSS_WAVE=1 selects it for comparisons)
+        hipLaunchKernelGGL(k_rank_cross<false>, dim3(grid), dim3(256), 0, st, *L);
     return hipGetLastError();
 }
 

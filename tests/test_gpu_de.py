@@ -325,12 +325,13 @@ def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6, frac=0.9):
 
 
 @pytest.mark.parametrize("frac", [0.9, 0.07])
-@pytest.mark.parametrize("resplit", ["1", "0"])
-def test_resplit_dense_value_stretch(eng, resplit, frac, monkeypatch):
+@pytest.mark.parametrize("resplit,cross_wave", [("1", "0"), ("0", "0"), ("1", "1")])
+def test_resplit_dense_value_stretch(eng, resplit, cross_wave, frac, monkeypatch):
     """Exact U / ties with and without the re-split route (SCC_RESPLIT=0: the
     fat buckets go to the LDS items as before); stretches of ~2700 elements
     (workgroup re-split) and ~210 (one wave per parent)."""
     monkeypatch.setenv("SCC_RESPLIT", resplit)
+    monkeypatch.setenv("SCC_CROSS_WAVE", cross_wave)
     d, X = _dense_stretch_matrix(frac=frac)
     names, code = api.select_clusters(d.labels, 10)
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)

@@ -31,9 +31,12 @@ def test_config_d_rows_sampled_parity(monkeypatch):
     assert np.all(r.u2 >= 0) and np.all(r.u2 <= 2 * nn[r.row_pair])
     assert 100 < len(g.union) <= 30 * len(pairs)
     # the same DE with the re-split route off (fat buckets ranked as LDS items)
+    # and the gene-level cross terms by the per-(gene, pair) wave kernel
     monkeypatch.setenv("SCC_RESPLIT", "0")
+    monkeypatch.setenv("SCC_CROSS_WAVE", "1")
     g0 = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows")
     monkeypatch.delenv("SCC_RESPLIT")
+    monkeypatch.delenv("SCC_CROSS_WAVE")
     np.testing.assert_array_equal(g0.rows.gene, r.gene)
     np.testing.assert_array_equal(g0.rows.u2, r.u2)
     np.testing.assert_array_equal(g0.rows.ties, r.ties)
