@@ -58,6 +58,8 @@ struct scc_ctx {
     std::map<std::string, scc_rt::Timer> timers;
     uint64_t generation = 0;
     std::vector<int> host_tables;  // cell permutation + chunk tables of the last scc_de_run
+    int* h_stage = nullptr;        // pinned: the DE result header, tested counts and union, one D2H
+    size_t h_stage_n = 0;
     // last PCA
     const double* d_last_scores = nullptr;  // N x 16 in the workspace
     int last_n = 0;

@@ -8,6 +8,8 @@
 // device every entry point returns SCC_ERR_HIP.
 #include "scc_internal.hpp"
 
+#include <cstring>
+
 using namespace scc_rt;
 
 // ====================================================================== ctx
@@ -58,6 +60,7 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
         hipEventDestroy(pe.b);
     }
     for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->h_stage) hipHostFree(c->h_stage);
     hipEventDestroy(c->ev_fork);
     hipEventDestroy(c->ev_join);
     hipStreamDestroy(c->s0);
@@ -789,10 +792,31 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_pair_select(&S, s0));
         HIPCHK(c, scc_launch_union(d_first, G, d_key, env_int("SCC_UNION_CAP", kUnionCap), d_union, d_nu, s0));
     }
-    int hdr[2] = {0, 0};
-    HIPCHK(c, hipMemcpyAsync(&hdr[0], d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
-    HIPCHK(c, hipMemcpyAsync(&hdr[1], d_err, sizeof(int), hipMemcpyDeviceToHost, s0));
+    // one pinned staging buffer, one synchronisation: [0] |U|, [1] error bits,
+    // [2..3] FAST row count (i64), [4, 4 + P) tested rows per pair, then the
+    // union (up to G entries)
+    const size_t stage_n = 4 + (size_t)P + (size_t)G;
+    if (c->h_stage_n < stage_n) {
+        if (c->h_stage) hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_n = 0;
+        if (hipHostMalloc((void**)&c->h_stage, sizeof(int) * stage_n, hipHostMallocDefault) != hipSuccess) {
+            hipGetLastError();
+            c->h_stage = nullptr;
+            return fail(c, SCC_ERR_OOM, "pinned staging allocation failed");
+        }
+        c->h_stage_n = stage_n;
+    }
+    int* hs = c->h_stage;
+    HIPCHK(c, hipMemcpyAsync(&hs[0], d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
+    HIPCHK(c, hipMemcpyAsync(&hs[1], d_err, sizeof(int), hipMemcpyDeviceToHost, s0));
+    if (fast) {
+        HIPCHK(c, hipMemcpyAsync(&hs[2], d_rowoff + P, sizeof(long long), hipMemcpyDeviceToHost, s0));
+        HIPCHK(c, hipMemcpyAsync(&hs[4], d_tested, sizeof(int) * P, hipMemcpyDeviceToHost, s0));
+    }
+    HIPCHK(c, hipMemcpyAsync(&hs[4 + P], d_union, sizeof(int) * G, hipMemcpyDeviceToHost, s0));
     HIPCHK(c, hipStreamSynchronize(s0));
+    const int hdr[2] = {hs[0], hs[1]};
     if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
     if (hdr[1] & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
@@ -806,14 +830,12 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     r->G = G;
     r->N = N;
     r->log_thr = log_thr;
-    r->union_genes.resize(hdr[0]);
-    if (hdr[0] > 0)
-        HIPCHK(c, hipMemcpy(r->union_genes.data(), d_union, sizeof(int) * hdr[0], hipMemcpyDeviceToHost));
+    if (hdr[0] < 0 || hdr[0] > G) return fail(c, SCC_ERR_HIP, "union size out of range");
+    r->union_genes.assign(hs + 4 + P, hs + 4 + P + hdr[0]);
     if (fast) {
-        r->pair_tested.resize(P);
         long long nrows = 0;
-        HIPCHK(c, hipMemcpy(r->pair_tested.data(), d_tested, sizeof(int) * P, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(&nrows, d_rowoff + P, sizeof(long long), hipMemcpyDeviceToHost));
+        std::memcpy(&nrows, &hs[2], sizeof(long long));
+        r->pair_tested.assign(hs + 4, hs + 4 + P);
         r->n_rows = nrows;
     }
     r->d_nodg = d_nodg;
