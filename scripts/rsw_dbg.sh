@@ -1,4 +1,6 @@
-# re-split timing experiments at config D (SCC_RW_DEBUG 11..15 cut the wave re-split short; results invalid)
+# re-split timing experiments at config D, as run for DESIGN §3.1 (SCC_RW_DEBUG 11..15 cut the wave
+# re-split short after each phase; results invalid).  The cut points were removed from the kernel
+# after the measurement: re-add them before running this again.
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for m in 0 11 12 13 14 15; do
