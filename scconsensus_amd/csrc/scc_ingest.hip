@@ -160,9 +160,14 @@ __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int
     const int g = blockIdx.y * 256 + threadIdx.x;
     if (g >= G) return;
     const int w0 = blockIdx.x * CS_SEG;
-    if (w0 >= nc_kept) {  // unkept chunks (and the totals row nc) add nothing
+    // Unkept chunks add nothing.  Of their rows only nc_kept (the end offset of
+    // the last kept cluster, cl_cc[K]) and the totals row nc are ever read, so
+    // only those two are written (at 1M cells with half the cells unkept the
+    // rest would be > 1 GB of dead stores per run).
+    if (w0 >= nc_kept) {
         const u32 tot = total[g];
-        for (int w = w0; w < min(nc + 1, w0 + CS_SEG); ++w) cnt[(size_t)w * G + g] = tot;
+        if (nc_kept >= w0 && nc_kept < w0 + CS_SEG) cnt[(size_t)nc_kept * G + g] = tot;
+        if (nc != nc_kept && nc >= w0 && nc < w0 + CS_SEG) cnt[(size_t)nc * G + g] = tot;
         return;
     }
     u32 run = part[(size_t)blockIdx.x * G + g];
@@ -174,7 +179,8 @@ __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int
     }
     if (w1 == nc_kept) {
         const u32 tot = total[g];
-        for (int w = w1; w < min(nc + 1, w0 + CS_SEG); ++w) cnt[(size_t)w * G + g] = tot;
+        if (nc_kept < w0 + CS_SEG) cnt[(size_t)nc_kept * G + g] = tot;
+        if (nc != nc_kept && nc < w0 + CS_SEG) cnt[(size_t)nc * G + g] = tot;
     }
 }
 
