@@ -1735,6 +1735,7 @@ __device__ inline void bitonic_merge(u64& key, u32& code, bool up, int lane)
 template <int RW_SLOTS>
 __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 {
+    __shared__ u64 cms[4][64];  // per-wave cluster masks (K > 16)
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
     const int cnt = min(A.counts[4], A.bucket_cap);
@@ -1880,9 +1881,19 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             }
             // ---- cluster masks over the sorted lanes (lane c holds cluster c's) and the hbg row
             u64 cm = 0;
-            for (int c = 0; c < K; ++c) {
-                const u64 m = __ballot(code == (u32)c);
-                if (lane == c) cm = m;
+            if (K <= 16) {  // one ballot per cluster
+                for (int c = 0; c < K; ++c) {
+                    const u64 m = __ballot(code == (u32)c);
+                    if (lane == c) cm = m;
+                }
+            } else {  // many clusters: 6 ballots match equal codes, each cluster's leader posts its mask
+                const u64 peers = match_bits<6>(code & 63u, __ballot(vl));
+                cms[wv][lane] = 0;
+                wsync();
+                if (vl && lanes_below(peers) == 0) cms[wv][code] = peers;
+                wsync();
+                cm = cms[wv][lane];
+                wsync();
             }
             if (lane < K) A.hbg[(size_t)bucket * K + lane] = (u32)__popcll(cm);
             // ---- tie groups (equal keys) and runs (equal key and cluster)
