@@ -823,6 +823,7 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 }
 
 #define RW_SLOTS_MAX 16  // tested pairs per gene the wave kernel holds: 64 * slots (2, 4, 8 or 16)
+#define RW_PAIRS_MAX (2 * 64 * RW_SLOTS_MAX)  // genes past 1024 tested pairs: two 16-slot passes
 #define RS_T 256          // re-split: threads per workgroup
 #define RS_KPT 8          // keys per thread (held in registers: the scatter is in place)
 #define RS_CAP (RS_T * RS_KPT)
@@ -894,7 +895,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         __syncthreads();
     }
     if (tid == 0) A.gene_nt[g] = (int)ntested;
-    const bool waves_ok = ntested <= 64u * (u32)A.rw_slots;
+    const bool waves_ok = ntested <= (A.rw_slots >= RW_SLOTS_MAX ? (u32)RW_PAIRS_MAX : 64u * (u32)A.rw_slots);
     // the gene's keys stay in registers when they fit (SP_KPT per thread);
     // larger genes re-read each chunk in every pass (from L2)
     u64 kr[SP_KPT];
@@ -1127,7 +1128,7 @@ struct ResplitLds {
     u64 rmn[RS_T / 64], rmx[RS_T / 64];
     u32 hs[RS_HCAP];  // [sub-bucket][cluster] counts (in-parent cross term), when nb * K fits
     u32 bs[RS_HCAP];  // [sub-bucket][cluster] elements of the cluster in lower sub-buckets
-    u64 acc[64 * RW_SLOTS_MAX];  // the gene's in-parent cross terms per tested pair
+    u64 acc[RW_PAIRS_MAX];  // the gene's in-parent cross terms per tested pair
     int nb, bk0, next, ovf, nw, w0;
 };
 
@@ -1353,7 +1354,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         }
     }
     __syncthreads();
-    const int ntp = min(A.gene_nt[g], 64 * RW_SLOTS_MAX);
+    const int ntp = min(A.gene_nt[g], RW_PAIRS_MAX);
     for (int j = tid; j < ntp; j += RS_T) {
         const u32 v = A.gene_tp[(size_t)g * A.P + j];
         const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
@@ -1379,7 +1380,7 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
         if (i >= ng) break;
         const int4 ge = A.fatg[i];
         const int g = ge.x;
-        const int ntp = min(A.gene_nt[g], 64 * RW_SLOTS_MAX);
+        const int ntp = min(A.gene_nt[g], RW_PAIRS_MAX);
         for (int j = threadIdx.x; j < ntp; j += RS_T) L.acc[j] = 0;
         __syncthreads();
         for (int f = ge.y; f < ge.y + ge.z; ++f) {
@@ -1635,7 +1636,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
             }
         }
         wsync();
-        const int ntp = min(A.gene_nt[g], 64 * RW_SLOTS_MAX);
+        const int ntp = min(A.gene_nt[g], RW_PAIRS_MAX);
         const u32* tl = A.gene_tp + (size_t)g * A.P;
         for (int j = lane; j < ntp; j += 64) {
             const u32 v = tl[j];
@@ -1809,8 +1810,10 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 cur = g;
                 gk = A.gkmin[g];
                 // tested pairs of g in pair order (compacted by the split)
-                ntp = min(A.gene_nt[g], 64 * RW_SLOTS);  // the host never routes genes with more here
-                const u32* tl = A.gene_tp + (size_t)g * P;
+                // this launch's window of the gene's tested pairs (wv_base > 0: the
+                // second pass over a gene with more than 64 * RW_SLOTS of them)
+                ntp = max(0, min(A.gene_nt[g] - A.wv_base, 64 * RW_SLOTS));
+                const u32* tl = A.gene_tp + (size_t)g * P + A.wv_base;
 #pragma unroll
                 for (int q = 0; q < RW_SLOTS; ++q) {
                     const int j = q * 64 + lane;
@@ -1843,7 +1846,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 }
                 if (lane < K) {
                     A.hbg[(size_t)bucket * K + lane] = myc;
-                    if (myc >= 2)
+                    if (myc >= 2 && A.wv_base == 0)  // per cluster: once, not per pair window
                         atomicAdd((unsigned long long*)&A.accF[(size_t)lane * G + g], (unsigned long long)f_tie(myc));
                 }
 #pragma unroll
@@ -1913,7 +1916,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                     const u64 raft = rst & ~le;
                     const int re = raft ? __builtin_ctzll(raft) : n;
                     const u64 len = (u64)(re - lane);
-                    if (len >= 2)
+                    if (len >= 2 && A.wv_base == 0)
                         atomicAdd((unsigned long long*)&A.accF[(size_t)code * G + g], (unsigned long long)f_tie(len));
                 }
             }
@@ -2116,18 +2119,21 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
     // one launch per slot class present: genes with <= 128 tested pairs on the
     // 2-slot kernel, <= 256 on 4, <= 512 on 8, <= 1024 on 16
     ScRankLaunch A = *L;
-    const int hi[4] = {128, 256, 512, 1024};
-    for (int c = 0; c < 4; ++c) {
-        if (64 * L->rw_slots < hi[c] && c > 0) break;
-        A.wv_lo = c ? hi[c - 1] : -1;
+    const int hi[6] = {128, 256, 512, 1024, RW_PAIRS_MAX, RW_PAIRS_MAX};
+    for (int c = 0; c < 6; ++c) {
+        if (64 * L->rw_slots < hi[c] && c > 0 && c < 4) break;
+        if (c >= 4 && L->rw_slots < RW_SLOTS_MAX) break;
+        // classes 4 and 5: genes with 1024 < tested pairs <= 2048, pairs [0, 1024) then [1024, 2048)
+        A.wv_lo = c ? hi[min(c, 4) - 1] : -1;
         A.wv_hi = hi[c];
+        A.wv_base = c == 5 ? 64 * RW_SLOTS_MAX : 0;
         if (c == 0)
             hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, A);
         else if (c == 1)
             hipLaunchKernelGGL(k_rank_waves<4>, dim3(grid), dim3(256), 0, st, A);
         else if (c == 2)
             hipLaunchKernelGGL(k_rank_waves<8>, dim3(grid), dim3(256), 0, st, A);
-        else
+        else  // c >= 3
             hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, A);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
