@@ -316,31 +316,33 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
                 }
             }
         };
-        for (int cb = 4 * wv; cb < ncell; cb += 4 * (ING_T / 64)) {
+        // lanes over the tile's entries as one flat range (entry e of the tile is
+        // entry e - cof[c] of cell c, found by a binary search of cof): every
+        // lane loads, however few entries a cell has in the tile (~8 at 1M-cell
+        // density; a lane per cell entry left most lanes idle)
+        for (u32 e0 = (u32)wv * 256; e0 < E; e0 += 4 * ING_T) {
             double x[4];
             int gq[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int c = cb + u;
+                const u32 e = e0 + (u32)(u * 64 + lane);
                 x[u] = 0.0;
                 gq[u] = -1;
-                if (c < ncell && (u32)lane < cof[c + 1] - cof[c]) {
-                    const i64 k = ckb[c] + lane;
+                if (e < E) {
+                    int lo = 0, hi = ncell;  // last cell c with cof[c] <= e
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (cof[mid] <= e) lo = mid;
+                        else hi = mid;
+                    }
+                    const u32 j = e - cof[lo];
+                    const i64 k = ckb[lo] + j;
                     x[u] = vals[k];
-                    gq[u] = DENSE ? lane : rows[k] - g0;
+                    gq[u] = DENSE ? (int)j : rows[k] - g0;
                 }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) put(x[u], gq[u]);
-            for (int u = 0; u < 4; ++u) {  // cells with more than 64 entries in the tile
-                const int c = cb + u;
-                if (c >= ncell) break;
-                const u32 len = cof[c + 1] - cof[c];
-                for (u32 j = 64 + lane; j < len; j += 64) {
-                    const i64 k = ckb[c] + j;
-                    put(vals[k], DENSE ? (int)j : rows[k] - g0);
-                }
-            }
         }
         __syncthreads();
         const int Er = (int)(loff[r1] - base);
