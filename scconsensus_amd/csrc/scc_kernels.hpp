@@ -60,7 +60,8 @@ struct ScRankLaunch {
     unsigned long long* gkmin;  // [G] key minimum of a split gene when its range fits 58 bits, else ~0
     ScRankItem* items;     // [3][item_cap]
     int* counts;           // [0..2] items per class, [3] split genes, [4] wave buckets, [5] bucket ids,
-                           // [8] fat buckets, [9] re-split queue, [10] re-split segments, [11] re-split genes
+                           // [8] fat buckets, [9] re-split queue, [10] re-split segments, [11] re-split genes,
+                           // [12] second-level re-split parents
     uint32_t* gene_tp;     // [G][P] tested pairs of each split gene, p | a << 16 | b << 24 (pair order)
     int* gene_nt;          // [G] their number
     int wv_lo, wv_hi;      // wave kernel launch: genes with wv_lo < tested pairs <= wv_hi
@@ -69,8 +70,11 @@ struct ScRankLaunch {
     int4* fatg;            // [G] {gene, first fatbk entry, parents}: the re-split work units
     int4* rsseg;           // [fat_cap] {gene, first sub-bucket id, sub-buckets}: in-parent cross terms
     int fat_cap;
-    int rsw_chunk;
-    int cross_wave;        // 1: gene-level cross terms by the per-(gene, pair) wave kernel         // wave re-split: bucket ids / list slots taken per global atomic
+    int rsw_chunk;         // wave re-split: bucket ids / list slots taken per global atomic
+    ScRankItem* fat2;      // [fat2_cap] second re-split level (counts[12])
+    int fat2_cap;
+    int rs_level;          // wave re-split launch: 0 reads fatbk, 1 reads fat2
+    int cross_wave;        // 1: gene-level cross terms by the per-(gene, pair) wave kernel
     int* split_genes;      // [G]
     unsigned long long* keys2;  // [nnz] bucket-ordered keys of split genes
     uint8_t* codes2;            // [nnz]

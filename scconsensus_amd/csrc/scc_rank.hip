@@ -1132,6 +1132,16 @@ struct ResplitLds {
     int nb, bk0, next, ovf, nw, w0;
 };
 
+// A sub-bucket that still holds > 64 distinct values goes to the second
+// re-split level (k_rank_resplit_w with rs_level 1) while its list has room.
+__device__ inline bool push_fat2(const ScRankLaunch& A, const ScRankItem& itm)
+{
+    const int f = atomicAdd(&A.counts[12], 1);
+    if (f >= A.fat2_cap) return false;
+    A.fat2[f] = itm;
+    return true;
+}
+
 __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitLds& L)
 {
     constexpr int W = RS_T / 64, BPT = RS_BINS / RS_T;
@@ -1328,6 +1338,8 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
                     const ScRankItem itm{it.base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
                     if (wv[r]) {
                         A.sbuckets[ow + lanes_below(bal)] = itm;
+                    } else if (A.fat2 && c <= RSW_CAP && push_fat2(A, itm)) {
+                        // still > 64 distinct values: a second re-split level
                     } else {
                         const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
                         A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
@@ -1428,7 +1440,8 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     ResplitWLds& L = Ls[wv];
     const int K = A.K;
-    const int cnt = min(A.counts[8], A.fat_cap);
+    const ScRankItem* list = A.rs_level ? A.fat2 : A.fatbk;
+    const int cnt = A.rs_level ? min(A.counts[12], A.fat2_cap) : min(A.counts[8], A.fat_cap);
     constexpr int EPL = RSW_CAP / 64, BPL = RSW_BINS / 64;
     // Bucket ids and wave-list slots come from wave-private chunks: one global
     // atomic per chunk, not per parent (same-address atomics serialise in L2:
@@ -1441,7 +1454,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
         for (int q = a + lane; q < b; q += 64) A.sbuckets[q] = nullit;
     };
     for (int f = blockIdx.x * 4 + wv; f < cnt; f += gridDim.x * 4) {
-        const ScRankItem it = A.fatbk[f];
+        const ScRankItem it = list[f];
         const int n = it.n, g = it.gene;
         if (n > RSW_CAP) continue;  // k_rank_resplit (a workgroup per parent)
         u64 kr[EPL];
@@ -1615,6 +1628,8 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
                         const ScRankItem itm{it.base + L.boff[q], c, g, ties_only ? 2 : 1, bid};
                         if (tw) {
                             A.sbuckets[o + lanes_below(bal)] = itm;
+                        } else if (A.rs_level == 0 && A.fat2 && push_fat2(A, itm)) {
+                            // still > 64 distinct values: a second re-split level
                         } else {
                             const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
                             A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
@@ -2165,8 +2180,13 @@ extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, h
     ScRankLaunch W = *L;
     const long long waves = 2LL * grid * 4;
     W.rsw_chunk = (int)std::max(8LL, std::min(128LL, (long long)L->bucket_cap / (16 * waves)));
+    W.rs_level = 0;
     hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
     hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), 0, st, *L);
+    if (L->fat2) {  // sub-buckets the first level left with > 64 distinct values
+        W.rs_level = 1;
+        hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
+    }
     return hipGetLastError();
 }
 

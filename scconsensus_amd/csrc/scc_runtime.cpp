@@ -628,6 +628,8 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             WS("fatbk", (size_t)L.fat_cap, L.fatbk);
             WS("rsseg", (size_t)L.fat_cap, L.rsseg);
             WS("fatg", (size_t)G, L.fatg);
+            L.fat2_cap = L.fat_cap;
+            WS("fat2", (size_t)L.fat2_cap, L.fat2);
         }
         unsigned long long* st_buf = nullptr;
         const bool stamps = env_int("SCC_STAMPS", 0) != 0;

@@ -304,7 +304,7 @@ def test_rank_size_classes(eng, cfg_a, caps, monkeypatch):
     _fast_compare(eng, ds, X, code, len(names))
 
 
-def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6, frac=0.9):
+def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6, frac=0.9, nested=0):
     """Genes whose nonzeros crowd a narrow stretch of the value axis (relative
     width 1e-7) next to a few large outliers: the split's 2048-bin window puts
     the whole stretch in one bin of > 64 distinct values, which k_rank_resplit
@@ -319,6 +319,9 @@ def _dense_stretch_matrix(seed=21, G=40, N=3000, K=6, frac=0.9):
         if g % 4 == 3:
             v = np.round(v, 9)
         X[g, m] = v[m]
+        if nested:  # a tighter stretch inside the stretch: one re-split bin of > 64 distinct values
+            idx = rng.choice(N, nested, replace=False)
+            X[g, idx] = 1.0 + 5e-8 + rng.permutation(nested) * 1e-15 * (1 + g % 3)
         out = rng.random(N) < 0.01
         X[g, out] = 50.0 + rng.random(out.sum())
     return synth.from_dense(X, names[lab]), X
@@ -337,3 +340,16 @@ def test_resplit_dense_value_stretch(eng, resplit, cross_wave, frac, monkeypatch
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     _slow_compare(eng, ds, X, code, len(names))
     _fast_compare(eng, ds, X, code, len(names), min_per_cent=5.0, log_fc_thrs=0.0)
+
+
+@pytest.mark.parametrize("frac", [0.02, 0.07])
+def test_resplit_second_level(eng, frac):
+    """A sub-bucket of the first re-split that still holds > 64 distinct values
+    goes to the second re-split level (from the wave re-split at ~210 elements
+    per stretch, from the workgroup re-split at ~360)."""
+    d, X = _dense_stretch_matrix(frac=frac, nested=150)
+    names, code = api.select_clusters(d.labels, 10)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    _slow_compare(eng, ds, X, code, len(names))
+    _fast_compare(eng, ds, X, code, len(names), min_per_cent=1.0, log_fc_thrs=0.0)
+
