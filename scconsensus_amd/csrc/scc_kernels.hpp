@@ -66,6 +66,7 @@ struct ScRankLaunch {
     int* gene_nt;          // [G] their number
     int wv_lo, wv_hi;      // wave kernel launch: genes with wv_lo < tested pairs <= wv_hi
     int wv_base;           // ... and their tested pairs [wv_base, wv_base + 64 * slots)
+    int wv_filter;         // 0: one launch holds every gene (no per-bucket class test)
     ScRankItem* fatbk;     // [fat_cap] buckets of > 64 distinct values (re-split into sub-buckets)
     int4* fatg;            // [G] {gene, first fatbk entry, parents}: the re-split work units
     int4* rsseg;           // [fat_cap] {gene, first sub-bucket id, sub-buckets}: in-parent cross terms

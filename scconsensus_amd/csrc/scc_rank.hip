@@ -1774,8 +1774,14 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
         if (lane < c1 - c0) D = A.sbuckets[c0 + lane];
         // this launch ranks the buckets of genes with wv_lo < tested pairs <= wv_hi
         // (the slot count of each launch fits its genes: fewer registers, more waves)
-        const int ntg = (lane < c1 - c0 && D.n > 0) ? A.gene_nt[D.gene] : -1;  // n = 0: an unused re-split slot
-        u64 rem = __ballot(ntg > A.wv_lo && ntg <= A.wv_hi);
+        // (one class launched: no filter, and no dependent load before the first bucket)
+        u64 rem;
+        if (A.wv_filter) {
+            const int ntg = (lane < c1 - c0 && D.n > 0) ? A.gene_nt[D.gene] : -1;  // n = 0: an unused re-split slot
+            rem = __ballot(ntg > A.wv_lo && ntg <= A.wv_hi);
+        } else {
+            rem = __ballot(lane < c1 - c0 && D.n > 0);
+        }
         if (!rem) continue;
         const u32 dlo = (u32)(u64)D.base, dhi = (u32)((u64)D.base >> 32);
         auto dbase = [&](int li) {
@@ -2142,6 +2148,7 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
         A.wv_lo = c ? hi[min(c, 4) - 1] : -1;
         A.wv_hi = hi[c];
         A.wv_base = c == 5 ? 64 * RW_SLOTS_MAX : 0;
+        A.wv_filter = L->rw_slots > 2 ? 1 : 0;  // rw_slots 2: class 0 is the only launch and holds every gene
         if (c == 0)
             hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, A);
         else if (c == 1)
@@ -2158,7 +2165,9 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
 
 extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hipStream_t st)
 {
-    if (L->P <= XC_J * XC_T && !L->cross_wave)
+    // per-gene workgroups pay off once genes have many tested pairs (at P = 66 the
+    // per-(gene, pair) waves are 12 us faster; at P >= 435 the gene kernel wins)
+    if (L->P > 128 && L->P <= XC_J * XC_T && !L->cross_wave)
         hipLaunchKernelGGL(k_rank_cross_gene, dim3(grid), dim3(XC_T), 0, st, *L);
     else  // one wave per (gene, pair) (SCC_CROSS_WAVE=1 selects it for comparisons)
         hipLaunchKernelGGL(k_rank_cross<false>, dim3(grid), dim3(256), 0, st, *L);

@@ -660,15 +660,22 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         } else {
             HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0));
         }
-        // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS items)
-        HIPCHK(c, hipEventRecord(c->ev_fork, s0));
-        HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
+        // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS
+        // items; SCC_ITEMS_SERIAL=1 runs them after the waves on one stream)
+        const bool items_serial = env_int("SCC_ITEMS_SERIAL", 0) != 0;
+        hipStream_t si = items_serial ? s0 : s1;
+        if (!items_serial) {
+            HIPCHK(c, hipEventRecord(c->ev_fork, s0));
+            HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
+        }
         HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0));
-        HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, s1));
-        HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, s1));
-        HIPCHK(c, scc_launch_rank_items(&L, 2, ncu, s1));
-        HIPCHK(c, hipEventRecord(c->ev_join, s1));
-        HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
+        HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, si));
+        HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, si));
+        HIPCHK(c, scc_launch_rank_items(&L, 2, ncu, si));
+        if (!items_serial) {
+            HIPCHK(c, hipEventRecord(c->ev_join, s1));
+            HIPCHK(c, hipStreamWaitEvent(s0, c->ev_join, 0));
+        }
         HIPCHK(c, scc_launch_rank_cross(&L, 4 * ncu, s0));
         HIPCHK(c, scc_launch_rank_cross_seg(&L, 4 * ncu, s0));
         if (stamps) {
