@@ -406,19 +406,27 @@ struct SelectArgs {
 template <int T>
 __device__ int block_excl_scan(int v, int* s, int& total)
 {
-    const int tid = threadIdx.x;
-    s[tid] = v;
-    __syncthreads();
-    for (int o = 1; o < T; o <<= 1) {
-        const int t = (tid >= o) ? s[tid - o] : 0;
-        __syncthreads();
-        s[tid] += t;
-        __syncthreads();
+    // wave scans (shuffles) + one exchange of the wave totals: 2 barriers
+    // (the Hillis-Steele form took 2 log2 T)
+    constexpr int W = T / 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
     }
-    total = s[T - 1];
-    const int ex = s[tid] - v;
+    if (lane == 63) s[w] = inc;
     __syncthreads();
-    return ex;
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+        const int x = s[q];
+        pre += q < w ? x : 0;
+        tot += x;
+    }
+    total = tot;
+    __syncthreads();  // s is reused by the next call
+    return pre + inc - v;
 }
 
 template <int T>
@@ -498,16 +506,18 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
             pv = A.p[pb + gg];
             v = (nbh / (double)(i + 1)) * pv;
         }
-        // inclusive suffix min within chunk (Hillis-Steele towards lower index)
-        sred[tid] = v;
-        __syncthreads();
-        for (int o = 1; o < T; o <<= 1) {
-            const double t2 = (tid + o < T) ? sred[tid + o] : INFINITY;
-            __syncthreads();
-            sred[tid] = fmin(sred[tid], t2);
-            __syncthreads();
+        // inclusive suffix min within the chunk: wave suffix mins by shuffles,
+        // then the later waves' minima (fmin is exact: order-free)
+        double wm = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_down(wm, o, 64);
+            if ((tid & 63) + o < 64) wm = fmin(wm, y);
         }
-        const double sm = fmin(sred[tid], carry);
+        if ((tid & 63) == 0) sred[tid >> 6] = wm;
+        __syncthreads();
+        double suf = wm;
+        for (int q = (tid >> 6) + 1; q < T / 64; ++q) suf = fmin(suf, sred[q]);
+        const double sm = fmin(suf, carry);
         const double q = fmin(1.0, sm);
         if (i < mnn) {
             if (fast) {
@@ -516,7 +526,9 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
                 A.slow_q[pb + gg] = q;
             }
         }
-        const double cmin = fmin(sred[0], carry);
+        double chunk_min = sred[0];
+        for (int q = 1; q < T / 64; ++q) chunk_min = fmin(chunk_min, sred[q]);
+        const double cmin = fmin(chunk_min, carry);
         __syncthreads();
         carry = cmin;
     }
