@@ -788,9 +788,10 @@ extern "C" hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_
 extern "C" hipError_t scc_launch_union(const u64* first_occ, int G, void* scratch, int cap, int* out, int* n_out,
                                        hipStream_t st)
 {
-    const size_t lds = (size_t)cap * sizeof(KeyRec) + sizeof(int) * SEL_T;
-    hipFuncSetAttribute((const void*)k_union<SEL_T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_union<SEL_T>, dim3(1), dim3(SEL_T), lds, st, first_occ, G, (KeyRec*)scratch, cap, out,
-                       n_out);
+    // one workgroup over all G genes: 1024 threads (a quarter of the chunk rounds of 256)
+    constexpr int UT = 1024;
+    const size_t lds = (size_t)cap * sizeof(KeyRec) + sizeof(int) * UT;
+    hipFuncSetAttribute((const void*)k_union<UT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_union<UT>, dim3(1), dim3(UT), lds, st, first_occ, G, (KeyRec*)scratch, cap, out, n_out);
     return hipGetLastError();
 }
