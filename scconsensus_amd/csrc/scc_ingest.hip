@@ -73,16 +73,22 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
         for (i64 k0 = b; k0 < e; k0 += 4 * 64) {  // four loads in flight per lane
             double xs[4];
             int gs[4], gps[4];
+            // clamped unconditional loads + select (a load under a lane
+            // condition becomes a branch with its own wait, one load at a time)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const i64 k = k0 + u * 64 + lane;
-                xs[u] = 0.0;
-                gs[u] = -1;
-                gps[u] = -1;
-                if (k < e) {
-                    xs[u] = vals[k];
-                    gs[u] = DENSE ? (int)(k - b) : rows[k];
-                    if (!DENSE && k > b) gps[u] = rows[k - 1];
+                const i64 kc = k < e ? k : e - 1;  // k0 < e, so e - 1 >= b
+                const double x = vals[kc];
+                xs[u] = k < e ? x : 0.0;
+                if (DENSE) {
+                    gs[u] = k < e ? (int)(k - b) : -1;
+                    gps[u] = -1;
+                } else {
+                    const int r = rows[kc];
+                    const int rp = rows[kc > b ? kc - 1 : b];
+                    gs[u] = k < e ? r : -1;
+                    gps[u] = (k < e && k > b) ? rp : -1;
                 }
             }
 #pragma unroll
