@@ -331,21 +331,22 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
             int gq[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
+                // clamped to the last entry (e0 < E) so the loads are
+                // unconditional and all four stay in flight (as in k_ing_hist)
                 const u32 e = e0 + (u32)(u * 64 + lane);
-                x[u] = 0.0;
-                gq[u] = -1;
-                if (e < E) {
-                    int lo = 0, hi = ncell;  // last cell c with cof[c] <= e
-                    while (hi - lo > 1) {
-                        const int mid = (lo + hi) >> 1;
-                        if (cof[mid] <= e) lo = mid;
-                        else hi = mid;
-                    }
-                    const u32 j = e - cof[lo];
-                    const i64 k = ckb[lo] + j;
-                    x[u] = vals[k];
-                    gq[u] = DENSE ? (int)j : rows[k] - g0;
+                const u32 ec = e < E ? e : E - 1;
+                int lo = 0, hi = ncell;  // last cell c with cof[c] <= ec
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (cof[mid] <= ec) lo = mid;
+                    else hi = mid;
                 }
+                const u32 j = ec - cof[lo];
+                const i64 k = ckb[lo] + j;
+                const double xv = vals[k];
+                const int gv = DENSE ? (int)j : rows[k] - g0;
+                x[u] = e < E ? xv : 0.0;
+                gq[u] = e < E ? gv : -1;
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) put(x[u], gq[u]);
