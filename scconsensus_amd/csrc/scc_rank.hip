@@ -120,7 +120,10 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
         for (int i = s0 + lane; i < s1; i += 256) {
             double x[4];  // 4 loads in flight; past the end adds +0 (exact no-op)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = (i + 64 * q < s1) ? scc_val_of(key[i + 64 * q]) : 0.0;
+            for (int q = 0; q < 4; ++q) {  // clamped unconditional load + select (i < s1)
+                const double v = scc_val_of(key[min(i + 64 * q, s1 - 1)]);
+                x[q] = (i + 64 * q < s1) ? v : 0.0;
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if (EXPM1) se = dd_add_d(se, expm1(x[q]));
