@@ -1,0 +1,126 @@
+"""Parity checks shared by the large-configuration GPU tests (configs B-E).
+
+Two halves, so that configurations too large for a full oracle run are still
+checked end to end:
+
+* ``check_rows_against_oracle_subset`` — the oracle (C restatement of
+  ``ComputePairWiseDE``, R/reclusterDEConsensusFast.R:229-351) run on a seeded
+  SUBSET of genes over ALL cells and ALL pairs.  Every per-(pair, gene)
+  quantity — the FAST filters (which genes a pair tests), W, the tie term, p,
+  avg_logFC, pct.1/pct.2 — depends on that gene alone, so for the sampled
+  genes the engine's rows must equal the oracle's exactly (and in the same
+  relative order inside each pair).
+* ``check_selection`` — the per-pair selection at FULL size, restated in numpy
+  from the engine's own per-row statistics: R's row order ``order(p,
+  -avg_logFC)`` (Fast:346), BH with the lazy n (Fast:347-350), the
+  ``dim(tmp)[1] > 1`` / ``q < qValThrs`` rule (Fast:376-377), ``top_n`` with
+  ties (Fast:391) and ``unique(Gene)`` (Fast:392).
+
+Test infrastructure only (imports the oracle).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle as O
+
+P_RTOL = 1e-6
+
+
+def pair_list(K):
+    return [(i, j) for i in range(K - 1) for j in range(i + 1, K)]
+
+
+def check_selection(rows, union, K, q_val_thrs=0.1, top_n=30):
+    """Full-size selection parity from the engine's own rows (FAST)."""
+    P = K * (K - 1) // 2
+    tested = np.asarray(rows.pair_tested, np.int64)
+    assert tested.shape == (P,)
+    starts = np.concatenate([[0], np.cumsum(tested)])
+    assert starts[-1] == len(rows.gene)
+    top_rows = []
+    for p in range(P):
+        a, b = int(starts[p]), int(starts[p + 1])
+        if a == b:
+            continue
+        g, pv, lfc = rows.gene[a:b], rows.p[a:b], rows.avg_logfc[a:b]
+        # order(p, -avg_logFC): p ascending with NaN last, then logFC descending, then gene row
+        nan = np.isnan(pv)
+        order = np.lexsort((g, -lfc, np.where(nan, 0.0, pv), nan))
+        assert np.array_equal(order, np.arange(b - a)), f"pair {p}: rows not in R's order(p, -avg_logFC)"
+        assert len(np.unique(g)) == b - a, f"pair {p}: repeated gene"
+        q = O.p_adjust_bh(pv)
+        np.testing.assert_allclose(rows.q[a:b], q, rtol=1e-12, atol=0, equal_nan=True,
+                                   err_msg=f"pair {p}: BH q")
+        de = (b - a > 1) & (rows.q[a:b] < q_val_thrs)
+        assert np.array_equal(rows.de[a:b], de), f"pair {p}: kept-row flags"
+        w = np.abs(lfc)
+        wd = w[de]
+        above = (wd[None, :] > w[:, None]).sum(axis=1)
+        top = de & (above + 1 <= top_n)
+        assert np.array_equal(rows.top[a:b], top), f"pair {p}: top_n flags"
+        top_rows.append(g[top])
+    top_genes = np.concatenate(top_rows) if top_rows else np.zeros(0, np.int32)
+    _, first = np.unique(top_genes, return_index=True)
+    np.testing.assert_array_equal(union, top_genes[np.sort(first)])
+
+
+def check_rows_against_oracle_subset(rows, Xsub, genes, code, K, **params):
+    """The oracle on genes ``genes`` (dense rows ``Xsub`` over all cells) vs the
+    engine's rows restricted to those genes: the same tested (pair, gene) set
+    in the same relative order, exact W / ties, pct, and p, logFC within the
+    bar.  Returns the number of (pair, gene) rows compared."""
+    genes = np.asarray(genes)
+    o = O.de_fast(Xsub, code, K, **params)
+    P = K * (K - 1) // 2
+    gstarts = np.concatenate([[0], np.cumsum(rows.pair_tested)])
+    ostarts = np.concatenate([[0], np.cumsum(o.pair_tested)])
+    n = 0
+    for p in range(P):
+        a, b = int(gstarts[p]), int(gstarts[p + 1])
+        g = rows.gene[a:b]
+        sel = np.nonzero(np.isin(g, genes))[0]
+        oa, ob = int(ostarts[p]), int(ostarts[p + 1])
+        og = genes[o.row_gene[oa:ob]]
+        assert np.array_equal(g[sel], og), f"pair {p}: tested genes / order differ from the oracle"
+        r = a + sel
+        np.testing.assert_array_equal(rows.u2[r], np.round(2 * o.row_W[oa:ob]).astype(np.int64), err_msg=f"pair {p} 2U")
+        np.testing.assert_array_equal(rows.ties[r], np.round(o.row_ties[oa:ob]).astype(np.int64),
+                                      err_msg=f"pair {p} ties")
+        np.testing.assert_allclose(rows.p[r], o.row_p[oa:ob], rtol=P_RTOL, atol=0, equal_nan=True,
+                                   err_msg=f"pair {p} p")
+        np.testing.assert_allclose(rows.avg_logfc[r], o.row_lfc[oa:ob], rtol=1e-12, atol=1e-15,
+                                   err_msg=f"pair {p} logFC")
+        np.testing.assert_array_equal(rows.pct1[r], o.row_pct1[oa:ob], err_msg=f"pair {p} pct.1")
+        np.testing.assert_array_equal(rows.pct2[r], o.row_pct2[oa:ob], err_msg=f"pair {p} pct.2")
+        n += ob - oa
+    return n
+
+
+def rows_of_gene_major(indptr, cols, vals, genes, N):
+    """Dense rows (len(genes) x N) from a gene-major CSR held as numpy arrays
+    or torch tensors (device or host)."""
+    out = np.zeros((len(genes), N))
+    for k, g in enumerate(np.asarray(genes)):
+        a, b = int(indptr[g]), int(indptr[g + 1])
+        c = cols[a:b]
+        v = vals[a:b]
+        if hasattr(c, "cpu"):
+            c, v = c.cpu().numpy(), v.cpu().numpy()
+        out[k, np.asarray(c, np.int64)] = v
+    return out
+
+
+def packed_index(i, j, N):
+    """Entry of cells i > j in R's packed `dist` vector (column-major lower triangle)."""
+    i = np.asarray(i, np.int64)
+    j = np.asarray(j, np.int64)
+    return j * (2 * N - j - 1) // 2 + (i - j - 1)
+
+
+def sample_cell_pairs(N, n, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, N, n)
+    b = rng.integers(0, N - 1, n)
+    b = np.where(b >= a, b + 1, b)
+    return np.maximum(a, b), np.minimum(a, b)

@@ -1,20 +1,26 @@
 """Config D shape (200k cells x 20k genes, K = 50, 1225 pairs) end to end on
 the device, with the input generated in HBM as a gene-major CSR (so the CSR
-transpose runs at full size too).  Parity at full size through properties
-(U within [0, 2 n_a n_b], the re-split route and the plain LDS-item route
-giving bit-identical rows) and exactly against the oracle on a seeded sample
-of tested (pair, gene) rows."""
+transpose runs at full size too).
+
+DE: full-size properties (U within [0, 2 n_a n_b]; the re-split route and the
+plain LDS-item route bit-identical), the oracle on a seeded gene subset over
+all cells and pairs (exact tested sets, U, ties, pct; p / logFC within the
+bar), and the full-size per-pair selection restated from the engine's rows.
+Distance: the 2e10-entry packed fp64 `dist` (160 GB, HBM-resident) on 2e5
+sampled entries against the exact SVD of X[U, ]."""
 import numpy as np
 import pytest
 import torch  # before the engine loads (torch's HIP runtime first)
 
 import oracle as O
+from parity_helpers import (check_rows_against_oracle_subset, check_selection, packed_index, rows_of_gene_major,
+                            sample_cell_pairs)
 from scconsensus_amd import api, synth
 
 pytestmark = pytest.mark.gpu
 
 
-def test_config_d_rows_sampled_parity(monkeypatch):
+def test_config_d_parity(monkeypatch):
     from scconsensus_amd import _native as nat
     d = synth.generate_device("D", "cuda:0", layout="csr")
     torch.cuda.synchronize()
@@ -30,6 +36,7 @@ def test_config_d_rows_sampled_parity(monkeypatch):
     nn = np.array([n[i] * n[j] for i, j in pairs])
     assert np.all(r.u2 >= 0) and np.all(r.u2 <= 2 * nn[r.row_pair])
     assert 100 < len(g.union) <= 30 * len(pairs)
+    check_selection(r, g.union, K)
     # the same DE with the re-split route off (fat buckets ranked as LDS items)
     # and the gene-level cross terms by the per-(gene, pair) wave kernel
     monkeypatch.setenv("SCC_RESPLIT", "0")
@@ -41,16 +48,33 @@ def test_config_d_rows_sampled_parity(monkeypatch):
     np.testing.assert_array_equal(g0.rows.u2, r.u2)
     np.testing.assert_array_equal(g0.rows.ties, r.ties)
     np.testing.assert_array_equal(g0.union, g.union)
-    # exact U / ties / p on sampled tested rows against the oracle
+    # the oracle on a seeded gene subset (half from the tested rows)
     ip = d.indptr.cpu().numpy()
     rng = np.random.default_rng(4)
-    for k in rng.choice(len(r.gene), 40, replace=False):
-        gene, p = int(r.gene[k]), int(r.row_pair[k])
-        i, j = pairs[p]
-        row = np.zeros(d.N)
-        row[d.indices[ip[gene]:ip[gene + 1]].cpu().numpy()] = d.data[ip[gene]:ip[gene + 1]].cpu().numpy()
-        po, W, T, _ = O.wilcox_test(row[code == i], row[code == j])
-        assert r.u2[k] == int(round(2 * W))
-        assert r.ties[k] == int(round(T))
-        assert r.p[k] == pytest.approx(po, rel=1e-6)
+    genes = np.unique(np.concatenate([rng.choice(np.unique(r.gene), 30, replace=False),
+                                      rng.choice(d.G, 30, replace=False)]))
+    Xs = rows_of_gene_major(ip, d.indices, d.data, genes, d.N)
+    assert check_rows_against_oracle_subset(r, Xs, genes, code, K) >= 200
+    del Xs
+    # stage 3: packed fp64 dist of 2e10 entries kept in HBM, sampled vs the exact SVD
+    N = d.N
+    out = torch.empty(N * (N - 1) // 2, dtype=torch.float64, device="cuda:0")
+    eng.distance(ds, g.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=out.data_ptr())
+    eng.synchronize()
+    Xu = rows_of_gene_major(ip, d.indices, d.data, g.union, N)
+    S = O.pca_scores(Xu, np.arange(len(g.union)))
+    i, j = sample_cell_pairs(N, 200_000, seed=6)
+    got = out[torch.from_numpy(packed_index(i, j, N)).to("cuda:0")].cpu().numpy()
+    want = np.sqrt(((S[i] - S[j]) ** 2).sum(axis=1))
+    err = float(np.max(np.abs(got - want)))
+    assert err < 1e-5, err
+    # the last column block (the packed vector's tail) in full
+    tail = out[-(200 * 199 // 2):].cpu().numpy()
+    ii, jj = np.tril_indices(200, -1)
+    ref_tail = np.sqrt(((S[N - 200 + ii] - S[N - 200 + jj]) ** 2).sum(axis=1))
+    order = np.argsort(packed_index(N - 200 + ii, N - 200 + jj, N))
+    assert np.max(np.abs(tail - ref_tail[order])) < 1e-5
+    assert float(out.min()) >= 0.0
+    del out
     ds.close()
+    eng.close()
