@@ -6,23 +6,30 @@ the 26k-cell PBMC shape (config B: 26,000 cells x 10,000 genes, 12 consensus
 clusters, 66 pairs), 1/2/4/8 GPUs.
 
 One step = one pass of the hot path over one synthetic job resident in HBM:
-  scc_de_run(FAST)   reclusterDEConsensusFast's pair loop, all 66 pairs x all
-                     genes (stats, Wilcoxon, BH, filters, top-N, union)
-  scc_distance       PCA(15) + packed Euclidean dist (N(N-1)/2 fp64, kept in HBM)
-value = cell-pairs / second = jobs * N(N-1)/2 / step time.
+  DE       reclusterDEConsensusFast's pair loop, all 66 pairs x all genes
+           (stats, Wilcoxon, BH, filters, top-N, union; Fast:57-392)
+  distance PCA(15) + packed Euclidean dist (N(N-1)/2 fp64, kept in HBM; Fast:398-400)
+value = cell-pairs / second = N(N-1)/2 / step time (HBM-resident; the
+transfer-inclusive times are reported beside it in "end_to_end_ms").
 
-Multi-GPU: one process per GPU (torchrun); by default every rank runs its own
-job (seed offset by rank) with no data-path collective ("scaling": "weak").
---mode shard runs ONE job over all ranks ("scaling": "strong"): DE on gene
-row-blocks combined by one RCCL all-reduce (scc_de_run_shard / scc_de_finish),
-then each rank's column slice of the packed distance (scc_distance_cols).  The
-step time is the max over ranks.
+Multi-GPU (`--gpus N`): one process per GPU.  Without torchrun's WORLD_SIZE in
+the environment, bench.py launches its own N ranks (torch.distributed.run on
+127.0.0.1) before touching the GPU.  Default `--mode shard`: ONE job over all
+ranks ("scaling": "strong"): gene row-blocks balanced by stored
+values + one all-gather of compact tested-cell records, the PCA over cell
+blocks (all-gather of column sums, all-reduce of the |U|^2 Gram and of the
+disjoint score rows), then each rank's equal-entry column slice of the packed
+distance.  `--mode jobs` (opt-in, "scaling": "weak"): every rank runs its own
+job (seed offset by rank) with no data-path collective.  The step time is the
+max over ranks.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,7 +43,7 @@ PEAK_FP64_TFS = 78.6     # MI355X FP64 matrix (spec)
 PEAK_FP32_TFS = 157.3    # MI355X FP32 matrix (v_mfma_f32_32x32x2_f32; MI355X_MICROARCH.md)
 
 
-def _args():
+def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -44,32 +51,59 @@ def _args():
     ap.add_argument("--config", default="B")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pearson", action="store_true", help="skip the side measurement of the Pearson kernel")
-    ap.add_argument("--cpu-sample-genes", type=int, default=300)
-    ap.add_argument("--mode", choices=["jobs", "shard"], default="jobs",
-                    help="jobs: one job per rank (weak scaling); shard: ONE job over all ranks (strong scaling: "
-                         "DE gene row-blocks + one all-reduce, distance column slices)")
-    return ap.parse_args()
+    ap.add_argument("--no-transfers", action="store_true", help="skip the D2H / H2D side measurements")
+    ap.add_argument("--cpu-sample-genes", type=int, default=1500)
+    ap.add_argument("--mode", choices=["shard", "jobs"], default="shard",
+                    help="shard: ONE job over all ranks (strong scaling); jobs: one job per rank (weak scaling)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: the launcher / rank / timing path with a placeholder step (tests)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a) -> int:
+    """Start N rank processes (torch.distributed.run, 127.0.0.1) running this
+    script with the same arguments; nothing here has touched the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 DEVICE_GEN = ("C", "D", "E")
 
 
 def cpu_baseline(d, code, K, union, sample_genes, seed=0):
-    """The oracle (C restatement of the R algorithm, 1 thread) on a bounded
-    sample of the same workload, scaled linearly: DE on a seeded gene sample
-    (all 66 pairs), exact PCA on the union, `dist` on a row sample."""
+    """The oracle (this repo's C restatement of the R algorithm, test
+    infrastructure) timed on the host beside the GPU:
+    * all cores: the FULL config-B DE (every gene, all pairs; genes split over
+      threads -- ctypes releases the GIL) + the exact PCA + the full `dist`
+      (row blocks over threads);
+    * 1 thread: a seeded gene sample, scaled linearly ("extrapolated")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import concurrent.futures as cf
+
     import oracle as O
     from scipy.spatial.distance import cdist
     rng = np.random.default_rng(seed)
     if not hasattr(d, "scipy_csc"):
         d = d.to_host()
-    genes = np.sort(rng.choice(d.G, min(sample_genes, d.G), replace=False))
     csr = d.scipy_csc().tocsr()
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 16,
+                         os.cpu_count() or 1))
+    # ---- 1 thread, gene sample
+    genes = np.sort(rng.choice(d.G, min(sample_genes, d.G), replace=False))
     Xs = np.asarray(csr[genes].todense())
     t0 = time.perf_counter()
     O.de_fast(Xs, code, K)
-    t_de = (time.perf_counter() - t0) * d.G / len(genes)
+    t_de1 = (time.perf_counter() - t0) * d.G / len(genes)
+    del Xs
     Xu = np.asarray(csr[union].todense())
     t0 = time.perf_counter()
     S = O.pca_scores(Xu, np.arange(len(union)))
@@ -77,19 +111,49 @@ def cpu_baseline(d, code, K, union, sample_genes, seed=0):
     rows = rng.choice(d.N, 256, replace=False)
     t0 = time.perf_counter()
     cdist(S[rows], S, "euclidean")
-    t_dist = (time.perf_counter() - t0) * (d.N / 2) / len(rows)
-    t = t_de + t_pca + t_dist
-    return {"value": d.N * (d.N - 1) / 2 / t, "unit": "cell-pairs/s", "cores": 1, "kind": "port",
-            "sample": f"oracle DE on {len(genes)}/{d.G} genes x all {K*(K-1)//2} pairs scaled x{d.G/len(genes):.1f}; "
-                      f"exact SVD PCA on |U|={len(union)}; dist on 256/{d.N} rows scaled; "
-                      f"est. end-to-end {t:.1f} s (DE {t_de:.1f}, PCA {t_pca:.1f}, dist {t_dist:.1f})",
-            "end_to_end_s": t}
+    t_dist1 = (time.perf_counter() - t0) * (d.N / 2) / len(rows)
+    t1 = t_de1 + t_pca + t_dist1
+    # ---- all cores, full workload (config A/B sizes)
+    full = d.G * d.N <= 400_000_000
+    out = {"unit": "cell-pairs/s", "kind": "port"}
+    if full:
+        blocks = np.array_split(np.arange(d.G), threads * 8)
+
+        def de_block(gs):
+            O.de_fast(np.asarray(csr[gs].todense()), code, K)
+
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            list(ex.map(de_block, blocks))
+        t_de = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        O.pca_scores(Xu, np.arange(len(union)))
+        t_pcaT = time.perf_counter() - t0
+        rb = np.array_split(np.arange(d.N), threads * 4)
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:  # each block: its rows x the earlier columns
+            list(ex.map(lambda r: cdist(S[r], S[: r[-1] + 1], "euclidean") if len(r) else None, rb))
+        t_dist = time.perf_counter() - t0
+        t = t_de + t_pcaT + t_dist
+        out.update({"value": d.N * (d.N - 1) / 2 / t, "cores": threads, "end_to_end_s": t,
+                    "sample": f"FULL workload on {threads} threads (not extrapolated): oracle DE over all {d.G} genes "
+                              f"x {K*(K-1)//2} pairs in {len(blocks)} gene blocks, exact SVD PCA on |U|={len(union)}, "
+                              f"full dist in {len(rb)} row blocks; DE {t_de:.2f} s, PCA {t_pcaT:.2f} s, "
+                              f"dist {t_dist:.2f} s"})
+    out["single_thread"] = {
+        "value": d.N * (d.N - 1) / 2 / t1, "cores": 1, "end_to_end_s": t1, "extrapolated": True,
+        "sample": f"oracle DE on {len(genes)}/{d.G} genes x all {K*(K-1)//2} pairs scaled x{d.G/len(genes):.1f}; "
+                  f"exact SVD PCA on |U|={len(union)}; dist on 256/{d.N} rows scaled; est. end-to-end {t1:.1f} s "
+                  f"(DE {t_de1:.1f}, PCA {t_pca:.1f}, dist {t_dist1:.1f})"}
+    if not full:
+        out.update({"value": out["single_thread"]["value"], "cores": 1, "end_to_end_s": t1, "extrapolated": True,
+                    "sample": out["single_thread"]["sample"]})
+    return out
 
 
 def de_only(a, eng, ds, d, code, K, dist, world):
     """Config E (BASELINE: "1M-cell sparse CSR input, 100 clusters (4950
-    pairs), DE-only"): the FAST DE over all pairs, K > 64 through the grouped
-    orchestration (scconsensus_amd/grouped.py), rows fetched to the host."""
+    pairs), DE-only"): the FAST DE over all pairs, rows fetched to the host."""
     from scconsensus_amd import grouped
 
     def step():
@@ -111,7 +175,7 @@ def de_only(a, eng, ds, d, code, K, dist, world):
     stage_ms = {}
     for f in fams:
         t, n = eng.kernel_time(f)
-        stage_ms[f] = round(t / max(a.steps, 1), 3)  # per step (several engine runs per step)
+        stage_ms[f] = round(t / max(a.steps, 1), 3)  # per step
     P = K * (K - 1) // 2
     out = {"metric": "DE-only seconds per reclusterDEConsensusFast DE at config E", "value": s_step, "unit": "s",
            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": s_step * 1e3,
@@ -119,9 +183,31 @@ def de_only(a, eng, ds, d, code, K, dist, world):
            "data": "synthetic (SURVEY §8d generator on the GPU, gene-major CSR)",
            "config": {"workload": f"config E: FAST DE (all {P} pairs, Wilcoxon), {d.N} cells x {d.G} genes CSR, K={K}",
                       "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": d.nnz,
-                      "union": len(r.union), "rows": int(len(r.rows.gene)), "engine_runs_per_step": max(1, -(-K // grouped.GROUP) * (-(-K // grouped.GROUP) - 1) // 2),
-                      "parallelism": f"jobs{world}"},
+                      "union": len(r.union), "rows": int(len(r.rows.gene)),
+                      "engine_runs_per_step": grouped.runs_for(K), "parallelism": f"jobs{world}"},
            "stage_ms_per_step": stage_ms}
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.close()
+
+
+def dry_run(a, dist):
+    """CPU rehearsal of the launcher / rank / timing path (tests)."""
+    def step():
+        time.sleep(0.002 * (1 + dist.rank))
+
+    for _ in range(a.warmup):
+        step()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    dist.barrier()
+    dt = dist.max_over_ranks(time.perf_counter() - t0)
+    shard = a.mode == "shard"
+    out = {"metric": "dry run", "value": 0.0, "n_gpus": dist.world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": dt / a.steps * 1e3, "scaling": "strong" if shard else "weak", "dry_run": True,
+           "config": {"parallelism": f"{'shard' if shard else 'jobs'}{dist.world}"}}
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     dist.close()
@@ -129,21 +215,28 @@ def de_only(a, eng, ds, d, code, K, dist, world):
 
 def main():
     a = _args()
-    if a.mode == "shard":
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    shard = a.mode == "shard"
+    if shard and not a.dry_run:
         import torch  # noqa: F401  (torch's HIP runtime first: the shard buffers are torch tensors)
     from scconsensus_amd import parallel
-    # RCCL ("nccl") when launched by torchrun with N > 1.  SCC_SHARE_GPU=1 with
+    # RCCL ("nccl") when launched with N > 1 GPUs.  SCC_SHARE_GPU=1 with
     # SCC_DIST_BACKEND=gloo rehearses several ranks on one GPU (tests only).
-    dist = parallel.init(os.environ.get("SCC_DIST_BACKEND") or None)
+    dist = parallel.init(os.environ.get("SCC_DIST_BACKEND") or ("gloo" if a.dry_run else None))
     rank, world, local = dist.rank, dist.world, dist.local_rank
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.dry_run:
+        return dry_run(a, dist)
     from scconsensus_amd import _native as nat
     from scconsensus_amd import api, synth
     from scconsensus_amd.synth import CONFIGS
 
     cfg = CONFIGS[a.config]
-    shard = a.mode == "shard"
     seed = cfg["seed"] if shard else parallel.job_seed(cfg["seed"], rank)
     gpu = 0 if os.environ.get("SCC_SHARE_GPU") else local
+    h2d_ms = None
     if a.config in DEVICE_GEN:  # C/D/E: generated in HBM (host generation takes minutes)
         import torch
         d = synth.generate_device(a.config, f"cuda:{gpu}", seed=seed, layout="csr" if a.config == "E" else "csc")
@@ -160,39 +253,57 @@ def main():
     if a.config in DEVICE_GEN:
         ds = eng.dataset_csc_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
     else:
-        ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)  # H2D before timing
+        ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)  # warm-up upload (allocations, first touch)
+        ds.close()
+        t0 = time.perf_counter()
+        ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)  # input H2D: before the timed region
+        h2d_ms = (time.perf_counter() - t0) * 1e3
     npairs_cells = d.N * (d.N - 1) / 2
-
-    if shard:
+    multi = shard and world > 1
+    if multi:
         import torch
         from scconsensus_amd import sharded
         tdev = torch.device(f"cuda:{gpu}")
+        if a.config in DEVICE_GEN:
+            gene_w = torch.bincount(d.indices.to(torch.int64), minlength=d.G).cpu().numpy()
+        else:
+            gene_w = np.bincount(d.indices, minlength=d.G)
 
-    def step():
-        if shard:  # one job: gene row-blocks + one RCCL all-reduce, then this rank's distance columns
-            r = sharded.de_sharded(eng, ds, code, K, dist, tdev, fetch="union")
-            sharded.distance_sharded(eng, ds, r.union, dist, device_out_ptr=0)
+    def step(dist_out=0):
+        """dist_out 0: the distance stays in HBM; a host array: streamed into it."""
+        if multi:  # one job: gene row-blocks + record all-gather, PCA over cell blocks, this rank's columns
+            r = sharded.de_sharded(eng, ds, code, K, dist, tdev, fetch="union", weights=gene_w)
+            if dist_out is None or isinstance(dist_out, int):
+                sharded.distance_sharded(eng, ds, r.union, dist, tdev, device_out_ptr=0)
+            else:
+                scores = sharded.pca_sharded(eng, ds, r.union, dist, tdev)
+                lo, hi = sharded.column_shard(ds.N, dist.rank, dist.world)
+                eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, out=dist_out[: hi * (2 * ds.N - hi - 1) // 2
+                                                                                 - lo * (2 * ds.N - lo - 1) // 2])
             return r
         r = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")
-        eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
+        if isinstance(dist_out, int):
+            eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
+        else:
+            eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, out=dist_out)
         return r
 
-    barrier = dist.barrier
+    def timed(nsteps, **kw):
+        eng.synchronize()
+        dist.barrier()
+        eng.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            r = step(**kw)
+        eng.synchronize()
+        dist.barrier()
+        return r, dist.max_over_ranks(time.perf_counter() - t0) / nsteps * 1e3
 
     for _ in range(a.warmup):
         r = step()
     eng.synchronize()
     eng.reset_timers()
-    barrier()
-    eng.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        r = step()
-    eng.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    dt = dist.max_over_ranks(t1 - t0)
-    ms = dt / a.steps * 1e3
+    r, ms = timed(a.steps)
     fams = ["ingest", "gene_stats", "pair_filter", "gene_rank", "pair_test", "pair_select", "gather", "center", "gram",
             "eigen", "eig_tridiag", "eig_vec", "eig_fin", "scores", "dist"]
     times = {f: eng.kernel_time(f) for f in fams}
@@ -201,22 +312,24 @@ def main():
     nu = len(r.union)
     nnz = d.nnz
     ncc = (d.N + 31) // 32
+    frac_entries = 1.0 / world if multi else 1.0  # a rank's share of the packed output (equal-entry slices)
     alg = {
         # packed fp64 R `dist` output + the N x 16 scores read
-        "dist": ("hbm", 8.0 * npairs_cells + 16 * 8.0 * d.N, "k_dist_euclid"),
+        "dist": ("hbm", 8.0 * npairs_cells * frac_entries + 16 * 8.0 * d.N, "k_dist_euclid"),
         # CSC read twice (12 B/nnz + 8 B/cell), keys written once (8 B/nnz), chunk counts (4 B, 3 passes)
-        "ingest": ("hbm", 2 * (12.0 * nnz + 8.0 * (d.N + 1)) + 8.0 * nnz + 3 * 4.0 * ncc * d.G, "k_ing_scatter"),
-        "gene_stats": ("hbm", 8.0 * nnz + 32.0 * K * d.G, "k_gene_stats"),
+        "ingest": ("hbm", 2 * (12.0 * nnz + 8.0 * (d.N + 1)) + 8.0 * nnz / world + 3 * 4.0 * ncc * d.G / world,
+                   "k_ing_scatter"),
+        "gene_stats": ("hbm", (8.0 * nnz + 32.0 * K * d.G) / world, "k_gene_stats"),
         # keys read once; per (pair, gene) accumulators written (S, E, X)
-        "gene_rank": ("hbm", 8.0 * nnz + 24.0 * P * d.G, "k_rank_item"),
+        "gene_rank": ("hbm", (8.0 * nnz + 24.0 * P * d.G) / world, "k_rank_item"),
         # Householder tridiagonalisation 4/3 n^3 fp64 flops (one hand-off per column: latency-bound)
         "eig_tridiag": ("mfma", 4.0 / 3.0 * nu ** 3, "k_tridiag"),
-        "gram": ("mfma", 2.0 * d.N * nu * nu / 2, "k_gram_f64"),
+        "gram": ("mfma", 2.0 * d.N * nu * nu / 2 / world, "k_gram_f64"),
     }
     dom = max(alg, key=lambda f: stage_ms.get(f, 0.0))
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and not multi:
         tk = json.load(open(tpath))["kernels"]
         hits = [v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith(alg[dom][2])]
         traffic = sum(hits) if hits else None
@@ -236,9 +349,32 @@ def main():
         return {"bound": "mfma", "achieved": ach, "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
                 "frac": ach / PEAK_FP64_TFS, "kernel": kname, "flops_per_launch": work, "avg_launch_ms": stage_ms[f]}
 
+    # transfers beside the HBM-resident step: the packed dist streamed to host
+    # memory (pageable: the pinned staging ring; pinned: direct DMA), and the
+    # input's H2D upload (host-generated configs)
+    e2e = {"hbm_resident": ms, "value_uses": "hbm_resident"}
+    if not a.no_transfers:
+        import torch
+        nloc = npairs_cells if not multi else (lambda lo, hi: hi * (2 * d.N - hi - 1) // 2 - lo * (2 * d.N - lo - 1) // 2)(
+            *sharded.column_shard(d.N, rank, world))
+        host = np.empty(int(nloc), np.float64)
+        host[::4096] = 0.0  # first touch outside the timed steps
+        step(dist_out=host)
+        _, e2e["with_dist_d2h_pageable"] = timed(max(1, min(a.steps, 3)), dist_out=host)
+        del host
+        pin = torch.empty(int(nloc), dtype=torch.float64, pin_memory=True).numpy()
+        step(dist_out=pin)
+        _, e2e["with_dist_d2h_pinned"] = timed(max(1, min(a.steps, 3)), dist_out=pin)
+        del pin
+        e2e["dist_gb"] = 8.0 * nloc / 1e9
+        e2e["d2h_gbs_pinned"] = 8.0 * nloc / 1e9 / max(1e-9, (e2e["with_dist_d2h_pinned"] - ms) / 1e3)
+        if h2d_ms is not None:
+            e2e["input_h2d"] = h2d_ms
+            e2e["with_input_h2d_and_dist_d2h_pinned"] = h2d_ms + e2e["with_dist_d2h_pinned"]
+
     # north_star's MFMA kernel: the Pearson 1 - cor distance (Fast:403) on the
     # same union, measured beside the step (not part of the reference's path)
-    if not a.no_pearson:
+    if not a.no_pearson and not multi:
         eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)  # warm-up (first launch, buffers)
         eng.synchronize()
         eng.reset_timers()
@@ -258,9 +394,11 @@ def main():
         roof_dom["note"] = ("fp64 vector work on a one-stage Householder reduction: n-1 dependent "
                             "cross-workgroup hand-offs, latency-bound (no MFMA shape)")
     kernels = {f: roof(f) for f in alg if f in stage_ms and stage_ms[f] > 0}
-    value = (1 if shard else world) * npairs_cells / (ms / 1e3)
+    jobs = world if not shard else 1
+    value = jobs * npairs_cells / (ms / 1e3)
     out = {
-        "metric": "end-to-end DE+distance cell-pairs/sec at 26k PBMC shape",
+        "metric": f"end-to-end DE+distance cell-pairs/sec at config {a.config}"
+                  + (" (26k PBMC shape)" if a.config == "B" else ""),
         "value": value,
         "unit": "cell-pairs/s",
         "n_gpus": world,
@@ -268,11 +406,12 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": ms,
         "end_to_end_s": ms / 1e3,
+        "end_to_end_ms": e2e,
         "higher_is_better": True,
         "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (SURVEY §8d NB log1p generator, seed per rank)",
+        "data": "synthetic (SURVEY §8d NB log1p generator" + (", seed per rank)" if not shard else ")"),
         "config": {"workload": f"config {a.config}: reclusterDEConsensusFast DE (all {P} pairs) + PCA15 "
                                f"Euclidean dist, {d.N} cells x {d.G} genes, K={K}",
                    "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": nnz, "union": nu,

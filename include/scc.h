@@ -134,6 +134,28 @@ SCC_API int scc_de_run_shard(scc_ctx* ctx, const scc_dataset* ds, const int32_t*
                      const scc_de_params* params, int64_t gene_lo, int64_t gene_hi, void* shard /* device */);
 SCC_API int scc_de_finish(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
                   const scc_de_params* params, const void* shards_sum /* device */, scc_de_result** out);
+/* The compact exchange (gather of per-(pair, tested gene)
+ * records): scc_de_run_shard_records runs the shard's per-(pair, gene) stage
+ * like scc_de_run_shard and packs, in (pair, gene) order, one scc_de_record per
+ * cell the pair tests (FAST: the cells that pass the feature filters; SLOW:
+ * every cell) into `records` (device, capacity `cap` records; cap >=
+ * n_pairs * (gene_hi - gene_lo) always suffices), *n_records = the count.
+ * The caller gathers every rank's records (block r = rank r's, stride
+ * `stride` records apart, counts[r] valid) and calls scc_de_finish_records on
+ * the same context: the result equals scc_de_run's. */
+typedef struct {
+    int32_t pair, gene;
+    double p, avg_logfc, pct1, pct2;
+    int64_t u2, ties;
+    uint32_t flags, reserved;
+} scc_de_record; /* 64 bytes */
+SCC_API int scc_de_run_shard_records(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */,
+                                     int32_t K, const scc_de_params* params, int64_t gene_lo, int64_t gene_hi,
+                                     void* records /* device */, int64_t cap, int64_t* n_records);
+SCC_API int scc_de_finish_records(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
+                                  const scc_de_params* params, const void* records /* device */,
+                                  const int64_t* counts /* host [n_blocks] */, int32_t n_blocks, int64_t stride,
+                                  scc_de_result** out);
 
 /* n_pairs = K(K-1)/2; n_rows = FAST tested rows over all pairs (0 for SLOW);
  * n_union = |deGeneUnion|. */
@@ -176,6 +198,35 @@ SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* gen
 SCC_API int scc_distance_cols(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */,
                       int32_t n_union, int32_t metric, int32_t ncomp, int64_t col_lo, int64_t col_hi,
                       void* dist_out, int32_t out_kind, int32_t out_f32);
+/* ---- stage 3 sharded over ranks (one process per GPU) --------
+ * prcomp_irlba + dist (Fast:398-400) of ONE job over the ranks of a process
+ * group: every rank holds the dataset and owns the cells [cell_lo, cell_hi)
+ * (ranks in order, covering [0, N)).  Each rank calls, with the same genes:
+ *   scc_pca_shard_colsum(.., part)      part: device, 2 * n_union doubles =
+ *       this rank's double-double column sums of X[U, cell_lo:cell_hi)
+ *   -> the caller all-gathers the parts in rank order: parts [world][2 n_union]
+ *   scc_pca_shard_gram(.., parts, world, gram)   gram: device, n_union^2
+ *       doubles = this rank's partial Gram of the centred rows
+ *   -> the caller all-reduces (sums) gram
+ *   scc_pca_shard_scores(.., gram_sum, ncomp, scores)   scores: device
+ *       [N][16] doubles; rows [cell_lo, cell_hi) written, others untouched
+ *   -> the caller combines the score rows of all ranks (disjoint)
+ *   scc_distance_scores(.., scores, ..)  the packed `dist` columns
+ *       [col_lo, col_hi) from the full score matrix.
+ * The mean is the same double-double sum as the unsharded path's, combined in
+ * rank order, so every rank sees identical bits; the eigensolve runs on every
+ * rank on the identical summed Gram (deterministic, identical scores). */
+SCC_API int scc_pca_shard_colsum(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */,
+                                 int32_t n_union, int64_t cell_lo, int64_t cell_hi, void* part /* device */);
+SCC_API int scc_pca_shard_gram(scc_ctx* ctx, const void* parts /* device [world][2 n_union] */, int32_t world,
+                               void* gram /* device [n_union][n_union] */);
+SCC_API int scc_pca_shard_scores(scc_ctx* ctx, const void* gram_sum /* device */, int32_t ncomp,
+                                 void* scores /* device [N][16] */);
+/* Packed `dist` columns [col_lo, col_hi) from a device score matrix [N][16]
+ * (components >= ncomp zero); output as in scc_distance_cols. */
+SCC_API int scc_distance_scores(scc_ctx* ctx, const void* scores /* device */, int64_t n_cells, int64_t col_lo,
+                                int64_t col_hi, void* dist_out, int32_t out_kind, int32_t out_f32);
+
 /* ---- silhouette on the distance vector (Fast:433) ---------
  * cluster::silhouette(groups, dmatrix = as.matrix(d)) without the N x N
  * matrix: widths[i] = s(i) (0 for a singleton cluster), clus_avg[k] = mean

@@ -36,9 +36,11 @@ SCC_PTR_DEVICE = 1
 EXPORTS = [
     "scc_ctx_create", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_kernel_time",
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_csr", "scc_dataset_create_dense", "scc_dataset_destroy",
-    "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
+    "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_run_shard_records",
+    "scc_de_finish_records", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
-    "scc_distance", "scc_distance_cols", "scc_silhouette", "scc_last_pca_scores",
+    "scc_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores",
+    "scc_distance_scores", "scc_silhouette", "scc_last_pca_scores",
     "scc_hclust_ward_d2", "scc_cutree_hybrid",
 ]
 
@@ -103,6 +105,8 @@ def load():
         "scc_de_shard_bytes": (i64, [i32, i64]),
         "scc_de_run_shard": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), i64, i64, vp]),
         "scc_de_finish": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), vp, P(vp)]),
+        "scc_de_run_shard_records": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), i64, i64, vp, i64, P(i64)]),
+        "scc_de_finish_records": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), vp, vp, i32, i64, P(vp)]),
         "scc_de_result_counts": (ctypes.c_int, [vp, P(i32), P(i64), P(i32)]),
         "scc_de_result_union": (ctypes.c_int, [vp, vp]),
         "scc_de_result_rows": (ctypes.c_int, [vp] + [vp] * 10),
@@ -112,6 +116,10 @@ def load():
         "scc_de_result_destroy": (None, [vp]),
         "scc_distance": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp, i32, i32]),
         "scc_distance_cols": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i64, i64, vp, i32, i32]),
+        "scc_pca_shard_colsum": (ctypes.c_int, [vp, vp, vp, i32, i64, i64, vp]),
+        "scc_pca_shard_gram": (ctypes.c_int, [vp, vp, i32, vp]),
+        "scc_pca_shard_scores": (ctypes.c_int, [vp, vp, i32, vp]),
+        "scc_distance_scores": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, i32, i32]),
         "scc_silhouette": (ctypes.c_int, [vp, i64, vp, vp, i32, vp, vp, P(i32)]),
         "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
         "scc_hclust_ward_d2": (ctypes.c_int, [vp, i64, vp, vp, vp]),
@@ -302,6 +310,37 @@ class Engine:
                                     ctypes.c_void_p(shards_sum_ptr), ctypes.byref(r))
         return self._collect(r, rc, ds, mode, K, fetch)
 
+    REC_BYTES = 64  # sizeof(scc_de_record)
+
+    def de_run_shard_records(self, ds: Dataset, code, K, gene_lo, gene_hi, rec_ptr, cap, mode=SCC_DE_FAST,
+                             q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5,
+                             mean_scaling_factor=5.0, test_all=False, test="wilcox") -> int:
+        """Compact records (scc_de_record, 64 B) of the tested (pair, gene)
+        cells of genes [gene_lo, gene_hi) into the device buffer at rec_ptr
+        (capacity ``cap`` records); returns their number."""
+        code = np.ascontiguousarray(code, np.int32)
+        prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
+                              test_all, test)
+        n = ctypes.c_int64()
+        self._check(self.lib.scc_de_run_shard_records(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), gene_lo,
+                                                      gene_hi, ctypes.c_void_p(rec_ptr), cap, ctypes.byref(n)))
+        return n.value
+
+    def de_finish_records(self, ds: Dataset, code, K, rec_ptr, counts, stride, mode=SCC_DE_FAST, q_val_thrs=0.1,
+                          log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0,
+                          fetch="all", test_all=False, test="wilcox") -> DeResult:
+        """Selection and union from the gathered records of every rank (device
+        blocks ``stride`` records apart, ``counts[r]`` valid in block r)."""
+        code = np.ascontiguousarray(code, np.int32)
+        prm = self._de_params(mode, q_val_thrs, log_fc_thrs, min_per_cent, top_n, fc_thrs, mean_scaling_factor,
+                              test_all, test)
+        cnt = np.ascontiguousarray(counts, np.int64)
+        r = ctypes.c_void_p()
+        rc = self.lib.scc_de_finish_records(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm),
+                                            ctypes.c_void_p(rec_ptr or None), _ptr(cnt), len(cnt), int(stride),
+                                            ctypes.byref(r))
+        return self._collect(r, rc, ds, mode, K, fetch)
+
     def _collect(self, r, rc, ds, mode, K, fetch) -> DeResult:
         msg = ""
         if rc != SCC_OK:
@@ -380,6 +419,33 @@ class Engine:
             out = np.empty(n, np.float32 if f32 else np.float64)
         self._check(self.lib.scc_distance_cols(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, col_lo,
                                                col_hi, _ptr(out), SCC_PTR_HOST, 1 if f32 else 0))
+        return out
+
+    # ---------------------------------------------------------- sharded PCA
+    def pca_shard_colsum(self, ds: Dataset, genes, cell_lo, cell_hi, part_ptr):
+        genes = np.ascontiguousarray(genes, np.int32)
+        self._check(self.lib.scc_pca_shard_colsum(self.ctx, ds.handle, _ptr(genes), len(genes), cell_lo, cell_hi,
+                                                  ctypes.c_void_p(part_ptr)))
+
+    def pca_shard_gram(self, parts_ptr, world, gram_ptr):
+        self._check(self.lib.scc_pca_shard_gram(self.ctx, ctypes.c_void_p(parts_ptr), world, ctypes.c_void_p(gram_ptr)))
+
+    def pca_shard_scores(self, gram_ptr, scores_ptr, ncomp=0):
+        self._check(self.lib.scc_pca_shard_scores(self.ctx, ctypes.c_void_p(gram_ptr), ncomp,
+                                                  ctypes.c_void_p(scores_ptr)))
+
+    def distance_scores(self, scores_ptr, N, col_lo, col_hi, out=None, f32=False, device_out_ptr=None):
+        """Packed `dist` columns [col_lo, col_hi) from a device [N][16] score matrix."""
+        n = col_hi * (2 * N - col_hi - 1) // 2 - col_lo * (2 * N - col_lo - 1) // 2
+        if device_out_ptr is not None:
+            self._check(self.lib.scc_distance_scores(self.ctx, ctypes.c_void_p(scores_ptr), N, col_lo, col_hi,
+                                                     ctypes.c_void_p(device_out_ptr or None), SCC_PTR_DEVICE,
+                                                     1 if f32 else 0))
+            return None
+        if out is None:
+            out = np.empty(n, np.float32 if f32 else np.float64)
+        self._check(self.lib.scc_distance_scores(self.ctx, ctypes.c_void_p(scores_ptr), N, col_lo, col_hi, _ptr(out),
+                                                 SCC_PTR_HOST, 1 if f32 else 0))
         return out
 
     def silhouette(self, N, groups, dist_device_ptr=None, f32=False):

@@ -540,6 +540,52 @@ extern "C" hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* p
     return hipGetLastError();
 }
 
+// one wave per column: the double-double column sum of rows [0, n) (partials
+// of k_colsum folded in the order k_colmean uses), not divided
+__global__ void __launch_bounds__(256) k_colsum_fold(const dd* __restrict__ part, int nchunk, int ld, int nu,
+                                                     dd* __restrict__ out)
+{
+    const int u = blockIdx.x * 4 + scc_wave_id(), lane = threadIdx.x & 63;
+    if (u >= nu) return;
+    dd s{0.0, 0.0};
+    for (int k = lane; k < nchunk; k += 64) s = dd_add(s, part[(size_t)k * ld + u]);
+    s = dd_wave_sum_dpp(s);
+    if (lane == 0) out[u] = s;
+}
+
+// mean[u] = (sum over ranks r, in rank order, of parts[r][u]) / N
+__global__ void __launch_bounds__(256) k_mean_of_parts(const dd* __restrict__ parts, int nparts, int nu, int ld,
+                                                       double N, double* __restrict__ mean)
+{
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= ld) return;
+    if (u >= nu) {
+        mean[u] = 0.0;
+        return;
+    }
+    dd s{0.0, 0.0};
+    for (int r = 0; r < nparts; ++r) s = dd_add(s, parts[(size_t)r * nu + u]);
+    mean[u] = dd_div_n(s, N);
+}
+
+extern "C" hipError_t scc_launch_colsum_dd(const double* Xc, int n, int ld, int nu, dd* part, int nchunk, dd* out,
+                                           hipStream_t st)
+{
+    const int rpc = (n + nchunk - 1) / nchunk;
+    hipLaunchKernelGGL(k_colsum, dim3((ld + 255) / 256, nchunk), dim3(256), 0, st, Xc, n, ld, rpc, part);
+    hipLaunchKernelGGL(k_colsum_fold, dim3((nu + 3) / 4), dim3(256), 0, st, part, nchunk, ld, nu, out);
+    return hipGetLastError();
+}
+
+// centre rows [0, n) of Xc with the mean of the ranks' column sums
+extern "C" hipError_t scc_launch_center_parts(double* Xc, int n, int nu, int ld, const dd* parts, int nparts,
+                                              double N, double* mean, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_mean_of_parts, dim3((ld + 255) / 256), dim3(256), 0, st, parts, nparts, nu, ld, N, mean);
+    hipLaunchKernelGGL(k_center, dim3(4096), dim3(256), 0, st, Xc, n, nu, ld, mean);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C,
                                       hipStream_t st)
 {

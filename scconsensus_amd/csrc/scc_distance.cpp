@@ -11,6 +11,9 @@
 // over U and an FP32 MFMA Gram with the 1 - r epilogue fused into the store.
 #include "scc_internal.hpp"
 
+#include <chrono>
+#include <thread>
+
 using namespace scc_rt;
 
 extern "C" {
@@ -32,6 +35,140 @@ hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z,
 }
 
 extern "C" void scc_distance_release(scc_ctx*) {}
+
+namespace {
+
+// Column tiles of the packed slice [col_lo, col_hi) with about `target`
+// entries each (column j holds N - 1 - j entries).
+std::vector<int64_t> column_tiles(int64_t N, int64_t col_lo, int64_t col_hi, int64_t target)
+{
+    std::vector<int64_t> t{col_lo};
+    int64_t acc = 0;
+    for (int64_t j = col_lo; j < col_hi; ++j) {
+        acc += N - 1 - j;
+        if (acc >= target && j + 1 < col_hi) {
+            t.push_back(j + 1);
+            acc = 0;
+        }
+    }
+    t.push_back(col_hi);
+    return t;
+}
+
+// host copy of one staged chunk, split over a few threads (a single core
+// copies pageable memory at ~10 GB/s, well below the PCIe rate)
+void parallel_copy(char* dst, const char* src, size_t n)
+{
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nt = std::min<size_t>(std::min(8u, hw), std::max<size_t>(1, n >> 22));
+    if (nt <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t part = (n / nt + 4095) & ~(size_t)4095;
+    for (size_t t = 0; t < nt; ++t) {
+        const size_t a = std::min(n, t * part), b = std::min(n, a + part);
+        if (a < b) th.emplace_back([=] { std::memcpy(dst + a, src + a, b - a); });
+    }
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+// Stream the packed distance slice to the caller's host buffer (north_star:
+// "the distance tiles stream back through pinned hipMemcpyAsync"): the
+// output kernel runs per column tile on s0; s1 copies each finished tile over
+// PCIe while s0 computes the next.  A pinned caller buffer (hipHostMalloc /
+// hipHostRegister / torch pin_memory) receives the DMA directly; a pageable
+// one goes through a 2-slot pinned staging ring whose host-side copy of slot
+// s overlaps the DMA into the other slot.  `emit(a, b, dst)` launches the
+// output kernel for columns [a, b) writing at dst.
+template <class Emit>
+static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi, size_t es, char* d_out,
+                          char* host, Emit emit)
+{
+    hipStream_t s0 = c->s0, s1 = c->s1;
+    auto colbase = [&](int64_t j) { return (size_t)j * (2 * (size_t)N - j - 1) / 2; };
+    const size_t base0 = colbase(col_lo);
+    const size_t total = (colbase(col_hi) - base0) * es;
+    const int64_t tile_entries = std::max<int64_t>(1, (int64_t)env_int("SCC_DIST_TILE_MB", 128) * (1 << 20) / (int64_t)es);
+    const std::vector<int64_t> tiles = column_tiles(N, col_lo, col_hi, tile_entries);
+    const int nt = (int)tiles.size() - 1;
+    std::vector<hipEvent_t> ev(nt);
+    std::vector<size_t> tile_end(nt);
+    for (int t = 0; t < nt; ++t) {
+        ev[t] = ev_take(c);
+        const size_t off = (colbase(tiles[t]) - base0) * es;
+        tile_end[t] = (colbase(tiles[t + 1]) - base0) * es;
+        HIPCHK(c, emit(tiles[t], tiles[t + 1], d_out + off));
+        HIPCHK(c, hipEventRecord(ev[t], s0));
+    }
+    auto release = [&]() {
+        for (auto e : ev) c->ev_pool.push_back(e);
+    };
+    hipPointerAttribute_t pa{};
+    const bool pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost;
+    hipGetLastError();
+    const auto t0 = std::chrono::steady_clock::now();
+    if (pinned) {  // DMA straight into the caller's buffer, tile by tile
+        size_t off = 0;
+        for (int t = 0; t < nt; ++t) {
+            HIPCHK(c, hipStreamWaitEvent(s1, ev[t], 0));
+            HIPCHK(c, hipMemcpyAsync(host + off, d_out + off, tile_end[t] - off, hipMemcpyDeviceToHost, s1));
+            off = tile_end[t];
+        }
+        const hipError_t e = hipStreamSynchronize(s1);
+        release();
+        HIPCHK(c, e);
+    } else {
+        const size_t S = (size_t)std::max(1, env_int("SCC_DIST_STAGE_MB", 64)) << 20;
+        if (c->dstage_bytes < S) {
+            if (c->h_dstage) hipHostFree(c->h_dstage);
+            c->h_dstage = nullptr;
+            c->dstage_bytes = 0;
+            if (hipHostMalloc((void**)&c->h_dstage, 2 * S, hipHostMallocDefault) != hipSuccess) {
+                hipGetLastError();
+                c->h_dstage = nullptr;
+                release();
+                return fail(c, SCC_ERR_OOM, "pinned distance staging allocation failed");
+            }
+            c->dstage_bytes = S;
+        }
+        const size_t nch = (total + S - 1) / S;
+        hipEvent_t done[2] = {ev_take(c), ev_take(c)};
+        int waited = 0;  // tiles s1 already waits for
+        auto enqueue = [&](size_t ch) -> hipError_t {
+            const size_t a = ch * S, b = std::min(total, a + S);
+            while (waited < nt && tile_end[waited] < b) ++waited;  // tiles that cover [a, b)
+            hipError_t e = hipStreamWaitEvent(s1, ev[std::min(waited, nt - 1)], 0);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(c->h_dstage + (ch & 1) * S, d_out + a, b - a, hipMemcpyDeviceToHost, s1);
+            if (e == hipSuccess) e = hipEventRecord(done[ch & 1], s1);
+            return e;
+        };
+        hipError_t e = nch ? enqueue(0) : hipSuccess;
+        for (size_t ch = 0; ch < nch && e == hipSuccess; ++ch) {
+            if (ch + 1 < nch) e = enqueue(ch + 1);  // DMA of the next chunk overlaps this chunk's host copy
+            if (e == hipSuccess) e = hipEventSynchronize(done[ch & 1]);
+            if (e == hipSuccess) {
+                const size_t a = ch * S, b = std::min(total, a + S);
+                parallel_copy(host + a, c->h_dstage + (ch & 1) * S, b - a);
+            }
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s1);
+        c->ev_pool.push_back(done[0]);
+        c->ev_pool.push_back(done[1]);
+        release();
+        HIPCHK(c, e);
+    }
+    if (c->profile) {  // wall time of the streamed output (kernel tiles + PCIe + host copy)
+        auto& tm = c->timers[pinned ? "d2h_pinned" : "d2h"];
+        tm.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        tm.n += 1;
+    }
+    return SCC_OK;
+}
 
 // columns [col_lo, col_hi) of the packed output (the whole matrix: [0, N))
 static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
@@ -145,9 +282,17 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
             Scope sc(c, "scores", s0);
             HIPCHK(c, scc_launch_scores(d_X, N, nu, ld, d_Z, k, d_P, s0));
         }
+        auto emit = [&](int64_t a, int64_t b, void* dst) {
+            return scc_launch_dist_euclid(d_P, N, (int)a, (int)b, dst, out_f32, s0);
+        };
         {
             Scope sc(c, "dist", s0);
-            HIPCHK(c, scc_launch_dist_euclid(d_P, N, (int)col_lo, (int)col_hi, d_out, out_f32, s0));
+            if (out_kind == SCC_PTR_HOST) {
+                if ((rc = stream_to_host(c, N, col_lo, col_hi, out_f32 ? 4 : 8, (char*)d_out, (char*)dist_out, emit)))
+                    return rc;
+            } else {
+                HIPCHK(c, emit(col_lo, col_hi, d_out));
+            }
         }
         c->d_last_scores = d_P;
         c->last_n = N;
@@ -162,13 +307,21 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
             Scope sz(c, "zscore", s0);
             HIPCHK(c, scc_launch_zscore(d_X, N, nu, ld, d_Zp, ldz, s0));
         }
+        auto emit = [&](int64_t a, int64_t b, void* dst) {
+            return scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, (int)a, (int)b, dst, out_f32, s0);
+        };
         Scope sc(c, "pearson", s0);
-        HIPCHK(c, scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, (int)col_lo, (int)col_hi, d_out, out_f32, s0));
+        if (out_kind == SCC_PTR_HOST) {
+            if ((rc = stream_to_host(c, N, col_lo, col_hi, out_f32 ? 4 : 8, (char*)d_out, (char*)dist_out, emit)))
+                return rc;
+        } else {
+            HIPCHK(c, emit(col_lo, col_hi, d_out));
+        }
     }
-    if (out_kind == SCC_PTR_HOST) {
-        HIPCHK(c, hipMemcpyAsync(dist_out, d_out, npairs * (out_f32 ? 4 : 8), hipMemcpyDeviceToHost, s0));
-    }
-    c->d_last_dist = (col_lo == 0 && col_hi == N) ? d_out : nullptr;  // what scc_silhouette(dist = NULL) reads
+    // what scc_silhouette(dist = NULL) reads: only an output the engine owns
+    // (a caller's device buffer may be freed or reused after this call)
+    const bool own = out_kind == SCC_PTR_HOST || !dist_out;
+    c->d_last_dist = (own && col_lo == 0 && col_hi == N) ? d_out : nullptr;
     c->last_dist_n = N;
     c->last_dist_f32 = out_f32 ? 1 : 0;
     HIPCHK(c, hipStreamSynchronize(s0));
@@ -189,6 +342,166 @@ extern "C" int scc_distance_cols(scc_ctx* c, const scc_dataset* ds, const int32_
                                  int32_t out_f32)
 {
     return dist_impl(c, ds, genes, nu, metric, ncomp, col_lo, col_hi, dist_out, out_kind, out_f32);
+}
+
+// ====================================================================== sharded PCA
+// (include/scc.h: scc_pca_shard_*; SURVEY 8e "per-GPU partial Gram over cell
+// shards, then an all-reduce of the |U| x |U| fp64 Gram")
+extern "C" hipError_t scc_launch_colsum_dd(const double* Xc, int n, int ld, int nu, dd* part, int nchunk, dd* out,
+                                           hipStream_t st);
+extern "C" hipError_t scc_launch_center_parts(double* Xc, int n, int nu, int ld, const dd* parts, int nparts, double N,
+                                              double* mean, hipStream_t st);
+
+extern "C" int scc_pca_shard_colsum(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu,
+                                    int64_t cell_lo, int64_t cell_hi, void* part)
+{
+    if (!c || !ds || !genes || !part) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_colsum: null argument");
+    if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
+    const int G = (int)ds->G, N = (int)ds->N;
+    if (nu < 1) return fail(c, SCC_ERR_INVALID, "empty gene union");
+    if (cell_lo < 0 || cell_hi > N || cell_lo > cell_hi) return fail(c, SCC_ERR_INVALID, "cell shard out of range");
+    for (int u = 0; u < nu; ++u)
+        if (genes[u] < 0 || genes[u] >= G) return fail(c, SCC_ERR_INVALID, "gene index out of range");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    const int ld = (nu + 63) & ~63;
+    const int n = (int)(cell_hi - cell_lo);
+    const int npad = std::max(16, (n + 15) & ~15);
+    int rc;
+    int *d_genes, *d_umap;
+    double* d_X;
+    void* d_part;
+    if ((rc = ws(c, "d_genes", nu, &d_genes))) return rc;
+    if ((rc = ws(c, "d_umap", G, &d_umap))) return rc;
+    if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
+    const int nchunk_mean = 512;
+    if ((rc = ws_get(c, "d_part", sizeof(double) * 2 * (size_t)nchunk_mean * ld, &d_part))) return rc;
+    HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
+    {
+        Scope sc(c, "gather", s0);
+        HIPCHK(c, hipMemsetAsync(d_X, 0, sizeof(double) * (size_t)npad * ld, s0));
+        HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
+        if (n > 0)
+            HIPCHK(c, scc_launch_gather(ds->dense ? nullptr : ds->d_indptr + cell_lo, ds->d_rows, ds->d_vals,
+                                        ds->dense ? ds->d_dense + (size_t)cell_lo * G : nullptr, G, n, d_umap, d_genes,
+                                        nu, ld, d_X, s0));
+    }
+    {
+        Scope sc(c, "center", s0);
+        HIPCHK(c, scc_launch_colsum_dd(d_X, n, ld, nu, (dd*)d_part, nchunk_mean, (dd*)part, s0));
+    }
+    c->pca_nu = nu;
+    c->pca_ld = ld;
+    c->pca_N = N;
+    c->pca_clo = cell_lo;
+    c->pca_chi = cell_hi;
+    c->pca_stage = 1;
+    HIPCHK(c, hipStreamSynchronize(s0));  // the caller's collective reads `part` on its own stream
+    return SCC_OK;
+}
+
+extern "C" int scc_pca_shard_gram(scc_ctx* c, const void* parts, int32_t world, void* gram)
+{
+    if (!c || !parts || !gram || world < 1) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_gram: bad argument");
+    if (c->pca_stage < 1) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_gram: call scc_pca_shard_colsum first");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    const int nu = c->pca_nu, ld = c->pca_ld;
+    const int n = (int)(c->pca_chi - c->pca_clo);
+    const int npad = std::max(16, (n + 15) & ~15);
+    int rc;
+    double *d_X, *d_mean, *d_slabs, *d_C;
+    if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
+    if ((rc = ws(c, "d_mean", ld, &d_mean))) return rc;
+    const int nchunk = std::max(1, std::min(32, npad / 512));
+    if ((rc = ws(c, "d_slabs", (size_t)nchunk * ld * ld, &d_slabs))) return rc;
+    if ((rc = ws(c, "d_C", (size_t)ld * ld, &d_C))) return rc;
+    {
+        Scope sc(c, "center", s0);
+        HIPCHK(c, scc_launch_center_parts(d_X, n, nu, ld, (const dd*)parts, world, (double)c->pca_N, d_mean, s0));
+    }
+    {
+        Scope sc(c, "gram", s0);
+        HIPCHK(c, scc_launch_gram(d_X, npad, ld, nchunk, d_slabs, d_C, s0));
+    }
+    HIPCHK(c, hipMemcpy2DAsync(gram, sizeof(double) * nu, d_C, sizeof(double) * ld, sizeof(double) * nu, nu,
+                               hipMemcpyDeviceToDevice, s0));
+    c->pca_stage = 2;
+    HIPCHK(c, hipStreamSynchronize(s0));
+    return SCC_OK;
+}
+
+extern "C" int scc_pca_shard_scores(scc_ctx* c, const void* gram_sum, int32_t ncomp, void* scores)
+{
+    if (!c || !gram_sum || !scores) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_scores: null argument");
+    if (c->pca_stage < 2) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_scores: call scc_pca_shard_gram first");
+    const int nu = c->pca_nu, ld = c->pca_ld;
+    const int k = ncomp > 0 ? ncomp : std::min(nu, 15);
+    if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    const int n = (int)(c->pca_chi - c->pca_clo);
+    const int npad = std::max(16, (n + 15) & ~15);
+    int rc;
+    double *d_X, *d_C, *d_W, *d_Z, *d_escr;
+    if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
+    if ((rc = ws(c, "d_C", (size_t)ld * ld, &d_C))) return rc;
+    if ((rc = ws(c, "d_W", ld, &d_W))) return rc;
+    if ((rc = ws(c, "d_Z", (size_t)ld * 16, &d_Z))) return rc;
+    if ((rc = ws(c, "d_escr", scc_eigen_scratch_doubles(nu, ld, k), &d_escr))) return rc;
+    HIPCHK(c, hipMemsetAsync(d_C, 0, sizeof(double) * (size_t)ld * ld, s0));
+    HIPCHK(c, hipMemcpy2DAsync(d_C, sizeof(double) * ld, gram_sum, sizeof(double) * nu, sizeof(double) * nu, nu,
+                               hipMemcpyDeviceToDevice, s0));
+    unsigned int* d_eig_err = nullptr;
+    {
+        Scope sc(c, "eigen", s0);
+        int nwg_used = 0;
+        HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, nullptr, nullptr, s0));
+    }
+    HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
+    if (n > 0) {
+        Scope sc(c, "scores", s0);
+        HIPCHK(c, scc_launch_scores(d_X, n, nu, ld, d_Z, k, (double*)scores + (size_t)c->pca_clo * 16, s0));
+    }
+    HIPCHK(c, hipStreamSynchronize(s0));
+    c->last_ncomp = k;
+    if (c->eig_err) return fail(c, SCC_ERR_HIP, "scc_pca_shard_scores: eigensolver workgroup hand-off timed out");
+    return SCC_OK;
+}
+
+extern "C" int scc_distance_scores(scc_ctx* c, const void* scores, int64_t N64, int64_t col_lo, int64_t col_hi,
+                                   void* dist_out, int32_t out_kind, int32_t out_f32)
+{
+    if (!c || !scores) return fail(c, SCC_ERR_INVALID, "scc_distance_scores: null argument");
+    if (!dist_out && out_kind != SCC_PTR_DEVICE) return fail(c, SCC_ERR_INVALID, "scc_distance_scores: null output");
+    if (N64 < 2 || N64 > INT32_MAX) return fail(c, SCC_ERR_INVALID, "scc_distance_scores: bad cell count");
+    const int N = (int)N64;
+    if (col_lo < 0 || col_hi > N || col_lo > col_hi) return fail(c, SCC_ERR_INVALID, "column slice out of range");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    auto colbase = [&](int64_t j) { return (size_t)j * (2 * (size_t)N - j - 1) / 2; };
+    const size_t npairs = colbase(col_hi) - colbase(col_lo);
+    const size_t es = out_f32 ? 4 : 8;
+    void* d_out = dist_out;
+    int rc;
+    if (out_kind == SCC_PTR_HOST || !dist_out)
+        if ((rc = ws_get(c, "d_dist", npairs * es, &d_out))) return rc;
+    const double* P = (const double*)scores;
+    auto emit = [&](int64_t a, int64_t b, void* dst) { return scc_launch_dist_euclid(P, N, (int)a, (int)b, dst, out_f32, s0); };
+    {
+        Scope sc(c, "dist", s0);
+        if (out_kind == SCC_PTR_HOST) {
+            if ((rc = stream_to_host(c, N, col_lo, col_hi, es, (char*)d_out, (char*)dist_out, emit))) return rc;
+        } else {
+            HIPCHK(c, emit(col_lo, col_hi, d_out));
+        }
+    }
+    const bool own = out_kind == SCC_PTR_HOST || !dist_out;
+    c->d_last_dist = (own && col_lo == 0 && col_hi == N) ? d_out : nullptr;
+    c->last_dist_n = N;
+    c->last_dist_f32 = out_f32 ? 1 : 0;
+    HIPCHK(c, hipStreamSynchronize(s0));
+    return SCC_OK;
 }
 
 extern "C" int scc_silhouette(scc_ctx* c, int64_t n_cells, const int32_t* groups, const void* dist, int32_t dist_f32,

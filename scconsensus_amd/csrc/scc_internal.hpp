@@ -70,6 +70,14 @@ struct scc_ctx {
     int last_dist_f32 = 0;
     int64_t shard_sig[6] = {-1, -1, -1, -1, -1, -1};  // inputs of the last scc_de_run_shard
     double shard_log_thr = 0.0;
+    // pinned staging ring of the streamed distance output (scc_distance to a
+    // pageable host buffer): 2 slots of dstage_bytes each
+    char* h_dstage = nullptr;
+    size_t dstage_bytes = 0;
+    // sharded PCA (scc_pca_shard_*): this rank's cells and the union width
+    int pca_nu = 0, pca_ld = 0;
+    int64_t pca_N = 0, pca_clo = 0, pca_chi = 0;
+    int pca_stage = 0;  // 1 after colsum, 2 after gram
 };
 
 struct scc_dataset {

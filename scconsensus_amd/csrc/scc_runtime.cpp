@@ -61,6 +61,7 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     }
     for (auto e : c->ev_pool) hipEventDestroy(e);
     if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->h_dstage) hipHostFree(c->h_dstage);
     hipEventDestroy(c->ev_fork);
     hipEventDestroy(c->ev_join);
     hipStreamDestroy(c->s0);
@@ -306,12 +307,40 @@ extern "C" void scc_dataset_destroy(scc_dataset* d)
 // stage DE_FINISH: `shard` holds every gene's (pair, gene) cells (the sum of
 //   all ranks' shards); per-pair BH, filters, top-N and the union, on the
 //   context that ran this rank's DE_SHARD for the same inputs.
-enum { DE_FULL = 0, DE_SHARD = 1, DE_FINISH = 2 };
+// stage DE_SHARD_REC / DE_FINISH_REC: the same with the compact exchange
+//   (scc_de_record per tested (pair, gene) cell; scc_exchange.hip).
+enum { DE_FULL = 0, DE_SHARD = 1, DE_FINISH = 2, DE_SHARD_REC = 3, DE_FINISH_REC = 4 };
+
+extern "C" {
+int scc_rec_blocks(long long cells);
+hipError_t scc_launch_rec_count(const uint8_t* flags, int G, int P, int glo, int ghi, int all, uint32_t* cnt,
+                                hipStream_t st);
+hipError_t scc_launch_rec_pack(const uint8_t* flags, int G, int P, int glo, int ghi, int all, const long long* off,
+                               const double* p, const double* lfc, const double* pct1, const double* pct2,
+                               const long long* u2, const long long* t, scc_de_record* out, hipStream_t st);
+hipError_t scc_launch_rec_scatter(const scc_de_record* rec, long long n, int G, int P, double* p, double* lfc,
+                                  double* pct1, double* pct2, long long* u2, long long* t, uint8_t* flags, int* err,
+                                  hipStream_t st);
+}
+
+struct RecIO {  // the compact exchange's buffers (DE_SHARD_REC out, DE_FINISH_REC in)
+    void* out = nullptr;
+    int64_t cap = 0;
+    int64_t* n_out = nullptr;
+    const void* in = nullptr;
+    const int64_t* counts = nullptr;
+    int nblocks = 0;
+    int64_t stride = 0;
+};
 
 static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
-                       int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out)
+                       int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
+                       const RecIO* rio = nullptr)
 {
-    if (!c || !ds || !code || !prm || (stage != DE_SHARD && !out) || (stage != DE_FULL && !shard))
+    const bool shard_stage = stage == DE_SHARD || stage == DE_SHARD_REC;
+    const bool finish_stage = stage == DE_FINISH || stage == DE_FINISH_REC;
+    if (!c || !ds || !code || !prm || (!shard_stage && !out) || ((stage == DE_SHARD || stage == DE_FINISH) && !shard) ||
+        ((stage == DE_SHARD_REC || stage == DE_FINISH_REC) && !rio))
         return fail(c, SCC_ERR_INVALID, "scc_de_run: null argument");
     if (out) *out = nullptr;
     if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
@@ -487,7 +516,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
 
     const int64_t sig[6] = {G, N, K, prm->mode, ds->nnz, (int64_t)(intptr_t)ds};
     double log_thr = 0.0;
-    if (stage == DE_FINISH) {
+    if (finish_stage) {
         if (!std::equal(sig, sig + 6, c->shard_sig))
             return fail(c, SCC_ERR_INVALID, "scc_de_finish: this context ran no scc_de_run_shard for these inputs");
         log_thr = c->shard_log_thr;
@@ -713,14 +742,36 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     };
     const Field fields[7] = {{d_p, 8}, {d_lfc, 8}, {fast ? (void*)d_pct1 : nullptr, 8}, {fast ? (void*)d_pct2 : nullptr, 8},
                              {d_u2, 8}, {d_t, 8}, {d_flags, 1}};
-    if (stage == DE_SHARD) {
-        char* dst = (char*)shard;
-        HIPCHK(c, hipMemsetAsync(dst, 0, scc_de_shard_bytes(K, G), s0));
-        for (const Field& f : fields) {
-            if (f.p && ghi > glo)
-                HIPCHK(c, hipMemcpy2DAsync(dst + glo * f.es, G * f.es, (const char*)f.p + glo * f.es, G * f.es,
-                                           (size_t)(ghi - glo) * f.es, P, hipMemcpyDeviceToDevice, s0));
-            dst += PG * f.es;
+    if (shard_stage) {
+        if (stage == DE_SHARD) {
+            char* dst = (char*)shard;
+            HIPCHK(c, hipMemsetAsync(dst, 0, scc_de_shard_bytes(K, G), s0));
+            for (const Field& f : fields) {
+                if (f.p && ghi > glo)
+                    HIPCHK(c, hipMemcpy2DAsync(dst + glo * f.es, G * f.es, (const char*)f.p + glo * f.es, G * f.es,
+                                               (size_t)(ghi - glo) * f.es, P, hipMemcpyDeviceToDevice, s0));
+                dst += PG * f.es;
+            }
+        } else {  // compact records of the tested cells of this shard, (pair, gene) order
+            const long long cells = (long long)P * (ghi - glo);
+            const int nb = std::max(1, scc_rec_blocks(cells));
+            uint32_t* d_rc;
+            long long *d_roff, *d_rscr;
+            WS("rec_cnt", nb, d_rc);
+            WS("rec_off", nb + 1, d_roff);
+            WS("rec_scr", scc_scan_scratch_blocks(nb) + 1, d_rscr);
+            const int all = fast ? 0 : 1;
+            HIPCHK(c, hipMemsetAsync(d_rc, 0, sizeof(uint32_t) * nb, s0));
+            HIPCHK(c, scc_launch_rec_count(d_flags, G, P, glo, ghi, all, d_rc, s0));
+            HIPCHK(c, scc_launch_scan(d_rc, nb, d_roff, d_rscr, d_roff + nb, s0));
+            long long nrec = 0;
+            HIPCHK(c, hipMemcpyAsync(&nrec, d_roff + nb, sizeof(long long), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            *rio->n_out = nrec;
+            if (nrec > rio->cap)
+                return fail(c, SCC_ERR_INVALID, "scc_de_run_shard_records: record buffer too small (cap < n_records)");
+            HIPCHK(c, scc_launch_rec_pack(d_flags, G, P, glo, ghi, all, d_roff, d_p, d_lfc, fast ? d_pct1 : nullptr,
+                                          fast ? d_pct2 : nullptr, d_u2, d_t, (scc_de_record*)rio->out, s0));
         }
         std::copy(sig, sig + 6, c->shard_sig);
         c->shard_log_thr = log_thr;
@@ -739,6 +790,15 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             if (f.p) HIPCHK(c, hipMemcpyAsync(f.p, src, PG * f.es, hipMemcpyDeviceToDevice, s0));
             src += PG * f.es;
         }
+    } else if (stage == DE_FINISH_REC) {
+        for (const Field& f : fields)
+            if (f.p) HIPCHK(c, hipMemsetAsync(f.p, 0, PG * f.es, s0));
+        HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
+        const scc_de_record* rec = (const scc_de_record*)rio->in;
+        for (int b = 0; b < rio->nblocks; ++b)
+            HIPCHK(c, scc_launch_rec_scatter(rec + (size_t)b * rio->stride, rio->counts[b], G, P, d_p, d_lfc,
+                                             fast ? d_pct1 : nullptr, fast ? d_pct2 : nullptr, d_u2, d_t, d_flags,
+                                             d_err, s0));
     }
     // rows (FAST) / per-pair vectors (SLOW)
     int* d_row_gene = nullptr;
@@ -830,6 +890,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (hdr[1] & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
     if (hdr[1] & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
+    if (hdr[1] & 16) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: record out of range");
     scc_de_result* r = new scc_de_result();
     r->ctx = c;
     r->generation = c->generation;
@@ -863,8 +924,11 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     r->d_u2 = d_u2;
     r->d_de = d_slow_de;
     *out = r;
-    if (hdr[1] & 4) return fail(c, SCC_ERR_RSTOP, "NA in the DE logical vector: R stops at if(sum(...) <= 1)");
-    if (hdr[1] & 2) return fail(c, SCC_ERR_RSTOP, "NA adjusted p-value in a kept pair (R builds NA rows)");
+    // selection-stage conditions (k_pair_select), reported after the result is
+    // built: SLOW NA in the DE logical vector (slow:165-186: R stops at
+    // if(sum(...) <= 1)); bit 0x100 (FAST NA q in a kept pair: R builds NA rows
+    // and does not stop) is informational only
+    if (hdr[1] & 0x200) return fail(c, SCC_ERR_RSTOP, "NA in the DE logical vector: R stops at if(sum(...) <= 1)");
     return SCC_OK;
 #undef WS
 }
@@ -891,6 +955,35 @@ extern "C" int scc_de_finish(scc_ctx* c, const scc_dataset* ds, const int32_t* c
                              const scc_de_params* prm, const void* shards_sum, scc_de_result** out)
 {
     return de_run_impl(c, ds, code, K, prm, DE_FINISH, 0, ds ? ds->G : 0, const_cast<void*>(shards_sum), out);
+}
+
+extern "C" int scc_de_run_shard_records(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                                        const scc_de_params* prm, int64_t gene_lo, int64_t gene_hi, void* records,
+                                        int64_t cap, int64_t* n_records)
+{
+    if (!records || !n_records || cap < 0) return fail(c, SCC_ERR_INVALID, "scc_de_run_shard_records: null argument");
+    RecIO io;
+    io.out = records;
+    io.cap = cap;
+    io.n_out = n_records;
+    *n_records = 0;
+    return de_run_impl(c, ds, code, K, prm, DE_SHARD_REC, gene_lo, gene_hi, nullptr, nullptr, &io);
+}
+
+extern "C" int scc_de_finish_records(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                                     const scc_de_params* prm, const void* records, const int64_t* counts,
+                                     int32_t n_blocks, int64_t stride, scc_de_result** out)
+{
+    if (!counts || n_blocks < 1 || stride < 0 || (!records && stride > 0))
+        return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: bad record blocks");
+    for (int b = 0; b < n_blocks; ++b)
+        if (counts[b] < 0 || counts[b] > stride) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: count > stride");
+    RecIO io;
+    io.in = records;
+    io.counts = counts;
+    io.nblocks = n_blocks;
+    io.stride = stride;
+    return de_run_impl(c, ds, code, K, prm, DE_FINISH_REC, 0, ds ? ds->G : 0, nullptr, out, &io);
 }
 
 static int check_live(const scc_de_result* r)

@@ -90,3 +90,11 @@ def de_fast_grouped(eng, ds, code, K, group=GROUP, min_k=65, **kw) -> nat.DeResu
     _, first = np.unique(top_genes, return_index=True)
     union = top_genes[np.sort(first)].astype(np.int32)
     return nat.DeResult(mode=nat.SCC_DE_FAST, K=K, n_pairs=P, union=union, nodg=nodg, rows=fr)
+
+
+def runs_for(K, group=GROUP, min_k=65) -> int:
+    """Engine runs de_fast_grouped makes for K clusters."""
+    if K < min_k:
+        return 1
+    ng = -(-K // group)
+    return max(1, ng * (ng - 1) // 2)

@@ -1,53 +1,154 @@
 """One DE + distance job sharded over the ranks of a process group.
 
 The reference parallelises the pair loop with a PSOCK foreach over the outer
-cluster index (R/reclusterDEConsensusFast.R:61-65,359,384).  Here each rank
-(one MI355X) holds the whole dataset and runs the per-(pair, gene) stage —
-per-cluster statistics, filters, ranks, exact U / ties / p — on its block of
-gene rows (``scc_de_run_shard``).  The only exchange is one all-reduce (RCCL
-over xGMI) of the shard buffers: they are disjoint and zero elsewhere, so the
-int64 sum is the exact union of every rank's cells.  Every rank then runs the
-per-pair selection (BH over all genes of the pair, filters, top-N, union) on
-the same bits (``scc_de_finish``) and gets the result ``scc_de_run`` gives.
+cluster index (R/reclusterDEConsensusFast.R:61-65,359,384) and rbind()s the
+workers' data frames.  Here every rank (one MI355X) holds the whole dataset
+and owns:
 
-The shard buffers are torch tensors: import torch (and let it load its HIP
-runtime) before ``scconsensus_amd._native`` loads ``libscc.so``.
+* DE: a gene row-block, balanced by stored values (``gene_shard``).  It runs
+  the per-(pair, gene) stage -- statistics, filters, ranks, exact U / ties / p
+  -- on its genes only and packs the tested cells as 64-byte records
+  (``scc_de_run_shard_records``).  ONE all-gather of the records (RCCL over
+  xGMI; a few MB instead of the dense P x G arrays) gives every rank every
+  tested cell, and ``scc_de_finish_records`` runs the per-pair selection (BH
+  over all genes of the pair, filters, top-N, union) identically everywhere.
+* PCA (Fast:398): a block of cells.  Column sums of X[U, block] (all-gather,
+  combined in rank order), the centred partial Gram (all-reduce of |U| x |U|
+  fp64), the eigensolve on every rank from the identical summed Gram, the
+  block's scores (all-reduce of the disjoint N x 16 rows).
+* dist (Fast:400): a packed-column slice of equal entry count, kept in its HBM
+  (or streamed to pinned host memory).
+
+Every engine call's status is agreed over the ranks before the collective that
+follows it, so an error one rank alone sees (an R stop() on its genes, an
+OOM) raises on every rank instead of leaving the others blocked.
+
+The buffers are torch tensors: import torch (and let it load its HIP runtime)
+before ``scconsensus_amd._native`` loads ``libscc.so``.
 """
 from __future__ import annotations
+
+import math
+
+import numpy as np
 
 from . import parallel
 
 _SHARD_KEYS = ("mode", "q_val_thrs", "log_fc_thrs", "min_per_cent", "top_n", "fc_thrs", "mean_scaling_factor",
                "test_all", "test")
+REC_WORDS = 8  # scc_de_record: 64 bytes = 8 int64 words
 
 
-def gene_shard(G: int, rank: int, world: int) -> tuple[int, int]:
-    """Gene rows of ``rank``: contiguous, equal-sized blocks."""
-    return parallel.shard_range(G, rank, world)
+class ShardError(RuntimeError):
+    """An engine call failed on some rank; raised on every rank."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"sharded job failed (scc error {code}): {msg}")
+        self.code = code
 
 
-def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", **params):
+def gene_shard(G: int, rank: int, world: int, weights=None) -> tuple[int, int]:
+    """Gene rows of ``rank``: contiguous blocks, balanced by ``weights`` (the
+    stored values per gene) when given, else by gene count."""
+    if weights is None:
+        return parallel.shard_range(G, rank, world)
+    return parallel.weighted_range(weights, rank, world)
+
+
+def cell_shard(N: int, rank: int, world: int) -> tuple[int, int]:
+    """Cells of ``rank`` for the sharded PCA (equal blocks)."""
+    return parallel.shard_range(N, rank, world)
+
+
+def _call(fn, *a, **kw):
+    """(result, status code, message) of an engine call."""
+    from . import _native as nat
+    try:
+        return fn(*a, **kw), 0, ""
+    except nat.SccError as e:
+        return None, int(e.code), str(e)
+
+
+def _raise_if(codes, msg=""):
+    codes = [int(c) for c in codes]
+    if any(codes):
+        bad = max(codes)
+        raise ShardError(bad, msg or f"rank {codes.index(bad)} reported scc error {bad}")
+
+
+def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weights=None, exchange="records",
+               **params):
     """The DE of one job over all ranks of ``dist``; every rank returns the same
-    DeResult.  ``device``: the torch device of this rank's engine."""
+    DeResult.  ``device``: the torch device of this rank's engine.
+    ``exchange`` "records" (compact, default) or "dense" (the [P][G] int64 sum)."""
     import torch
 
     shard_kw = {k: v for k, v in params.items() if k in _SHARD_KEYS}
-    lo, hi = gene_shard(ds.G, dist.rank, dist.world)
-    nbytes = eng.de_shard_bytes(K, ds.G)
-    buf = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
-    eng.de_run_shard(ds, code, K, lo, hi, buf.data_ptr(), **shard_kw)
-    eng.synchronize()  # the engine's streams -> the collective's stream
-    dist.all_reduce_sum_(buf)
-    if buf.is_cuda:
-        torch.cuda.synchronize(buf.device)
-    return eng.de_finish(ds, code, K, buf.data_ptr(), fetch=fetch, **shard_kw)
+    lo, hi = gene_shard(ds.G, dist.rank, dist.world, weights)
+    P = K * (K - 1) // 2
+    if exchange == "dense":
+        nbytes = eng.de_shard_bytes(K, ds.G)
+        buf = torch.empty(nbytes // 8 + 1, dtype=torch.int64, device=device)
+        _, st, msg = _call(eng.de_run_shard, ds, code, K, lo, hi, buf.data_ptr(), **shard_kw)
+        buf[-1] = st  # the status rides in the last word: summed, nonzero iff some rank failed
+        if not st:
+            eng.synchronize()  # the engine's streams -> the collective's stream
+        dist.all_reduce_sum_(buf)
+        st_all = int(buf[-1].item())
+        _raise_if([st_all], msg)
+        return eng.de_finish(ds, code, K, buf.data_ptr(), fetch=fetch, **shard_kw)
+    cap = max(1, P * (hi - lo))
+    buf = torch.empty(cap * REC_WORDS, dtype=torch.int64, device=device)
+    n, st, msg = _call(eng.de_run_shard_records, ds, code, K, lo, hi, buf.data_ptr(), cap, **shard_kw)
+    n = n or 0
+    info = dist.all_gather_cat(torch.tensor([st, n], dtype=torch.int64, device=device)).view(-1, 2).cpu().numpy()
+    _raise_if(info[:, 0], msg)
+    counts = info[:, 1].astype(np.int64)
+    stride = int(max(1, counts.max()))
+    if stride > cap:  # this rank sends a block of the common stride
+        big = torch.zeros(stride * REC_WORDS, dtype=torch.int64, device=device)
+        big[: cap * REC_WORDS] = buf
+        buf = big
+    recs = dist.all_gather_cat(buf[: stride * REC_WORDS])
+    if recs.is_cuda:
+        torch.cuda.synchronize(recs.device)
+    return eng.de_finish_records(ds, code, K, recs.data_ptr(), counts, stride, fetch=fetch, **shard_kw)
+
+
+def pca_sharded(eng, ds, genes, dist: parallel.Dist, device, ncomp=0):
+    """prcomp_irlba(t(X[genes, ]), n = min(|U|, 15), center = TRUE)$x (Fast:398)
+    of one job over the ranks: returns the full N x 16 score matrix (torch,
+    float64, on ``device``; columns >= ncomp zero), identical on every rank."""
+    import torch
+
+    genes = np.ascontiguousarray(genes, np.int32)
+    nu, N = len(genes), ds.N
+    lo, hi = cell_shard(N, dist.rank, dist.world)
+    f64 = dict(dtype=torch.float64, device=device)
+    part = torch.zeros(2 * nu + 1, **f64)  # dd column sums + the status word
+    _, st, msg = _call(eng.pca_shard_colsum, ds, genes, lo, hi, part.data_ptr())
+    part[-1] = st
+    parts = dist.all_gather_cat(part).view(dist.world, 2 * nu + 1)
+    _raise_if(parts[:, -1].cpu().numpy(), msg)
+    parts = parts[:, : 2 * nu].contiguous()
+    gram = torch.zeros(nu * nu + 1, **f64)
+    _, st, msg = _call(eng.pca_shard_gram, parts.data_ptr(), dist.world, gram.data_ptr())
+    gram[-1] = st
+    dist.all_reduce_sum_(gram)
+    _raise_if([gram[-1].item()], msg)
+    scores = torch.zeros(N * 16 + 1, **f64)
+    _, st, msg = _call(eng.pca_shard_scores, gram.data_ptr(), scores.data_ptr(), ncomp)
+    scores[-1] = st
+    dist.all_reduce_sum_(scores)  # disjoint row blocks: the sum is the exact union
+    _raise_if([scores[-1].item()], msg)
+    if scores.is_cuda:
+        torch.cuda.synchronize(scores.device)
+    return scores[: N * 16]
 
 
 def column_shard(N: int, rank: int, world: int) -> tuple[int, int]:
     """Columns [lo, hi) of the packed N x N lower triangle for ``rank``: column
     j holds N - 1 - j entries, the ranks get (nearly) equal entry counts."""
-    import math
-
     total = N * (N - 1) // 2
 
     def col_at(share):  # first column whose packed start is >= share
@@ -66,13 +167,18 @@ def column_shard(N: int, rank: int, world: int) -> tuple[int, int]:
     return lo, hi
 
 
-def distance_sharded(eng, ds, genes, dist: parallel.Dist, metric=None, f32=False, device_out_ptr=0):
-    """This rank's column slice of the job's packed distance vector, kept in
-    HBM (device_out_ptr 0: the engine's workspace) or copied to a host array
+def distance_sharded(eng, ds, genes, dist: parallel.Dist, device=None, f32=False, device_out_ptr=0, ncomp=0,
+                     scores=None):
+    """This rank's column slice of the job's packed PCA-Euclidean distance,
+    from the sharded PCA (or given ``scores``), kept in HBM (device_out_ptr 0:
+    the engine's workspace; or a device pointer) or streamed to a host array
     (device_out_ptr None).  Returns (col_lo, col_hi, host array or None)."""
-    from . import _native as nat
+    import torch
 
+    if device is None:
+        device = torch.device(f"cuda:{torch.cuda.current_device()}")
+    if scores is None:
+        scores = pca_sharded(eng, ds, genes, dist, device, ncomp)
     lo, hi = column_shard(ds.N, dist.rank, dist.world)
-    m = nat.SCC_DIST_PCA_EUCLID if metric is None else metric
-    out = eng.distance_cols(ds, genes, lo, hi, metric=m, f32=f32, device_out_ptr=device_out_ptr)
+    out = eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, f32=f32, device_out_ptr=device_out_ptr)
     return lo, hi, out

@@ -1,8 +1,10 @@
 """GPU, 2 processes: the sharded job through a real process
 group.  Both ranks share the one MI355X of the test box (gloo carries the
-all-reduce; on a node each rank owns a GPU and RCCL carries it).  Every rank
-must end with the unsharded union, and its distance column slice must equal
-the same slice of the unsharded distance."""
+collectives; on a node each rank owns a GPU and RCCL carries them).  Every
+rank must end with the unsharded union and rows (bit for bit: the record
+exchange is exact), and its distance column slice -- from the PCA sharded
+over cell blocks -- must equal the same slice of the unsharded distance
+within 1e-6 (the Gram's partial sums are added in another order and config A's PC 15 is near-degenerate)."""
 import json
 import os
 import socket
@@ -27,14 +29,14 @@ names, code = api.select_clusters(data.labels, 10)
 K = len(names)
 ds = eng.dataset_csc(data.indptr, data.indices, data.data, data.G, data.N)
 got = sharded.de_sharded(eng, ds, code, K, d, torch.device("cuda:0"), fetch="rows")
-lo, hi, part = sharded.distance_sharded(eng, ds, got.union, d, device_out_ptr=None)
+lo, hi, part = sharded.distance_sharded(eng, ds, got.union, d, torch.device("cuda:0"), device_out_ptr=None)
 ref = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows")
 full = eng.distance(ds, ref.union)
 N = data.N
 s0, s1 = lo * (2 * N - lo - 1) // 2, hi * (2 * N - hi - 1) // 2
 print(json.dumps({"rank": d.rank, "union": bool(np.array_equal(got.union, ref.union)),
                   "p": bool(np.array_equal(got.rows.p, ref.rows.p)), "u2": bool(np.array_equal(got.rows.u2, ref.rows.u2)),
-                  "dist": bool(np.array_equal(part, full[s0:s1])), "lo": lo, "hi": hi, "n": len(got.union)}))
+                  "dist": bool(np.max(np.abs(part - full[s0:s1])) < 1e-6), "lo": lo, "hi": hi, "n": len(got.union)}))
 d.close()
 '''
 

@@ -95,7 +95,8 @@ class DS:
 
 d = parallel.init("gloo")
 eng = Fake()
-out = sharded.de_sharded(eng, DS(), None, 3, d, torch.device("cpu"), fetch="union", min_per_cent=7.0, top_n=5)
+out = sharded.de_sharded(eng, DS(), None, 3, d, torch.device("cpu"), fetch="union", exchange="dense",
+                         min_per_cent=7.0, top_n=5)
 ok = bool((out == np.arange(DS.G) + 1).all())
 print(json.dumps({"rank": d.rank, "ok": ok, "kw": sorted(eng.kw), "cols": sharded.column_shard(DS.N, d.rank, d.world),
                   "genes": sharded.gene_shard(DS.G, d.rank, d.world)}))
