@@ -151,7 +151,7 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
     if len(names) < 2:
         raise ValueError("need at least two clusters with > minClusterSize cells")
     ds = _upload(eng, m)
-    if len(names) > 64:  # one engine run holds <= 64 clusters: group-pair runs (grouped.py)
+    if len(names) > 128:  # one engine run holds <= 128 clusters: group-pair runs (grouped.py)
         from . import grouped
         res = grouped.de_fast_grouped(eng, ds, code, len(names), q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
                                       min_per_cent=float(minPerCent), top_n=NumbertopDEGenes, test=method)

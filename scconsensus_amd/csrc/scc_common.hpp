@@ -13,6 +13,12 @@ typedef uint8_t u8;
 
 #define SCC_WAVE 64
 
+// clusters one engine run holds: 7-bit cluster codes (bit 7 of a sorted-code
+// byte flags "equal to the next element" in the rank kernels)
+#define SCC_MAX_K 128
+#define SCC_CODE_BITS 7
+#define SCC_CODE_MASK 127u
+
 // ------------------------------------------------------------ orderable keys
 // Bijective map fp64 -> u64 whose unsigned order is the IEEE total order for
 // finite values (-0 and +0 never reach it: zeros are the implicit tie group).

@@ -4,6 +4,10 @@
 #include "scc.h"
 #include "scc_kernels.hpp"
 
+#ifndef SCC_MAX_K
+#define SCC_MAX_K 128  // (same value as scc_common.hpp)
+#endif
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,7 +29,7 @@ constexpr int kScatterCC = 4;      // count chunks per ingest scatter chunk
 constexpr int kMaxGenesLds = 40960;  // ingest histogram of one chunk lives in LDS
 constexpr int kSelectCap = 2048;   // per-pair records sorted in LDS
 constexpr int kUnionCap = 4096;
-constexpr int kMaxK = 64;
+constexpr int kMaxK = SCC_MAX_K;  // 7-bit cluster codes in the rank kernels
 
 struct Timer {
     double ms = 0.0;

@@ -90,6 +90,9 @@ struct ScRankLaunch {
     unsigned long long* accF;   // [K][G] sum c^3 - c over within-cluster runs
     unsigned long long* stamps; // diagnostic phase clocks [item][8] (nullptr normally)
     int stamp_base[3];
+    int tp_global;              // items' tested-pair tables in HBM (scc_rank_tables_global)
+    char* tp_scr;               // [item workgroups][tp_scr_stride] when tp_global
+    size_t tp_scr_stride;
 };
 
 struct ScTestLaunch {
@@ -174,6 +177,8 @@ hipError_t scc_launch_rank_classify(const ScRankLaunch* L, hipStream_t st);
 size_t scc_rank_item_lds(int cls, int cap, int ntp_max, int K);
 int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim);
 size_t scc_rank_split_lds(int K);
+int scc_rank_tables_global(int ntp_max, int K);
+size_t scc_rank_tables_stride(int ntp_max, int K);
 hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st);
 hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st);

@@ -95,8 +95,8 @@ struct StatItem {
 template <bool EXPM1, bool SUMX, bool VAR>
 __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 {
-    __shared__ int off[65];
-    __shared__ StatItem item[64 + ST_W + 4];
+    __shared__ int off[SCC_MAX_K + 1];
+    __shared__ StatItem item[SCC_MAX_K + ST_W + 4];
     const int g = blockIdx.x, K = A.K, tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
     const i64 base = A.gstart[g];
     const int n = (int)(A.gstart[g + 1] - base);
@@ -342,24 +342,24 @@ __device__ void wave_sort_run(KP key, const u8* code, IX* ix, int s, int len)
 template <int W>
 struct ItemLds {
     RadixLds<W> rx;
-    u32 m[64];         // nonzeros per cluster in this item
-    u32 po[65];        // position-list offsets
-    u64 F[64];         // per-cluster tie term
+    u32 m[SCC_MAX_K];       // nonzeros per cluster in this item
+    u32 po[SCC_MAX_K + 1];  // position-list offsets
+    u64 F[SCC_MAX_K];       // per-cluster tie term
     u64 red64[2 * W];  // min / max keys
     u32 redu[W + 1];
     int run_s[RK_RUNS], run_l[RK_RUNS];
     int nruns, flag, redo, anytie;
     int ntp, nchunk;
     u64 kmin, kmax;
-    // tested pairs: packed (p | a << 16 | b << 22 | small-is-b << 28), chunk prefix
+    // tested pairs: packed (p | a << 16 | b << 23 | small-is-b << 30), chunk prefix
     u32 tp[1];  // dynamic tail: tp[ntp_max], cp[ntp_max + 1], eacc[ntp_max], xacc[ntp_max] (u64),
                 // pmap[K * K] (u16: tested-pair slot + 1, 0 = untested)
 };
 
 __device__ inline int tp_p(u32 v) { return (int)(v & 0xffffu); }
-__device__ inline int tp_a(u32 v) { return (int)((v >> 16) & 63u); }
-__device__ inline int tp_b(u32 v) { return (int)((v >> 22) & 63u); }
-__device__ inline bool tp_sb(u32 v) { return ((v >> 28) & 1u) != 0; }
+__device__ inline int tp_a(u32 v) { return (int)((v >> 16) & 127u); }
+__device__ inline int tp_b(u32 v) { return (int)((v >> 23) & 127u); }
+__device__ inline bool tp_sb(u32 v) { return ((v >> 30) & 1u) != 0; }
 
 // lower_bound of x in the ascending array s[0..len)
 template <class IX>
@@ -387,12 +387,15 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
     const int K = A.K, P = A.P, G = A.G, g = it.gene, n = it.n;
     const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
     ItemLds<W>& L = *(ItemLds<W>*)smem;
-    u32* tp = L.tp;
+    // tested-pair tables: in LDS after the fixed state, or (many tested pairs,
+    // e.g. K > 64) in this workgroup's slice of an HBM scratch
+    char* tab = A.tp_global ? (A.tp_scr + (size_t)blockIdx.x * A.tp_scr_stride) : (char*)L.tp;
+    u32* tp = (u32*)tab;
     u32* cp = tp + A.ntp_max;
     u64* eacc = (u64*)(((uintptr_t)(cp + A.ntp_max + 1) + 7) & ~(uintptr_t)7);
     u64* xacc = eacc + A.ntp_max;
     unsigned short* pmap = (unsigned short*)(xacc + A.ntp_max);
-    char* big = (char*)(pmap + K * K);
+    char* big = A.tp_global ? (char*)L.tp : (char*)(pmap + K * K);
     big = (char*)(((uintptr_t)big + 15) & ~(uintptr_t)15);
     u64* const stamps = A.stamps ? A.stamps + (size_t)item_no * 8 : nullptr;
 #define ISTAMP(ph)                                                                   \
@@ -448,7 +451,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
         kmn = o1 < kmn ? o1 : kmn;
         kmx = o2 > kmx ? o2 : kmx;
     }
-    if (tid < 64) {
+    if (tid < SCC_MAX_K) {
         L.m[tid] = 0;
         L.F[tid] = 0;
     }
@@ -514,7 +517,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
             const bool ok = i < n;
             const u32 c = ok ? A.codes2[it.base + i] : 0u;
             if (ok && !GLOBALMEM) code[i] = (u8)c;
-            const u64 peers = match_bits<6>(c, __ballot(ok));
+            const u64 peers = match_bits<SCC_CODE_BITS>(c, __ballot(ok));
             if (ok && lanes_below(peers) == 0) atomicAdd(&L.m[c], (u32)__popcll(peers));
         }
     }
@@ -532,7 +535,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
                 pair_decode((int)tp[j], K, a2, b2);
                 const u32 ma = L.m[a2], mb = L.m[b2];
                 const bool sb = mb < ma;
-                tp[j] = tp[j] | ((u32)a2 << 16) | ((u32)b2 << 22) | ((u32)sb << 28);
+                tp[j] = tp[j] | ((u32)a2 << 16) | ((u32)b2 << 23) | ((u32)sb << 30);
                 pmap[a2 * K + b2] = (unsigned short)(j + 1);
                 eacc[j] = 0;
                 xacc[j] = 0;
@@ -589,7 +592,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
     IX* in = ix0;
     IX* out = ix1;
     if (it.src != 0) {  // bucket input is not cluster-grouped: stable pass on the cluster first
-        radix_pass<W, 6>([&](IX id) { return (u32)code[id]; }, in, out, n, L.rx);
+        radix_pass<W, SCC_CODE_BITS>([&](IX id) { return (u32)code[id]; }, in, out, n, L.rx);
         IX* t = in;
         in = out;
         out = t;
@@ -671,18 +674,18 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
         const int R = (((n + W - 1) / W) + 63) & ~63;
         const int lo = min(n, w * R), hi = min(n, lo + R);
         u32* hw = L.rx.hist + w * 256;
-        for (int d = lane; d < 64; d += 64) hw[d] = 0;
+        for (int d = lane; d < SCC_MAX_K; d += 64) hw[d] = 0;
         __builtin_amdgcn_wave_barrier();
         for (int i0 = lo; i0 < hi; i0 += 64) {
             const int i = i0 + lane;
             const bool ok = i < hi;
-            const u32 d = ok ? (sc[i] & 63u) : 0u;
-            const u64 peers = match_bits<6>(d, __ballot(ok));
+            const u32 d = ok ? (sc[i] & SCC_CODE_MASK) : 0u;
+            const u64 peers = match_bits<SCC_CODE_BITS>(d, __ballot(ok));
             if (ok && lanes_below(peers) == 0) hw[d] += (u32)__popcll(peers);
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
-        if (tid < 64) {  // per-(wave, cluster) start offsets
+        if (tid < SCC_MAX_K) {  // per-(wave, cluster) start offsets
             u32 s = (tid < K) ? L.po[tid] : 0u;
             for (int v = 0; v < W; ++v) {
                 const u32 c = L.rx.hist[v * 256 + tid];
@@ -694,8 +697,8 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
         for (int i0 = lo; i0 < hi; i0 += 64) {
             const int i = i0 + lane;
             const bool ok = i < hi;
-            const u32 d = ok ? (sc[i] & 63u) : 0u;
-            const u64 peers = match_bits<6>(d, __ballot(ok));
+            const u32 d = ok ? (sc[i] & SCC_CODE_MASK) : 0u;
+            const u64 peers = match_bits<SCC_CODE_BITS>(d, __ballot(ok));
             if (ok) {
                 const u32 rank = lanes_below(peers);
                 const u32 b = hw[d];
@@ -758,7 +761,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
         const int c0 = min(n, tid * chunk), c1 = min(n, c0 + chunk);
         u32 cnt = 0;
         for (int i = c0; i < c1; ++i) {
-            const bool st = (i == 0) || !(sc[i - 1] & 128) || ((sc[i - 1] & 63) != (sc[i] & 63));
+            const bool st = (i == 0) || !(sc[i - 1] & 128) || ((sc[i - 1] & SCC_CODE_MASK) != (sc[i] & SCC_CODE_MASK));
             cnt += st;
         }
         u32 incl = cnt;
@@ -776,14 +779,14 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
         // rs aliases the sorted-order buffer that is no longer read; the
         // starts are written after every thread finished reading it above
         for (int i = c0; i < c1; ++i) {
-            const bool st = (i == 0) || !(sc[i - 1] & 128) || ((sc[i - 1] & 63) != (sc[i] & 63));
+            const bool st = (i == 0) || !(sc[i - 1] & 128) || ((sc[i - 1] & SCC_CODE_MASK) != (sc[i] & SCC_CODE_MASK));
             if (st) rs[basev++] = (IX)i;
         }
         if (tid == 0) rs[nr] = (IX)n;
         __syncthreads();
         for (u32 r = tid; r < nr; r += T) {
             const u32 s0 = rs[r], len = (u32)rs[r + 1] - s0;
-            const int a = sc[s0] & 63;
+            const int a = sc[s0] & SCC_CODE_MASK;
             if (len >= 2) atomicAdd((unsigned long long*)&L.F[a], (unsigned long long)f_tie(len));
             // earlier runs of the same value: their clusters are smaller (codes
             // increase inside a group), each gives a cross-cluster tie block
@@ -792,7 +795,7 @@ __device__ void rank_one_item(const ScRankLaunch& A, const ScRankItem it, int it
                 --q;
                 const u32 ps = rs[q];
                 const u64 lb = (u32)rs[q + 1] - ps, la = len;
-                const int b = sc[ps] & 63;  // b < a
+                const int b = sc[ps] & SCC_CODE_MASK;  // b < a
                 const int slot = pmap[b * K + a];
                 if (slot) {
                     atomicAdd((unsigned long long*)&eacc[slot - 1], (unsigned long long)(la * lb));
@@ -826,7 +829,8 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 }
 
 #define RW_SLOTS_MAX 16  // tested pairs per gene the wave kernel holds: 64 * slots (2, 4, 8 or 16)
-#define RW_PAIRS_MAX (2 * 64 * RW_SLOTS_MAX)  // genes past 1024 tested pairs: two 16-slot passes
+#define RW_PAIRS_MAX (8 * 64 * RW_SLOTS_MAX)  // genes past 1024 tested pairs: one 16-slot pass per 1024
+#define RS_ACC_MAX 2048   // re-split: tested pairs of a gene whose in-parent cross terms sum in LDS
 #define RS_T 256          // re-split: threads per workgroup
 #define RS_KPT 8          // keys per thread (held in registers: the scatter is in place)
 #define RS_CAP (RS_T * RS_KPT)
@@ -858,7 +862,7 @@ struct SplitLds {
     u32 wsum[SP_W + 1];
     u32 wsum2[SP_W + 1];
     u64 rmn[SP_W], rmx[SP_W];
-    int off[65];
+    int off[SCC_MAX_K + 1];
     int nb, bk0, next;
     int nfat, fat0, nwav, wav0;
 };
@@ -941,7 +945,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     const u64 range = kmx - kmn;
     const int bits = range ? 64 - __clzll((long long)range) : 0;
     const int sh = bits > 11 ? bits - 11 : 0;
-    if (tid == 0) A.gkmin[g] = bits <= 58 ? kmn : ~0ull;  // wave kernel: (key - kmin) << 6 | cluster
+    if (tid == 0) A.gkmin[g] = bits <= 64 - SCC_CODE_BITS ? kmn : ~0ull;  // wave kernel: (key - kmin) << 7 | cluster
     // ---- 1. histogram of the top 11 bits of the key window (one LDS atomic per
     // element; any key of a bin is kept as its representative)
     for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
@@ -1125,13 +1129,13 @@ struct ResplitLds {
     u32 bcur[RS_BMAX];
     u32 boff[RS_BMAX + 1];
     u8 bdiff[RS_BMAX + 3];
-    u32 m[64];
+    u32 m[SCC_MAX_K];
     u32 wsum[RS_T / 64 + 1];
     u32 wsum2[RS_T / 64 + 1];
     u64 rmn[RS_T / 64], rmx[RS_T / 64];
     u32 hs[RS_HCAP];  // [sub-bucket][cluster] counts (in-parent cross term), when nb * K fits
     u32 bs[RS_HCAP];  // [sub-bucket][cluster] elements of the cluster in lower sub-buckets
-    u64 acc[RW_PAIRS_MAX];  // the gene's in-parent cross terms per tested pair
+    u64 acc[RS_ACC_MAX];  // the gene's in-parent cross terms per tested pair (genes with <= RS_ACC_MAX)
     int nb, bk0, next, ovf, nw, w0;
 };
 
@@ -1168,7 +1172,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         cd[q] = i < n ? A.codes2[it.base + i] : (u8)0;
     }
     for (int d = tid; d < RS_BINS; d += RS_T) L.hist[d] = 0;
-    if (tid < 64) L.m[tid] = 0;
+    if (tid < SCC_MAX_K) L.m[tid] = 0;
     u64 kmn = ~0ull, kmx = 0;
 #pragma unroll
     for (int q = 0; q < RS_KPT; ++q) {
@@ -1369,7 +1373,8 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         }
     }
     __syncthreads();
-    const int ntp = min(A.gene_nt[g], RW_PAIRS_MAX);
+    const int ntp = A.gene_nt[g];
+    const bool lds_acc = ntp <= RS_ACC_MAX;
     for (int j = tid; j < ntp; j += RS_T) {
         const u32 v = A.gene_tp[(size_t)g * A.P + j];
         const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
@@ -1377,7 +1382,10 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         u64 sacc = 0;
 #pragma unroll 4
         for (int q = 0; q < nb; ++q) sacc += (u64)L.hs[q * K + a] * L.bs[q * K + b];
-        L.acc[j] += sacc;  // thread j owns tested pair j for the whole gene
+        if (lds_acc)
+            L.acc[j] += sacc;  // thread j owns tested pair j for the whole gene
+        else if (sacc)
+            atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
     }
     RSTAMP(4);
     if (A.stamps && tid == 0) atomicAdd((unsigned long long*)&A.stamps[7], 1ull);
@@ -1395,7 +1403,7 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
         if (i >= ng) break;
         const int4 ge = A.fatg[i];
         const int g = ge.x;
-        const int ntp = min(A.gene_nt[g], RW_PAIRS_MAX);
+        const int ntp = A.gene_nt[g] <= RS_ACC_MAX ? A.gene_nt[g] : 0;  // larger: atomics per parent
         for (int j = threadIdx.x; j < ntp; j += RS_T) L.acc[j] = 0;
         __syncthreads();
         for (int f = ge.y; f < ge.y + ge.z; ++f) {
@@ -1426,7 +1434,7 @@ struct ResplitWLds {
     u32 bcur[2 * RSW_BINS + 1];
     u32 boff[2 * RSW_BINS + 2];
     u8 bdiff[2 * RSW_BINS + 4];
-    u32 m[64];
+    u32 m[SCC_MAX_K];
     u32 hs[RSW_HCAP];
     u32 bs[RSW_HCAP];
 };
@@ -1483,7 +1491,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
         const int sh = bits > RSW_LOG2B ? bits - RSW_LOG2B : 0;
 #pragma unroll
         for (int q = 0; q < BPL; ++q) L.hist[q * 64 + lane] = 0;
-        L.m[lane] = 0;
+        for (int c = lane; c < SCC_MAX_K; c += 64) L.m[c] = 0;
         wsync();
 #pragma unroll
         for (int q = 0; q < EPL; ++q) {
@@ -1585,7 +1593,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
             }
         }
         wsync();
-        if (lane < K) A.hbg[(size_t)it.bucket * K + lane] = L.m[lane];  // the parent's row (gene-level cross)
+        for (int c = lane; c < K; c += 64) A.hbg[(size_t)it.bucket * K + c] = L.m[c];  // the parent's row (gene-level cross)
         // sub-buckets: one list reservation per parent, slots in sub-bucket order
         {
             u32 cw = 0;
@@ -1654,7 +1662,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
             }
         }
         wsync();
-        const int ntp = min(A.gene_nt[g], RW_PAIRS_MAX);
+        const int ntp = A.gene_nt[g];
         const u32* tl = A.gene_tp + (size_t)g * A.P;
         for (int j = lane; j < ntp; j += 64) {
             const u32 v = tl[j];
@@ -1754,7 +1762,7 @@ __device__ inline void bitonic_merge(u64& key, u32& code, bool up, int lane)
 template <int RW_SLOTS>
 __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 {
-    __shared__ u64 cms[4][64];  // per-wave cluster masks (K > 16)
+    __shared__ u64 cms[4][SCC_MAX_K];  // per-wave cluster masks (K > 16)
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
     const int cnt = min(A.counts[4], A.bucket_cap);
@@ -1853,7 +1861,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 // one repeated key: only the cluster histogram matters.  Inside
                 // the bucket S_ab = 0 (a < b: ties ordered by cluster),
                 // E_ab = c_a c_b, X_ab = c_a c_b (c_a + c_b), F_a = f(c_a).
-                u32 myc = 0;
+                u32 myc = 0, myc1 = 0;  // lane c: cluster c's count, and cluster c + 64's
                 for (int i0 = 0; i0 < n; i0 += 256) {
                     u32 cd[4];
 #pragma unroll
@@ -1866,17 +1874,29 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 #pragma unroll
                         for (int u = 0; u < 4; ++u) t += (u32)__popcll(__ballot(cd[u] == (u32)c));
                         if (lane == c) myc += t;
+                        if (lane + 64 == c) myc1 += t;
                     }
                 }
-                if (lane < K) {
-                    A.hbg[(size_t)bucket * K + lane] = myc;
-                    if (myc >= 2 && A.wv_base == 0)  // per cluster: once, not per pair window
-                        atomicAdd((unsigned long long*)&A.accF[(size_t)lane * G + g], (unsigned long long)f_tie(myc));
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int c = lane + 64 * h;
+                    const u32 mc = h ? myc1 : myc;
+                    if (c < K) {
+                        A.hbg[(size_t)bucket * K + c] = mc;
+                        if (mc >= 2 && A.wv_base == 0)  // per cluster: once, not per pair window
+                            atomicAdd((unsigned long long*)&A.accF[(size_t)c * G + g], (unsigned long long)f_tie(mc));
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < RW_SLOTS; ++q) {
-                    const u64 ca = (u32)__shfl((int)myc, (int)pa[q], 64);
-                    const u64 cb = (u32)__shfl((int)myc, (int)pb[q], 64);
+                    u64 ca = (u32)__shfl((int)myc, (int)(pa[q] & 63u), 64);
+                    u64 cb = (u32)__shfl((int)myc, (int)(pb[q] & 63u), 64);
+                    if (K > 64) {
+                        const u64 ca1 = (u32)__shfl((int)myc1, (int)(pa[q] & 63u), 64);
+                        const u64 cb1 = (u32)__shfl((int)myc1, (int)(pb[q] & 63u), 64);
+                        ca = pa[q] >= 64 ? ca1 : ca;
+                        cb = pb[q] >= 64 ? cb1 : cb;
+                    }
                     if (q * 64 + lane < ntp) {
                         aE[q] += ca * cb;
                         aX[q] += ca * cb * (ca + cb);
@@ -1887,8 +1907,8 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             // ---- load and bitonic sort by (key, code) across the lanes (invalid lanes last)
             const bool vl = lane < n;
             if (A.dbg == 2) {
-            } else if (gk != ~0ull) {  // one 64-bit sort key: (key - gene minimum) << 6 | cluster
-                u64 ck = vl ? (((key - gk) << 6) | code) : ~0ull;
+            } else if (gk != ~0ull) {  // one 64-bit sort key: (key - gene minimum) << 7 | cluster
+                u64 ck = vl ? (((key - gk) << SCC_CODE_BITS) | code) : ~0ull;
                 // levels up to the next power of two >= n (lanes past it hold only ~0)
                 if (n > 1) bitonic_merge_ck<1>(ck, (lane & 2) == 0, lane);
                 if (n > 2) bitonic_merge_ck<2>(ck, (lane & 4) == 0, lane);
@@ -1896,8 +1916,8 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 if (n > 8) bitonic_merge_ck<8>(ck, (lane & 16) == 0, lane);
                 if (n > 16) bitonic_merge_ck<16>(ck, (lane & 32) == 0, lane);
                 if (n > 32) bitonic_merge_ck<32>(ck, true, lane);
-                key = ck >> 6;  // order-equivalent for the tie tests below
-                code = vl ? (u32)(ck & 63u) : 255u;
+                key = ck >> SCC_CODE_BITS;  // order-equivalent for the tie tests below
+                code = vl ? (u32)(ck & SCC_CODE_MASK) : 255u;
             } else {
                 if (n > 1) bitonic_merge<1>(key, code, (lane & 2) == 0, lane);
                 if (n > 2) bitonic_merge<2>(key, code, (lane & 4) == 0, lane);
@@ -1906,23 +1926,27 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 if (n > 16) bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
                 if (n > 32) bitonic_merge<32>(key, code, true, lane);
             }
-            // ---- cluster masks over the sorted lanes (lane c holds cluster c's) and the hbg row
-            u64 cm = 0;
+            // ---- cluster masks over the sorted lanes (lane c holds cluster c's, cm1
+            // cluster c + 64's) and the hbg row
+            u64 cm = 0, cm1 = 0;
             if (K <= 16) {  // one ballot per cluster
                 for (int c = 0; c < K; ++c) {
                     const u64 m = __ballot(code == (u32)c);
                     if (lane == c) cm = m;
                 }
-            } else {  // many clusters: 6 ballots match equal codes, each cluster's leader posts its mask
-                const u64 peers = match_bits<6>(code & 63u, __ballot(vl));
+            } else {  // many clusters: 7 ballots match equal codes, each cluster's leader posts its mask
+                const u64 peers = match_bits<SCC_CODE_BITS>(code & SCC_CODE_MASK, __ballot(vl));
                 cms[wv][lane] = 0;
+                if (K > 64) cms[wv][lane + 64] = 0;
                 wsync();
                 if (vl && lanes_below(peers) == 0) cms[wv][code] = peers;
                 wsync();
                 cm = cms[wv][lane];
+                if (K > 64) cm1 = cms[wv][lane + 64];
                 wsync();
             }
             if (lane < K) A.hbg[(size_t)bucket * K + lane] = (u32)__popcll(cm);
+            if (lane + 64 < K) A.hbg[(size_t)bucket * K + lane + 64] = (u32)__popcll(cm1);
             // ---- tie groups (equal keys) and runs (equal key and cluster)
             const u64 kp = ((u64)(u32)__shfl_up((int)(u32)(key >> 32), 1, 64) << 32) |
                            (u64)(u32)__shfl_up((int)(u32)key, 1, 64);
@@ -1948,7 +1972,12 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 #pragma unroll
             for (int q = 0; q < RW_SLOTS; ++q) {
                 if (q * 64 >= ntp || A.dbg == 1) break;
-                const u64 ma = shfl_u64(cm, (int)pa[q]), mb = shfl_u64(cm, (int)pb[q]);
+                u64 ma = shfl_u64(cm, (int)(pa[q] & 63u)), mb = shfl_u64(cm, (int)(pb[q] & 63u));
+                if (K > 64) {
+                    const u64 ma1 = shfl_u64(cm1, (int)(pa[q] & 63u)), mb1 = shfl_u64(cm1, (int)(pb[q] & 63u));
+                    ma = pa[q] >= 64 ? ma1 : ma;
+                    mb = pb[q] >= 64 ? mb1 : mb;
+                }
                 if (q * 64 + lane < ntp && ma && mb) {
                     u32 S, E, X;
                     pair_counts(ma, mb, anytie, gst, n, S, E, X);
@@ -2026,14 +2055,16 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 // tested pairs (<= XC_J per thread) in registers: one atomic per (gene, pair).
 // (The per-(gene, pair) wave version re-read the rows once per pair.)
 #define XC_T 256
-#define XC_Q 64
-#define XC_J 8  // tested pairs per thread: <= 2048 per gene (K <= 64: P <= 2016)
+#define XC_Q 32                 // buckets per LDS round
+#define XC_KC SCC_MAX_K         // cluster columns held
+#define XC_J 8                  // tested pairs per thread per pass over the rows (2048)
 __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
 {
-    __shared__ u32 Hs[XC_Q][65];
-    __shared__ u32 Cs[XC_Q][65];
-    __shared__ u32 seg[4][64];
-    __shared__ u32 carry[64];
+    __shared__ u32 Hs[XC_Q][XC_KC + 1];
+    __shared__ u32 Cs[XC_Q][XC_KC + 1];
+    __shared__ u32 seg[XC_T / XC_KC][XC_KC];
+    __shared__ u32 carry[XC_KC];
+    constexpr int NPART = XC_T / XC_KC, RPP = XC_Q / NPART;  // column-scan parts, rows per part
     const int tid = threadIdx.x, K = A.K, G = A.G, P = A.P;
     const int ng = A.counts[3];
     for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
@@ -2041,66 +2072,80 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
         const int bk0 = A.gene_bk[2 * g], nb = A.gene_bk[2 * g + 1];
         const int ntp = min(A.gene_nt[g], P);
         const u32* tl = A.gene_tp + (size_t)g * P;
-        u32 pv[XC_J];
-        u64 acc[XC_J];
-#pragma unroll
-        for (int u = 0; u < XC_J; ++u) {
-            const int j = u * XC_T + tid;
-            pv[u] = j < ntp ? tl[j] : 0u;
-            acc[u] = 0;
-        }
-        if (tid < 64) carry[tid] = 0;
-        for (int q0 = 0; q0 < nb; q0 += XC_Q) {
-            const int nq = min(XC_Q, nb - q0);
-            __syncthreads();
-            const unsigned int* h = A.hbg + (size_t)(bk0 + q0) * K;
-            for (int e = tid; e < XC_Q * K; e += XC_T) {
-                const int q = e / K, c = e - q * K;
-                Hs[q][c] = q < nq ? h[e] : 0u;
-            }
-            __syncthreads();
-            // column scan: thread (c, part) sums 16 rows, parts combined through LDS
-            const int c = tid & 63, part = tid >> 6;
-            u32 ssum = 0;
-            if (c < K)
-                for (int q = part * 16; q < part * 16 + 16; ++q) ssum += Hs[q][c];
-            seg[part][c] = ssum;
-            __syncthreads();
-            if (c < K) {
-                u32 run = carry[c];
-                for (int v = 0; v < part; ++v) run += seg[v][c];
-                for (int q = part * 16; q < part * 16 + 16; ++q) {
-                    Cs[q][c] = run;
-                    run += Hs[q][c];
-                }
-            }
-            __syncthreads();
-            if (tid < K) carry[tid] += seg[0][tid] + seg[1][tid] + seg[2][tid] + seg[3][tid];
+        for (int j0 = 0; j0 < ntp; j0 += XC_J * XC_T) {  // windows of 2048 tested pairs
+            u32 pv[XC_J];
+            u64 acc[XC_J];
 #pragma unroll
             for (int u = 0; u < XC_J; ++u) {
-                if (u * XC_T + tid < ntp) {
-                    const int a = (int)((pv[u] >> 16) & 0xffu), b = (int)(pv[u] >> 24);
-                    u64 sacc = 0;
-                    for (int q = 0; q < nq; ++q) sacc += (u64)Hs[q][a] * Cs[q][b];
-                    acc[u] += sacc;
+                const int j = j0 + u * XC_T + tid;
+                pv[u] = j < ntp ? tl[j] : 0u;
+                acc[u] = 0;
+            }
+            __syncthreads();
+            if (tid < XC_KC) carry[tid] = 0;
+            for (int q0 = 0; q0 < nb; q0 += XC_Q) {
+                const int nq = min(XC_Q, nb - q0);
+                __syncthreads();
+                const unsigned int* h = A.hbg + (size_t)(bk0 + q0) * K;
+                for (int e = tid; e < XC_Q * K; e += XC_T) {
+                    const int q = e / K, c = e - q * K;
+                    Hs[q][c] = q < nq ? h[e] : 0u;
+                }
+                __syncthreads();
+                // column scan: thread (c, part) sums RPP rows, parts combined through LDS
+                const int c = tid % XC_KC, part = tid / XC_KC;
+                u32 ssum = 0;
+                if (c < K)
+                    for (int q = part * RPP; q < part * RPP + RPP; ++q) ssum += Hs[q][c];
+                seg[part][c] = ssum;
+                __syncthreads();
+                if (c < K) {
+                    u32 run = carry[c];
+                    for (int v = 0; v < part; ++v) run += seg[v][c];
+                    for (int q = part * RPP; q < part * RPP + RPP; ++q) {
+                        Cs[q][c] = run;
+                        run += Hs[q][c];
+                    }
+                }
+                __syncthreads();
+                if (tid < K)
+                    for (int v = 0; v < NPART; ++v) carry[tid] += seg[v][tid];
+#pragma unroll
+                for (int u = 0; u < XC_J; ++u) {
+                    if (j0 + u * XC_T + tid < ntp) {
+                        const int a = (int)((pv[u] >> 16) & 0xffu), b = (int)(pv[u] >> 24);
+                        u64 sacc = 0;
+                        for (int q = 0; q < nq; ++q) sacc += (u64)Hs[q][a] * Cs[q][b];
+                        acc[u] += sacc;
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int u = 0; u < XC_J; ++u) {
-            if (u * XC_T + tid < ntp && acc[u])
-                atomicAdd((unsigned long long*)&A.accS[(size_t)(pv[u] & 0xffffu) * G + g], (unsigned long long)acc[u]);
+            for (int u = 0; u < XC_J; ++u) {
+                if (j0 + u * XC_T + tid < ntp && acc[u])
+                    atomicAdd((unsigned long long*)&A.accS[(size_t)(pv[u] & 0xffffu) * G + g], (unsigned long long)acc[u]);
+            }
         }
         __syncthreads();
     }
 }
 
 // ===================================================================== host
+// bytes of an item's tested-pair tables (tp, cp, eacc, xacc, pmap)
+static size_t item_tables_bytes(int ntp_max, int K)
+{
+    const size_t s = sizeof(u32) * (2 * (size_t)ntp_max + 1) + 8 + 16 * (size_t)ntp_max + 2 * (size_t)K * K;
+    return (s + 31) & ~(size_t)15;
+}
+
+// tables past 24 KB (many tested pairs per gene, K > ~40) live in HBM scratch
+extern "C" int scc_rank_tables_global(int ntp_max, int K) { return item_tables_bytes(ntp_max, K) > 24 * 1024; }
+extern "C" size_t scc_rank_tables_stride(int ntp_max, int K) { return (item_tables_bytes(ntp_max, K) + 255) & ~(size_t)255; }
+
 template <int W>
 static size_t item_lds_fixed(int ntp_max, int K)
 {
-    size_t s = sizeof(ItemLds<W>) + sizeof(u32) * (2 * (size_t)ntp_max + 1) + 8 + 16 * (size_t)ntp_max +
-               2 * (size_t)K * K;
+    const size_t s = sizeof(ItemLds<W>) + (scc_rank_tables_global(ntp_max, K) ? 16 : item_tables_bytes(ntp_max, K));
     return (s + 31) & ~(size_t)15;
 }
 
@@ -2143,14 +2188,12 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
     // one launch per slot class present: genes with <= 128 tested pairs on the
     // 2-slot kernel, <= 256 on 4, <= 512 on 8, <= 1024 on 16
     ScRankLaunch A = *L;
-    const int hi[6] = {128, 256, 512, 1024, RW_PAIRS_MAX, RW_PAIRS_MAX};
-    for (int c = 0; c < 6; ++c) {
-        if (64 * L->rw_slots < hi[c] && c > 0 && c < 4) break;
-        if (c >= 4 && L->rw_slots < RW_SLOTS_MAX) break;
-        // classes 4 and 5: genes with 1024 < tested pairs <= 2048, pairs [0, 1024) then [1024, 2048)
-        A.wv_lo = c ? hi[min(c, 4) - 1] : -1;
+    const int hi[4] = {128, 256, 512, 1024};
+    for (int c = 0; c < 4; ++c) {
+        if (c > 0 && 64 * L->rw_slots < hi[c]) break;
+        A.wv_lo = c ? hi[c - 1] : -1;
         A.wv_hi = hi[c];
-        A.wv_base = c == 5 ? 64 * RW_SLOTS_MAX : 0;
+        A.wv_base = 0;
         A.wv_filter = L->rw_slots > 2 ? 1 : 0;  // rw_slots 2: class 0 is the only launch and holds every gene
         if (c == 0)
             hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, A);
@@ -2158,10 +2201,25 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
             hipLaunchKernelGGL(k_rank_waves<4>, dim3(grid), dim3(256), 0, st, A);
         else if (c == 2)
             hipLaunchKernelGGL(k_rank_waves<8>, dim3(grid), dim3(256), 0, st, A);
-        else  // c >= 3
+        else
             hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, A);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+    }
+    // genes with more than 1024 tested pairs (SLOW at K > 45, K > 64 runs): one
+    // 16-slot pass per window of 1024 pairs, window k over the genes that reach it
+    if (L->rw_slots >= RW_SLOTS_MAX) {
+        const int per = 64 * RW_SLOTS_MAX;
+        const int npass = (std::min(L->ntp_max, RW_PAIRS_MAX) + per - 1) / per;
+        for (int k = 0; k < npass; ++k) {
+            A.wv_lo = std::max(per, k * per);
+            A.wv_hi = RW_PAIRS_MAX;
+            A.wv_base = k * per;
+            A.wv_filter = 1;
+            hipLaunchKernelGGL(k_rank_waves<RW_SLOTS_MAX>, dim3(grid), dim3(256), 0, st, A);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }
@@ -2170,7 +2228,7 @@ extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hip
 {
     // per-gene workgroups pay off once genes have many tested pairs (at P = 66 the
     // per-(gene, pair) waves are 12 us faster; at P >= 435 the gene kernel wins)
-    if (L->P > 128 && L->P <= XC_J * XC_T && !L->cross_wave)
+    if (L->P > 128 && !L->cross_wave)
         hipLaunchKernelGGL(k_rank_cross_gene, dim3(grid), dim3(XC_T), 0, st, *L);
     else  // one wave per (gene, pair) (SCC_CROSS_WAVE=1 selects it for comparisons)
         hipLaunchKernelGGL(k_rank_cross<false>, dim3(grid), dim3(256), 0, st, *L);

@@ -348,7 +348,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (prm->test != SCC_TEST_WILCOX && (prm->test != SCC_TEST_T || prm->mode != SCC_DE_FAST))
         return fail(c, SCC_ERR_INVALID, "test: SCC_TEST_WILCOX, or SCC_TEST_T with SCC_DE_FAST");
     if (K < 2) return fail(c, SCC_ERR_INVALID, "need at least two clusters");
-    if (K > kMaxK) return fail(c, SCC_ERR_UNSUPPORTED, "K > 64 clusters is not supported by this build");
+    if (K > kMaxK) return fail(c, SCC_ERR_UNSUPPORTED, "K > 128 clusters is not supported by this build");
     hipSetDevice(c->device);
     const int G = (int)ds->G, N = (int)ds->N, P = K * (K - 1) / 2;
     const bool fast = prm->mode == SCC_DE_FAST;
@@ -652,6 +652,12 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.accF = accF;
         WS("gene_tp", (size_t)G * P, L.gene_tp);
         WS("gene_nt", (size_t)G, L.gene_nt);
+        if (scc_rank_tables_global(ntp_max, K)) {  // items' tested-pair tables in HBM, one slice per workgroup
+            L.tp_global = 1;
+            L.tp_scr_stride = scc_rank_tables_stride(ntp_max, K);
+            const int ncu_items = c->n_cu > 0 ? c->n_cu : 256;
+            WS("tp_scr", (size_t)4 * ncu_items * L.tp_scr_stride, L.tp_scr);
+        }
         if (env_int("SCC_RESPLIT", 1)) {
             L.fat_cap = (int)std::min<int64_t>(nnz1 / 64 + 64, 1 << 28);
             WS("fatbk", (size_t)L.fat_cap, L.fatbk);

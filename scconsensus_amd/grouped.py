@@ -1,12 +1,12 @@
-"""More than 64 consensus clusters (BASELINE config E: K = 100, 4950 pairs).
+"""More consensus clusters than one engine run holds (> 128).
 
-The device kernels hold a cluster in 6 bits and one ballot mask per cluster,
-so one scc_de_run covers at most 64 clusters.  Every per-pair quantity of the
+The rank kernels hold a cluster in 7 bits, so one scc_de_run covers up to 128
+clusters (BASELINE config E's K = 100 is one run).  Every per-pair quantity of the
 FAST path is a function of the pair's two clusters alone (pct, log-mean
 logFC, the filters, the Wilcoxon test, BH with the pair's own tested-row
 count, the pair's top-N; Fast:57-392), so the K clusters are cut into groups
-of <= 32 and the engine runs once per group pair (u < v) on the cells of
-those <= 64 clusters (the rest get code -1).  Each global pair (i, j) is taken
+of <= 64 and the engine runs once per group pair (u < v) on the cells of
+those <= 128 clusters (the rest get code -1).  Each global pair (i, j) is taken
 from exactly one run -- the run of its two groups, or for a pair inside one
 group the first run containing that group -- and the rows are concatenated
 in the reference's (i, j) order; the union is `unique(Gene)` over the top
@@ -21,21 +21,22 @@ import numpy as np
 
 from . import _native as nat
 
-GROUP = 32
+GROUP = 64
+MIN_K = 129  # K <= 128: one engine run
 
 
 def _groups(K, group):
     return [np.arange(s, min(K, s + group)) for s in range(0, K, group)]
 
 
-def de_fast_grouped(eng, ds, code, K, group=GROUP, min_k=65, **kw) -> nat.DeResult:
-    """scc_de_run(SCC_DE_FAST, fetch="rows") for any K (group <= 32); K < min_k
+def de_fast_grouped(eng, ds, code, K, group=GROUP, min_k=MIN_K, **kw) -> nat.DeResult:
+    """scc_de_run(SCC_DE_FAST, fetch="rows") for any K (group <= 64); K < min_k
     runs the engine once."""
     code = np.ascontiguousarray(code, np.int32)
     if K < min_k:
         return eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows", **kw)
-    if not 2 <= group <= 32:
-        raise ValueError("group must be in [2, 32]")
+    if not 2 <= group <= 64:
+        raise ValueError("group must be in [2, 64]")
     grp = _groups(K, group)
     gid = np.concatenate([np.full(len(g), u) for u, g in enumerate(grp)])
     P = K * (K - 1) // 2
@@ -92,7 +93,7 @@ def de_fast_grouped(eng, ds, code, K, group=GROUP, min_k=65, **kw) -> nat.DeResu
     return nat.DeResult(mode=nat.SCC_DE_FAST, K=K, n_pairs=P, union=union, nodg=nodg, rows=fr)
 
 
-def runs_for(K, group=GROUP, min_k=65) -> int:
+def runs_for(K, group=GROUP, min_k=MIN_K) -> int:
     """Engine runs de_fast_grouped makes for K clusters."""
     if K < min_k:
         return 1

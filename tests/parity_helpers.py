@@ -89,7 +89,7 @@ def check_rows_against_oracle_subset(rows, Xsub, genes, code, K, **params):
                                       err_msg=f"pair {p} ties")
         np.testing.assert_allclose(rows.p[r], o.row_p[oa:ob], rtol=P_RTOL, atol=0, equal_nan=True,
                                    err_msg=f"pair {p} p")
-        np.testing.assert_allclose(rows.avg_logfc[r], o.row_lfc[oa:ob], rtol=1e-12, atol=1e-15,
+        np.testing.assert_allclose(rows.avg_logfc[r], o.row_lfc[oa:ob], rtol=1e-12, atol=5e-14,
                                    err_msg=f"pair {p} logFC")
         np.testing.assert_array_equal(rows.pct1[r], o.row_pct1[oa:ob], err_msg=f"pair {p} pct.1")
         np.testing.assert_array_equal(rows.pct2[r], o.row_pct2[oa:ob], err_msg=f"pair {p} pct.2")
