@@ -2058,6 +2058,9 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 #define XC_Q 32                 // buckets per LDS round
 #define XC_KC SCC_MAX_K         // cluster columns held
 #define XC_J 8                  // tested pairs per thread per pass over the rows (2048)
+// SEG: the same sum over the sub-buckets of each re-split parent (the
+// in-parent cross term; segments from k_rank_resplit*, rsseg).
+template <bool SEG>
 __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
 {
     __shared__ u32 Hs[XC_Q][XC_KC + 1];
@@ -2066,10 +2069,19 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
     __shared__ u32 carry[XC_KC];
     constexpr int NPART = XC_T / XC_KC, RPP = XC_Q / NPART;  // column-scan parts, rows per part
     const int tid = threadIdx.x, K = A.K, G = A.G, P = A.P;
-    const int ng = A.counts[3];
+    const int ng = SEG ? A.counts[10] : A.counts[3];
     for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
-        const int g = A.split_genes[gi];
-        const int bk0 = A.gene_bk[2 * g], nb = A.gene_bk[2 * g + 1];
+        int g, bk0, nb;
+        if (SEG) {
+            const int4 sg = A.rsseg[gi];
+            g = sg.x;
+            bk0 = sg.y;
+            nb = sg.z;
+        } else {
+            g = A.split_genes[gi];
+            bk0 = A.gene_bk[2 * g];
+            nb = A.gene_bk[2 * g + 1];
+        }
         const int ntp = min(A.gene_nt[g], P);
         const u32* tl = A.gene_tp + (size_t)g * P;
         for (int j0 = 0; j0 < ntp; j0 += XC_J * XC_T) {  // windows of 2048 tested pairs
@@ -2229,7 +2241,7 @@ extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hip
     // per-gene workgroups pay off once genes have many tested pairs (at P = 66 the
     // per-(gene, pair) waves are 12 us faster; at P >= 435 the gene kernel wins)
     if (L->P > 128 && !L->cross_wave)
-        hipLaunchKernelGGL(k_rank_cross_gene, dim3(grid), dim3(XC_T), 0, st, *L);
+        hipLaunchKernelGGL(k_rank_cross_gene<false>, dim3(grid), dim3(XC_T), 0, st, *L);
     else  // one wave per (gene, pair) (SCC_CROSS_WAVE=1 selects it for comparisons)
         hipLaunchKernelGGL(k_rank_cross<false>, dim3(grid), dim3(256), 0, st, *L);
     return hipGetLastError();
@@ -2238,7 +2250,10 @@ extern "C" hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid, hip
 extern "C" hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid, hipStream_t st)
 {
     if (!L->fatbk) return hipSuccess;
-    hipLaunchKernelGGL(k_rank_cross<true>, dim3(grid), dim3(256), 0, st, *L);
+    if (L->P > 128 && !L->cross_wave)  // one workgroup per segment, its rows read once (as the gene level)
+        hipLaunchKernelGGL(k_rank_cross_gene<true>, dim3(grid), dim3(XC_T), 0, st, *L);
+    else
+        hipLaunchKernelGGL(k_rank_cross<true>, dim3(grid), dim3(256), 0, st, *L);
     return hipGetLastError();
 }
 
