@@ -883,25 +883,37 @@ struct VecArgs {
     u32* err;
     int wait;          // 1: xcd_item_wait (grid co-resident), 0: xcd_next
     u64* stamps;    // diagnostic: workgroup 0's phase boundaries at [3..7] (nullptr normally)
+    int bt_none;    // 1: leave the tridiagonal's eigenvector (the two-stage path back-transforms it)
 };
 
-// number of eigenvalues of T (d, e^2) strictly below x (Sturm sequence, dstebz)
-__device__ inline int sturm_count(const double* d, const double* e2, int n, double x, double pivmin)
+// numbers of eigenvalues of T (d, e^2) strictly below x[0..SP) (Sturm
+// sequences, dstebz): SP independent recurrences interleaved so that each
+// step's latency chain is shared by SP shifts (one pass over d, e^2)
+#define VEC_SP 1
+__device__ inline void sturm_counts(const double* d, const double* e2, int n, const double* x, double pivmin, int* c)
 {
-    int c = 0;
-    double q = d[0] - x;
-    q = fabs(q) < pivmin ? -pivmin : q;
-    c += (q < 0.0);
-    for (int i = 1; i < n; ++i) {
-        // e2 / q as the hardware reciprocal refined by one Newton step (a few
-        // ulp from the IEEE quotient; the count is insensitive to that)
-        const double r0 = __builtin_amdgcn_rcp(q);
-        const double r = fma(fma(-q, r0, 1.0), r0, r0);
-        q = fma(-e2[i - 1], r, d[i] - x);
-        q = fabs(q) < pivmin ? -pivmin : q;
-        c += (q < 0.0);
+    double q[VEC_SP];
+#pragma unroll
+    for (int p = 0; p < VEC_SP; ++p) {
+        q[p] = d[0] - x[p];
+        q[p] = fabs(q[p]) < pivmin ? -pivmin : q[p];
+        c[p] = (q[p] < 0.0);
     }
-    return c;
+#pragma unroll 4
+    for (int i = 1; i < n; ++i) {
+        const double di = d[i], ei = e2[i - 1];
+#pragma unroll
+        for (int p = 0; p < VEC_SP; ++p) {
+            // e2 / q as the hardware reciprocal refined by one Newton step (a few
+            // ulp from the IEEE quotient; the count is insensitive to that)
+            const double r0 = __builtin_amdgcn_rcp(q[p]);
+            const double r = fma(fma(-q[p], r0, 1.0), r0, r0);
+            double t = fma(-ei, r, di - x[p]);
+            t = fabs(t) < pivmin ? -pivmin : t;
+            q[p] = t;
+            c[p] += (t < 0.0);
+        }
+    }
 }
 
 __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
@@ -956,19 +968,29 @@ __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
     const double pivmin = fmax(2.2250738585072014e-308 * fmax(1.0, em), 1e-300);
     double lo = gl - 2.0 * tnorm * kEps * n - 1e-300;
     double hi = gu + 2.0 * tnorm * kEps * n + 1e-300;
-    // ---- multisection: 256 Sturm counts per round
+    // ---- multisection: VEC_T x VEC_SP Sturm counts per round (point tid * SP + p)
     const int target = n - 1 - q;  // ascending index of the q-th largest
+    constexpr int NP = VEC_T * VEC_SP;
     for (int it = 0; it < 64; ++it) {
-        const double x = lo + (hi - lo) * (double)(tid + 1) / (double)(VEC_T + 1);
-        const int c = sturm_count(dl, e2l, n, x, pivmin);
-        const unsigned long long above = __ballot(c > target);  // lambda_target < x
-        if (lane == 0) ired[wv] = above ? wv * 64 + __builtin_ctzll(above) : VEC_T;
+        double x[VEC_SP];
+        int c[VEC_SP];
+#pragma unroll
+        for (int p = 0; p < VEC_SP; ++p) x[p] = lo + (hi - lo) * (double)(tid * VEC_SP + p + 1) / (double)(NP + 1);
+        sturm_counts(dl, e2l, n, x, pivmin, c);
+        int fp = VEC_SP;  // my first point with lambda_target < x
+#pragma unroll
+        for (int p = VEC_SP - 1; p >= 0; --p)
+            if (c[p] > target) fp = p;
+        const unsigned long long above = __ballot(fp < VEC_SP);
+        const int src = above ? __builtin_ctzll(above) : 0;
+        const int fsrc = __shfl(fp, src, 64);
+        if (lane == 0) ired[wv] = above ? (wv * 64 + src) * VEC_SP + fsrc : NP;
         __syncthreads();
-        int first = VEC_T;
+        int first = NP;
         for (int w = 0; w < VEC_W; ++w) first = min(first, ired[w]);
         __syncthreads();
-        const double nlo = (first == 0) ? lo : lo + (hi - lo) * (double)first / (double)(VEC_T + 1);
-        const double nhi = (first == VEC_T) ? hi : lo + (hi - lo) * (double)(first + 1) / (double)(VEC_T + 1);
+        const double nlo = (first == 0) ? lo : lo + (hi - lo) * (double)first / (double)(NP + 1);
+        const double nhi = (first == NP) ? hi : lo + (hi - lo) * (double)(first + 1) / (double)(NP + 1);
         if (nlo == lo && nhi == hi) break;
         lo = nlo;
         hi = nhi;
@@ -1011,7 +1033,9 @@ __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
                 const bool piv = fabs(dcur) < fabs(li[u]);  // LAPACK dgttrf: swap rows i, i+1
                 const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
                 const double den = piv ? li[u] : dc;
-                const double f = (piv ? dc : li[u]) / den;
+                // (piv ? dc : l) / den as a refined hardware reciprocal (a few ulp)
+                const double r0 = __builtin_amdgcn_rcp(den);
+                const double f = (piv ? dc : li[u]) * fma(fma(-den, r0, 1.0), r0, r0);
                 fl[i] = f;
                 fdr[i] = den;  // the pivot; its reciprocal is taken below, off the chain
                 // operands selected first, one FMA each on the chain (no branch)
@@ -1111,7 +1135,7 @@ __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
     // k_refl_T), three barrier-separated steps per block
     const u64 t3 = stmp ? clock64() : 0;
     __shared__ double bw[BT_NB], bt[BT_NB];
-    const int nr = n - 2;
+    const int nr = a.bt_none ? 0 : n - 2;
     for (int b = (nr > 0 ? (nr + BT_NB - 1) / BT_NB : 0) - 1; b >= 0; --b) {
         const int kb = b * BT_NB, nb = min(BT_NB, nr - kb);
         {  // bw = V^T y: wave wv takes i = wv + VEC_W t, all its loads in flight together
@@ -1301,12 +1325,88 @@ __global__ void __launch_bounds__(FIN_T) k_eig_finish(double* Zq, int n, int lda
     }
 }
 
+// Same result with the k vectors in LDS (k n doubles <= 160 KB): vectors
+// with no cluster predecessor ("heads", almost all of them) are normalised
+// and signed in parallel, one wave each, with no workgroup barrier; the rest
+// follow in order with block-wide Gram-Schmidt against their predecessors.
+// Reduction orders are fixed (bitwise deterministic).
+__device__ inline void fin_wave_finalize(double* z, int n, int lane)
+{
+    double ss = 0.0, best = -1.0;
+    int bi = 0;
+    for (int i = lane; i < n; i += 64) {
+        const double v = z[i];
+        ss = fma(v, v, ss);
+        if (fabs(v) > best) {
+            best = fabs(v);
+            bi = i;
+        }
+    }
+    ss = wave_sum_d(ss);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const double ob = __shfl_xor(best, m, 64);
+        const int oi = __shfl_xor(bi, m, 64);
+        if (ob > best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+        }
+    }
+    const double inv = 1.0 / sqrt(ss);
+    const double sg = (z[bi] < 0.0) ? -inv : inv;
+    for (int i = lane; i < n; i += 64) z[i] *= sg;
+}
+
+__global__ void __launch_bounds__(FIN_T) k_eig_finish_lds(const double* Zq, int n, int lda, int k, const double* W,
+                                                         const double* tnorm_p, double* Z)
+{
+    extern __shared__ __attribute__((aligned(16))) double zl[];  // [k][n]
+    __shared__ double red[FIN_W];
+    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    const double tnorm = tnorm_p[0];
+    for (int x = tid; x < k * n; x += FIN_T) zl[x] = Zq[(size_t)(x / n) * lda + x % n];
+    __syncthreads();
+    auto head = [&](int q) { return q == 0 || !(fabs(W[q - 1] - W[q]) <= 1e-3 * tnorm); };
+    if (wv < k && head(wv)) fin_wave_finalize(zl + (size_t)wv * n, n, lane);
+    __syncthreads();
+    for (int q = 1; q < k; ++q) {
+        if (head(q)) continue;
+        double* z = zl + (size_t)q * n;
+        for (int rr = q - 1; rr >= 0 && fabs(W[rr] - W[rr + 1]) <= 1e-3 * tnorm; --rr) {
+            const double* zr = zl + (size_t)rr * n;
+            double s = 0.0;
+            for (int i = tid; i < n; i += FIN_T) s += zr[i] * z[i];
+            s = block_sum<FIN_W>(s, red);
+            for (int i = tid; i < n; i += FIN_T) z[i] -= s * zr[i];
+            __syncthreads();
+        }
+        if (wv == 0) fin_wave_finalize(z, n, lane);
+        __syncthreads();
+    }
+    for (int i = tid; i < n * 16; i += FIN_T) {
+        const int u = i >> 4, q = i & 15;
+        Z[i] = (q < k) ? zl[(size_t)q * n + u] : 0.0;
+    }
+}
+
+static void launch_eig_finish(double* Zq, int n, int lda, int k, const double* W, const double* tnorm, double* Z,
+                              hipStream_t st)
+{
+    const size_t lds = sizeof(double) * (size_t)k * n;
+    if (lds <= 150 * 1024) {
+        hipFuncSetAttribute((const void*)k_eig_finish_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(k_eig_finish_lds, dim3(1), dim3(FIN_T), lds, st, Zq, n, lda, k, W, tnorm, Z);
+    } else {
+        hipLaunchKernelGGL(k_eig_finish, dim3(1), dim3(FIN_T), 0, st, Zq, n, lda, k, W, tnorm, Z);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side
-static int eig_local()
+static int eig_local_env()
 {
     const char* env = getenv("SCC_EIG_XCD");
-    return (env && *env) ? atoi(env) : 1;
+    return (env && *env) ? atoi(env) : -1;
 }
 
 struct EigLayout {
@@ -1366,21 +1466,40 @@ static int eig_nwg(int n)
     return nwg;
 }
 
+// One XCD (32 CUs, hand-offs through its L2) while the rows fit those CUs'
+// LDS; beyond that the rows spread over more XCDs and stay in LDS, which
+// measured faster than one XCD with rows in HBM (n = 845: 7.1 vs 13.0 ms;
+// n = 1000: 9.3 vs 21.3 ms).  SCC_EIG_XCD=0/1 forces either.
+static bool eig_local(int n)
+{
+    const int env = eig_local_env();
+    if (env >= 0) return env != 0;
+    int nwg = eig_nwg(n);
+    if (nwg > 32) nwg = 32;
+    return tri_lds_bytes(n, (n + nwg - 1) / nwg, true) <= EIG_LDS_MAX;
+}
+
 static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
 {
     nwg = eig_nwg(n);
-    if (eig_local() && nwg > 32) nwg = 32;  // one XCD holds 32 CUs
+    if (eig_local(n) && nwg > 32) nwg = 32;  // one XCD holds 32 CUs
     const int R = (n + nwg - 1) / nwg;
     rows_lds = tri_lds_bytes(n, R, true) <= EIG_LDS_MAX;
     lu_lds = sizeof(double) * 10 * (size_t)n <= EIG_LDS_MAX;
 }
+
+extern "C" int scc_sbr_band(int n);
+extern "C" size_t scc_sbr_scratch_doubles(int n, int lda);
+extern "C" hipError_t scc_launch_sbr_reduce(const double* A, int n, int lda, double* scr, double* d, double* e,
+                                            unsigned long long* stamps, hipStream_t st);
+extern "C" hipError_t scc_launch_sbr_back(double* Zq, int n, int lda, int k, const double* scr, hipStream_t st);
 
 extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 {
     int nwg;
     bool rl, ll;
     eig_plan(n, nwg, rl, ll);
-    return eig_layout(n, lda, k, nwg, rl, ll).total;
+    return eig_layout(n, lda, k, nwg, rl, ll).total + scc_sbr_scratch_doubles(n, lda);
 }
 
 // A: n x n symmetric (full), row-major, lda (read only).  scratch: see
@@ -1400,6 +1519,42 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if (nwg_out) *nwg_out = nwg;
     hipError_t e = hipMemsetAsync(flags, 0, 64, st);  // counter, err, XCD pick [3], follow-up counters [6]
     if (e != hipSuccess) return e;
+    if (scc_sbr_band(n)) {
+        // two-stage reduction (scc_sbr.hip): dense -> band -> tridiagonal, no
+        // per-column hand-off; eigenvectors of the tridiagonal as below, then
+        // the two back-transformations
+        double* sbr = scratch + L.total;
+        if (marks) hipEventRecord(marks[0], st);
+        if ((e = scc_launch_sbr_reduce(A, n, lda, sbr, scratch + L.d, scratch + L.e, stamps, st)) != hipSuccess) return e;
+        if (marks) hipEventRecord(marks[1], st);
+        VecArgs v{};
+        v.d = scratch + L.d;
+        v.e = scratch + L.e;
+        v.n = n;
+        v.lda = lda;
+        v.k = k;
+        v.lu_lds = lu_lds ? 1 : 0;
+        v.lu = scratch + L.lu;
+        v.Zq = scratch + L.zq;
+        v.W = W;
+        v.tnorm = scratch + L.tnorm;
+        v.stamps = stamps;
+        v.xcd = nullptr;
+        v.vcount = flags + 5;
+        v.err = flags + 1;
+        v.bt_none = 1;
+        const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
+        hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
+        if (marks) hipEventRecord(marks[2], st);
+        hipLaunchKernelGGL(k_tri_vectors, dim3(k), dim3(VEC_T), vlds, st, v);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = scc_launch_sbr_back(v.Zq, n, lda, k, sbr, st)) != hipSuccess) return e;
+        if (marks) hipEventRecord(marks[3], st);
+        if (marks) hipEventRecord(marks[4], st);
+        launch_eig_finish(v.Zq, n, lda, k, W, v.tnorm, Z, st);
+        if (marks) hipEventRecord(marks[5], st);
+        return hipGetLastError();
+    }
     // granule tags restart at 1 every launch
     e = hipMemsetAsync(scratch + L.pg, 0, sizeof(double) * (L.zq - L.pg), st);
     if (e != hipSuccess) return e;
@@ -1419,7 +1574,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.work = scratch + L.work;
     t.counter = flags;
     t.reg = flags + 2;
-    t.xcd_local = eig_local();
+    t.xcd_local = eig_local(n) ? 1 : 0;
     t.stamps = stamps;
     t.err = flags + 1;
     const int R = (n + nwg - 1) / nwg;
@@ -1468,7 +1623,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (marks) hipEventRecord(marks[1], st);
-    VecArgs v;
+    VecArgs v{};
     v.d = t.d;
     v.e = t.e;
     v.tau = t.tau;
@@ -1507,7 +1662,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (marks) hipEventRecord(marks[3], st);
     if (marks) hipEventRecord(marks[4], st);
-    hipLaunchKernelGGL(k_eig_finish, dim3(1), dim3(FIN_T), 0, st, v.Zq, n, lda, k, W, v.tnorm, Z);
+    launch_eig_finish(v.Zq, n, lda, k, W, v.tnorm, Z, st);
     if (marks) hipEventRecord(marks[5], st);
     return hipGetLastError();
 }

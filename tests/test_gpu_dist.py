@@ -80,11 +80,14 @@ def test_dist_packed_order_small(eng):
     np.testing.assert_allclose(dist, [1, 3, 6, 2, 5, 3], atol=1e-12)
 
 
+@pytest.mark.parametrize("sbr", ["0", "1"])
 @pytest.mark.parametrize("n", [2, 3, 5, 8, 17, 40, 130, 700])
-def test_eigensolver_sizes(eng, n):
+def test_eigensolver_sizes(eng, n, sbr, monkeypatch):
     """Multi-workgroup tridiagonalisation + per-eigenpair vectors at many |U|
-    (workgroup counts 2..70, rows in LDS) against numpy's exact SVD."""
+    (workgroup counts 2..70, rows in LDS) against numpy's exact SVD; the
+    one-stage solver (default) and the opt-in two-stage path (48 <= n <= 1026)."""
     from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SBR", sbr)
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
     ds = eng.dataset_dense(X)
@@ -127,6 +130,51 @@ def test_eigensolver_rows_beyond_lds(eng):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
+@pytest.mark.parametrize("n", [48, 64, 97, 200, 323, 586, 587, 845, 1026])
+def test_two_stage_eigensolver(eng, n, monkeypatch):
+    """The two-stage reduction (scc_sbr.hip, SCC_EIG_SBR=1: dense -> band of 16
+    (n <= 586) or 8 columns -> tridiagonal) against numpy's exact SVD, and
+    against the one-stage solver on the PCA scores."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SBR", "1")
+    rng = np.random.default_rng(300 + n)
+    X = rng.standard_normal((n, 1000)) * np.linspace(3.0, 0.5, n)[:, None]
+    X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 1000)) * 4.0
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
+    S2 = eng.last_pca_scores(X.shape[1])
+    monkeypatch.setenv("SCC_EIG_SBR", "0")
+    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    S1 = eng.last_pca_scores(X.shape[1])
+    # two exact methods: they agree to rounding amplified by the 15/16 gap
+    assert np.max(np.abs(dist - d1)) < 1e-6
+    np.testing.assert_allclose(np.abs(S2), np.abs(S1), rtol=0, atol=1e-7 * np.abs(S1).max())
+
+
+def test_two_stage_rank_deficient_and_repeated(eng, monkeypatch):
+    """Identical genes (rank-deficient panels: zero-norm reflectors) and exactly
+    repeated eigenvalues inside the top 15, n = 90 (two-stage path)."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SBR", "1")
+    rng = np.random.default_rng(8)
+    n, N = 90, 600
+    sv = np.array([9.0] * 3 + [7.0] * 4 + [5.0] * 2 + [4.0] * 6 + [1.0] * (n - 15))
+    Q, _ = np.linalg.qr(rng.standard_normal((N, n)))
+    Q -= Q.mean(axis=0)
+    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    X = (Q @ np.diag(sv) @ V.T).T
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    assert np.max(np.abs(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID) - O.dist_euclidean(O.pca_scores(X, g)))) < 1e-5
+    X2 = np.concatenate([X[:30], X[:30], X[:30]])  # 90 genes, rank <= 30
+    ds2 = eng.dataset_dense(X2)
+    dist = eng.distance(ds2, g, nat.SCC_DIST_PCA_EUCLID)
+    assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
+
+
 @pytest.mark.parametrize("xcd", ["0", "1"])
 @pytest.mark.parametrize("wave", ["0", "1"])
 @pytest.mark.parametrize("n,nwg", [(323, 8), (323, 32), (323, 64), (500, 48), (700, 70), (700, 256), (1500, 40),
@@ -136,6 +184,7 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, wave, monkeypatch):
     hand-off (cross-XCD write-through or one-XCD L2), either kernel (wave
     agents or workgroup barriers), rows in LDS or in HBM."""
     from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SBR", "0")  # the one-stage solver
     monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
     monkeypatch.setenv("SCC_EIG_XCD", xcd)
     monkeypatch.setenv("SCC_EIG_WAVE", wave)
