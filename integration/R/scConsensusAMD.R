@@ -8,12 +8,20 @@
 # (table / grepl("grey") / locale order), hclust(ward.D2), cutreeDynamic,
 # labels2colors, silhouette, saveRDS, printing and cellTypeDEPlot.
 
-.scc_codes <- function(labels, minClusterSize) {
-  counts <- table(labels)                       # locale collation, as in R
-  keep <- names(counts)[counts > minClusterSize]
+# Cluster selection exactly as Fast:39-47 / slow:38-48: table() over ALL of
+# consensusClusterLabels (locale collation), "> minClusterSize", no "grey";
+# then each matrix column's code (0-based index into the kept clusters, -1
+# for cells of other clusters or without a label).
+.scc_codes <- function(consensusClusterLabels, dataMatrix, minClusterSize) {
+  colorCounts <- table(consensusClusterLabels)
+  keep <- names(colorCounts[colorCounts > minClusterSize])
   keep <- keep[!grepl("grey", keep)]
-  code <- match(as.character(labels), keep) - 1L
+  if (is.null(names(consensusClusterLabels))) names(consensusClusterLabels) <- colnames(dataMatrix)
+  colLabels <- consensusClusterLabels[colnames(dataMatrix)]
+  code <- match(as.character(colLabels), keep) - 1L
   code[is.na(code)] <- -1L
+  if (length(keep) > 128L)
+    stop("scConsensus engine: ", length(keep), " clusters; one engine run holds at most 128")
   list(clusters = keep, code = as.integer(code))
 }
 
@@ -30,8 +38,15 @@
   }
 }
 
-.scc_dist <- function(s, genes, n_cells, metric = 0L) {
-  d <- .Call("C_scc_distance", s$x, s$p, s$i, s$dim, as.integer(genes), as.integer(metric), 0L)
+# the matrix uploaded ONCE per call of the R function; DE and distance share
+# the device copy through this handle (freed by C_scc_release or the GC)
+.scc_dataset <- function(m) {
+  s <- .scc_slots(m)
+  .Call("C_scc_dataset", s$x, s$p, s$i, s$dim)
+}
+
+.scc_dist <- function(h, genes, n_cells, metric = 0L) {
+  d <- .Call("C_scc_distance", h, as.integer(genes), as.integer(metric), 0L)
   structure(d, Size = n_cells, Diag = FALSE, Upper = FALSE,
             method = if (metric == 0L) "euclidean" else "pearson", class = "dist")
 }
@@ -59,16 +74,15 @@ reclusterDEConsensusFast <- function(dataMatrix, consensusClusterLabels, method 
   # test.use = method (Fast:372): "wilcox" and "t" run on the engine; "bimod" /
   # "roc" need Seurat helpers the reference never loads
   if (!(method %in% c("wilcox", "t"))) stop("Unknown test: ", method)
-  if (is.null(names(consensusClusterLabels))) names(consensusClusterLabels) <- colnames(dataMatrix)
-  labels <- consensusClusterLabels[colnames(dataMatrix)]
-  sel <- .scc_codes(labels, minClusterSize)
-  s <- .scc_slots(dataMatrix)
-  res <- .Call("C_scc_de_fast", s$x, s$p, s$i, s$dim, sel$code, length(sel$clusters),
+  sel <- .scc_codes(consensusClusterLabels, dataMatrix, minClusterSize)
+  h <- .scc_dataset(dataMatrix)
+  on.exit(.Call("C_scc_release", h), add = TRUE)
+  res <- .Call("C_scc_de_fast", h, sel$code, length(sel$clusters),
                as.double(qValThrs), as.double(logFCThrs), as.double(minPerCent),
                as.integer(NumbertopDEGenes), as.integer(method == "t"))
   deGeneUnion <- rownames(dataMatrix)[res[[1]]]
   print(str(deGeneUnion))
-  d <- .scc_dist(s, res[[1]], ncol(dataMatrix))
+  d <- .scc_dist(h, res[[1]], ncol(dataMatrix))
   tc <- .scc_tree_and_colors(d, deepSplitValues, minClusterSize, with_si = TRUE)
   out <- list("deGeneUnion" = deGeneUnion, "cellTree" = tc$tree, "dynamicColors" = tc$colors)
   saveRDS(object = out, file = filename)
@@ -86,11 +100,10 @@ reclusterDEConsensus <- function(dataMatrix, consensusClusterLabels, method = "W
     print("Incorrect method chosen.")
     return(NULL)
   }
-  if (is.null(names(consensusClusterLabels))) names(consensusClusterLabels) <- colnames(dataMatrix)
-  labels <- consensusClusterLabels[colnames(dataMatrix)]
-  sel <- .scc_codes(labels, minClusterSize)
-  s <- .scc_slots(dataMatrix)
-  res <- .Call("C_scc_de_slow", s$x, s$p, s$i, s$dim, sel$code, length(sel$clusters),
+  sel <- .scc_codes(consensusClusterLabels, dataMatrix, minClusterSize)
+  h <- .scc_dataset(dataMatrix)
+  on.exit(.Call("C_scc_release", h), add = TRUE)
+  res <- .Call("C_scc_de_slow", h, sel$code, length(sel$clusters),
                as.double(qValThrs), as.double(fcThrs), as.double(meanScalingFactor))
   K <- length(sel$clusters)
   qValueList <- rep(list(list()), K); logFCList <- rep(list(list()), K); deGeneList <- rep(list(list()), K)
@@ -110,7 +123,7 @@ reclusterDEConsensus <- function(dataMatrix, consensusClusterLabels, method = "W
   deGeneUnion <- rownames(dataMatrix)[res[[1]]]
   print(str(deGeneUnion))
   saveRDS(deGeneUnion, file = "deGeneUnion.rds")
-  d <- .scc_dist(s, res[[1]], ncol(dataMatrix))
+  d <- .scc_dist(h, res[[1]], ncol(dataMatrix))
   tc <- .scc_tree_and_colors(d, deepSplitValues, minClusterSize, with_si = FALSE)
   out <- list("deGeneUnion" = deGeneUnion, "cellTree" = tc$tree, "dynamicColors" = tc$colors)
   saveRDS(object = out, file = filename)

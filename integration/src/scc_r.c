@@ -1,14 +1,18 @@
 /*
  * scc_r.c — R `.Call` glue for libscc (include/scc.h).  Compiled only where R
- * headers exist (R CMD INSTALL of the wrapper package; R is absent from the
- * build container).  The glue never lets a C++ frame unwind through R: every
- * libscc entry point returns an int status, and Rf_error() is raised only
- * here, after the library call returned.
+ * headers exist (R CMD INSTALL of the scConsensus package with this file in
+ * src/; R is absent from the build container).  The glue never lets a C++
+ * frame unwind through R: every libscc entry point returns an int status, and
+ * Rf_error() is raised only here, after the library call returned.
  *
  * Bindings (reference call sites they replace):
+ *   C_scc_dataset   as.matrix(dataMatrix) per pair (Fast:368) / dataIn (slow:32):
+ *                   ONE upload per call of the R function, held as an external
+ *                   pointer that the DE and distance calls share
  *   C_scc_de_fast   R/reclusterDEConsensusFast.R:57-392 (pair loop, ComputePairWiseDE, top_n, unique)
  *   C_scc_de_slow   R/reclusterDEConsensus.R:32-227
  *   C_scc_distance  R/reclusterDEConsensusFast.R:398-400 (prcomp_irlba + dist), :403 (1 - cor)
+ *   C_scc_release   frees the device copy early (the finalizer does it otherwise)
  */
 #include <R.h>
 #include <Rinternals.h>
@@ -33,10 +37,36 @@ static void check(int rc)
     if (rc != SCC_OK) Rf_error("scConsensus engine error %d: %s", rc, scc_ctx_last_error(g_ctx));
 }
 
-/* dgCMatrix slots (@p int, @i int, @x double), dgRMatrix slots (@p, @j, @x;
- * dim has a third entry 1) or a base double matrix */
-static scc_dataset* dataset_from(SEXP x, SEXP p, SEXP i, SEXP dim)
+/* ---- the dataset handle: external pointer tagged "scc_dataset", its
+ * protected slot holding c(G, N) */
+static SEXP ds_tag(void) { return Rf_install("scc_dataset"); }
+
+static void ds_finalize(SEXP h)
 {
+    scc_dataset* ds = (scc_dataset*)R_ExternalPtrAddr(h);
+    if (ds) {
+        scc_dataset_destroy(ds);
+        R_ClearExternalPtr(h);
+    }
+}
+
+static scc_dataset* ds_of(SEXP h, int* G, int* N)
+{
+    if (TYPEOF(h) != EXTPTRSXP || R_ExternalPtrTag(h) != ds_tag())
+        Rf_error("scConsensus engine: not a dataset handle (use C_scc_dataset)");
+    scc_dataset* ds = (scc_dataset*)R_ExternalPtrAddr(h);
+    if (!ds) Rf_error("scConsensus engine: the dataset handle was released");
+    SEXP dims = R_ExternalPtrProtected(h);
+    if (G) *G = INTEGER(dims)[0];
+    if (N) *N = INTEGER(dims)[1];
+    return ds;
+}
+
+/* dgCMatrix slots (@p int, @i int, @x double), dgRMatrix slots (@p, @j, @x;
+ * dim has a third entry 1) or a base double matrix -> device-resident dataset */
+SEXP C_scc_dataset(SEXP x, SEXP p, SEXP i, SEXP dim)
+{
+    ensure_ctx();
     scc_dataset* ds = NULL;
     const int G = INTEGER(dim)[0], N = INTEGER(dim)[1];
     if (Rf_isNull(p)) {
@@ -52,15 +82,28 @@ static scc_dataset* dataset_from(SEXP x, SEXP p, SEXP i, SEXP dim)
         for (int c = 0; c <= N; ++c) p64[c] = INTEGER(p)[c];
         check(scc_dataset_create_csc(g_ctx, p64, INTEGER(i), REAL(x), G, N, (int64_t)XLENGTH(x), SCC_PTR_HOST, &ds));
     }
-    return ds;
+    SEXP dims = PROTECT(Rf_allocVector(INTSXP, 2));
+    INTEGER(dims)[0] = G;
+    INTEGER(dims)[1] = N;
+    SEXP h = PROTECT(R_MakeExternalPtr(ds, ds_tag(), dims));
+    R_RegisterCFinalizerEx(h, ds_finalize, TRUE);
+    UNPROTECT(2);
+    return h;
+}
+
+SEXP C_scc_release(SEXP h)
+{
+    if (TYPEOF(h) == EXTPTRSXP && R_ExternalPtrTag(h) == ds_tag()) ds_finalize(h);
+    return R_NilValue;
 }
 
 /* returns list(union = int (1-based gene rows), nodg = int[N]) */
-SEXP C_scc_de_fast(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qthr, SEXP lfc, SEXP minpct, SEXP topn,
-                   SEXP ttest)
+SEXP C_scc_de_fast(SEXP h, SEXP code, SEXP K, SEXP qthr, SEXP lfc, SEXP minpct, SEXP topn, SEXP ttest)
 {
     ensure_ctx();
-    scc_dataset* ds = dataset_from(x, p, i, dim);
+    int N = 0;
+    scc_dataset* ds = ds_of(h, NULL, &N);
+    if (XLENGTH(code) != N) Rf_error("scConsensus engine: %d cluster codes for %d cells", (int)XLENGTH(code), N);
     scc_de_params prm;
     memset(&prm, 0, sizeof(prm));
     prm.mode = SCC_DE_FAST;
@@ -71,20 +114,16 @@ SEXP C_scc_de_fast(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qth
     prm.test = Rf_asInteger(ttest) ? SCC_TEST_T : SCC_TEST_WILCOX; /* test.use = method (Fast:372) */
     scc_de_result* r = NULL;
     int rc = scc_de_run(g_ctx, ds, INTEGER(code), Rf_asInteger(K), &prm, &r);
-    if (rc != SCC_OK && !r) {
-        scc_dataset_destroy(ds);
-        check(rc);
-    }
+    if (rc != SCC_OK && !r) check(rc);
     int32_t npairs = 0, nu = 0;
     int64_t nrows = 0;
     scc_de_result_counts(r, &npairs, &nrows, &nu);
     SEXP uni = PROTECT(Rf_allocVector(INTSXP, nu));
     scc_de_result_union(r, INTEGER(uni));
     for (int k = 0; k < nu; ++k) INTEGER(uni)[k] += 1;
-    SEXP nodg = PROTECT(Rf_allocVector(INTSXP, INTEGER(dim)[1]));
+    SEXP nodg = PROTECT(Rf_allocVector(INTSXP, N));
     scc_de_result_nodg(r, INTEGER(nodg));
     scc_de_result_destroy(r);
-    scc_dataset_destroy(ds);
     if (rc != SCC_OK) {
         UNPROTECT(2);
         check(rc);
@@ -96,11 +135,13 @@ SEXP C_scc_de_fast(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qth
     return out;
 }
 
-/* returns list(union, q = matrix[G, P], logfc = matrix[G, P], de = logical matrix, nodg) */
-SEXP C_scc_de_slow(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qthr, SEXP fc, SEXP msf)
+/* returns list(union, q = matrix[G, P], logfc = matrix[G, P], de = raw matrix, nodg) */
+SEXP C_scc_de_slow(SEXP h, SEXP code, SEXP K, SEXP qthr, SEXP fc, SEXP msf)
 {
     ensure_ctx();
-    scc_dataset* ds = dataset_from(x, p, i, dim);
+    int G = 0, N = 0;
+    scc_dataset* ds = ds_of(h, &G, &N);
+    if (XLENGTH(code) != N) Rf_error("scConsensus engine: %d cluster codes for %d cells", (int)XLENGTH(code), N);
     scc_de_params prm;
     memset(&prm, 0, sizeof(prm));
     prm.mode = SCC_DE_SLOW;
@@ -110,12 +151,10 @@ SEXP C_scc_de_slow(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qth
     prm.mean_scaling_factor = Rf_asReal(msf);
     scc_de_result* r = NULL;
     int rc = scc_de_run(g_ctx, ds, INTEGER(code), Rf_asInteger(K), &prm, &r);
-    if (rc != SCC_OK) {  /* includes SCC_ERR_RSTOP: R itself would stop() here */
+    if (rc != SCC_OK) { /* includes SCC_ERR_RSTOP: R itself would stop() here */
         if (r) scc_de_result_destroy(r);
-        scc_dataset_destroy(ds);
         check(rc);
     }
-    const int G = INTEGER(dim)[0];
     int32_t npairs = 0, nu = 0;
     int64_t nrows = 0;
     scc_de_result_counts(r, &npairs, &nrows, &nu);
@@ -126,10 +165,9 @@ SEXP C_scc_de_slow(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qth
     SEXP lf = PROTECT(Rf_allocMatrix(REALSXP, G, npairs));
     SEXP de = PROTECT(Rf_allocMatrix(RAWSXP, G, npairs));
     scc_de_result_pair_vectors(r, NULL, REAL(q), REAL(lf), NULL, RAW(de));
-    SEXP nodg = PROTECT(Rf_allocVector(INTSXP, INTEGER(dim)[1]));
+    SEXP nodg = PROTECT(Rf_allocVector(INTSXP, N));
     scc_de_result_nodg(r, INTEGER(nodg));
     scc_de_result_destroy(r);
-    scc_dataset_destroy(ds);
     SEXP out = PROTECT(Rf_allocVector(VECSXP, 5));
     SET_VECTOR_ELT(out, 0, uni);
     SET_VECTOR_ELT(out, 1, q);
@@ -141,18 +179,22 @@ SEXP C_scc_de_slow(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP code, SEXP K, SEXP qth
 }
 
 /* returns a "dist" object body (double vector, N(N-1)/2, R order); the R
- * wrapper sets the Size/Diag/Upper/method attributes and class "dist". */
-SEXP C_scc_distance(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP genes, SEXP metric, SEXP ncomp)
+ * wrapper sets the Size/Diag/Upper/method attributes and class "dist".  The
+ * engine streams it from HBM into this vector in column tiles (pageable
+ * memory: a pinned staging ring). */
+SEXP C_scc_distance(SEXP h, SEXP genes, SEXP metric, SEXP ncomp)
 {
     ensure_ctx();
-    scc_dataset* ds = dataset_from(x, p, i, dim);
-    const int N = INTEGER(dim)[1];
+    int G = 0, N = 0;
+    scc_dataset* ds = ds_of(h, &G, &N);
     const int nu = LENGTH(genes);
     int32_t* g0 = (int32_t*)R_alloc((size_t)nu, sizeof(int32_t));
-    for (int k = 0; k < nu; ++k) g0[k] = INTEGER(genes)[k] - 1;
+    for (int k = 0; k < nu; ++k) {
+        g0[k] = INTEGER(genes)[k] - 1;
+        if (g0[k] < 0 || g0[k] >= G) Rf_error("scConsensus engine: gene row %d out of range", g0[k] + 1);
+    }
     SEXP d = PROTECT(Rf_allocVector(REALSXP, (R_xlen_t)N * (N - 1) / 2));
     int rc = scc_distance(g_ctx, ds, g0, nu, Rf_asInteger(metric), Rf_asInteger(ncomp), REAL(d), SCC_PTR_HOST, 0);
-    scc_dataset_destroy(ds);
     if (rc != SCC_OK) {
         UNPROTECT(1);
         check(rc);
@@ -162,12 +204,15 @@ SEXP C_scc_distance(SEXP x, SEXP p, SEXP i, SEXP dim, SEXP genes, SEXP metric, S
 }
 
 static const R_CallMethodDef call_methods[] = {
-    {"C_scc_de_fast", (DL_FUNC)&C_scc_de_fast, 11},
-    {"C_scc_de_slow", (DL_FUNC)&C_scc_de_slow, 9},
-    {"C_scc_distance", (DL_FUNC)&C_scc_distance, 7},
+    {"C_scc_dataset", (DL_FUNC)&C_scc_dataset, 4},
+    {"C_scc_release", (DL_FUNC)&C_scc_release, 1},
+    {"C_scc_de_fast", (DL_FUNC)&C_scc_de_fast, 8},
+    {"C_scc_de_slow", (DL_FUNC)&C_scc_de_slow, 6},
+    {"C_scc_distance", (DL_FUNC)&C_scc_distance, 4},
     {NULL, NULL, 0}};
 
-void R_init_scConsensusAMD(DllInfo* dll)
+/* the package is scConsensus (NAMESPACE: useDynLib(scConsensus, .registration = TRUE)) */
+void R_init_scConsensus(DllInfo* dll)
 {
     R_registerRoutines(dll, NULL, call_methods, NULL, NULL);
     R_useDynamicSymbols(dll, FALSE);

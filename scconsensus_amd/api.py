@@ -40,8 +40,12 @@ def select_clusters(labels, min_cluster_size: int, cluster_order=None):
     cells not compared.  R orders table() names by the locale's collation;
     the default here is code-point order (R's C locale) — pass
     ``cluster_order`` to reproduce another collation."""
-    labels = np.asarray(labels).astype(str)
-    names, counts = np.unique(labels, return_counts=True)
+    raw = np.asarray(labels, dtype=object)
+    # R's table() drops NA and `labels == x` never matches NA (Fast:40-44): a
+    # missing label (None / NaN / pandas NA) is no cluster, its cell coded -1
+    missing = np.fromiter((_is_missing(v) for v in raw), bool, len(raw))
+    labels = raw.astype(str)
+    names, counts = np.unique(labels[~missing], return_counts=True)
     if cluster_order is not None:
         pos = {n: i for i, n in enumerate(cluster_order)}
         idx = sorted(range(len(names)), key=lambda i: pos.get(names[i], len(pos) + i))
@@ -49,7 +53,20 @@ def select_clusters(labels, min_cluster_size: int, cluster_order=None):
     keep = [str(n) for n, c in zip(names, counts) if c > min_cluster_size and "grey" not in str(n)]
     lut = {n: i for i, n in enumerate(keep)}
     code = np.fromiter((lut.get(s, -1) for s in labels), np.int32, len(labels))
+    code[missing] = -1
     return keep, code
+
+
+def _is_missing(v) -> bool:
+    if v is None:
+        return True
+    if isinstance(v, (float, np.floating)):
+        return bool(np.isnan(v))
+    try:
+        import pandas as pd
+        return v is pd.NA or v is pd.NaT
+    except ImportError:  # pragma: no cover
+        return False
 
 
 def _as_matrix(dataMatrix):

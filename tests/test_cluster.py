@@ -128,3 +128,19 @@ def test_deeper_split_never_fewer_clusters_on_blobs():
 def test_labels2colors():
     assert labels2colors([0, 1, 2, 3, 7, 17, 34]) == ["grey", "turquoise", "blue", "brown", "black", "grey60",
                                                         "darkmagenta"]
+
+
+def test_select_clusters_table_filters_and_missing_labels():
+    """Cluster selection as Fast:39-47: table() counts, `> minClusterSize`, no
+    "grey", names in code-point (C locale) order; NA / None / NaN labels are no
+    cluster (R's table() drops NA) and their cells get code -1."""
+    import pandas as pd
+    from scconsensus_amd.api import select_clusters
+    labels = ["b"] * 5 + ["a"] * 4 + ["grey"] * 9 + ["c"] * 2 + [None] * 6 + [float("nan")] * 6 + [pd.NA] * 6
+    names, code = select_clusters(labels, 3)
+    assert names == ["a", "b"]
+    want = [1] * 5 + [0] * 4 + [-1] * 9 + [-1] * 2 + [-1] * 18
+    assert code.tolist() == want
+    # the string "nan" is a real label (R would count it)
+    names2, code2 = select_clusters(["nan"] * 5 + ["x"] * 5, 3)
+    assert names2 == ["nan", "x"] and code2.tolist() == [0] * 5 + [1] * 5
