@@ -195,10 +195,12 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
 // ------------------------------------------------------------------ Euclidean dist
 // Tile = DT_ROWS rows (i, one per thread) x DT_COLS columns (j); the stores of
 // one column are contiguous in the packed R order out[j*(2N-j-1)/2 + i-j-1].
-// Column j's scores are uniform across the tile (scalar loads); per element
-// the sum of squared differences over the k <= 15 components (padding column
-// 15 is zero), FMA-accumulated, and the hardware sqrt: the distance contract
-// is 1e-5 absolute (BASELINE north_star).  The kernel is bound by the HBM
+// Column j's scores are uniform across the tile (LDS broadcast); per element
+// |p_i|^2 + |p_j|^2 - 2 p_i.p_j over the k <= 15 components (the difference
+// form where that cancels) and the hardware sqrt: the distance contract is
+// 1e-5 absolute (BASELINE north_star).  Line-aligned variants (a wave or a
+// workgroup walking a run of rows and storing 128-byte-aligned windows through
+// an LDS ring) measured slower at config B (0.74-1.34 ms vs 0.69 ms).  The kernel is bound by the HBM
 // write stream (practical ceiling ~5.1 TB/s: scripts/write_bw.py).  Only
 // lower-triangle tiles are enumerated (column blocks in order, row blocks
 // rb >= cb / DT_RATIO), dealt to the XCDs in runs of DT_RUN consecutive tiles:
@@ -236,8 +238,26 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
     if (t >= ntiles) return;
     int cb, rb;
     dist_tile_of(t0 + t, nrb, cb, rb);
+    // the tile's column scores in LDS, |p_j|^2 in the zero padding slot 15;
+    // every lane reads a column at the same address (broadcast), and LDS
+    // returns in order, so the next column's reads overlap this column's
+    // arithmetic (scalar loads cannot: their counter is waited to zero)
+    __shared__ __attribute__((aligned(16))) double cs[DT_COLS][16];
+    const int jb = cb * DT_COLS;
+    for (int e = threadIdx.x; e < DT_COLS * 16; e += DT_ROWS) {
+        const int jj = jb + e / 16;
+        cs[e / 16][e % 16] = (jj < N) ? P[(size_t)jj * 16 + e % 16] : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x < DT_COLS) {
+        double nn = 0.0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) nn = fma(cs[threadIdx.x][q], cs[threadIdx.x][q], nn);
+        cs[threadIdx.x][15] = nn;
+    }
+    __syncthreads();
     const int i = rb * DT_ROWS + (int)threadIdx.x;
-    const int j0 = max(cb * DT_COLS, c_lo), j1 = min(min(N, cb * DT_COLS + DT_COLS), c_hi);
+    const int j0 = max(jb, c_lo), j1 = min(min(N, jb + DT_COLS), c_hi);
     if (i >= N) return;
     double pi[15];
 #pragma unroll
@@ -245,13 +265,28 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
     const int jend = min(j1, i);  // columns j < i only
     // o(j, i) = B(j) + i with B(j) = j(2N - j - 1)/2 - j - 1, B(j + 1) = B(j) + N - j - 2
     long long B = (long long)j0 * (2LL * N - j0 - 1) / 2 - j0 - 1 - obase;
-    for (int j = j0; j < jend; ++j) {
-        const double* pj = P + (size_t)j * 16;
-        double s = 0.0;
+    double ni = 0.0;
 #pragma unroll
-        for (int q = 0; q < 15; ++q) {
-            const double dv = pi[q] - pj[q];
-            s = fma(dv, dv, s);
+    for (int q = 0; q < 15; ++q) ni = fma(pi[q], pi[q], ni);
+    for (int j = j0; j < jend; ++j) {
+        const double* pc = cs[j - jb];
+        // |p_i - p_j|^2 = |p_i|^2 + |p_j|^2 - 2 p_i.p_j: 15 FMAs instead of 15
+        // subtractions + 15 FMAs.  Its rounding error is below 20 eps (|p_i|^2 +
+        // |p_j|^2); where the result is under 2^-20 of that (near-identical
+        // cells: cancellation) the difference form is evaluated instead, so
+        // every entry is within ~1e-9 relative of the exact distance.
+        double dot = 0.0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) dot = fma(pi[q], pc[q], dot);
+        const double nsum = ni + pc[15];
+        double s = fma(-2.0, dot, nsum);
+        if (s < 0x1p-20 * nsum) {
+            s = 0.0;
+#pragma unroll
+            for (int q = 0; q < 15; ++q) {
+                const double dv = pi[q] - pc[q];
+                s = fma(dv, dv, s);
+            }
         }
         const double d = __builtin_amdgcn_sqrt(s);
         if (F32)

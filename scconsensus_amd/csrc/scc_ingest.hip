@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int
 #define SC_GT 256       // genes per tile
 #define SC_CAP 4096     // default staged entries per round (u64 key + u16 gene = 10 B each): 3 blocks per CU
 #define SC_CMAX 128     // cells per scatter chunk (kScatterCC * kCountChunk)
+#define SC_RUN 8        // consecutive gene tiles of one chunk dealt to one XCD
 
 template <bool DENSE>
 __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ indptr, const int* __restrict__ rows,
@@ -200,7 +201,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
                                                        const int* __restrict__ perm, const int* __restrict__ cc_p0,
                                                        const int* __restrict__ sc_cc0, const u32* __restrict__ cnt,
                                                        const i64* __restrict__ gstart, const i64* __restrict__ bnd,
-                                                       int ntile, int cap, int glo, int ghi, int t0,
+                                                       int ntile, int cap, int glo, int ghi, int t0, int nsc, int ntl,
                                                        u64* __restrict__ keys)
 {
     __shared__ u32 loff[SC_GT + 1];
@@ -216,7 +217,14 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     extern __shared__ __attribute__((aligned(16))) u64 skey[];  // [SC_CAP]
     unsigned short* sg = (unsigned short*)(skey + cap);        // [cap]
     const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
-    const int s = blockIdx.x, t = t0 + (int)blockIdx.y;  // gene tiles from t0 (a gene shard's tiles)
+    // dispatch slot -> (scatter chunk, gene tile): slot x runs on XCD x % 8, and
+    // runs of SC_RUN consecutive tiles of one chunk share an XCD, so the cache
+    // line a cell's entries of tiles t and t + 1 share is fetched once into
+    // that XCD's L2 instead of twice from HBM
+    const long long lin = blockIdx.x, kq = lin >> 3, xq = lin & 7;
+    const long long L = ((kq / SC_RUN) * 8 + xq) * SC_RUN + kq % SC_RUN;
+    if (L >= (long long)nsc * ntl) return;
+    const int s = (int)(L / ntl), t = t0 + (int)(L % ntl);  // gene tiles from t0 (a gene shard's tiles)
     const int g0 = t * SC_GT, g1 = min(G, g0 + SC_GT), ng = g1 - g0;
     const int cc0 = sc_cc0[s], cc1 = sc_cc0[s + 1];
     const int p0 = cc_p0[cc0], p1 = cc_p0[cc1];
@@ -492,7 +500,9 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
 {
     if (ns <= 0 || ghi <= glo) return hipSuccess;
     const int t0 = glo / SC_GT, t1 = (ghi + SC_GT - 1) / SC_GT;  // the gene tiles of [glo, ghi)
-    const dim3 grid(ns, t1 - t0);
+    const int ntl = t1 - t0;
+    const long long nrun = ((long long)ns * ntl + SC_RUN - 1) / SC_RUN;
+    const dim3 grid((unsigned)(((nrun + 7) / 8) * 8 * SC_RUN));
     static const int cap = [] {
         const char* v = getenv("SCC_SC_CAP");
         return (v && *v) ? std::max(SC_GT, atoi(v)) : SC_CAP;
@@ -502,10 +512,10 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
     hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (dense)
         hipLaunchKernelGGL(k_ing_scatter<true>, grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, keys);
+                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, keys);
     else
         hipLaunchKernelGGL(k_ing_scatter<false>, grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0, sc_cc0,
-                           cnt, gstart, bnd, ntile, cap, glo, ghi, t0, keys);
+                           cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, keys);
     return hipGetLastError();
 }
 
