@@ -245,11 +245,11 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
                 marks = mk;
             }
             unsigned long long* st_buf = nullptr;
-            if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 16, st_buf);
+            if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 24, st_buf);
             int nwg_used = 0;
             HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, marks, st_buf, s0));
             if (st_buf) {
-                unsigned long long h[16];
+                unsigned long long h[24];
                 HIPCHK(c, hipMemcpyAsync(h, st_buf, sizeof(h), hipMemcpyDeviceToHost, s0));
                 HIPCHK(c, hipStreamSynchronize(s0));
                 fprintf(stderr, "[scc stamps] tridiag n=%d nwg=%d: phase B %llu (wave 0 rows %llu), hand-off wait %llu, "
@@ -258,6 +258,8 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
                         "back-transform %llu cycles\n", h[3], h[4], h[5], h[6]);
                 fprintf(stderr, "[scc stamps] two-stage panel 0: load %llu, columns %llu, T %llu, rows %llu cycles\n",
                         h[8], h[9], h[10], h[11]);
+                fprintf(stderr, "[scc stamps] block back-transform: stage %llu, V^T Y %llu, T W %llu, Y update %llu, "
+                        "load %llu cycles\n", h[12], h[13], h[14], h[15], h[16]);
             }
             if (marks) {
                 c->pending.push_back({"eig_tridiag", mk[0], mk[1]});

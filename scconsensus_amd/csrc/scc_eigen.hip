@@ -289,9 +289,9 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                 double sd = 0.0;
 #pragma unroll
                 for (int t = 0; t < NJA; ++t) {
-                    const double x = rr[m][t] - vr * wpr[t] - wr * vpr[t];
+                    const double x = fma(-vr, wpr[t], fma(-wr, vpr[t], rr[m][t]));
                     rr[m][t] = x;
-                    sd += x * vcr[t];
+                    sd = fma(x, vcr[t], sd);
                 }
                 if (r == i + 1) {
 #pragma unroll
@@ -317,11 +317,11 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
             for (int j = i + 1 + lane; j < n; j += 64) {
                 double x = row[j];
                 if (prev) {
-                    x = x - vr * wp[j] - wr * vp[j];
+                    x = fma(-vr, wp[j], fma(-wr, vp[j], x));
                     row[j] = x;
                 }
                 if (pub) put_g<LOCAL>(rg + 2 * j, x, tag);
-                s += x * vc[j];
+                s = fma(x, vc[j], s);
             }
             s = wave_sum_d(s);
             const double p = tc * s;
@@ -430,15 +430,15 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         pdt = wave_sum_d(pdt);
         const double a2 = -0.5 * tc * pdt;
         const double v1 = vc[i + 1];
-        const double w1 = (tc != 0.0) ? pp[i + 1] + a2 * v1 : 0.0;
+        const double w1 = (tc != 0.0) ? fma(a2, v1, pp[i + 1]) : 0.0;
         double xp = 0.0;
         for (int j = i + 1 + tid; j < n; j += TRI_T) {
             const double vj = vc[j];
-            const double wj = (tc != 0.0) ? pp[j] + a2 * vj : 0.0;
-            const double yj = y[j] - v1 * wj - w1 * vj;
+            const double wj = (tc != 0.0) ? fma(a2, vj, pp[j]) : 0.0;
+            const double yj = fma(-v1, wj, fma(-w1, vj, y[j]));
             wp[j] = wj;
             y[j] = yj;
-            if (j >= i + 3) xp += yj * yj;
+            if (j >= i + 3) xp = fma(yj, yj, xp);
         }
         if (i + 1 <= n - 2) {
             // Householder reflector from y[i+2..] (LAPACK dlarfg)
@@ -994,7 +994,11 @@ __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
         if (nlo == lo && nhi == hi) break;
         lo = nlo;
         hi = nhi;
-        if (hi - lo <= 2.0 * kEps * fmax(fabs(lo), fabs(hi)) + pivmin) break;
+        // 1e-11 relative (or 2 eps ||T||) is enough: the eigenvector comes from
+        // inverse iteration, whose error does not depend on the shift's last
+        // digits (two solves gain (shift error / gap)^2), and the eigenvalue
+        // itself only feeds the 1e-3 ||T|| cluster rule of the finish
+        if (hi - lo <= fmax(1e-11 * fmax(fabs(lo), fabs(hi)), 2.0 * kEps * tnorm) + pivmin) break;
     }
     const double lam = 0.5 * (lo + hi);
     const u64 t1 = stmp ? clock64() : 0;
@@ -1325,6 +1329,152 @@ __global__ void __launch_bounds__(FIN_T) k_eig_finish(double* Zq, int n, int lda
     }
 }
 
+// Back-transformation of all k eigenvectors at once, one workgroup: the
+// vectors and one block of BT_NB reflectors at a time in LDS (the block is
+// read from global memory once, with every load in flight, instead of once
+// per eigenpair workgroup behind dependent waits), then per block
+// W = V^T Y, W <- T W, Y <- Y - V W (compact WY, last block first).  Used when
+// (k + BT_NB) n doubles fit the LDS; k_tri_vectors then leaves its vector
+// untransformed (bt_none).
+#define TB_T 1024
+__global__ void __launch_bounds__(TB_T) k_tri_back(double* __restrict__ Zq, int n, int lda, int k,
+                                                   const double* __restrict__ refl, const double* __restrict__ tf,
+                                                   u64* __restrict__ stamps)
+{
+    const bool stmp = stamps && threadIdx.x == 0;  // diagnostic: per-phase cycles
+    u64 ph[5] = {0, 0, 0, 0, 0}, tq = stmp ? clock64() : 0;
+    auto mark = [&](int i) {
+        if (stmp) {
+            const u64 t = clock64();
+            ph[i] += t - tq;
+            tq = t;
+        }
+    };
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Y = sm;                          // [k][n]
+    double* Vs = Y + (size_t)k * n;          // [BT_NB][n]: v_i at rows kb+1 .. n-1 (zero at rows <= kb+i)
+    __shared__ double W[BT_NB][16], W2[BT_NB][16], Ts[BT_NB][BT_NB];  // Ts: zero below the diagonal and past nb
+    __shared__ double Wp[4][BT_NB][16];  // per-wave partials of V^T Y
+    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    for (int x0 = 0; x0 < k * n; x0 += 8 * TB_T) {
+        double yv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int x = min(x0 + u * TB_T + tid, k * n - 1);
+            yv[u] = Zq[(size_t)(x / n) * lda + x % n];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int x = x0 + u * TB_T + tid;
+            if (x < k * n) Y[x] = yv[u];
+        }
+    }
+    const int nr = n - 2;
+    mark(4);
+    // block b's reflectors and T factor are loaded into registers while block
+    // b + 1 is applied (SB clamped unconditional loads per thread, in flight
+    // across the block's compute), then stored to LDS at the top of block b
+    constexpr int SB = 12;
+    double vv[SB], tv = 0.0;
+    auto fetch = [&](int b) {
+        const int kb = b * BT_NB, nb = min(BT_NB, nr - kb), m0 = kb + 1, m = n - m0;
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int x = min(u * TB_T + tid, BT_NB * m - 1);
+            const int i = x / m, j = m0 + x % m;
+            vv[u] = refl[(size_t)(kb + min(i, nb - 1)) * lda + j];
+        }
+        tv = tf[(size_t)b * BT_NB * BT_NB + min(tid, BT_NB * BT_NB - 1)];
+    };
+    const int nblk = nr > 0 ? (nr + BT_NB - 1) / BT_NB : 0;
+    if (nblk > 0) fetch(nblk - 1);
+    for (int b = nblk - 1; b >= 0; --b) {
+        const int kb = b * BT_NB, nb = min(BT_NB, nr - kb), m0 = kb + 1, m = n - m0;
+        __syncthreads();  // the previous block's Y update is complete before Vs is reused
+        mark(3);
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int x = u * TB_T + tid;
+            if (x < BT_NB * m) {
+                const int i = x / m, j = m0 + x % m;
+                Vs[x] = (i < nb && j > kb + i) ? vv[u] : 0.0;
+            }
+        }
+        if (tid < BT_NB * BT_NB) Ts[tid / BT_NB][tid % BT_NB] = tv;
+        __syncthreads();
+        if (b > 0) fetch(b - 1);
+        mark(0);
+        // W = V^T Y on fp64 MFMA (16x16x4: A = V, 16 reflectors x 4 rows; B =
+        // Y^T, 4 rows x 16 vectors): waves 0-3 the reflectors 0-15, waves 4-7
+        // 16-31, each wave every 4th group of 4 rows; partials summed below in
+        // wave order (deterministic).  Rows of Vs past nb are zero, vectors
+        // past k are masked to zero.
+        if (wv < 8) {
+            const int tile = wv >> 2, part = wv & 3, qv = lane & 15;
+            const double* va = Vs + (size_t)(tile * 16 + (lane & 15)) * m;
+            const double* yb = Y + (size_t)min(qv, k - 1) * n + m0;
+            typedef double d4v __attribute__((ext_vector_type(4)));
+            d4v acc = {0.0, 0.0, 0.0, 0.0};
+            for (int j0 = part * 4; j0 < m; j0 += 16) {
+                const int j = j0 + (lane >> 4), jc = min(j, m - 1);
+                const double av = va[jc], yv = yb[jc];  // unconditional (clamped) loads, then masks
+                const double a = (j < m) ? av : 0.0;
+                const double bq = (j < m && qv < k) ? yv : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Wp[part][tile * 16 + (lane >> 4) + 4 * r][lane & 15] = acc[r];
+        }
+        __syncthreads();
+        if (tid < BT_NB * 16) {
+            const int i = tid >> 4, q = tid & 15;
+            W[i][q] = ((Wp[0][i][q] + Wp[1][i][q]) + Wp[2][i][q]) + Wp[3][i][q];
+        }
+        if (tid < BT_NB * 16) {  // W2 = T W (T upper triangular, zero past nb)
+            const int i = tid >> 4, q = tid & 15;
+            double s = 0.0;
+#pragma unroll
+            for (int c = 0; c < BT_NB; ++c) s = fma(Ts[i][c], W[c][q], s);
+            W2[i][q] = s;
+        }
+        __syncthreads();
+        mark(2);
+        // Y -= V W2 on fp64 MFMA: output tile = 16 rows of Y^T x 16 vectors,
+        // A[j][i] = V[i][j], B = W2 (32 x 16), K = the block's 32 reflectors
+        {
+            typedef double d4v __attribute__((ext_vector_type(4)));
+            const int ntile = (m + 15) / 16;
+            for (int t = wv; t < ntile; t += TB_T / 64) {
+                d4v acc = {0.0, 0.0, 0.0, 0.0};
+                const int jr = t * 16 + (lane & 15);
+#pragma unroll
+                for (int i0 = 0; i0 < BT_NB; i0 += 4) {
+                    const int i = i0 + (lane >> 4);
+                    const double av = Vs[(size_t)i * m + min(jr, m - 1)];
+                    const double a = (jr < m) ? av : 0.0;
+                    const double bq = W2[i][lane & 15];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq, acc, 0, 0, 0);
+                }
+                // D[row][col]: row = (lane >> 4) + 4 r indexes the 16 rows of the
+                // A tile (rows of Y^T = positions j), col = lane & 15 the vector q
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = t * 16 + (lane >> 4) + 4 * r, q = lane & 15;
+                    if (j < m && q < k) Y[(size_t)q * n + m0 + j] -= acc[r];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    mark(3);
+    for (int x = tid; x < k * n; x += TB_T) Zq[(size_t)(x / n) * lda + x % n] = Y[x];
+    if (stmp)
+        for (int i = 0; i < 5; ++i) stamps[12 + i] = ph[i];
+}
+
+// dynamic LDS of k_tri_back (its static arrays take 32 KB more)
+static size_t tri_back_lds(int n, int k) { return sizeof(double) * ((size_t)k + BT_NB) * n; }
+
 // Same result with the k vectors in LDS (k n doubles <= 160 KB): vectors
 // with no cluster predecessor ("heads", almost all of them) are normalised
 // and signed in parallel, one wave each, with no workgroup barrier; the rest
@@ -1494,6 +1644,32 @@ extern "C" hipError_t scc_launch_sbr_reduce(const double* A, int n, int lda, dou
                                             unsigned long long* stamps, hipStream_t st);
 extern "C" hipError_t scc_launch_sbr_back(double* Zq, int n, int lda, int k, const double* scr, hipStream_t st);
 
+// A non-blocking side stream (and fork / join events) per device for work
+// that overlaps the eigensolver's main chain; created once, never destroyed
+// (process lifetime, like the HIP runtime's own streams).
+static void side_stream(hipStream_t* s, hipEvent_t* fork_ev, hipEvent_t* join_ev)
+{
+    static hipStream_t ss[64] = {};
+    static hipEvent_t fe[64] = {}, je[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        *s = nullptr;
+        return;
+    }
+    if (!ss[dev]) {
+        if (hipStreamCreateWithFlags(&ss[dev], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&fe[dev], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&je[dev], hipEventDisableTiming) != hipSuccess) {
+            ss[dev] = nullptr;
+            *s = nullptr;
+            return;
+        }
+    }
+    *s = ss[dev];
+    *fork_ev = fe[dev];
+    *join_ev = je[dev];
+}
+
 extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 {
     int nwg;
@@ -1649,17 +1825,47 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     v.xcd = pin && (pin_mode == 1 || 8 * k <= 256) ? t.reg : nullptr;  // wait needs co-residency
     v.vcount = flags + 5;
     v.err = flags + 1;
-    if (n > 2) {
-        const int nblk = (n - 2 + BT_NB - 1) / BT_NB;
-        hipLaunchKernelGGL(k_refl_T, dim3(pin ? 8 * nblk : nblk), dim3(1024), 0, st, t.refl, t.tau, n, lda,
-                           scratch + L.tf, pin ? t.reg : nullptr, flags + 9);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
     hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
+    // one workgroup back-transforms all k vectors when they and a reflector
+    // block fit its LDS (SCC_EIG_BT=0: per-eigenpair back-transformation)
+    const char* bt_env = getenv("SCC_EIG_BT");
+    const bool bt_one = n > 2 && n - 1 <= 12 * TB_T / BT_NB && tri_back_lds(n, k) + 33 * 1024 <= EIG_LDS_MAX &&
+                        !(bt_env && *bt_env && atoi(bt_env) == 0);  // one fetch batch covers a block
+    v.bt_none = bt_one ? 1 : 0;
+    // k_refl_T (reflectors -> T factors) does not depend on the tridiagonal's
+    // eigenpairs: with the one-workgroup back-transformation it runs on a side
+    // stream beside k_tri_vectors, which then needs nothing from the
+    // reflectors' XCD either
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    if (bt_one) {
+        v.xcd = nullptr;
+        side_stream(&side, &fork_ev, &join_ev);
+    }
+    if (n > 2) {
+        const int nblk = (n - 2 + BT_NB - 1) / BT_NB;
+        hipStream_t rs = st;
+        if (side) {
+            hipEventRecord(fork_ev, st);
+            hipStreamWaitEvent(side, fork_ev, 0);
+            rs = side;
+        }
+        hipLaunchKernelGGL(k_refl_T, dim3(pin ? 8 * nblk : nblk), dim3(1024), 0, rs, t.refl, t.tau, n, lda,
+                           scratch + L.tf, pin ? t.reg : nullptr, flags + 9);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (side) hipEventRecord(join_ev, side);
+    }
     if (marks) hipEventRecord(marks[2], st);
     hipLaunchKernelGGL(k_tri_vectors, dim3(v.xcd ? 8 * k : k), dim3(VEC_T), vlds, st, v);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (side && n > 2) hipStreamWaitEvent(st, join_ev, 0);
+    if (bt_one) {
+        const size_t blds = tri_back_lds(n, k);
+        hipFuncSetAttribute((const void*)k_tri_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
+        hipLaunchKernelGGL(k_tri_back, dim3(1), dim3(TB_T), blds, st, v.Zq, n, lda, k, v.refl, v.tf, stamps);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (marks) hipEventRecord(marks[3], st);
     if (marks) hipEventRecord(marks[4], st);
     launch_eig_finish(v.Zq, n, lda, k, W, v.tnorm, Z, st);
