@@ -208,10 +208,12 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
 // column boundary, and a run keeps those lines in one XCD's L2 instead of two
 // partial write-backs.
 #define DT_ROWS 256
-#define DT_COLS 64
-#define DT_RATIO (DT_ROWS / DT_COLS)
+// columns per tile: 64, or 256 when the scores outgrow the L2 (N >= 64k):
+// every tile reloads its rows' scores (128 B per row), 4x less often with
+// 256 columns (config D: 40 GB of score fetches at 64)
 #define DT_RUN 8
 
+template <int DT_RATIO>
 __device__ inline void dist_tile_of(long long t, int nrb, int& cb, int& rb)
 {
     // column blocks come in groups Q = cb / DT_RATIO of DT_RATIO * (nrb - Q) tiles
@@ -227,7 +229,7 @@ __device__ inline void dist_tile_of(long long t, int nrb, int& cb, int& rb)
 
 // Columns [c_lo, c_hi) only (a rank's slice of the packed output, which
 // starts at packed index obase); t0 = the tiles of the column blocks before.
-template <bool F32>
+template <bool F32, int DT_COLS>
 __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restrict__ P, int N, int nrb, long long ntiles,
                                                          long long t0, int c_lo, int c_hi, long long obase,
                                                          void* __restrict__ out)
@@ -237,7 +239,7 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
     const long long t = ((k / DT_RUN) * 8 + x) * DT_RUN + k % DT_RUN;
     if (t >= ntiles) return;
     int cb, rb;
-    dist_tile_of(t0 + t, nrb, cb, rb);
+    dist_tile_of<DT_ROWS / DT_COLS>(t0 + t, nrb, cb, rb);
     // the tile's column scores in LDS, |p_j|^2 in the zero padding slot 15;
     // every lane reads a column at the same address (broadcast), and LDS
     // returns in order, so the next column's reads overlap this column's
@@ -639,10 +641,10 @@ extern "C" hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld,
     return hipGetLastError();
 }
 
-extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32,
-                                             hipStream_t st)
+template <int DT_COLS>
+static void launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
 {
-    if (N < 2 || c_hi <= c_lo) return hipSuccess;
+    constexpr int DT_RATIO = DT_ROWS / DT_COLS;
     const int nrb = (N + DT_ROWS - 1) / DT_ROWS;
     const int cb0 = c_lo / DT_COLS, cb1 = (c_hi + DT_COLS - 1) / DT_COLS;
     long long t0 = 0, ntiles = 0;
@@ -651,11 +653,23 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     const long long ngrp = (ntiles + DT_RUN - 1) / DT_RUN;
     const dim3 grid((unsigned)(((ngrp + 7) / 8) * 8 * DT_RUN));
     if (f32)
-        hipLaunchKernelGGL(k_dist_euclid<true>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo, c_hi, obase,
-                           out);
+        hipLaunchKernelGGL((k_dist_euclid<true, DT_COLS>), grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo,
+                           c_hi, obase, out);
     else
-        hipLaunchKernelGGL(k_dist_euclid<false>, grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo, c_hi, obase,
-                           out);
+        hipLaunchKernelGGL((k_dist_euclid<false, DT_COLS>), grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo,
+                           c_hi, obase, out);
+}
+
+extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32,
+                                             hipStream_t st)
+{
+    if (N < 2 || c_hi <= c_lo) return hipSuccess;
+    const char* env = getenv("SCC_DIST_COLS");  // 64 or 256 (default: by N)
+    const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? 256 : 64);
+    if (cols == 256)
+        launch_dist_euclid<256>(P, N, c_lo, c_hi, out, f32, st);
+    else
+        launch_dist_euclid<64>(P, N, c_lo, c_hi, out, f32, st);
     return hipGetLastError();
 }
 
