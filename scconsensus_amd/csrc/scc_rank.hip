@@ -842,6 +842,7 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 #define RSW_BINS (1 << RSW_LOG2B)
 #define RSW_CAP 256
 #define RSW_HCAP 512
+#define RSW_PACC 1280     // genes with <= this many tested pairs keep them (and their sums) in registers
 
 // ===================================================================== split
 #define SP_T 1024
@@ -1464,9 +1465,48 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     auto fill_null = [&](int a, int b) {
         for (int q = a + lane; q < b; q += 64) A.sbuckets[q] = nullit;
     };
-    for (int f = blockIdx.x * 4 + wv; f < cnt; f += gridDim.x * 4) {
+    // Each wave takes a contiguous run of the parent list.  The list holds a
+    // gene's parents together, so the gene's tested pairs are loaded into
+    // registers once per run (lane l: pairs l, l + 64, ...) and the in-parent
+    // cross terms of consecutive parents add up there, reaching accS with one
+    // atomic per (run of one gene, pair) instead of one per (parent, pair).
+    // The consecutive sub-buckets also keep the wave kernel's register
+    // accumulation on one gene.
+    constexpr int TS = RSW_PACC / 64;
+    const int nw = gridDim.x * 4, w = blockIdx.x * 4 + wv;
+    const int f0 = (int)((long long)cnt * w / nw), f1 = (int)((long long)cnt * (w + 1) / nw);
+    u32 tpr[TS], par[TS];
+#pragma unroll
+    for (int s = 0; s < TS; ++s) tpr[s] = par[s] = 0;
+    int pg = -1, pnt = 0, pn = 0;
+    auto flush_par = [&]() {
+        if (pg >= 0 && pn > 0 && pnt <= RSW_PACC) {
+#pragma unroll
+            for (int s = 0; s < TS; ++s) {
+                if (s * 64 >= pnt) break;
+                if (par[s])
+                    atomicAdd((unsigned long long*)&A.accS[(size_t)(tpr[s] & 0xffffu) * A.G + pg], (unsigned long long)par[s]);
+                par[s] = 0;
+            }
+        }
+        pn = 0;
+    };
+    for (int f = f0; f < f1; ++f) {
         const ScRankItem it = list[f];
         const int n = it.n, g = it.gene;
+        // a parent adds at most 128 * 128 to one pair: flush before u32 could wrap
+        if (g != pg || pn >= 65536) {
+            flush_par();
+            if (g != pg) {
+                pg = g;
+                pnt = A.gene_nt[g];
+                if (pnt > 0 && pnt <= RSW_PACC) {
+                    const u32* tl = A.gene_tp + (size_t)g * A.P;
+#pragma unroll
+                    for (int s = 0; s < TS; ++s) tpr[s] = tl[min(s * 64 + lane, pnt - 1)];
+                }
+            }
+        }
         if (n > RSW_CAP) continue;  // k_rank_resplit (a workgroup per parent)
         u64 kr[EPL];
         u32 cd[EPL];
@@ -1662,18 +1702,33 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
             }
         }
         wsync();
-        const int ntp = A.gene_nt[g];
-        const u32* tl = A.gene_tp + (size_t)g * A.P;
-        for (int j = lane; j < ntp; j += 64) {
-            const u32 v = tl[j];
-            const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
-            if (!L.m[a] || !L.m[b]) continue;
-            u64 sacc = 0;
-            for (int q = 0; q < nb; ++q) sacc += (u64)L.hs[q * K + a] * L.bs[q * K + b];
-            if (sacc) atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
+        const int ntp = pnt;
+        if (ntp <= RSW_PACC) {
+            // m[a] = 0 or m[b] = 0 makes every product zero: no test needed
+            ++pn;
+#pragma unroll
+            for (int s = 0; s < TS; ++s) {
+                if (s * 64 >= ntp) break;
+                const u32 v = tpr[s];
+                const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+                u32 sacc = 0;  // <= m[a] * m[b] <= 128 * 128
+                for (int q = 0; q < nb; ++q) sacc += L.hs[q * K + a] * L.bs[q * K + b];
+                par[s] += (s * 64 + lane < ntp) ? sacc : 0u;
+            }
+        } else {
+            const u32* tl = A.gene_tp + (size_t)g * A.P;
+            for (int j = lane; j < ntp; j += 64) {
+                const u32 v = tl[j];
+                const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+                if (!L.m[a] || !L.m[b]) continue;
+                u64 sacc = 0;
+                for (int q = 0; q < nb; ++q) sacc += (u64)L.hs[q * K + a] * L.bs[q * K + b];
+                if (sacc) atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
+            }
         }
         wsync();
     }
+    flush_par();
     fill_null(sl_cur, sl_end);
 }
 
