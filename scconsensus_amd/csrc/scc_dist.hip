@@ -17,6 +17,7 @@
 //                   LDS-pipelined FP32 MFMA (v_mfma_f32_32x32x2_f32) Gram with the
 //                   1 - r epilogue fused into coalesced packed-column stores.
 #include "scc_common.hpp"
+#include <algorithm>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -297,6 +298,137 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
             ((double*)out)[B + i] = d;
         B += N - j - 2;
     }
+}
+
+// Line-aligned variant (default; SCC_DIST_ALIGNED=0 selects k_dist_euclid).
+// In R's packed order a column's entries are contiguous but start at any
+// offset, so a fixed row partition leaves two partial 128-B lines per (column,
+// tile) that the neighbouring tile completes later: read-modify-writes in HBM
+// (0.5 GB fetched by a write-only kernel at config B).  Here tile rb owns, for
+// column j, the rows whose packed addresses fall in the 128-B-aligned window
+// [rb TR - delta_j, rb TR + TR - delta_j) (delta_j = that address mod one line;
+// TR a multiple of the line, so consecutive tiles partition every column
+// exactly): its 256 threads compute rows rb TR - HALO + t (HALO = one line of
+// outputs), the values go through an LDS stage (NB columns at a time) and are
+// stored as whole lines.  Partial lines remain only where one column's segment
+// ends and the next begins.  Column scores are wave-uniform loads (scalar
+// registers, no LDS broadcast per element); |p_j|^2 is formed once per tile.
+#define DA_T 256
+#define DA_NB 8
+
+template <int TR, int DC>
+__device__ __host__ inline int da_rbmin(int cb)
+{
+    const int r = (cb * DC + 1) / TR - 1;
+    return r > 0 ? r : 0;
+}
+
+template <bool F32, int DC>
+__global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict__ P, int N, int nrb, int cb_lo,
+                                                       int ncbl, int c_lo, int c_hi, long long obase,
+                                                       void* __restrict__ out)
+{
+    constexpr int HALO = F32 ? 32 : 16;  // outputs per 128-B line
+    constexpr int TR = DA_T - HALO;      // rows owned per tile
+    __shared__ double stage[DA_NB][DA_T];
+    __shared__ double cn[DC];
+    // folded triangle: grid row y holds column block y then its mirror
+    const int y = blockIdx.y;
+    int x = blockIdx.x;
+    int cb = cb_lo + y;
+    const int cntA = nrb - da_rbmin<TR, DC>(cb);
+    if (x >= cntA) {
+        x -= cntA;
+        const int cb2 = cb_lo + ncbl - 1 - y;
+        if (cb2 <= cb) return;
+        cb = cb2;
+        if (x >= nrb - da_rbmin<TR, DC>(cb)) return;
+    }
+    const int r0 = (da_rbmin<TR, DC>(cb) + x) * TR;
+    const int jb = max(cb * DC, c_lo);
+    const int je = min(min(cb * DC + DC, c_hi), min(N - 1, r0 + TR - 1));  // columns with a row in the window
+    if (jb >= je) return;
+    const int t = threadIdx.x;
+    for (int e = t; e < DC; e += DA_T) {
+        const int jj = min(cb * DC + e, N - 1);
+        double nn = 0.0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) nn = fma(P[(size_t)jj * 16 + q], P[(size_t)jj * 16 + q], nn);
+        cn[e] = nn;
+    }
+    const int i = r0 - HALO + t;  // this thread's row
+    const int ic = min(max(i, 0), N - 1);
+    double pi[15];
+#pragma unroll
+    for (int q = 0; q < 15; ++q) pi[q] = P[(size_t)ic * 16 + q];
+    double ni = 0.0;
+#pragma unroll
+    for (int q = 0; q < 15; ++q) ni = fma(pi[q], pi[q], ni);
+    __syncthreads();
+    for (int j0 = jb; j0 < je; j0 += DA_NB) {
+#pragma unroll
+        for (int c = 0; c < DA_NB; ++c) {
+            const int j = j0 + c;
+            if (j >= je) break;
+            const double* pj = P + (size_t)j * 16;
+            double dot = 0.0;
+#pragma unroll
+            for (int q = 0; q < 15; ++q) dot = fma(pi[q], pj[q], dot);
+            const double nsum = ni + cn[j - cb * DC];
+            double s = fma(-2.0, dot, nsum);
+            if (s < 0x1p-20 * nsum) {  // near-identical cells: the difference form
+                s = 0.0;
+#pragma unroll
+                for (int q = 0; q < 15; ++q) {
+                    const double dv = pi[q] - pj[q];
+                    s = fma(dv, dv, s);
+                }
+            }
+            stage[c][t] = __builtin_amdgcn_sqrt(s);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < DA_NB; ++c) {
+            const int j = j0 + c;
+            if (j >= je) break;
+            const long long B = (long long)j * (2LL * N - j - 1) / 2 - j - 1 - obase;  // out index of (i, j) = B + i
+            const int delta = (int)((B + r0) & (HALO - 1));
+            const int i2 = r0 - delta + t;
+            if (t < TR && i2 > j && i2 < N) {
+                const double v = stage[c][HALO - delta + t];
+                if (F32)
+                    ((float*)out)[B + i2] = (float)v;
+                else
+                    ((double*)out)[B + i2] = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int DC>
+static void launch_dist_aligned(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
+{
+    const int HALO = f32 ? 32 : 16, TR = DA_T - HALO;
+    const int nrb = (N + HALO - 1) / TR + 1;
+    const int cb_lo = c_lo / DC, cb_hi = (c_hi + DC - 1) / DC, ncbl = cb_hi - cb_lo;
+    const int npair = (ncbl + 1) / 2;
+    int gx = 1;
+    for (int y = 0; y < npair; ++y) {
+        const int a = cb_lo + y, b = cb_lo + ncbl - 1 - y;
+        const int ra = f32 ? da_rbmin<DA_T - 32, DC>(a) : da_rbmin<DA_T - 16, DC>(a);
+        const int rbb = f32 ? da_rbmin<DA_T - 32, DC>(b) : da_rbmin<DA_T - 16, DC>(b);
+        const int cnt = (nrb - ra) + (b > a ? nrb - rbb : 0);
+        gx = std::max(gx, cnt);
+    }
+    const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
+    const dim3 grid((unsigned)gx, (unsigned)npair);
+    if (f32)
+        hipLaunchKernelGGL((k_dist_aligned<true, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
+                           obase, out);
+    else
+        hipLaunchKernelGGL((k_dist_aligned<false, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
+                           obase, out);
 }
 
 // ------------------------------------------------------------------ Pearson
@@ -666,6 +798,14 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     if (N < 2 || c_hi <= c_lo) return hipSuccess;
     const char* env = getenv("SCC_DIST_COLS");  // 64 or 256 (default: by N)
     const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? 256 : 64);
+    const char* al = getenv("SCC_DIST_ALIGNED");
+    if (!(al && *al && atoi(al) == 0)) {
+        if (cols == 256)
+            launch_dist_aligned<256>(P, N, c_lo, c_hi, out, f32, st);
+        else
+            launch_dist_aligned<64>(P, N, c_lo, c_hi, out, f32, st);
+        return hipGetLastError();
+    }
     if (cols == 256)
         launch_dist_euclid<256>(P, N, c_lo, c_hi, out, f32, st);
     else

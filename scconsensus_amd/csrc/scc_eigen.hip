@@ -1639,6 +1639,10 @@ static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
 }
 
 extern "C" int scc_sbr_band(int n);
+extern "C" int scc_tridiag_cu_fits(int n);
+extern "C" hipError_t scc_launch_tridiag_cu(const double* A, int n, int lda, double* grows, double* d, double* e,
+                                            double* tau, double* refl, unsigned int* reg, unsigned long long* stamps,
+                                            hipStream_t st);
 extern "C" size_t scc_sbr_scratch_doubles(int n, int lda);
 extern "C" hipError_t scc_launch_sbr_reduce(const double* A, int n, int lda, double* scr, double* d, double* e,
                                             unsigned long long* stamps, hipStream_t st);
@@ -1766,11 +1770,21 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 64;
     }
+    // opt-in (SCC_EIG_CU=1, n <= 336): the whole matrix resident in ONE compute
+    // unit (scc_tridiag_cu.hip), no cross-CU hand-off, fixed reduction order
+    // (bit-reproducible).  Measured 4x SLOWER than the kernels below (n = 323:
+    // 4.48 vs 1.07 ms; n = 64: 0.35 vs 0.20 ms): the per-row latency chains of
+    // one workgroup cost more than the per-column hand-off they remove.
+    const char* cu_env = getenv("SCC_EIG_CU");
+    const bool one_cu = scc_tridiag_cu_fits(n) && cu_env && *cu_env && atoi(cu_env) != 0;
     const char* wa_env = getenv("SCC_EIG_WAVE");
     const bool wave_agents = (wa_env && *wa_env) ? atoi(wa_env) != 0 : false;  // measured slower (polling load)
     // wave agents: the planned participants' rows in LDS (HBM fall-back in the kernel)
     const size_t wa_lds = sizeof(double) * (size_t)TRI_W * ((n + TRI_W * nwg - 1) / (TRI_W * nwg)) * n;
-    if (wave_agents && n <= 64 * TW_NJ && wa_lds <= EIG_LDS_MAX && nwg * TRI_W <= TW_MAXA) {
+    if (one_cu) {
+        e = scc_launch_tridiag_cu(A, n, lda, t.work, t.d, t.e, t.tau, t.refl, t.reg, stamps, st);
+        if (e != hipSuccess) return e;
+    } else if (wave_agents && n <= 64 * TW_NJ && wa_lds <= EIG_LDS_MAX && nwg * TRI_W <= TW_MAXA) {
         size_t l2 = wa_lds < 82 * 1024 ? 82 * 1024 : wa_lds;
         t.lds_rows_cap = (int)(l2 / sizeof(double));
         if (t.xcd_local) {

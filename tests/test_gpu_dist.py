@@ -196,3 +196,52 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, wave, monkeypatch):
     dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+@pytest.mark.parametrize("n", [2, 3, 17, 64, 65, 128, 150, 191, 200, 241, 250, 300, 323, 336])
+def test_one_cu_tridiagonalisation(eng, n, monkeypatch):
+    """Single-CU tridiagonalisation (scc_tridiag_cu.hip, n <= 336: rows in
+    registers, in LDS and, past n ~ 190, in a global scratch store) against the
+    exact SVD and the multi-workgroup kernel; bit-identical from run to run
+    (fixed reduction order)."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SBR", "0")
+    rng = np.random.default_rng(500 + n)
+    N = 800
+    X = rng.standard_normal((n, N)) * np.linspace(3.0, 0.5, n)[:, None]
+    k = min(20, n)
+    X[:k] += rng.standard_normal((k, 1)) * rng.standard_normal((1, N)) * 4.0
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    monkeypatch.setenv("SCC_EIG_CU", "1")
+    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    d1b = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    assert np.array_equal(d1, d1b)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(d1 - ref)) < 1e-5
+    monkeypatch.setenv("SCC_EIG_CU", "0")
+    d0 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    assert np.max(np.abs(d1 - d0)) < 1e-6
+
+
+@pytest.mark.parametrize("n", [90, 300])
+def test_one_cu_rank_deficient_and_repeated(eng, n, monkeypatch):
+    """One-CU path: exactly repeated eigenvalues in the top 15, then identical
+    genes (zero-norm columns: tau = 0 reflectors), with rows in every store."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SBR", "0")
+    monkeypatch.setenv("SCC_EIG_CU", "1")
+    rng = np.random.default_rng(9 + n)
+    N = 700
+    sv = np.array([9.0] * 3 + [7.0] * 4 + [5.0] * 2 + [4.0] * 6 + [1.0] * (n - 15))
+    Q, _ = np.linalg.qr(rng.standard_normal((N, n)))
+    Q -= Q.mean(axis=0)
+    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    X = (Q @ np.diag(sv) @ V.T).T
+    g = np.arange(n)
+    ds = eng.dataset_dense(X)
+    assert np.max(np.abs(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID) - O.dist_euclidean(O.pca_scores(X, g)))) < 1e-5
+    X2 = np.concatenate([X[: n // 3]] * 3)  # rank <= n / 3
+    ds2 = eng.dataset_dense(X2)
+    dist = eng.distance(ds2, g, nat.SCC_DIST_PCA_EUCLID)
+    assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
