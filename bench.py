@@ -315,7 +315,7 @@ def main():
     frac_entries = 1.0 / world if multi else 1.0  # a rank's share of the packed output (equal-entry slices)
     alg = {
         # packed fp64 R `dist` output + the N x 16 scores read
-        "dist": ("hbm", 8.0 * npairs_cells * frac_entries + 16 * 8.0 * d.N, "k_dist_euclid"),
+        "dist": ("hbm", 8.0 * npairs_cells * frac_entries + 16 * 8.0 * d.N, "k_dist_aligned"),
         # CSC read twice (12 B/nnz + 8 B/cell), keys written once (8 B/nnz), chunk counts (4 B, 3 passes)
         "ingest": ("hbm", 2 * (12.0 * nnz + 8.0 * (d.N + 1)) + 8.0 * nnz / world + 3 * 4.0 * ncc * d.G / world,
                    "k_ing_scatter"),

@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
     }
 }
 
-// Line-aligned variant (default; SCC_DIST_ALIGNED=0 selects k_dist_euclid).
+// Line-aligned variant with a workgroup stage (SCC_DIST_KERNEL=1).
 // In R's packed order a column's entries are contiguous but start at any
 // offset, so a fixed row partition leaves two partial 128-B lines per (column,
 // tile) that the neighbouring tile completes later: read-modify-writes in HBM
@@ -323,14 +323,14 @@ __device__ __host__ inline int da_rbmin(int cb)
     return r > 0 ? r : 0;
 }
 
-template <bool F32, int DC>
+template <bool F32, int DC, int NB, bool NT>
 __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict__ P, int N, int nrb, int cb_lo,
                                                        int ncbl, int c_lo, int c_hi, long long obase,
                                                        void* __restrict__ out)
 {
     constexpr int HALO = F32 ? 32 : 16;  // outputs per 128-B line
     constexpr int TR = DA_T - HALO;      // rows owned per tile
-    __shared__ double stage[DA_NB][DA_T];
+    __shared__ double stage[NB][DA_T];
     __shared__ double cn[DC];
     // folded triangle: grid row y holds column block y then its mirror
     const int y = blockIdx.y;
@@ -365,9 +365,9 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
 #pragma unroll
     for (int q = 0; q < 15; ++q) ni = fma(pi[q], pi[q], ni);
     __syncthreads();
-    for (int j0 = jb; j0 < je; j0 += DA_NB) {
+    for (int j0 = jb; j0 < je; j0 += NB) {
 #pragma unroll
-        for (int c = 0; c < DA_NB; ++c) {
+        for (int c = 0; c < NB; ++c) {
             const int j = j0 + c;
             if (j >= je) break;
             const double* pj = P + (size_t)j * 16;
@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
         }
         __syncthreads();
 #pragma unroll
-        for (int c = 0; c < DA_NB; ++c) {
+        for (int c = 0; c < NB; ++c) {
             const int j = j0 + c;
             if (j >= je) break;
             const long long B = (long long)j * (2LL * N - j - 1) / 2 - j - 1 - obase;  // out index of (i, j) = B + i
@@ -396,17 +396,128 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
             const int i2 = r0 - delta + t;
             if (t < TR && i2 > j && i2 < N) {
                 const double v = stage[c][HALO - delta + t];
-                if (F32)
-                    ((float*)out)[B + i2] = (float)v;
-                else
-                    ((double*)out)[B + i2] = v;
+                if (F32) {
+                    if (NT)
+                        __builtin_nontemporal_store((float)v, (float*)out + B + i2);
+                    else
+                        ((float*)out)[B + i2] = (float)v;
+                } else {
+                    if (NT)
+                        __builtin_nontemporal_store(v, (double*)out + B + i2);
+                    else
+                        ((double*)out)[B + i2] = v;
+                }
             }
         }
         __syncthreads();
     }
 }
 
+// Wave-window variant (default): no workgroup barrier at all.  Each wave
+// computes 64 consecutive rows [R - HALO, R + WR) of every column (WR = 64 -
+// HALO, R a multiple of one line) and stores the WR-row window [R - delta_j,
+// R + WR - delta_j), which is line-aligned: the shift is a lane rotation of
+// the computed values (ds_bpermute, no LDS storage), and the first HALO rows
+// are computed twice (by this wave and the one below).  Four waves per tile,
+// tiles of 4 WR rows; column scores as wave-uniform (scalar) loads.
+template <bool F32, int DC>
+__global__ void __launch_bounds__(DA_T) k_dist_wave(const double* __restrict__ P, int N, int nrb, int cb_lo,
+                                                    int ncbl, int c_lo, int c_hi, long long obase,
+                                                    void* __restrict__ out)
+{
+    constexpr int HALO = F32 ? 32 : 16;  // outputs per 128-B line
+    constexpr int WR = 64 - HALO;        // rows stored per wave
+    constexpr int TR = (DA_T / 64) * WR; // rows per tile
+    __shared__ double cn[DC];
+    const int y = blockIdx.y;
+    int x = blockIdx.x;
+    int cb = cb_lo + y;
+    const int cntA = nrb - da_rbmin<TR, DC>(cb);
+    if (x >= cntA) {
+        x -= cntA;
+        const int cb2 = cb_lo + ncbl - 1 - y;
+        if (cb2 <= cb) return;
+        cb = cb2;
+        if (x >= nrb - da_rbmin<TR, DC>(cb)) return;
+    }
+    const int r0 = (da_rbmin<TR, DC>(cb) + x) * TR;
+    const int jb = max(cb * DC, c_lo);
+    const int je = min(min(cb * DC + DC, c_hi), min(N - 1, r0 + TR - 1));
+    if (jb >= je) return;
+    const int t = threadIdx.x, lane = t & 63;
+    for (int e = t; e < DC; e += DA_T) {
+        const int jj = min(cb * DC + e, N - 1);
+        double nn = 0.0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) nn = fma(P[(size_t)jj * 16 + q], P[(size_t)jj * 16 + q], nn);
+        cn[e] = nn;
+    }
+    __syncthreads();
+    const int R = r0 + WR * scc_wave_id();
+    const int wje = min(je, R + WR - 1);  // this wave's columns with a row in its window
+    const int i = R - HALO + lane;
+    const int ic = min(max(i, 0), N - 1);
+    double pi[15];
+#pragma unroll
+    for (int q = 0; q < 15; ++q) pi[q] = P[(size_t)ic * 16 + q];
+    double ni = 0.0;
+#pragma unroll
+    for (int q = 0; q < 15; ++q) ni = fma(pi[q], pi[q], ni);
+    long long B = (long long)jb * (2LL * N - jb - 1) / 2 - jb - 1 - obase;  // out index of (i, j) = B + i
+    for (int j = jb; j < wje; ++j) {
+        const double* pj = P + (size_t)j * 16;
+        double dot = 0.0;
+#pragma unroll
+        for (int q = 0; q < 15; ++q) dot = fma(pi[q], pj[q], dot);
+        const double nsum = ni + cn[j - cb * DC];
+        double s = fma(-2.0, dot, nsum);
+        if (s < 0x1p-20 * nsum) {  // near-identical cells: the difference form
+            s = 0.0;
+#pragma unroll
+            for (int q = 0; q < 15; ++q) {
+                const double dv = pi[q] - pj[q];
+                s = fma(dv, dv, s);
+            }
+        }
+        const double d = __builtin_amdgcn_sqrt(s);
+        const int delta = (int)((B + R) & (HALO - 1));
+        const double v = __shfl(d, min(lane + HALO - delta, 63), 64);
+        const int i2 = R - delta + lane;
+        if (lane < WR && i2 > j && i2 < N) {
+            if (F32)
+                ((float*)out)[B + i2] = (float)v;
+            else
+                ((double*)out)[B + i2] = v;
+        }
+        B += N - j - 2;
+    }
+}
+
 template <int DC>
+static void launch_dist_wave(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
+{
+    const int HALO = f32 ? 32 : 16, TR = (DA_T / 64) * (64 - HALO);
+    const int nrb = (N + HALO - 1) / TR + 1;
+    const int cb_lo = c_lo / DC, cb_hi = (c_hi + DC - 1) / DC, ncbl = cb_hi - cb_lo;
+    const int npair = (ncbl + 1) / 2;
+    int gx = 1;
+    for (int y = 0; y < npair; ++y) {
+        const int a = cb_lo + y, b = cb_lo + ncbl - 1 - y;
+        const int ra = f32 ? da_rbmin<(DA_T / 64) * 32, DC>(a) : da_rbmin<(DA_T / 64) * 48, DC>(a);
+        const int rbb = f32 ? da_rbmin<(DA_T / 64) * 32, DC>(b) : da_rbmin<(DA_T / 64) * 48, DC>(b);
+        gx = std::max(gx, (nrb - ra) + (b > a ? nrb - rbb : 0));
+    }
+    const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
+    const dim3 grid((unsigned)gx, (unsigned)npair);
+    if (f32)
+        hipLaunchKernelGGL((k_dist_wave<true, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
+                           obase, out);
+    else
+        hipLaunchKernelGGL((k_dist_wave<false, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
+                           obase, out);
+}
+
+template <int DC, int NB, bool NT>
 static void launch_dist_aligned(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
 {
     const int HALO = f32 ? 32 : 16, TR = DA_T - HALO;
@@ -424,10 +535,10 @@ static void launch_dist_aligned(const double* P, int N, int c_lo, int c_hi, void
     const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
     const dim3 grid((unsigned)gx, (unsigned)npair);
     if (f32)
-        hipLaunchKernelGGL((k_dist_aligned<true, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
+        hipLaunchKernelGGL((k_dist_aligned<true, DC, NB, NT>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
                            obase, out);
     else
-        hipLaunchKernelGGL((k_dist_aligned<false, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
+        hipLaunchKernelGGL((k_dist_aligned<false, DC, NB, NT>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
                            obase, out);
 }
 
@@ -796,14 +907,30 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
                                              hipStream_t st)
 {
     if (N < 2 || c_hi <= c_lo) return hipSuccess;
-    const char* env = getenv("SCC_DIST_COLS");  // 64 or 256 (default: by N)
-    const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? 256 : 64);
-    const char* al = getenv("SCC_DIST_ALIGNED");
-    if (!(al && *al && atoi(al) == 0)) {
+    // SCC_DIST_KERNEL: 1 = workgroup-staged line windows (default), 2 = wave
+    // windows, 0 = the unaligned tiles (k_dist_euclid).  Measured at config B:
+    // 0.51 (nontemporal stores) / 0.54 / 0.59 / 0.69 ms; config D: 33.2 (64
+    // columns per tile, nontemporal) / 35.0 (64) / 36.2 (256) / 38.5 / 38.1 ms.
+    const char* ke = getenv("SCC_DIST_KERNEL");
+    const int kind = (ke && *ke) ? atoi(ke) : 1;
+    const char* env = getenv("SCC_DIST_COLS");  // 64 or 256 columns per tile
+    const int cols = (env && *env) ? atoi(env) : ((kind == 0 && N >= 65536) ? 256 : 64);
+    if (kind == 1) {
+        const char* nte = getenv("SCC_DIST_NT");  // nontemporal stores (default on)
+        const bool nt = !(nte && *nte && atoi(nte) == 0);
         if (cols == 256)
-            launch_dist_aligned<256>(P, N, c_lo, c_hi, out, f32, st);
+            nt ? launch_dist_aligned<256, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
+               : launch_dist_aligned<256, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
         else
-            launch_dist_aligned<64>(P, N, c_lo, c_hi, out, f32, st);
+            nt ? launch_dist_aligned<64, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
+               : launch_dist_aligned<64, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
+        return hipGetLastError();
+    }
+    if (kind == 2) {
+        if (cols == 256)
+            launch_dist_wave<256>(P, N, c_lo, c_hi, out, f32, st);
+        else
+            launch_dist_wave<64>(P, N, c_lo, c_hi, out, f32, st);
         return hipGetLastError();
     }
     if (cols == 256)

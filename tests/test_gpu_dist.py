@@ -245,3 +245,37 @@ def test_one_cu_rank_deficient_and_repeated(eng, n, monkeypatch):
     ds2 = eng.dataset_dense(X2)
     dist = eng.distance(ds2, g, nat.SCC_DIST_PCA_EUCLID)
     assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
+
+
+@pytest.mark.parametrize("cols", ["64", "256"])
+@pytest.mark.parametrize("f32", [False, True])
+def test_distance_kernels_agree(eng, cols, f32, monkeypatch):
+    """The three distance store kernels (SCC_DIST_KERNEL 1 = workgroup-staged
+    windows, plain or nontemporal stores, 2 = wave windows, 0 = unaligned tiles) give bit-identical packed
+    output (same arithmetic, only the store pattern differs), over the full
+    vector and over column slices whose starts are not line-aligned."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(41)
+    G, N = 60, 1337
+    X = np.abs(rng.standard_normal((G, N))) * (rng.random((G, N)) < 0.4)
+    X[:, 7] = X[:, 8]  # two identical cells: a zero distance (difference form)
+    ds = eng.dataset_dense(X)
+    g = np.arange(0, G, 2)
+    monkeypatch.setenv("SCC_DIST_COLS", cols)
+    outs = []
+    for kind, nt in [("1", "1"), ("1", "0"), ("2", "1"), ("0", "1")]:
+        monkeypatch.setenv("SCC_DIST_KERNEL", kind)
+        monkeypatch.setenv("SCC_DIST_NT", nt)
+        outs.append(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID, f32=f32))
+    monkeypatch.setenv("SCC_DIST_NT", "1")
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(outs[0] - ref)) < (1e-4 if f32 else 1e-5)
+    assert outs[0][7 * (2 * N - 7 - 1) // 2] == 0.0  # pair (8, 7)
+    for c_lo, c_hi in [(5, 77), (700, 1336)]:
+        lo = c_lo * (2 * N - c_lo - 1) // 2
+        hi = c_hi * (2 * N - c_hi - 1) // 2
+        for kind in ["2", "1"]:
+            monkeypatch.setenv("SCC_DIST_KERNEL", kind)
+            part = eng.distance_cols(ds, g, c_lo, c_hi, nat.SCC_DIST_PCA_EUCLID, f32=f32)
+            assert np.array_equal(part, outs[0][lo:hi])
