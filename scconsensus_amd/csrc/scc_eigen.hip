@@ -199,7 +199,10 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         nwg = s_nwg;
     }
     const int R = (n + nwg - 1) / nwg;
-    const bool rows_lds = LOCAL ? (R <= a.lds_rows_cap) : (a.rows_lds != 0);
+    // the first TRI_W * TRI_MR own rows live in registers (when n <= 64 NJ),
+    // the others in LDS (or the HBM row store when they do not fit)
+    const int nreg_max = (NJ > 0 && n <= 64 * NJA) ? TRI_W * TRI_MR : 0;
+    const bool rows_lds = LOCAL ? (max(R - nreg_max, 0) <= a.lds_rows_cap) : (a.rows_lds != 0);
     double* vA = sm;           // v_i   (support i+1..n-1)
     double* vB = vA + n;       // v_{i-1}, then v_{i+1}
     double* wp = vB + n;       // w_{i-1}, then w_i
@@ -209,10 +212,10 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     double* part = red + 64;   // EIG_MAX_WG
     double* rows = rows_lds ? (part + EIG_MAX_WG) : (a.work + (size_t)me * R * n);
     const int nown = (me < n) ? (n - me + nwg - 1) / nwg : 0;
-    const bool in_regs = NJ > 0 && nown <= TRI_W * TRI_MR && n <= 64 * NJA;
+    const int nreg = min(nown, nreg_max);
     double rr[TRI_MR][NJA];
     if (tid == 0) s_abort = 0;
-    if (in_regs) {
+    if (nreg > 0) {
 #pragma unroll
         for (int m = 0; m < TRI_MR; ++m) {
             const int l = wv + TRI_W * m;
@@ -220,14 +223,13 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
             for (int t = 0; t < NJA; ++t) {
                 const int j = lane + 64 * t;
                 const double x = a.A[(size_t)(me + nwg * min(l, nown - 1)) * lda + min(j, n - 1)];
-                rr[m][t] = (l < nown && j < n) ? x : 0.0;
+                rr[m][t] = (l < nreg && j < n) ? x : 0.0;
             }
         }
-    } else {
-        for (int l = 0; l < nown; ++l) {
-            const double* src = a.A + (size_t)(me + nwg * l) * lda;
-            for (int j = tid; j < n; j += TRI_T) rows[(size_t)l * n + j] = src[j];
-        }
+    }
+    for (int l = nreg; l < nown; ++l) {
+        const double* src = a.A + (size_t)(me + nwg * l) * lda;
+        for (int j = tid; j < n; j += TRI_T) rows[(size_t)(l - nreg) * n + j] = src[j];
     }
     for (int j = tid; j < n; j += TRI_T) y[j] = a.A[j];  // row 0
     __syncthreads();
@@ -267,7 +269,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         // publish p_r (and row i+1 by its owner) as tagged granules
         double pd = 0.0;
         const int l0 = (i + 1 > me) ? (i + 1 - me + nwg - 1) / nwg : 0;
-        if (in_regs) {
+        if (nreg > 0) {
             // this lane's columns of v_i, v_{i-1}, w_{i-1} (zero outside i+1..n-1, so
             // the dead columns of a row stay untouched and add nothing)
             double vcr[NJA], vpr[NJA], wpr[NJA];
@@ -283,7 +285,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
 #pragma unroll
             for (int m = 0; m < TRI_MR; ++m) {
                 const int l = wv + TRI_W * m;
-                if (l >= nown || l < l0) continue;
+                if (l >= nreg || l < l0) continue;
                 const int r = me + nwg * l;
                 const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
                 double sd = 0.0;
@@ -308,9 +310,9 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                 }
             }
         }
-        for (int l = l0 + wv; !in_regs && l < nown; l += TRI_W) {
+        for (int l = max(l0, nreg) + wv; l < nown; l += TRI_W) {
             const int r = me + nwg * l;
-            double* row = rows + (size_t)l * n;
+            double* row = rows + (size_t)(l - nreg) * n;
             const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
             const bool pub = (r == i + 1);
             double s = 0.0;
@@ -1597,6 +1599,11 @@ static size_t tri_lds_bytes(int n, int R, bool rows_lds)
     return sizeof(double) * (5 * (size_t)n + 64 + EIG_MAX_WG + (rows_lds ? (size_t)R * n : 0));
 }
 
+// register row slots (64 columns each) of k_tridiag for this n, 0: rows in LDS / HBM only
+static int tri_nj(int n) { return n <= 384 ? 6 : (n <= 512 ? 8 : (n <= 896 ? 14 : 0)); }
+// own rows per workgroup k_tridiag keeps in registers
+static int tri_reg_rows(int n) { return tri_nj(n) ? TRI_W * TRI_MR : 0; }
+
 static int eig_nwg(int n)
 {
     static int cus = -1;
@@ -1626,14 +1633,14 @@ static bool eig_local(int n)
     if (env >= 0) return env != 0;
     int nwg = eig_nwg(n);
     if (nwg > 32) nwg = 32;
-    return tri_lds_bytes(n, (n + nwg - 1) / nwg, true) <= EIG_LDS_MAX;
+    return tri_lds_bytes(n, std::max((n + nwg - 1) / nwg - tri_reg_rows(n), 0), true) <= EIG_LDS_MAX;
 }
 
 static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
 {
     nwg = eig_nwg(n);
     if (eig_local(n) && nwg > 32) nwg = 32;  // one XCD holds 32 CUs
-    const int R = (n + nwg - 1) / nwg;
+    const int R = std::max((n + nwg - 1) / nwg - tri_reg_rows(n), 0);  // rows outside registers
     rows_lds = tri_lds_bytes(n, R, true) <= EIG_LDS_MAX;
     lu_lds = sizeof(double) * 10 * (size_t)n <= EIG_LDS_MAX;
 }
@@ -1759,7 +1766,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.err = flags + 1;
     const int R = (n + nwg - 1) / nwg;
     // at least 82 KB so that every workgroup has a CU of its own
-    size_t lds = tri_lds_bytes(n, R, rows_lds);
+    size_t lds = tri_lds_bytes(n, std::max(R - tri_reg_rows(n), 0), rows_lds);
     if (lds < 82 * 1024) lds = 82 * 1024;
     t.lds_rows_cap = rows_lds ? (int)((lds / sizeof(double) - (5 * (size_t)n + 64 + EIG_MAX_WG)) / n) : 0;
     if (marks) hipEventRecord(marks[0], st);
@@ -1796,15 +1803,20 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
             hipLaunchKernelGGL(k_tridiag_wa<false>, dim3(nwg), dim3(TRI_T), l2, st, t);
         }
     } else {
-        // register rows for n <= 512 (6 or 8 column slots per lane), else LDS / HBM rows
-        const int nj = n <= 384 ? 6 : (n <= 512 ? 8 : 0);
+        // register rows for n <= 896 (6, 8 or 14 column slots per lane; the rest
+        // of a workgroup's rows in LDS), else LDS / HBM rows
+        const int nj = tri_nj(n);
         const void* fn;
         if (t.xcd_local)
-            fn = nj == 6 ? (const void*)(k_tridiag<true, 6>) : nj == 8 ? (const void*)(k_tridiag<true, 8>)
-                                                                      : (const void*)(k_tridiag<true, 0>);
+            fn = nj == 6    ? (const void*)(k_tridiag<true, 6>)
+                 : nj == 8  ? (const void*)(k_tridiag<true, 8>)
+                 : nj == 14 ? (const void*)(k_tridiag<true, 14>)
+                            : (const void*)(k_tridiag<true, 0>);
         else
-            fn = nj == 6 ? (const void*)(k_tridiag<false, 6>) : nj == 8 ? (const void*)(k_tridiag<false, 8>)
-                                                                       : (const void*)(k_tridiag<false, 0>);
+            fn = nj == 6    ? (const void*)(k_tridiag<false, 6>)
+                 : nj == 8  ? (const void*)(k_tridiag<false, 8>)
+                 : nj == 14 ? (const void*)(k_tridiag<false, 14>)
+                            : (const void*)(k_tridiag<false, 0>);
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         const dim3 grid(t.xcd_local ? std::min(8 * nwg, cus) : nwg);
         void* args[] = {&t};
