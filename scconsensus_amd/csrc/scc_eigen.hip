@@ -1681,12 +1681,24 @@ static void side_stream(hipStream_t* s, hipEvent_t* fork_ev, hipEvent_t* join_ev
     *join_ev = je[dev];
 }
 
-extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
+extern "C" size_t scc_si_scratch_doubles(int n);
+extern "C" int scc_si_wanted(int n);
+extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
+                                   int* ok, hipStream_t st);
+
+// scratch of the direct solver alone
+extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k)
 {
     int nwg;
     bool rl, ll;
     eig_plan(n, nwg, rl, ll);
     return eig_layout(n, lda, k, nwg, rl, ll).total + scc_sbr_scratch_doubles(n, lda);
+}
+
+// direct solver + (for large n) the subspace iteration tried first (scc_subspace.hip)
+extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
+{
+    return scc_eigen_topk_scratch_direct(n, lda, k) + (scc_si_wanted(n) ? scc_si_scratch_doubles(n) : 0);
 }
 
 // A: n x n symmetric (full), row-major, lda (read only).  scratch: see
@@ -1706,6 +1718,21 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if (nwg_out) *nwg_out = nwg;
     hipError_t e = hipMemsetAsync(flags, 0, 64, st);  // counter, err, XCD pick [3], follow-up counters [6]
     if (e != hipSuccess) return e;
+    if (scc_si_wanted(n)) {
+        // large |U|: block subspace iteration first; accepted only when every
+        // Ritz residual passes (else the direct solver below runs)
+        if (marks) hipEventRecord(marks[0], st);
+        int ok = 0;
+        e = scc_eigen_si(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, st);
+        if (e != hipSuccess) return e;
+        if (ok) {
+            if (marks) {
+                hipEventRecord(marks[1], st);
+                for (int m = 2; m < 6; ++m) hipEventRecord(marks[m], st);
+            }
+            return hipSuccess;
+        }
+    }
     if (scc_sbr_band(n)) {
         // two-stage reduction (scc_sbr.hip): dense -> band -> tridiagonal, no
         // per-column hand-off; eigenvectors of the tridiagonal as below, then

@@ -1,0 +1,402 @@
+// scc_subspace.hip — top-k eigenpairs of the PCA Gram by block subspace
+// iteration with Rayleigh–Ritz, for large |U| (reference: irlba::prcomp_irlba,
+// R/reclusterDEConsensusFast.R:398; R/reclusterDEConsensus.R:234).
+//
+// The direct solver (scc_eigen.hip) costs one cross-CU hand-off per column of
+// the tridiagonalisation: 6.3 ms at |U| = 845 (config D), and it is the one
+// stage every rank repeats in a sharded job.  When the top 15 eigenvalues are
+// well separated from the 65th (configs C and D: lambda_65 / lambda_15 = 0.36,
+// many clusters -> many spikes), a 64-column block converges to the top-15
+// subspace at that rate per iteration, and an iteration is four small launches
+// spread over the whole chip (k_si_cholinv: one wave):
+//   W = C V            k_si_mul    fp64 MFMA 16x16x4, 4 waves split the k range
+//   G = W^T W          k_si_gram   16 tiles, 4 waves over the rows, fixed-order sums
+//   G = R^T R, T = R^-1  k_si_cholinv  one wave, a column per lane (readlane)
+//   V = W T            k_si_apply  fp64 MFMA, one wave per 16x16 tile
+// The orthonormalisation (the last three) runs after every third product.
+// then H = V^T C V, its top-k eigenpairs by the direct solver (n = 64), the
+// Ritz vectors U = V Y and their residuals |C u - theta u|.  The result is
+// accepted only when every residual is below SI_TOL * theta_1 (subspace error
+// ~ that / (lambda_15 - lambda_16)); otherwise — slow convergence (config B:
+// lambda_65 / lambda_15 = 0.88, the 15th eigenvalue inside the noise bulk), a
+// rank-deficient Gram (Cholesky breakdown) — the caller runs the direct solver.
+// Every reduction has a fixed order (deterministic, rank-identical in a
+// sharded job).  Output layout as scc_launch_eigen_topk: Z[u*16 + q], W[q],
+// largest-magnitude component of each vector positive.
+#include "scc_common.hpp"
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#define SI_B 64
+#define SI_TOL 1e-11
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// X^T Y tile (16 x 16) over rows [0, n) of two n x 64 row-major blocks, the 4
+// waves of the workgroup taking interleaved 4-row steps with four steps' loads
+// in flight; LDS sum in wave order (deterministic)
+__device__ inline d4 si_tile_xty(const double* __restrict__ X, const double* __restrict__ Y, int i0, int j0, int n)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kr = lane >> 4, cc = lane & 15;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 4 * w; k < n; k += 64) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int kk = k + 16 * u + kr;
+            const int kc = kk < n ? kk : 0;
+            a[u] = X[(size_t)kc * SI_B + i0 + cc];
+            b[u] = Y[(size_t)kc * SI_B + j0 + cc];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = k + 16 * u + kr < n;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ok ? a[u] : 0.0, ok ? b[u] : 0.0, acc, 0, 0, 0);
+        }
+    }
+    __shared__ d4 red[3][64];
+    if (w > 0) red[w - 1][lane] = acc;
+    __syncthreads();
+    if (w == 0) acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
+    return acc;
+}
+
+// W = C V (C symmetric n x n, ldc; V, W n x 64): grid (ceil(n/16), 4); the
+// 4 waves take interleaved 4-row k-steps, four steps' loads in flight at once
+__global__ void __launch_bounds__(256) k_si_mul(const double* __restrict__ C, int ldc, int n,
+                                                const double* __restrict__ V, double* __restrict__ W)
+{
+    const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kr = lane >> 4, cc = lane & 15;
+    // A[i][k] = C[i0 + i][k] = C[k][i0 + i]: rows of C read contiguously
+    const int ic = min(i0 + cc, n - 1);
+    const bool icok = i0 + cc < n;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 4 * w; k < n; k += 64) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int kk = k + 16 * u + kr;
+            const int kc = kk < n ? kk : 0;
+            a[u] = C[(size_t)kc * ldc + ic];
+            b[u] = V[(size_t)kc * SI_B + j0 + cc];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = k + 16 * u + kr < n;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((ok && icok) ? a[u] : 0.0, ok ? b[u] : 0.0, acc, 0, 0, 0);
+        }
+    }
+    __shared__ d4 red[3][64];
+    if (w > 0) red[w - 1][lane] = acc;
+    __syncthreads();
+    if (w != 0) return;
+    acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = i0 + kr + 4 * r;
+        if (row < n) W[(size_t)row * SI_B + j0 + cc] = acc[r];
+    }
+}
+
+// G = X^T Y (64 x 64): grid (4, 4), one 16 x 16 tile per workgroup
+__global__ void __launch_bounds__(256) k_si_gram(const double* __restrict__ X, const double* __restrict__ Y, int n,
+                                                 double* __restrict__ G)
+{
+    const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+    const d4 acc = si_tile_xty(X, Y, i0, j0, n);
+    if ((threadIdx.x >> 6) != 0) return;
+    const int lane = threadIdx.x & 63, kr = lane >> 4, cc = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) G[(i0 + kr + 4 * r) * SI_B + j0 + cc] = acc[r];
+}
+
+// uniform value of lane `l` (compile-time) of a lane-varying double
+__device__ __forceinline__ double si_rl(double x, int l)
+{
+    const u64 b = (u64)__double_as_longlong(x);
+    const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)b, l);
+    const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(b >> 32), l);
+    return __longlong_as_double((long long)(((u64)hi << 32) | lo));
+}
+
+// T = R^-1 where G = R^T R (R upper), G the upper half of the 64 x 64 Gram
+// (mirrored): ONE wave, lane j holding column j of G (then of R, then of T) in
+// registers; every other lane's entry arrives by readlane, so there is no
+// barrier and no LDS.  Cholesky of G + 1e-13 tr(G) I: always positive
+// definite, and R stays invertible, so span(W R^-1) = span(W) — all the
+// iteration needs; directions of W far below the shift come out as (harmless)
+// orthogonalised rounding noise.  A non-finite pivot sets flag bit 0.
+__global__ void __launch_bounds__(64) k_si_cholinv(const double* __restrict__ Gm, double* __restrict__ T,
+                                                   u32* __restrict__ flag)
+{
+    const int j = threadIdx.x;
+    double g[SI_B];
+#pragma unroll
+    for (int i = 0; i < SI_B; ++i) g[i] = Gm[(i <= j) ? i * SI_B + j : j * SI_B + i];
+    double tr = 0.0;
+#pragma unroll
+    for (int i = 0; i < SI_B; ++i) tr += si_rl(g[i], i);
+    const double shift = 1e-13 * tr;
+    bool bad = !(tr > 0.0) || !(tr < INFINITY);
+    double dinv[SI_B];
+#pragma unroll
+    for (int k = 0; k < SI_B; ++k) {
+        const double d = si_rl(g[k], k) + shift;
+        bad |= !(d > 0.0);
+        const double dk = sqrt(d > 0.0 ? d : 1.0);
+        dinv[k] = 1.0 / dk;
+        const double r = (j > k) ? g[k] * dinv[k] : ((j == k) ? dk : 0.0);  // R[k][j]
+        g[k] = r;
+#pragma unroll
+        for (int i = k + 1; i < SI_B; ++i) g[i] = fma(-si_rl(r, i), r, g[i]);  // G[i][j] -= R[k][i] R[k][j]
+    }
+    if (bad && j == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // column j of T: descending i, t_i = s_i / R_ii, s_m -= R[m][i] t_i (m < i)
+    double t[SI_B];
+#pragma unroll
+    for (int m = 0; m < SI_B; ++m) t[m] = (m == j) ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = SI_B - 1; i >= 0; --i) {
+        t[i] = (i <= j) ? t[i] * dinv[i] : 0.0;
+#pragma unroll
+        for (int m = 0; m < i; ++m) t[m] = fma(-si_rl(g[m], i), t[i], t[m]);  // R[m][i] = lane i's g[m]
+    }
+#pragma unroll
+    for (int i = 0; i < SI_B; ++i) T[i * SI_B + j] = t[i];
+}
+
+// V = W T (n x 64 by 64 x 64, T upper): grid (ceil(n/16), 4), one wave per
+// 16 x 16 output tile
+__global__ void __launch_bounds__(64) k_si_apply(const double* __restrict__ W, const double* __restrict__ T, int n,
+                                                 double* __restrict__ V)
+{
+    const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+    const int lane = threadIdx.x & 63, kr = lane >> 4, cc = lane & 15;
+    const int ic = min(i0 + cc, n - 1);
+    double a[16], b[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        a[s] = W[(size_t)ic * SI_B + 4 * s + kr];      // A[i][k] = W[i0 + i][k]
+        b[s] = T[(4 * s + kr) * SI_B + j0 + cc];       // B[k][j] = T[k][j0 + j]
+    }
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int rw = i0 + kr + 4 * r;
+        if (rw < n) V[(size_t)rw * SI_B + j0 + cc] = acc[r];
+    }
+}
+
+// deterministic pseudo-random start block
+__global__ void k_si_init(int n, double* __restrict__ V)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * SI_B) return;
+    unsigned h = (unsigned)e * 2654435761u ^ 0x9e3779b9u;
+    h ^= h >> 13;
+    h *= 0x5bd1e995u;
+    h ^= h >> 15;
+    V[e] = (double)(h & 0xffffff) / 16777216.0 - 0.5;
+}
+
+// H = (V^T W + (V^T W)^T) / 2
+__global__ void __launch_bounds__(256) k_si_hsym(const double* __restrict__ G, double* __restrict__ H)
+{
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < SI_B * SI_B; e += gridDim.x * blockDim.x) {
+        const int i = e / SI_B, j = e % SI_B;
+        H[e] = 0.5 * (G[e] + G[j * SI_B + i]);
+    }
+}
+
+// Ritz vectors U = V Y into Z (n x 16) and per-block partial sums of
+// |W y_q - theta_q V y_q|^2 and of the signed largest component: grid ceil(n/256)
+__global__ void __launch_bounds__(256) k_si_ritz(const double* __restrict__ V, const double* __restrict__ W,
+                                                 const double* __restrict__ Y, const double* __restrict__ theta, int n,
+                                                 int k, double* __restrict__ Z, double* __restrict__ rpart,
+                                                 double* __restrict__ mpart)
+{
+    __shared__ double Ys[SI_B][16];
+    __shared__ double rs[4][16], ms[4][16], ns[4][16];
+    for (int e = threadIdx.x; e < SI_B * 16; e += blockDim.x) Ys[e / 16][e % 16] = (e % 16 < k) ? Y[e] : 0.0;
+    __syncthreads();
+    const int row = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double u[16], cu[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[q] = cu[q] = 0.0;
+    if (row < n) {
+        for (int j = 0; j < SI_B; ++j) {
+            const double v = V[(size_t)row * SI_B + j], wv = W[(size_t)row * SI_B + j];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                u[q] = fma(v, Ys[j][q], u[q]);
+                cu[q] = fma(wv, Ys[j][q], cu[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Z[(size_t)row * 16 + q] = u[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const double r = (q < k) ? fma(-theta[q < k ? q : 0], u[q], cu[q]) : 0.0;
+        double s = r * r, nn = u[q] * u[q];
+        // largest magnitude (ties: the lower row), carried with its sign
+        double m = u[q];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            s += __shfl_xor(s, o, 64);
+            nn += __shfl_xor(nn, o, 64);
+            const double mo = __shfl_xor(m, o, 64);
+            m = (fabs(mo) > fabs(m)) ? mo : m;
+        }
+        if (lane == 0) {
+            rs[w][q] = s;
+            ms[w][q] = m;
+            ns[w][q] = nn;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        const int q = threadIdx.x;
+        double s = 0.0, m = 0.0, nn = 0.0;
+        for (int i = 0; i < 4; ++i) {
+            s += rs[i][q];
+            nn += ns[i][q];
+            m = (fabs(ms[i][q]) > fabs(m)) ? ms[i][q] : m;
+        }
+        rpart[(size_t)blockIdx.x * 32 + q] = s;
+        rpart[(size_t)blockIdx.x * 32 + 16 + q] = nn;
+        mpart[(size_t)blockIdx.x * 16 + q] = m;
+    }
+}
+
+// convergence test and sign: flag bit 1 when a residual exceeds SI_TOL theta_1;
+// sgn[q] = sign of the largest component; W out = theta
+__global__ void k_si_check(const double* __restrict__ rpart, const double* __restrict__ mpart, int nblk,
+                           const double* __restrict__ theta, int k, double tol, double* __restrict__ sgn,
+                           double* __restrict__ Wout, u32* __restrict__ flag)
+{
+    const int q = threadIdx.x;
+    if (q >= 16) return;
+    double s = 0.0, m = 0.0, nn = 0.0;
+    for (int b = 0; b < nblk; ++b) {
+        s += rpart[(size_t)b * 32 + q];
+        nn += rpart[(size_t)b * 32 + 16 + q];
+        m = (fabs(mpart[(size_t)b * 16 + q]) > fabs(m)) ? mpart[(size_t)b * 16 + q] : m;
+    }
+    sgn[q] = (m < 0.0) ? -1.0 : 1.0;
+    if (q < k) {
+        Wout[q] = theta[q];
+        if (!(sqrt(s) <= tol * fabs(theta[0]))) atomicOr(flag, 2u);  // residual
+        if (!(fabs(nn - 1.0) <= 1e-9)) atomicOr(flag, 4u);              // basis not orthonormal
+    }
+}
+
+__global__ void k_si_sign(double* __restrict__ Z, const double* __restrict__ sgn, int n)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n * 16) Z[e] *= sgn[e & 15];
+}
+
+static size_t si_npad(int n) { return ((size_t)n + 15) & ~(size_t)15; }
+
+extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k);  // scc_eigen.hip (direct path)
+
+extern "C" size_t scc_si_scratch_doubles(int n)
+{
+    const size_t np = si_npad(n), nblk = (np + 255) / 256;
+    return 2 * np * SI_B + (size_t)SI_B * SI_B + 3 * SI_B * SI_B + SI_B * 16 + 64 + 3 * nblk * 16 + 64 +
+           scc_eigen_topk_scratch_direct(SI_B, SI_B, 16) + 256;
+}
+
+// Auto rule: the subspace iteration is tried for n >= 400 (SCC_EIG_SI=0: never,
+// =1: for every n >= 128).  Iterations: SCC_EIG_SI_IT (default 30).
+extern "C" int scc_si_wanted(int n)
+{
+    const char* e = getenv("SCC_EIG_SI");
+    if (e && *e) return atoi(e) != 0 && n >= 128;
+    return n >= 400;
+}
+
+extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
+                                            double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
+                                            unsigned long long* stamps, hipStream_t st);
+
+// Returns hipSuccess and *ok = 1 when the subspace result was accepted (Z, W
+// written); *ok = 0: nothing usable, run the direct solver.  Synchronises st.
+extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
+                                   int* ok, hipStream_t st)
+{
+    *ok = 0;
+    if (n < 2 * SI_B || k > 16) return hipSuccess;
+    const size_t np = si_npad(n);
+    const int nblk = (int)((np + 255) / 256);
+    double* V = scr;
+    double* Wm = V + np * SI_B;
+    double* part = Wm + np * SI_B;
+    double* R = part + (size_t)SI_B * SI_B;
+    double* H = R + SI_B * SI_B;
+    double* Y = H + SI_B * SI_B;  // [64][16]
+    double* theta = Y + SI_B * 16;
+    double* sgn = theta + 16;
+    double* rpart = sgn + 16;
+    double* mpart = rpart + (size_t)nblk * 32;
+    u32* flag = (u32*)(mpart + (size_t)nblk * 16);
+    double* escr = (double*)(flag + 64);
+    hipError_t e;
+    if ((e = hipMemsetAsync(flag, 0, sizeof(u32) * 4, st)) != hipSuccess) return e;
+    const char* ite = getenv("SCC_EIG_SI_IT");
+    const int iters = (ite && *ite) ? atoi(ite) : 30;
+    const dim3 gmul((n + 15) / 16, SI_B / 16), ggram(SI_B / 16, SI_B / 16);
+    auto orth = [&](const double* src, double* dst) {  // dst = src R^-1, src^T src + shift = R^T R
+        hipLaunchKernelGGL(k_si_gram, ggram, dim3(256), 0, st, src, src, n, part);
+        hipLaunchKernelGGL(k_si_cholinv, dim3(1), dim3(64), 0, st, part, R, flag);
+        hipLaunchKernelGGL(k_si_apply, gmul, dim3(64), 0, st, src, R, n, dst);
+    };
+    // CholQR after every `every` products (the block's condition grows by about
+    // lambda_1 / lambda_64 per product; the shifted Cholesky absorbs whatever
+    // falls below 1e-13 of the top, far below the top-15 subspace), and twice
+    // more before Rayleigh-Ritz
+    const char* oe = getenv("SCC_EIG_SI_ORTH");
+    const int every = (oe && *oe) ? std::max(1, atoi(oe)) : 4;
+    double* a = V;   // the current block
+    double* b = Wm;  // the product
+    hipLaunchKernelGGL(k_si_init, dim3((n * SI_B + 255) / 256), dim3(256), 0, st, n, b);
+    orth(b, a);
+    for (int it = 0; it < iters; ++it) {
+        hipLaunchKernelGGL(k_si_mul, gmul, dim3(256), 0, st, C, ldc, n, a, b);
+        if ((it + 1) % every == 0 || it == iters - 1)
+            orth(b, a);
+        else
+            std::swap(a, b);
+    }
+    orth(a, b);  // two more passes: orthonormal to working precision (checked below through |u_q|)
+    orth(b, a);
+    // Rayleigh-Ritz on span(a): b = C a, H = a^T b
+    hipLaunchKernelGGL(k_si_mul, gmul, dim3(256), 0, st, C, ldc, n, a, b);
+    hipLaunchKernelGGL(k_si_gram, ggram, dim3(256), 0, st, a, b, n, part);
+    hipLaunchKernelGGL(k_si_hsym, dim3(16), dim3(256), 0, st, part, H);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    unsigned int* inner_err = nullptr;
+    if ((e = scc_launch_eigen_topk(H, SI_B, SI_B, k, escr, Y, theta, &inner_err, nullptr, nullptr, nullptr, st)) !=
+        hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k_si_ritz, dim3(nblk), dim3(256), 0, st, a, b, Y, theta, n, k, Z, rpart, mpart);
+    hipLaunchKernelGGL(k_si_check, dim3(1), dim3(64), 0, st, rpart, mpart, nblk, theta, k, SI_TOL, sgn, Wout, flag);
+    hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, st, Z, sgn, n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    u32 h[2] = {0, 0};
+    if ((e = hipMemcpyAsync(&h[0], flag, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if (inner_err && (e = hipMemcpyAsync(&h[1], inner_err, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc si] n=%d iters=%d flag=%u inner=%u\n", n, iters, h[0], h[1]);
+    *ok = (h[0] == 0 && h[1] == 0) ? 1 : 0;
+    return hipSuccess;
+}

@@ -88,6 +88,7 @@ def test_eigensolver_sizes(eng, n, sbr, monkeypatch):
     one-stage solver (default) and the opt-in two-stage path (48 <= n <= 1026)."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SBR", sbr)
+    monkeypatch.setenv("SCC_EIG_SI", "0")  # the direct solvers (subspace iteration: its own tests)
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
     ds = eng.dataset_dense(X)
@@ -116,9 +117,10 @@ def test_eigensolver_repeated_eigenvalues(eng):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
-def test_eigensolver_rows_beyond_lds(eng):
+def test_eigensolver_rows_beyond_lds(eng, monkeypatch):
     """|U| = 2100: each workgroup's rows no longer fit its LDS (global row store)."""
     from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SI", "0")
     rng = np.random.default_rng(11)
     n, N = 2100, 1200
     X = rng.standard_normal((n, N)) * np.linspace(3.0, 0.5, n)[:, None]
@@ -137,6 +139,7 @@ def test_two_stage_eigensolver(eng, n, monkeypatch):
     against the one-stage solver on the PCA scores."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SBR", "1")
+    monkeypatch.setenv("SCC_EIG_SI", "0")
     rng = np.random.default_rng(300 + n)
     X = rng.standard_normal((n, 1000)) * np.linspace(3.0, 0.5, n)[:, None]
     X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 1000)) * 4.0
@@ -185,6 +188,7 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, wave, monkeypatch):
     agents or workgroup barriers), rows in LDS or in HBM."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SBR", "0")  # the one-stage solver
+    monkeypatch.setenv("SCC_EIG_SI", "0")
     monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
     monkeypatch.setenv("SCC_EIG_XCD", xcd)
     monkeypatch.setenv("SCC_EIG_WAVE", wave)
@@ -279,3 +283,61 @@ def test_distance_kernels_agree(eng, cols, f32, monkeypatch):
             monkeypatch.setenv("SCC_DIST_KERNEL", kind)
             part = eng.distance_cols(ds, g, c_lo, c_hi, nat.SCC_DIST_PCA_EUCLID, f32=f32)
             assert np.array_equal(part, outs[0][lo:hi])
+
+
+def _spiky(n, N, nspike, seed):
+    """Genes x cells with `nspike` cluster-like directions well above a noise
+    bulk (the many-cluster spectrum of configs C/D)."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, N)) * 0.5
+    lab = rng.integers(0, nspike, N)
+    M = rng.standard_normal((n, nspike)) * np.linspace(4.0, 1.5, nspike)[None, :]
+    return X + M[:, lab]
+
+
+@pytest.mark.parametrize("n", [450, 845, 1200])
+def test_subspace_iteration(eng, n, monkeypatch, capfd):
+    """Block subspace iteration (scc_subspace.hip, tried first for |U| >= 400)
+    on a many-cluster spectrum: accepted (its residual test passes), equal to
+    the exact SVD and to the direct solver, bit-identical from run to run."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SI_LOG", "1")
+    X = _spiky(n, 3000, 40, 900 + n)
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    S1 = eng.last_pca_scores(X.shape[1])
+    d1b = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    err = capfd.readouterr().err
+    assert f"[scc si] n={n}" in err and "flag=0 inner=0" in err, err
+    assert np.array_equal(d1, d1b)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(d1 - ref)) < 1e-5
+    monkeypatch.setenv("SCC_EIG_SI", "0")
+    d0 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    S0 = eng.last_pca_scores(X.shape[1])
+    assert np.max(np.abs(d1 - d0)) < 1e-6
+    np.testing.assert_allclose(S1, S0, rtol=0, atol=1e-7 * np.abs(S0).max())  # same sign rule
+
+
+@pytest.mark.parametrize("case", ["bulk", "few_cells"])
+def test_subspace_iteration_falls_back(eng, case, monkeypatch, capfd):
+    """Slow convergence (15th eigenvalue inside a smooth bulk): the subspace
+    result fails its residual test and the direct solver's answer is returned.
+    A Gram of rank < 64 (40 cells): whichever path answers, the distance is the
+    exact SVD's."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SI_LOG", "1")
+    rng = np.random.default_rng(77)
+    n = 500
+    N = 2000 if case == "bulk" else 40
+    X = rng.standard_normal((n, N)) * np.linspace(1.0, 0.9, n)[:, None]
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    err = capfd.readouterr().err
+    assert f"[scc si] n={n}" in err, err
+    if case == "bulk":
+        assert "flag=0 inner=0" not in err, err
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
