@@ -214,14 +214,27 @@ SCC_API int scc_distance_cols(scc_ctx* ctx, const scc_dataset* ds, const int32_t
  *   scc_distance_scores(.., scores, ..)  the packed `dist` columns
  *       [col_lo, col_hi) from the full score matrix.
  * The mean is the same double-double sum as the unsharded path's, combined in
- * rank order, so every rank sees identical bits; the eigensolve runs on every
- * rank on the identical summed Gram (deterministic, identical scores). */
+ * rank order, so every rank sees identical bits; the eigensolve of the summed
+ * Gram runs once (scc_pca_shard_eigen on rank 0, vectors broadcast) or on every
+ * rank (scc_pca_shard_scores = eigen + project, single-rank use). */
 SCC_API int scc_pca_shard_colsum(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */,
                                  int32_t n_union, int64_t cell_lo, int64_t cell_hi, void* part /* device */);
 SCC_API int scc_pca_shard_gram(scc_ctx* ctx, const void* parts /* device [world][2 n_union] */, int32_t world,
                                void* gram /* device [n_union][n_union] */);
 SCC_API int scc_pca_shard_scores(scc_ctx* ctx, const void* gram_sum /* device */, int32_t ncomp,
                                  void* scores /* device [N][16] */);
+/* scc_pca_shard_scores in two halves, so the eigenvectors can come from ONE
+ * rank: scc_pca_shard_eigen writes the top-ncomp eigenvectors of gram_sum as
+ * vecs [n_union][16] doubles (device; columns >= ncomp zero); the caller
+ * broadcasts rank 0's vecs; scc_pca_shard_project scores this rank's cells
+ * with them (rows [cell_lo, cell_hi) of scores).  The eigensolver's hand-off
+ * kernel sums per-workgroup partials and how many workgroups join depends on
+ * arrival order, so separate eigensolves may differ in the last bits; one
+ * broadcast set of vectors makes every rank's block a block of one embedding. */
+SCC_API int scc_pca_shard_eigen(scc_ctx* ctx, const void* gram_sum /* device */, int32_t ncomp,
+                                void* vecs /* device [n_union][16] */);
+SCC_API int scc_pca_shard_project(scc_ctx* ctx, const void* vecs /* device [n_union][16] */, int32_t ncomp,
+                                  void* scores /* device [N][16] */);
 /* Packed `dist` columns [col_lo, col_hi) from a device score matrix [N][16]
  * (components >= ncomp zero); output as in scc_distance_cols. */
 SCC_API int scc_distance_scores(scc_ctx* ctx, const void* scores /* device */, int64_t n_cells, int64_t col_lo,

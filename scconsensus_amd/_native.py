@@ -39,7 +39,7 @@ EXPORTS = [
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_run_shard_records",
     "scc_de_finish_records", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
-    "scc_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores",
+    "scc_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores", "scc_pca_shard_eigen", "scc_pca_shard_project",
     "scc_distance_scores", "scc_silhouette", "scc_last_pca_scores",
     "scc_hclust_ward_d2", "scc_cutree_hybrid",
 ]
@@ -119,6 +119,8 @@ def load():
         "scc_pca_shard_colsum": (ctypes.c_int, [vp, vp, vp, i32, i64, i64, vp]),
         "scc_pca_shard_gram": (ctypes.c_int, [vp, vp, i32, vp]),
         "scc_pca_shard_scores": (ctypes.c_int, [vp, vp, i32, vp]),
+        "scc_pca_shard_eigen": (ctypes.c_int, [vp, vp, i32, vp]),
+        "scc_pca_shard_project": (ctypes.c_int, [vp, vp, i32, vp]),
         "scc_distance_scores": (ctypes.c_int, [vp, vp, i64, i64, i64, vp, i32, i32]),
         "scc_silhouette": (ctypes.c_int, [vp, i64, vp, vp, i32, vp, vp, P(i32)]),
         "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
@@ -433,6 +435,13 @@ class Engine:
     def pca_shard_scores(self, gram_ptr, scores_ptr, ncomp=0):
         self._check(self.lib.scc_pca_shard_scores(self.ctx, ctypes.c_void_p(gram_ptr), ncomp,
                                                   ctypes.c_void_p(scores_ptr)))
+
+    def pca_shard_eigen(self, gram_ptr, vecs_ptr, ncomp=0):
+        self._check(self.lib.scc_pca_shard_eigen(self.ctx, ctypes.c_void_p(gram_ptr), ncomp, ctypes.c_void_p(vecs_ptr)))
+
+    def pca_shard_project(self, vecs_ptr, scores_ptr, ncomp=0):
+        self._check(self.lib.scc_pca_shard_project(self.ctx, ctypes.c_void_p(vecs_ptr), ncomp,
+                                                   ctypes.c_void_p(scores_ptr)))
 
     def distance_scores(self, scores_ptr, N, col_lo, col_hi, out=None, f32=False, device_out_ptr=None):
         """Packed `dist` columns [col_lo, col_hi) from a device [N][16] score matrix."""

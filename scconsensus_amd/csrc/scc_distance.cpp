@@ -435,20 +435,22 @@ extern "C" int scc_pca_shard_gram(scc_ctx* c, const void* parts, int32_t world, 
     return SCC_OK;
 }
 
-extern "C" int scc_pca_shard_scores(scc_ctx* c, const void* gram_sum, int32_t ncomp, void* scores)
+// The eigensolve of the summed Gram (Fast:398): top-k eigenvectors as [n_union][16]
+// doubles (columns >= k zero) in `vecs` (device).  Run on ONE rank and broadcast:
+// the hand-off kernel's workgroup count depends on arrival order, so two ranks
+// could differ in the last bits (scc_pca_shard_project then scores every cell
+// block with the same vectors).
+extern "C" int scc_pca_shard_eigen(scc_ctx* c, const void* gram_sum, int32_t ncomp, void* vecs)
 {
-    if (!c || !gram_sum || !scores) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_scores: null argument");
-    if (c->pca_stage < 2) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_scores: call scc_pca_shard_gram first");
+    if (!c || !gram_sum || !vecs) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_eigen: null argument");
+    if (c->pca_stage < 2) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_eigen: call scc_pca_shard_gram first");
     const int nu = c->pca_nu, ld = c->pca_ld;
     const int k = ncomp > 0 ? ncomp : std::min(nu, 15);
     if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
     hipSetDevice(c->device);
     hipStream_t s0 = c->s0;
-    const int n = (int)(c->pca_chi - c->pca_clo);
-    const int npad = std::max(16, (n + 15) & ~15);
     int rc;
-    double *d_X, *d_C, *d_W, *d_Z, *d_escr;
-    if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
+    double *d_C, *d_W, *d_Z, *d_escr;
     if ((rc = ws(c, "d_C", (size_t)ld * ld, &d_C))) return rc;
     if ((rc = ws(c, "d_W", ld, &d_W))) return rc;
     if ((rc = ws(c, "d_Z", (size_t)ld * 16, &d_Z))) return rc;
@@ -462,15 +464,48 @@ extern "C" int scc_pca_shard_scores(scc_ctx* c, const void* gram_sum, int32_t nc
         int nwg_used = 0;
         HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, nullptr, nullptr, s0));
     }
+    HIPCHK(c, hipMemcpyAsync(vecs, d_Z, sizeof(double) * (size_t)nu * 16, hipMemcpyDeviceToDevice, s0));
     HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
+    HIPCHK(c, hipStreamSynchronize(s0));
+    c->last_ncomp = k;
+    if (c->eig_err) return fail(c, SCC_ERR_HIP, "scc_pca_shard_eigen: eigensolver workgroup hand-off timed out");
+    return SCC_OK;
+}
+
+// Scores of this rank's cell block from eigenvectors [n_union][16] (device).
+extern "C" int scc_pca_shard_project(scc_ctx* c, const void* vecs, int32_t ncomp, void* scores)
+{
+    if (!c || !vecs || !scores) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_project: null argument");
+    if (c->pca_stage < 2) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_project: call scc_pca_shard_gram first");
+    const int nu = c->pca_nu, ld = c->pca_ld;
+    const int k = ncomp > 0 ? ncomp : std::min(nu, 15);
+    if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    const int n = (int)(c->pca_chi - c->pca_clo);
+    const int npad = std::max(16, (n + 15) & ~15);
+    int rc;
+    double* d_X;
+    if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
     if (n > 0) {
         Scope sc(c, "scores", s0);
-        HIPCHK(c, scc_launch_scores(d_X, n, nu, ld, d_Z, k, (double*)scores + (size_t)c->pca_clo * 16, s0));
+        HIPCHK(c, scc_launch_scores(d_X, n, nu, ld, (const double*)vecs, k, (double*)scores + (size_t)c->pca_clo * 16, s0));
     }
     HIPCHK(c, hipStreamSynchronize(s0));
     c->last_ncomp = k;
-    if (c->eig_err) return fail(c, SCC_ERR_HIP, "scc_pca_shard_scores: eigensolver workgroup hand-off timed out");
     return SCC_OK;
+}
+
+extern "C" int scc_pca_shard_scores(scc_ctx* c, const void* gram_sum, int32_t ncomp, void* scores)
+{
+    if (!c || !gram_sum || !scores) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_scores: null argument");
+    if (c->pca_stage < 2) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_scores: call scc_pca_shard_gram first");
+    const int nu = c->pca_nu;
+    int rc;
+    double* d_V;
+    if ((rc = ws(c, "d_V", (size_t)std::max(nu, 1) * 16, &d_V))) return rc;
+    if ((rc = scc_pca_shard_eigen(c, gram_sum, ncomp, d_V))) return rc;
+    return scc_pca_shard_project(c, d_V, ncomp, scores);
 }
 
 extern "C" int scc_distance_scores(scc_ctx* c, const void* scores, int64_t N64, int64_t col_lo, int64_t col_hi,

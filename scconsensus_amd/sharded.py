@@ -14,8 +14,8 @@ and owns:
   over all genes of the pair, filters, top-N, union) identically everywhere.
 * PCA (Fast:398): a block of cells.  Column sums of X[U, block] (all-gather,
   combined in rank order), the centred partial Gram (all-reduce of |U| x |U|
-  fp64), the eigensolve on every rank from the identical summed Gram, the
-  block's scores (all-reduce of the disjoint N x 16 rows).
+  fp64), the eigensolve of the summed Gram on rank 0 (its vectors broadcast),
+  the block's scores (all-reduce of the disjoint N x 16 rows).
 * dist (Fast:400): a packed-column slice of equal entry count, kept in its HBM
   (or streamed to pinned host memory).
 
@@ -136,8 +136,17 @@ def pca_sharded(eng, ds, genes, dist: parallel.Dist, device, ncomp=0):
     gram[-1] = st
     dist.all_reduce_sum_(gram)
     _raise_if([gram[-1].item()], msg)
+    # the eigenvectors of rank 0, broadcast (a sum with zeros elsewhere): the
+    # hand-off eigensolver's partial sums follow how many workgroups joined, so
+    # per-rank eigensolves could differ in the last bits
+    vecs = torch.zeros(nu * 16 + 1, **f64)
+    if dist.rank == 0:
+        _, st, msg = _call(eng.pca_shard_eigen, gram.data_ptr(), vecs.data_ptr(), ncomp)
+        vecs[-1] = st
+    dist.all_reduce_sum_(vecs)
+    _raise_if([vecs[-1].item()], msg if dist.rank == 0 else "rank 0's eigensolve failed")
     scores = torch.zeros(N * 16 + 1, **f64)
-    _, st, msg = _call(eng.pca_shard_scores, gram.data_ptr(), scores.data_ptr(), ncomp)
+    _, st, msg = _call(eng.pca_shard_project, vecs.data_ptr(), scores.data_ptr(), ncomp)
     scores[-1] = st
     dist.all_reduce_sum_(scores)  # disjoint row blocks: the sum is the exact union
     _raise_if([scores[-1].item()], msg)

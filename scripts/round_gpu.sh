@@ -1,4 +1,5 @@
-# one GPU session: full gpu tests, config-B bench (with CPU baseline), rocprof kernel stats at B, config-D bench
+# one GPU session: full gpu tests, config-B bench (with CPU baseline), rocprof kernel stats at B,
+# config C / D / E benches (DE + distance, D without the CPU baseline)
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -6,7 +7,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -2 gpurun_out/r_tests.log
 timeout -k 10 300 python bench.py > gpurun_out/r_bench_b.json 2> gpurun_out/r_bench_b.err || { echo "bench rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r_prof_b -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-pearson --no-transfers --steps 5 --warmup 2 > gpurun_out/r_prof_b.log 2>&1 || { echo "prof rc=$?"; exit 1; }
+timeout -k 10 300 python bench.py --config C --no-cpu-baseline --no-pearson --no-transfers --steps 3 --warmup 1 > gpurun_out/r_bench_c.json 2> gpurun_out/r_bench_c.err || { echo "benchC rc=$?"; exit 1; }
 timeout -k 10 400 python bench.py --config D --no-cpu-baseline --no-pearson --no-transfers --steps 3 --warmup 1 > gpurun_out/r_bench_d.json 2> gpurun_out/r_bench_d.err || { echo "benchD rc=$?"; exit 1; }
-SCC_GRAM_V1=1 timeout -k 10 300 python bench.py --config D --no-cpu-baseline --no-pearson --no-transfers --steps 3 --warmup 1 > gpurun_out/r_bench_d_gram1.json 2>/dev/null || { echo "benchD1 rc=$?"; exit 1; }
-SCC_GRAM_V1=1 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pearson --no-transfers > gpurun_out/r_bench_b_gram1.json 2>/dev/null || { echo "benchB1 rc=$?"; exit 1; }
+timeout -k 10 400 python bench.py --config E --no-cpu-baseline --no-pearson --no-transfers --steps 3 --warmup 1 > gpurun_out/r_bench_e.json 2> gpurun_out/r_bench_e.err || { echo "benchE rc=$?"; exit 1; }
 echo ALLDONE

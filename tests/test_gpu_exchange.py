@@ -139,13 +139,23 @@ def test_sharded_pca_matches_unsharded(cfg_a, world):
     scores = torch.zeros(N * 16, dtype=torch.float64, device="cuda:0")
     for e in engs:
         e.pca_shard_scores(gram.data_ptr(), scores.data_ptr())
+    # as sharded.pca_sharded runs it: one eigensolve (rank 0), every rank projects its block
+    vecs = torch.zeros(nu * 16, dtype=torch.float64, device="cuda:0")
+    engs[0].pca_shard_eigen(gram.data_ptr(), vecs.data_ptr())
+    scores_b = torch.zeros(N * 16, dtype=torch.float64, device="cuda:0")
+    for e in engs:
+        e.pca_shard_project(vecs.data_ptr(), scores_b.data_ptr())
     torch.cuda.synchronize()
+    got_b = engs[0].distance_scores(scores_b.data_ptr(), N, 0, N)
+    if world == 1:
+        assert torch.equal(scores, scores_b)
     got = engs[0].distance_scores(scores.data_ptr(), N, 0, N)
     if world == 1:
         np.testing.assert_array_equal(got, full)
     else:
         # config A: sigma15 / sigma16 = 1.00035, so a 1e-16 change of the Gram rotates PC 15 by ~1e-8
         assert np.max(np.abs(got - full)) < 1e-6
+    assert np.max(np.abs(got_b - full)) < 1e-6
     ref = O.dist_euclidean(O.pca_scores(d.dense(), union))
     assert np.max(np.abs(got - ref)) < 1e-5
     # a rank's slice from the same scores

@@ -69,14 +69,22 @@ class Stand:
         mean = (parts[:, 0::2] + parts[:, 1::2]).sum(axis=0) / self.ds.N
         self.Xc = self.ds.X[self.genes][:, self.lo:self.hi].T - mean
         view(gram_ptr, nu * nu, np.float64)[:] = (self.Xc.T @ self.Xc).ravel()
-    def pca_shard_scores(self, gram_ptr, scores_ptr, ncomp):
+    def pca_shard_eigen(self, gram_ptr, vecs_ptr, ncomp):
         nu = len(self.genes)
+        self.eigen_calls = getattr(self, "eigen_calls", 0) + 1
+        if self.fail == "eigen":
+            raise nat.SccError(6, "eigensolver hand-off timed out")
         C = view(gram_ptr, nu * nu, np.float64).reshape(nu, nu)
         w, V = np.linalg.eigh(C)
         k = ncomp or min(nu, 15)
-        V = V[:, ::-1][:, :k]
+        Z = view(vecs_ptr, nu * 16, np.float64).reshape(nu, 16)
+        Z[:, :k] = V[:, ::-1][:, :k]
+    def pca_shard_project(self, vecs_ptr, scores_ptr, ncomp):
+        nu = len(self.genes)
+        k = ncomp or min(nu, 15)
+        Z = view(vecs_ptr, nu * 16, np.float64).reshape(nu, 16)
         S = view(scores_ptr, self.ds.N * 16, np.float64).reshape(self.ds.N, 16)
-        S[self.lo:self.hi, :k] = self.Xc @ V
+        S[self.lo:self.hi, :k] = self.Xc @ Z[:, :k]
     def synchronize(self):
         pass
 
@@ -99,6 +107,7 @@ try:
     R = O.pca_scores(X, genes)
     from scipy.spatial.distance import pdist
     res["dist_err"] = float(np.max(np.abs(pdist(S[:, :R.shape[1]]) - pdist(R))))
+    res["eigen_calls"] = getattr(eng, "eigen_calls", 0)
 except sharded.ShardError as e:
     res["error"] = e.code
 print(json.dumps(res))
@@ -141,13 +150,15 @@ def test_sharded_job_two_ranks():
         assert r["dist_err"] < 1e-9, r
     assert res[0]["genes"][0] == 0 and res[0]["genes"][1] == res[1]["genes"][0] and res[1]["genes"][1] == 40
     assert res[0]["genes"][1] > 20  # weights 1..40: the lighter genes make the bigger block
+    # one eigensolve (rank 0), its vectors broadcast to every rank
+    assert [r["eigen_calls"] for r in res] == [1, 0]
 
 
 def test_error_on_one_rank_raises_everywhere():
     """a failure one rank alone sees (an R stop() on its genes, an
     OOM) must raise on every rank, not leave the other blocked in a collective."""
-    for stage, code in (("de", 5), ("pca", 3)):
-        res = _run({"SCC_FAIL_RANK_STAGE": f"1:{stage}"})
+    for rank, stage, code in ((1, "de", 5), (1, "pca", 3), (0, "eigen", 6)):
+        res = _run({"SCC_FAIL_RANK_STAGE": f"{rank}:{stage}"})
         assert [r.get("error") for r in res] == [code, code], (stage, res)
 
 
