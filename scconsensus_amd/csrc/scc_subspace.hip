@@ -30,7 +30,6 @@
 
 #define SI_B 64
 #define SI_TOL 1e-11
-#define SI_CHEB_MAX 256  // Chebyshev steps at most
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -305,93 +304,6 @@ __global__ void k_si_sign(double* __restrict__ Z, const double* __restrict__ sgn
     if (e < n * 16) Z[e] *= sgn[e & 15];
 }
 
-// Chebyshev step (filtered subspace iteration, B-class spectra):
-// Y2 = alpha C Y1 + beta Y1 + gamma Y0 with (alpha, beta, gamma) = coef[3 step ..]:
-// the product as k_si_mul, the three-term recurrence fused into its store
-__global__ void __launch_bounds__(256) k_si_cheb(const double* __restrict__ C, int ldc, int n,
-                                                 const double* __restrict__ Y1, const double* __restrict__ Y0,
-                                                 const double* __restrict__ coef, int step, double* __restrict__ Y2)
-{
-    const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int kr = lane >> 4, cc = lane & 15;
-    const int ic = min(i0 + cc, n - 1);
-    const bool icok = i0 + cc < n;
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int k = 4 * w; k < n; k += 64) {
-        double a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int kk = k + 16 * u + kr;
-            const int kc = kk < n ? kk : 0;
-            a[u] = C[(size_t)kc * ldc + ic];
-            b[u] = Y1[(size_t)kc * SI_B + j0 + cc];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const bool ok = k + 16 * u + kr < n;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((ok && icok) ? a[u] : 0.0, ok ? b[u] : 0.0, acc, 0, 0, 0);
-        }
-    }
-    __shared__ d4 red[3][64];
-    if (w > 0) red[w - 1][lane] = acc;
-    __syncthreads();
-    if (w != 0) return;
-    acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
-    const double al = coef[3 * step], be = coef[3 * step + 1], ga = coef[3 * step + 2];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = i0 + kr + 4 * r;
-        if (row < n) {
-            const size_t e = (size_t)row * SI_B + j0 + cc;
-            Y2[e] = fma(al, acc[r], fma(be, Y1[e], ga * Y0[e]));
-        }
-    }
-}
-
-// Filter interval and the scaled Chebyshev coefficients (Zhou & Saad) from the
-// Rayleigh quotient matrix H = V^T C V of the orthonormal block after the
-// first plain products: the damped interval is [0, a] (the Gram is positive
-// semi-definite) with a = min_j H_jj (>= theta_64, in practice just below
-// lambda_65 once the block holds the top directions), the scale point
-// up = max_j H_jj.  Step 0: Y1 = (C - c) Y0 sigma_1 / e; step j:
-// Y_{j+1} = 2 sigma_{j+1} / e (C - c) Y_j - sigma_j sigma_{j+1} Y_{j-1}.
-// Flag bit 3 when the interval is degenerate (the caller falls back).
-__global__ void k_si_est(const double* __restrict__ H, int m, double* __restrict__ coef, u32* __restrict__ flag)
-{
-    __shared__ double smin[64], smax[64];
-    const int t = threadIdx.x;
-    const double d = H[t * SI_B + t];
-    smin[t] = d;
-    smax[t] = d;
-    __syncthreads();
-    if (t != 0) return;
-    double a = smin[0], up = smax[0];
-    for (int i = 1; i < SI_B; ++i) {
-        a = fmin(a, smin[i]);
-        up = fmax(up, smax[i]);
-    }
-    if (!(a > 0.0) || !(up > 1.0001 * a) || !(up < INFINITY)) {
-        atomicOr(flag, 8u);
-        a = 1.0;
-        up = 2.0;
-    }
-    const double e = 0.5 * a, c = 0.5 * a;
-    const double s1 = e / (up - c);
-    double sg = s1;
-    coef[0] = s1 / e;
-    coef[1] = -c * coef[0];
-    coef[2] = 0.0;
-    for (int j = 1; j < m; ++j) {
-        const double sn = 1.0 / (2.0 / s1 - sg);
-        const double al = 2.0 * sn / e;
-        coef[3 * j] = al;
-        coef[3 * j + 1] = -c * al;
-        coef[3 * j + 2] = -sg * sn;
-        sg = sn;
-    }
-}
-
 static size_t si_npad(int n) { return ((size_t)n + 15) & ~(size_t)15; }
 
 extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k);  // scc_eigen.hip (direct path)
@@ -399,26 +311,17 @@ extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k);  // scc_
 extern "C" size_t scc_si_scratch_doubles(int n)
 {
     const size_t np = si_npad(n), nblk = (np + 255) / 256;
-    return 4 * np * SI_B + (size_t)SI_B * SI_B + 3 * SI_B * SI_B + SI_B * 16 + 64 + 3 * nblk * 16 + 64 +
-           3 * SI_CHEB_MAX + scc_eigen_topk_scratch_direct(SI_B, SI_B, 16) + 256;
+    return 2 * np * SI_B + (size_t)SI_B * SI_B + 3 * SI_B * SI_B + SI_B * 16 + 64 + 3 * nblk * 16 + 64 +
+           scc_eigen_topk_scratch_direct(SI_B, SI_B, 16) + 256;
 }
 
-// Chebyshev-filtered variant for 128 <= n < 400 (SCC_EIG_CHEB=1; 0: off)
-static bool si_cheb(int n)
-{
-    const char* e = getenv("SCC_EIG_CHEB");
-    const bool on = (e && *e) ? atoi(e) != 0 : false;
-    return on && n >= 2 * SI_B && n < 400;
-}
-
-// Auto rule: the subspace iteration is tried for n >= 400 and, Chebyshev
-// filtered, for smaller n when si_cheb (SCC_EIG_SI=0: never, =1: for every
-// n >= 128).  Plain iterations: SCC_EIG_SI_IT (default 30).
+// Auto rule: the subspace iteration is tried for n >= 400 (SCC_EIG_SI=0: never,
+// =1: for every n >= 128).  Iterations: SCC_EIG_SI_IT (default 30).
 extern "C" int scc_si_wanted(int n)
 {
     const char* e = getenv("SCC_EIG_SI");
     if (e && *e) return atoi(e) != 0 && n >= 128;
-    return n >= 400 || si_cheb(n);
+    return n >= 400;
 }
 
 extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
@@ -436,9 +339,7 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     const int nblk = (int)((np + 255) / 256);
     double* V = scr;
     double* Wm = V + np * SI_B;
-    double* X3 = Wm + np * SI_B;
-    double* X4 = X3 + np * SI_B;
-    double* part = X4 + np * SI_B;
+    double* part = Wm + np * SI_B;
     double* R = part + (size_t)SI_B * SI_B;
     double* H = R + SI_B * SI_B;
     double* Y = H + SI_B * SI_B;  // [64][16]
@@ -447,8 +348,7 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     double* rpart = sgn + 16;
     double* mpart = rpart + (size_t)nblk * 32;
     u32* flag = (u32*)(mpart + (size_t)nblk * 16);
-    double* coef = (double*)(flag + 64);
-    double* escr = coef + 3 * SI_CHEB_MAX;
+    double* escr = (double*)(flag + 64);
     hipError_t e;
     if ((e = hipMemsetAsync(flag, 0, sizeof(u32) * 4, st)) != hipSuccess) return e;
     const char* ite = getenv("SCC_EIG_SI_IT");
@@ -467,55 +367,14 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     const int every = (oe && *oe) ? std::max(1, atoi(oe)) : 4;
     double* a = V;   // the current block
     double* b = Wm;  // the product
-    const bool cheb = si_cheb(n);
-    const char* ce = getenv("SCC_EIG_CHEB_EST");
-    const char* cm = getenv("SCC_EIG_CHEB_M");
-    const int est = (ce && *ce) ? std::max(1, atoi(ce)) : 6;
-    const int m = std::min(SI_CHEB_MAX, std::max(2, (cm && *cm) ? atoi(cm) : 64));
-    const int nplain = cheb ? est : iters;
     hipLaunchKernelGGL(k_si_init, dim3((n * SI_B + 255) / 256), dim3(256), 0, st, n, b);
     orth(b, a);
-    for (int it = 0; it < nplain; ++it) {
+    for (int it = 0; it < iters; ++it) {
         hipLaunchKernelGGL(k_si_mul, gmul, dim3(256), 0, st, C, ldc, n, a, b);
-        if ((it + 1) % every == 0 || it == nplain - 1)
+        if ((it + 1) % every == 0 || it == iters - 1)
             orth(b, a);
         else
             std::swap(a, b);
-    }
-    if (cheb) {
-        // filter interval from H = a^T C a, then m Chebyshev steps with the
-        // pair (Y_j, Y_{j-1}) right-multiplied by the same R^-1 every `every`
-        // steps (the recurrence is linear in the block, so it stays exact)
-        hipLaunchKernelGGL(k_si_mul, gmul, dim3(256), 0, st, C, ldc, n, a, b);
-        hipLaunchKernelGGL(k_si_gram, ggram, dim3(256), 0, st, a, b, n, part);
-        hipLaunchKernelGGL(k_si_hsym, dim3(16), dim3(256), 0, st, part, H);
-        hipLaunchKernelGGL(k_si_est, dim3(1), dim3(64), 0, st, H, m, coef, flag);
-        double* y0 = a;
-        double* y1 = a;
-        double* blk[4] = {V, Wm, X3, X4};
-        auto other = [&](const double* u, const double* v, int nth) -> double* {  // nth block not u / v
-            for (double* x : blk)
-                if (x != u && x != v && nth-- == 0) return x;
-            return nullptr;
-        };
-        for (int j = 0; j < m; ++j) {
-            double* y2 = other(y0, y1, 0);
-            hipLaunchKernelGGL(k_si_cheb, gmul, dim3(256), 0, st, C, ldc, n, y1, y0, coef, j, y2);
-            y0 = y1;
-            y1 = y2;
-            if ((j + 1) % every == 0 && j + 1 < m) {
-                double* n1 = other(y0, y1, 0);
-                double* n0 = other(y0, y1, 1);
-                hipLaunchKernelGGL(k_si_gram, ggram, dim3(256), 0, st, y1, y1, n, part);
-                hipLaunchKernelGGL(k_si_cholinv, dim3(1), dim3(64), 0, st, part, R, flag);
-                hipLaunchKernelGGL(k_si_apply, gmul, dim3(64), 0, st, y1, R, n, n1);
-                hipLaunchKernelGGL(k_si_apply, gmul, dim3(64), 0, st, y0, R, n, n0);
-                y1 = n1;
-                y0 = n0;
-            }
-        }
-        a = y1;
-        b = other(y1, y1, 0);
     }
     orth(a, b);  // two more passes: orthonormal to working precision (checked below through |u_q|)
     orth(b, a);
@@ -537,9 +396,7 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     if (inner_err && (e = hipMemcpyAsync(&h[1], inner_err, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess)
         return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    if (getenv("SCC_EIG_SI_LOG"))
-        fprintf(stderr, "[scc si] n=%d %s iters=%d flag=%u inner=%u\n", n, cheb ? "chebyshev" : "plain",
-                cheb ? est + m : iters, h[0], h[1]);
+    if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc si] n=%d iters=%d flag=%u inner=%u\n", n, iters, h[0], h[1]);
     *ok = (h[0] == 0 && h[1] == 0) ? 1 : 0;
     return hipSuccess;
 }

@@ -342,30 +342,3 @@ def test_subspace_iteration_falls_back(eng, case, monkeypatch, capfd):
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
 
-
-@pytest.mark.parametrize("n", [150, 323, 399])
-def test_chebyshev_subspace_iteration(eng, n, monkeypatch, capfd):
-    """Chebyshev-filtered subspace iteration (SCC_EIG_CHEB, 128 <= |U| < 400)
-    on config B's kind of spectrum: 10 cluster directions, the 15th eigenvalue
-    inside the noise bulk (lambda_65 / lambda_15 ~ 0.85).  Accepted by its
-    residual test, equal to the exact SVD and to the direct solver,
-    bit-identical from run to run."""
-    from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SI_LOG", "1")
-    monkeypatch.setenv("SCC_EIG_CHEB", "1")
-    X = _spiky(n, 3000, 10, 500 + n)
-    ds = eng.dataset_dense(X)
-    g = np.arange(n)
-    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    S1 = eng.last_pca_scores(X.shape[1])
-    d1b = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    err = capfd.readouterr().err
-    assert f"[scc si] n={n} chebyshev" in err and "flag=0 inner=0" in err, err
-    assert np.array_equal(d1, d1b)
-    ref = O.dist_euclidean(O.pca_scores(X, g))
-    assert np.max(np.abs(d1 - ref)) < 1e-5
-    monkeypatch.setenv("SCC_EIG_CHEB", "0")
-    d0 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    S0 = eng.last_pca_scores(X.shape[1])
-    assert np.max(np.abs(d1 - d0)) < 1e-6
-    np.testing.assert_allclose(S1, S0, rtol=0, atol=1e-7 * np.abs(S0).max())
