@@ -318,14 +318,21 @@ def main():
         "dist": ("hbm", 8.0 * npairs_cells * frac_entries + 16 * 8.0 * d.N, "k_dist_aligned"),
         # CSC read twice (12 B/nnz + 8 B/cell), keys written once (8 B/nnz), chunk counts (4 B, 3 passes)
         "ingest": ("hbm", 2 * (12.0 * nnz + 8.0 * (d.N + 1)) + 8.0 * nnz / world + 3 * 4.0 * ncc * d.G / world,
-                   "k_ing_scatter"),
+                   "ingest stage (k_ing_hist, k_ing_colsum/segscan/colapply, scans, k_ing_scatter)"),
         "gene_stats": ("hbm", (8.0 * nnz + 32.0 * K * d.G) / world, "k_gene_stats"),
         # keys read once; per (pair, gene) accumulators written (S, E, X)
-        "gene_rank": ("hbm", (8.0 * nnz + 24.0 * P * d.G) / world, "k_rank_item"),
+        "gene_rank": ("hbm", (8.0 * nnz + 24.0 * P * d.G) / world,
+                      "rank stage (k_rank_classify/split/resplit/waves/cross; k_rank_item on a second stream)"),
         # Householder tridiagonalisation 4/3 n^3 fp64 flops (one hand-off per column: latency-bound)
         "eig_tridiag": ("mfma", 4.0 / 3.0 * nu ** 3, "k_tridiag"),
         "gram": ("mfma", 2.0 * d.N * nu * nu / 2 / world, "k_gram_f64"),
     }
+    if stage_ms.get("eig_vec", 0.0) == 0.0 and nu >= 400:
+        # the subspace iteration answered (scc_subspace.hip, |U| >= 400): 31 products of
+        # C (n x n) by the 64-column block + the n = 64 Rayleigh-Ritz; no k_tridiag at size n
+        alg["eig_tridiag"] = ("mfma", 31 * 2.0 * nu * nu * 64,
+                              "eigen stage: block subspace iteration (k_si_mul/gram/cholinv/apply, "
+                              "Rayleigh-Ritz through the direct solver at n = 64)")
     dom = max(alg, key=lambda f: stage_ms.get(f, 0.0))
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
@@ -390,7 +397,9 @@ def main():
     roof_dom["traffic"] = traffic
     roof_dom["traffic_source"] = (f"profiles/pmc_traffic_{a.config}.json (scripts/pmc_traffic.sh)"
                                   if traffic is not None else None)
-    if dom == "eig_tridiag":
+    if alg[dom][2].endswith("stage") or " stage" in alg[dom][2]:
+        roof_dom["note"] = "avg_launch_ms is the whole stage (its kernels back to back), not one kernel"
+    elif dom == "eig_tridiag":
         roof_dom["note"] = ("fp64 vector work on a one-stage Householder reduction: n-1 dependent "
                             "cross-workgroup hand-offs, latency-bound (no MFMA shape)")
     kernels = {f: roof(f) for f in alg if f in stage_ms and stage_ms[f] > 0}
