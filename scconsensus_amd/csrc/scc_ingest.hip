@@ -43,6 +43,27 @@ __device__ inline void cell_range(const i64* indptr, int c, int G, i64& b, i64& 
     }
 }
 
+// first k in [lo, hi) with rows[k] >= v (hi if none), rows[lo, hi) sorted: a
+// 64-way search (one probe per lane and a ballot per round), wave-uniform result
+__device__ inline i64 wave_lower_bound(const int* __restrict__ rows, i64 lo, i64 hi, int v)
+{
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const i64 step = (hi - lo + 63) / 64;
+        const i64 k = lo + (i64)lane * step;
+        const bool ge = k < hi ? rows[k] >= v : true;
+        const u64 m = __ballot(ge);
+        const int f = m ? __builtin_ctzll(m) : 64;
+        const i64 nlo = f == 0 ? lo : lo + (i64)(f - 1) * step + 1;
+        hi = min(hi, lo + (i64)f * step);
+        lo = nlo;
+    }
+    const i64 k = lo + lane;
+    const bool ge = k < hi ? rows[k] >= v : true;
+    const u64 m = __ballot(ge);
+    return lo + (m ? __builtin_ctzll(m) : 64);
+}
+
 // err bits: 1 non-finite value, 2 row index out of range, 4 rows not sorted
 template <bool DENSE>
 __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
@@ -50,10 +71,13 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
                                                     int* __restrict__ nodg, dd* __restrict__ wave_expm1,
-                                                    int want_expm1, int glo, int ghi, int* __restrict__ err)
+                                                    int want_expm1, int glo, int ghi, int rng, int* __restrict__ err)
 {
     // genes outside [glo, ghi) (a shard of the gene rows) are not counted; nodg
-    // and the expm1 sum still see every entry
+    // and the expm1 sum still see every entry -- unless rng (a validated CSC
+    // dataset, FAST mode): then each cell's entries of the tiles covering
+    // [glo, ghi) are found by two wave-parallel binary searches (rows sorted)
+    // and only those are read; nodg comes from the dataset's cache
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int ch = blockIdx.x;
@@ -62,6 +86,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
         for (int g = threadIdx.x; g < G; g += IH_T) hist[g] = 0;
     __syncthreads();
     const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
+    const int t0r = glo / gt, t1r = min(ntile, (ghi + gt - 1) / gt);  // rng: the tiles [t0r, t1r) cover [glo, ghi)
     dd se{0.0, 0.0};
     int bad = 0;
     for (int p = p0 + wv; p < p1; p += IH_T / 64) {
@@ -70,7 +95,12 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
         cell_range<DENSE>(indptr, c, G, b, e);
         u32 pos = 0;
         i64* bp = bnd + (size_t)p * (ntile + 1);
-        for (i64 k0 = b; k0 < e; k0 += 4 * 64) {  // four loads in flight per lane
+        i64 kb = b, ke = e;
+        if (!DENSE && rng) {
+            kb = wave_lower_bound(rows, b, e, t0r * gt);
+            ke = wave_lower_bound(rows, kb, e, t1r * gt);
+        }
+        for (i64 k0 = kb; k0 < ke; k0 += 4 * 64) {  // four loads in flight per lane
             double xs[4];
             int gs[4], gps[4];
             // clamped unconditional loads + select (a load under a lane
@@ -78,23 +108,23 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const i64 k = k0 + u * 64 + lane;
-                const i64 kc = k < e ? k : e - 1;  // k0 < e, so e - 1 >= b
+                const i64 kc = k < ke ? k : ke - 1;  // k0 < ke, so ke - 1 >= b
                 const double x = vals[kc];
-                xs[u] = k < e ? x : 0.0;
+                xs[u] = k < ke ? x : 0.0;
                 if (DENSE) {
-                    gs[u] = k < e ? (int)(k - b) : -1;
+                    gs[u] = k < ke ? (int)(k - b) : -1;
                     gps[u] = -1;
                 } else {
                     const int r = rows[kc];
                     const int rp = rows[kc > b ? kc - 1 : b];
-                    gs[u] = k < e ? r : -1;
-                    gps[u] = (k < e && k > b) ? rp : -1;
+                    gs[u] = k < ke ? r : -1;
+                    gps[u] = (k < ke && k > b) ? rp : -1;
                 }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const i64 k = k0 + u * 64 + lane;
-                if (k >= e) break;
+                if (k >= ke) break;
                 const double x = xs[u];
                 const int g = gs[u];
                 const bool gok = (g >= 0) & (g < G);
@@ -113,13 +143,15 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
             }
         }
         if (!DENSE && a >= 0) {
-            // tiles after the last entry (and every tile of an empty cell) end at e
-            const int gl = (e > b) ? rows[e - 1] : -1;
+            // tiles after the last entry read (and every tile of an empty cell) end
+            // at ke (= e, or in rng mode the first entry past tile t1r - 1)
+            const int gl = (ke > b) ? rows[ke - 1] : -1;
             const int tl = (gl < 0) ? -1 : min(gl / gt, ntile - 1);
-            for (int t = tl + 1 + lane; t <= ntile; t += 64) bp[t] = e;
+            const int tend = rng ? t1r : ntile;
+            for (int t = tl + 1 + lane; t <= tend; t += 64) bp[t] = ke;
         }
         pos = u32_wave_sum(pos);
-        if (lane == 0) nodg[c] = (int)pos;
+        if (lane == 0 && !rng) nodg[c] = (int)pos;
     }
     if (want_expm1) {
         se = dd_wave_sum(se);
@@ -461,18 +493,18 @@ extern "C" int scc_ingest_gene_tile(void) { return SC_GT; }
 extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows, const double* vals,
                                              const double* dense, int G, const int* perm, const int* cc_p0,
                                              const int* cc_code, int nc, int ntile, u32* cnt, i64* bnd, int* nodg,
-                                             dd* wave_expm1, int want_expm1, int glo, int ghi, int* err,
+                                             dd* wave_expm1, int want_expm1, int glo, int ghi, int rng, int* err,
                                              hipStream_t st)
 {
     const size_t lds = sizeof(u32) * (size_t)G;
     if (dense) {
         hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, err);
     } else {
         hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, err);
     }
     return hipGetLastError();
 }

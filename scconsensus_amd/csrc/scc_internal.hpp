@@ -94,6 +94,12 @@ struct scc_dataset {
     double* d_vals = nullptr;
     double* d_dense = nullptr;
     bool owned = false;
+    // set by the first DE run that read every entry without an input error
+    // (rows in range and sorted): a gene shard of a later FAST run then reads
+    // only its tiles (k_ing_hist rng) and takes nodg (clustering-independent)
+    // from this device cache.  The data must not change while the dataset lives.
+    mutable bool validated = false;
+    mutable int* d_nodg = nullptr;  // [N], always owned
 };
 
 struct scc_de_result {

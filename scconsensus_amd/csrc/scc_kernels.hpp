@@ -155,7 +155,7 @@ int scc_ingest_gene_tile(void);
 hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
                                   int G, const int* perm, const int* cc_p0, const int* cc_code, int nc, int ntile,
                                   uint32_t* cnt, long long* bnd, int* nodg, dd* wave_expm1, int want_expm1, int glo,
-                                  int ghi, int* err, hipStream_t st);
+                                  int ghi, int rng, int* err, hipStream_t st);
 int scc_ingest_colscan_scratch(int nc, int G);
 hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nc, int nc_kept, int G, uint32_t* scratch, hipStream_t st);
 hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, const double* vals,

@@ -288,14 +288,17 @@ extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, 
 extern "C" void scc_dataset_destroy(scc_dataset* d)
 {
     if (!d) return;
-    if (d->owned) {
+    if (d->owned || d->d_nodg) {
         hipSetDevice(d->device);
         hipDeviceSynchronize();
+    }
+    if (d->owned) {
         hipFree(d->d_indptr);
         hipFree(d->d_rows);
         hipFree(d->d_vals);
         hipFree(d->d_dense);
     }
+    hipFree(d->d_nodg);
     delete d;
 }
 
@@ -516,19 +519,38 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
 
     const int64_t sig[6] = {G, N, K, prm->mode, ds->nnz, (int64_t)(intptr_t)ds};
     double log_thr = 0.0;
+    bool hist_rng = false, hist_full = false;
+    // after an error-free run whose ingest read every entry: the dataset is
+    // validated and its nodg cached (for later gene-shard runs)
+    auto note_validated = [&]() -> int {
+        if (!hist_full || ds->validated || ds->dense) return SCC_OK;
+        if (!ds->d_nodg && hipMalloc((void**)&ds->d_nodg, sizeof(int) * N) != hipSuccess) {
+            hipGetLastError();
+            ds->d_nodg = nullptr;
+            return SCC_OK;  // no cache: later shards keep reading everything
+        }
+        HIPCHK(c, hipMemcpyAsync(ds->d_nodg, d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
+        HIPCHK(c, hipStreamSynchronize(s0));
+        ds->validated = true;
+        return SCC_OK;
+    };
     if (finish_stage) {
         if (!std::equal(sig, sig + 6, c->shard_sig))
             return fail(c, SCC_ERR_INVALID, "scc_de_finish: this context ran no scc_de_run_shard for these inputs");
         log_thr = c->shard_log_thr;
     } else {
     HIPCHK(c, hipMemcpyAsync(d_tab, H.data(), sizeof(int) * H.size(), hipMemcpyHostToDevice, s0));
+    const char* ife = getenv("SCC_INGEST_FULL");
+    hist_rng = !ds->dense && ds->validated && ds->d_nodg && fast && (glo > 0 || ghi < G) && !(ife && atoi(ife));
+    hist_full = !hist_rng;
     {
         Scope sc(c, "ingest", s0);
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
         HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 16, s0));
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
-                                         d_err, s0));
+                                         hist_rng ? 1 : 0, d_err, s0));
+        if (hist_rng) HIPCHK(c, hipMemcpyAsync(d_nodg, ds->d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
         uint32_t* d_cscr;
         WS("colscan", scc_ingest_colscan_scratch(nc, G), d_cscr);
         HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, d_cscr, s0));
@@ -788,7 +810,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         if (e & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
         if (e & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
         if (e & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
-        return SCC_OK;
+        return note_validated();
     }
     if (stage == DE_FINISH) {
         const char* src = (const char*)shard;
@@ -897,6 +919,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
     if (hdr[1] & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
     if (hdr[1] & 16) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: record out of range");
+    if ((rc = note_validated())) return rc;
     scc_de_result* r = new scc_de_result();
     r->ctx = c;
     r->generation = c->generation;

@@ -78,6 +78,31 @@ def test_records_fast_match_unsharded(eng, cfg_a, bounds):
     _same(ref, got)
 
 
+@pytest.mark.parametrize("bounds", [[(0, 300), (300, 1301), (1301, 2000)], [(0, 255), (255, 257), (257, 2000)],
+                                    [(0, 1), (1, 1999), (1999, 2000)], [(0, 0), (0, 2000)]])
+def test_records_range_ingest_matches_full(eng, cfg_a, bounds, monkeypatch):
+    """Gene-shard ingest of a validated dataset (k_ing_hist rng: two wave-parallel
+    binary searches per cell, only the shard's gene tiles read, nodg from the
+    dataset's cache) gives the same records and nodg as reading every entry:
+    first pass on a fresh dataset (full read, validates), second pass (range
+    read), third with SCC_INGEST_FULL=1."""
+    d, names, code = cfg_a
+    K = len(names)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    runs = []
+    for full in ("0", "0", "1"):
+        monkeypatch.setenv("SCC_INGEST_FULL", full)
+        allr, counts, stride = _records(eng, ds, code, K, bounds)
+        got = eng.de_finish_records(ds, code, K, allr.data_ptr(), counts, stride, fetch="rows")
+        runs.append((allr.cpu().numpy(), counts, got))
+    for allr, counts, got in runs[1:]:
+        assert counts == runs[0][1]
+        np.testing.assert_array_equal(allr, runs[0][0])
+        _same(runs[0][2], got)
+    ref = eng.de_run(eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N), code, K, nat.SCC_DE_FAST, fetch="rows")
+    _same(ref, runs[1][2])
+
+
 def test_records_t_and_slow_match_unsharded(eng, cfg_a):
     d, names, code = cfg_a
     K = len(names)
