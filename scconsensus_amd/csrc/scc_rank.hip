@@ -832,6 +832,7 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 #define RW_PAIRS_MAX (8 * 64 * RW_SLOTS_MAX)  // genes past 1024 tested pairs: one 16-slot pass per 1024
 #define RS_ACC_MAX 2048   // re-split: tested pairs of a gene whose in-parent cross terms sum in LDS
 #define RS_T 256          // re-split: threads per workgroup
+#define RS_SLICES 8       // re-split: workgroups sharing one gene's large parents
 #define RS_KPT 8          // keys per thread (held in registers: the scatter is in place)
 #define RS_CAP (RS_T * RS_KPT)
 #define RS_LOG2B 9
@@ -1397,17 +1398,24 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
 {
     __shared__ ResplitLds L;
     const int ng = A.counts[11];
-    for (;;) {  // one gene (all its parents, a contiguous run of fatbk) at a time, from a queue
+    // work items from a queue: slice sl of gene i takes the gene's parents
+    // ge.y + sl, ge.y + sl + RS_SLICES, ... (a contiguous run of fatbk), so the
+    // large parents of one heavy gene spread over RS_SLICES workgroups (one
+    // workgroup per gene left the kernel waiting on its heaviest gene: ~1.5 ms
+    // for 1/8 of config D's genes as for all of them).  Every slice adds its
+    // in-parent cross terms with integer atomics: order-free.
+    for (;;) {
         if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[9], 1);
         __syncthreads();
-        const int i = L.next;
-        if (i >= ng) break;
+        const int wi = L.next;
+        if (wi >= ng * RS_SLICES) break;
+        const int i = wi / RS_SLICES, sl = wi - i * RS_SLICES;
         const int4 ge = A.fatg[i];
         const int g = ge.x;
         const int ntp = A.gene_nt[g] <= RS_ACC_MAX ? A.gene_nt[g] : 0;  // larger: atomics per parent
         for (int j = threadIdx.x; j < ntp; j += RS_T) L.acc[j] = 0;
         __syncthreads();
-        for (int f = ge.y; f < ge.y + ge.z; ++f) {
+        for (int f = ge.y + sl; f < ge.y + ge.z; f += RS_SLICES) {
             const ScRankItem it = A.fatbk[f];
             if (it.n <= RSW_CAP) continue;  // k_rank_resplit_w (one wave per parent)
             resplit_one(A, it, L);
