@@ -97,6 +97,7 @@ struct ScRankLaunch {
 
 struct ScTestLaunch {
     int K, G, P, mode;
+    int glo, ghi;          // genes [glo, ghi): a run's gene shard (all genes: 0, G)
     double min_pct, lfc_thr, log_thr;
     const int* n_clu;
     const double* mean_x;

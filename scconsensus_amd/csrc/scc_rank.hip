@@ -192,8 +192,16 @@ __global__ void k_rank_classify(ScRankLaunch A)
     const i64 n = A.gstart[g + 1] - base;
     if (n <= 0) return;
     if (!A.all_pairs) {
+        // 16 pairs' flags per round (clamped loads in flight together): an untested
+        // gene costs P / 16 dependent rounds instead of P
         bool any = false;
-        for (int p = 0; p < A.P && !any; ++p) any = (A.flags[(size_t)p * A.G + g] & 1) != 0;
+        for (int p0 = 0; p0 < A.P && !any; p0 += 16) {
+            u8 f[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) f[u] = A.flags[(size_t)min(p0 + u, A.P - 1) * A.G + g];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) any |= (f[u] & 1) != 0;
+        }
         if (!any) return;
     }
     const int s = atomicAdd(&A.counts[3], 1);  // every ranked gene is split into value buckets

@@ -599,6 +599,8 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     ScTestLaunch T{};
     T.K = K;
     T.G = G;
+    T.glo = glo;
+    T.ghi = ghi;
     T.P = P;
     T.mode = prm->mode;
     T.min_pct = prm->min_per_cent;

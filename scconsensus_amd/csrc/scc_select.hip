@@ -209,9 +209,9 @@ __device__ inline u64 f_tie3(u64 c) { return c * c * c - c; }
 // flags bit0 tested, bit1 expression gate (SLOW).
 __global__ void __launch_bounds__(256) k_pair_filter(ScTestLaunch A)
 {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = A.glo + blockIdx.x * blockDim.x + threadIdx.x;  // the run's gene shard only
     const int p = blockIdx.y;
-    if (g >= A.G) return;
+    if (g >= A.ghi) return;
     int a, b;
     {
         a = 0;
@@ -256,9 +256,9 @@ __global__ void __launch_bounds__(256) k_pair_filter(ScTestLaunch A)
 // Untested cells (FAST, not requested) carry u2 = t = -1 and p = NaN.
 __global__ void __launch_bounds__(256) k_pair_test(ScTestLaunch A)
 {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = A.glo + blockIdx.x * blockDim.x + threadIdx.x;  // the run's gene shard only
     const int p = blockIdx.y;
-    if (g >= A.G) return;
+    if (g >= A.ghi) return;
     int a, b;
     {
         a = 0;
@@ -720,13 +720,15 @@ extern "C" int scc_wilcox_table_layout(int* woff /* WT_DIM*WT_DIM */)
 
 extern "C" hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_pair_filter, dim3((L->G + 255) / 256, L->P), dim3(256), 0, st, *L);
+    if (L->ghi <= L->glo) return hipSuccess;
+    hipLaunchKernelGGL(k_pair_filter, dim3((L->ghi - L->glo + 255) / 256, L->P), dim3(256), 0, st, *L);
     return hipGetLastError();
 }
 
 extern "C" hipError_t scc_launch_pair_test(const ScTestLaunch* L, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_pair_test, dim3((L->G + 255) / 256, L->P), dim3(256), 0, st, *L);
+    if (L->ghi <= L->glo) return hipSuccess;
+    hipLaunchKernelGGL(k_pair_test, dim3((L->ghi - L->glo + 255) / 256, L->P), dim3(256), 0, st, *L);
     return hipGetLastError();
 }
 
