@@ -156,6 +156,22 @@ SCC_API int scc_de_finish_records(scc_ctx* ctx, const scc_dataset* ds, const int
                                   const scc_de_params* params, const void* records /* device */,
                                   const int64_t* counts /* host [n_blocks] */, int32_t n_blocks, int64_t stride,
                                   scc_de_result** out);
+/* The per-pair selection of a FAST job split over the ranks by PAIRS (each
+ * rank the pairs [pair_lo, pair_hi); the pairs are independent until the
+ * union, Fast:359-392): scatters the gathered records like
+ * scc_de_finish_records, runs BH / filters / top_n for its pairs only and
+ * writes the first-occurrence key of every gene (u64 [G], device: pair-major
+ * order key, all ones = not selected; ordered by (pair, rank in the pair)).
+ * The caller combines the ranks' arrays by an element-wise MIN (all-reduce)
+ * and scc_de_union_first_occ turns the combined array into deGeneUnion in
+ * the reference's order (unique() over the pairs' top lists, Fast:392): the
+ * same union scc_de_finish_records returns.  No result object. */
+SCC_API int scc_de_finish_records_pairs(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */,
+                                        int32_t K, const scc_de_params* params, const void* records /* device */,
+                                        const int64_t* counts /* host [n_blocks] */, int32_t n_blocks, int64_t stride,
+                                        int32_t pair_lo, int32_t pair_hi, void* first_occ /* device u64 [G] */);
+SCC_API int scc_de_union_first_occ(scc_ctx* ctx, const void* first_occ /* device u64 [G] */, int64_t n_genes,
+                                   int32_t* genes /* host [G] */, int32_t* n_union);
 
 /* n_pairs = K(K-1)/2; n_rows = FAST tested rows over all pairs (0 for SLOW);
  * n_union = |deGeneUnion|. */

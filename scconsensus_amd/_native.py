@@ -37,7 +37,7 @@ EXPORTS = [
     "scc_ctx_create", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_kernel_time",
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_csr", "scc_dataset_create_dense", "scc_dataset_destroy",
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_run_shard_records",
-    "scc_de_finish_records", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
+    "scc_de_finish_records", "scc_de_finish_records_pairs", "scc_de_union_first_occ", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
     "scc_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores", "scc_pca_shard_eigen", "scc_pca_shard_project",
     "scc_distance_scores", "scc_silhouette", "scc_last_pca_scores",
@@ -107,6 +107,8 @@ def load():
         "scc_de_finish": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), vp, P(vp)]),
         "scc_de_run_shard_records": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), i64, i64, vp, i64, P(i64)]),
         "scc_de_finish_records": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), vp, vp, i32, i64, P(vp)]),
+        "scc_de_finish_records_pairs": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), vp, vp, i32, i64, i32, i32, vp]),
+        "scc_de_union_first_occ": (ctypes.c_int, [vp, vp, i64, vp, P(i32)]),
         "scc_de_result_counts": (ctypes.c_int, [vp, P(i32), P(i64), P(i32)]),
         "scc_de_result_union": (ctypes.c_int, [vp, vp]),
         "scc_de_result_rows": (ctypes.c_int, [vp] + [vp] * 10),
@@ -342,6 +344,28 @@ class Engine:
                                             ctypes.c_void_p(rec_ptr or None), _ptr(cnt), len(cnt), int(stride),
                                             ctypes.byref(r))
         return self._collect(r, rc, ds, mode, K, fetch)
+
+    def de_finish_records_pairs(self, ds: Dataset, code, K, rec_ptr, counts, stride, pair_lo, pair_hi, first_ptr,
+                                q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, test_all=False,
+                                test="wilcox", **_):
+        """FAST selection of the pairs [pair_lo, pair_hi) from the gathered
+        records; the genes' first-occurrence keys go to ``first_ptr`` (device
+        uint64 [G]; combine the ranks' arrays by MIN, then de_union_first_occ)."""
+        code = np.ascontiguousarray(code, np.int32)
+        prm = self._de_params(SCC_DE_FAST, q_val_thrs, log_fc_thrs, min_per_cent, top_n, 1.5, 5.0, test_all, test)
+        cnt = np.ascontiguousarray(counts, np.int64)
+        self._check(self.lib.scc_de_finish_records_pairs(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm),
+                                                         ctypes.c_void_p(rec_ptr or None), _ptr(cnt), len(cnt),
+                                                         int(stride), int(pair_lo), int(pair_hi),
+                                                         ctypes.c_void_p(first_ptr)))
+
+    def de_union_first_occ(self, first_ptr, G):
+        """deGeneUnion (reference order) from a combined first-occurrence array."""
+        out = np.zeros(G, np.int32)
+        nu = ctypes.c_int32()
+        self._check(self.lib.scc_de_union_first_occ(self.ctx, ctypes.c_void_p(first_ptr), G, _ptr(out),
+                                                    ctypes.byref(nu)))
+        return out[: nu.value].copy()
 
     def _collect(self, r, rc, ds, mode, K, fetch) -> DeResult:
         msg = ""

@@ -25,25 +25,33 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 // ------------------------------------------------------------------ gather
 // One wave per cell: its row indices stream in with 8 loads per lane in
 // flight; the value is fetched only for the union genes (a few per cent of
-// the nnz).
+// the nnz).  Row-index and union-map loads are clamped and unconditional, the
+// bounds applied by selects afterwards: a load under a lane condition is a
+// branch with its own wait, which issued the batch one load at a time.  Rows
+// outside [0, G) (invalid input, reported by the DE's ingest) map to no slot.
 __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indptr, const int* __restrict__ rows,
-                                                    const double* __restrict__ vals, int N,
+                                                    const double* __restrict__ vals, int N, int G,
                                                     const int* __restrict__ umap, int ld, double* __restrict__ Xc)
 {
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * (blockDim.x >> 6) + scc_wave_id();
     if (c >= N) return;
-    const i64 e = indptr[c + 1];
-    for (i64 k0 = indptr[c] + lane; k0 < e; k0 += 512) {
+    const i64 b = indptr[c], e = indptr[c + 1];
+    if (e <= b) return;
+    for (i64 k0 = b + lane; k0 < e; k0 += 512) {
         int r[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const i64 k = k0 + 64 * q;
-            r[q] = k < e ? rows[k] : -1;
+            r[q] = rows[k < e ? k : e - 1];
         }
         int u[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) u[q] = r[q] >= 0 ? umap[r[q]] : -1;
+        for (int q = 0; q < 8; ++q) {
+            const int rc = min(max(r[q], 0), G - 1);
+            const int x = umap[rc];
+            u[q] = (k0 + 64 * q < e && r[q] == rc) ? x : -1;
+        }
 #pragma unroll
         for (int q = 0; q < 8; ++q)
             if (u[q] >= 0) Xc[(size_t)c * ld + u[q]] = vals[k0 + 64 * q];
@@ -806,7 +814,7 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
     if (dense)
         hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
     else
-        hipLaunchKernelGGL(k_gather_csc, dim3((N + 3) / 4), dim3(256), 0, st, indptr, rows, vals, N, umap, ld, Xc);
+        hipLaunchKernelGGL(k_gather_csc, dim3((N + 3) / 4), dim3(256), 0, st, indptr, rows, vals, N, G, umap, ld, Xc);
     return hipGetLastError();
 }
 

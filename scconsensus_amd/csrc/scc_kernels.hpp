@@ -125,6 +125,7 @@ struct ScTestLaunch {
 
 struct ScSelectLaunch {
     int K, G, P, mode, top_n, cap;
+    int plo, phi;          // pairs [plo, phi) (all: 0, P)
     double q_thr, lfc_cut;
     const double* p;
     const double* lfc;

@@ -334,6 +334,10 @@ struct RecIO {  // the compact exchange's buffers (DE_SHARD_REC out, DE_FINISH_R
     const int64_t* counts = nullptr;
     int nblocks = 0;
     int64_t stride = 0;
+    // DE_FINISH_REC for pairs [pair_lo, pair_hi) only: the per-gene first
+    // occurrence keys go to first_out (device u64 [G]) and no result is built
+    int pair_lo = 0, pair_hi = 0;
+    void* first_out = nullptr;
 };
 
 static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
@@ -342,7 +346,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
 {
     const bool shard_stage = stage == DE_SHARD || stage == DE_SHARD_REC;
     const bool finish_stage = stage == DE_FINISH || stage == DE_FINISH_REC;
-    if (!c || !ds || !code || !prm || (!shard_stage && !out) || ((stage == DE_SHARD || stage == DE_FINISH) && !shard) ||
+    if (!c || !ds || !code || !prm || (!shard_stage && !out && !(rio && rio->first_out)) || ((stage == DE_SHARD || stage == DE_FINISH) && !shard) ||
         ((stage == DE_SHARD_REC || stage == DE_FINISH_REC) && !rio))
         return fail(c, SCC_ERR_INVALID, "scc_de_run: null argument");
     if (out) *out = nullptr;
@@ -888,7 +892,20 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         S.slow_de = d_slow_de;
         S.first_occ = d_first;
         S.err = d_err;
+        const bool pairs_only = rio && rio->first_out;
+        S.plo = pairs_only ? rio->pair_lo : 0;
+        S.phi = pairs_only ? rio->pair_hi : P;
         HIPCHK(c, scc_launch_pair_select(&S, s0));
+        if (pairs_only) {
+            HIPCHK(c, hipMemcpyAsync(rio->first_out, d_first, sizeof(unsigned long long) * G, hipMemcpyDeviceToDevice,
+                                     s0));
+            int e = 0;
+            HIPCHK(c, hipMemcpyAsync(&e, d_err, sizeof(int), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            if (e & 16) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records_pairs: record out of range");
+            if (e & 0x200) return fail(c, SCC_ERR_RSTOP, "NA in the DE logical vector: R stops at if(sum(...) <= 1)");
+            return SCC_OK;
+        }
         HIPCHK(c, scc_launch_union(d_first, G, d_key, env_int("SCC_UNION_CAP", kUnionCap), d_union, d_nu, s0));
     }
     // one pinned staging buffer, one synchronisation: [0] |U|, [1] error bits,
@@ -1015,6 +1032,57 @@ extern "C" int scc_de_finish_records(scc_ctx* c, const scc_dataset* ds, const in
     io.nblocks = n_blocks;
     io.stride = stride;
     return de_run_impl(c, ds, code, K, prm, DE_FINISH_REC, 0, ds ? ds->G : 0, nullptr, out, &io);
+}
+
+extern "C" int scc_de_finish_records_pairs(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                                           const scc_de_params* prm, const void* records, const int64_t* counts,
+                                           int32_t n_blocks, int64_t stride, int32_t pair_lo, int32_t pair_hi,
+                                           void* first_occ)
+{
+    if (!counts || n_blocks < 1 || stride < 0 || (!records && stride > 0) || !first_occ)
+        return fail(c, SCC_ERR_INVALID, "scc_de_finish_records_pairs: bad arguments");
+    const int P = K * (K - 1) / 2;
+    if (pair_lo < 0 || pair_hi > P || pair_lo > pair_hi)
+        return fail(c, SCC_ERR_INVALID, "scc_de_finish_records_pairs: pair range out of bounds");
+    if (!prm || prm->mode != SCC_DE_FAST)
+        return fail(c, SCC_ERR_UNSUPPORTED, "scc_de_finish_records_pairs: FAST mode only");
+    for (int b = 0; b < n_blocks; ++b)
+        if (counts[b] < 0 || counts[b] > stride)
+            return fail(c, SCC_ERR_INVALID, "scc_de_finish_records_pairs: count > stride");
+    RecIO io;
+    io.in = records;
+    io.counts = counts;
+    io.nblocks = n_blocks;
+    io.stride = stride;
+    io.pair_lo = pair_lo;
+    io.pair_hi = pair_hi;
+    io.first_out = first_occ;
+    return de_run_impl(c, ds, code, K, prm, DE_FINISH_REC, 0, ds ? ds->G : 0, nullptr, nullptr, &io);
+}
+
+extern "C" int scc_de_union_first_occ(scc_ctx* c, const void* first_occ, int64_t G64, int32_t* genes,
+                                      int32_t* n_union)
+{
+    if (!c || !first_occ || !genes || !n_union || G64 < 1 || G64 > INT32_MAX)
+        return fail(c, SCC_ERR_INVALID, "scc_de_union_first_occ: bad arguments");
+    const int G = (int)G64;
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    int rc;
+    void* d_key = nullptr;
+    int *d_union = nullptr, *d_nu = nullptr;
+    if ((rc = ws_get(c, "key_scratch", (size_t)G * scc_select_key_bytes(), &d_key))) return rc;
+    if ((rc = ws(c, "union", G, &d_union))) return rc;
+    if ((rc = ws(c, "nu", 4, &d_nu))) return rc;
+    HIPCHK(c, scc_launch_union((const unsigned long long*)first_occ, G, d_key, env_int("SCC_UNION_CAP", kUnionCap),
+                               d_union, d_nu, s0));
+    int nu = 0;
+    HIPCHK(c, hipMemcpyAsync(&nu, d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
+    HIPCHK(c, hipStreamSynchronize(s0));
+    if (nu < 0 || nu > G) return fail(c, SCC_ERR_HIP, "scc_de_union_first_occ: bad union size");
+    if (nu) HIPCHK(c, hipMemcpy(genes, d_union, sizeof(int) * nu, hipMemcpyDeviceToHost));
+    *n_union = nu;
+    return SCC_OK;
 }
 
 static int check_live(const scc_de_result* r)

@@ -373,6 +373,7 @@ __device__ inline u64 p_key(double p) { return (p != p) ? ~0ull : scc_key_of(p +
 
 struct SelectArgs {
     int K, G, P, mode, top_n, cap;
+    int plo;                 // first pair of this launch (blockIdx.x = p - plo)
     double q_thr;
     double lfc_cut;          // SLOW: log(fcThrs)
     const double* p;         // [P][G]
@@ -438,7 +439,7 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
     double* sred = (double*)(smem + tail);
     int* sc = (int*)(smem + tail + sizeof(double) * T);
     u64& sthr = *(u64*)(smem + tail + (sizeof(double) + sizeof(int)) * T);
-    const int p = blockIdx.x, tid = threadIdx.x;
+    const int p = A.plo + blockIdx.x, tid = threadIdx.x;
     const int G = A.G;
     const size_t pb = (size_t)p * G;
     // 1) compact tested genes (gene order) into records
@@ -753,6 +754,7 @@ extern "C" hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_
     A.K = L->K;
     A.G = L->G;
     A.P = L->P;
+    A.plo = L->plo;
     A.mode = L->mode;
     A.top_n = L->top_n;
     A.cap = L->cap;
@@ -783,7 +785,8 @@ extern "C" hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_
     A.err = L->err;
     const size_t lds = scc_select_lds_bytes(L->cap);
     hipFuncSetAttribute((const void*)k_pair_select<SEL_T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_pair_select<SEL_T>, dim3(L->P), dim3(SEL_T), lds, st, A);
+    if (L->phi <= L->plo) return hipSuccess;
+    hipLaunchKernelGGL(k_pair_select<SEL_T>, dim3(L->phi - L->plo), dim3(SEL_T), lds, st, A);
     return hipGetLastError();
 }
 

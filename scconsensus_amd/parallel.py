@@ -59,6 +59,17 @@ class Dist:
                 self.dist.all_reduce(tensor, op=self.dist.ReduceOp.SUM)
         return tensor
 
+    def all_reduce_min_(self, tensor):
+        """In-place element-wise minimum over ranks."""
+        if self.active:
+            if self._host_staged(tensor):
+                h = tensor.cpu()
+                self.dist.all_reduce(h, op=self.dist.ReduceOp.MIN)
+                tensor.copy_(h)
+            else:
+                self.dist.all_reduce(tensor, op=self.dist.ReduceOp.MIN)
+        return tensor
+
     def all_gather_cat(self, tensor):
         """The ranks' equal-sized 1-D tensors concatenated in rank order."""
         if not self.active:

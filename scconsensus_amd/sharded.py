@@ -37,6 +37,7 @@ from . import parallel
 _SHARD_KEYS = ("mode", "q_val_thrs", "log_fc_thrs", "min_per_cent", "top_n", "fc_thrs", "mean_scaling_factor",
                "test_all", "test")
 REC_WORDS = 8  # scc_de_record: 64 bytes = 8 int64 words
+_I64_MAX = (1 << 63) - 1
 
 
 class ShardError(RuntimeError):
@@ -77,10 +78,13 @@ def _raise_if(codes, msg=""):
 
 
 def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weights=None, exchange="records",
-               **params):
+               pair_split=True, **params):
     """The DE of one job over all ranks of ``dist``; every rank returns the same
     DeResult.  ``device``: the torch device of this rank's engine.
-    ``exchange`` "records" (compact, default) or "dense" (the [P][G] int64 sum)."""
+    ``exchange`` "records" (compact, default) or "dense" (the [P][G] int64 sum).
+    FAST with fetch="union" over > 1 rank (``pair_split``): each rank runs the
+    selection of a block of pairs and the union comes from the MIN-combined
+    first-occurrence keys (the result then carries the union only)."""
     import torch
 
     shard_kw = {k: v for k, v in params.items() if k in _SHARD_KEYS}
@@ -112,6 +116,26 @@ def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weig
     recs = dist.all_gather_cat(buf[: stride * REC_WORDS])
     if recs.is_cuda:
         torch.cuda.synchronize(recs.device)
+    if fetch == "union" and params.get("mode", 0) == 0 and dist.world > 1 and pair_split:
+        # the pairs are independent until the union: each rank selects its
+        # pairs; the genes' first-occurrence keys are combined by MIN
+        from . import _native as nat
+        plo, phi = parallel.shard_range(P, dist.rank, dist.world)
+        first = torch.empty(ds.G + 1, dtype=torch.int64, device=device)
+        _, st, msg = _call(eng.de_finish_records_pairs, ds, code, K, recs.data_ptr(), counts, stride, plo, phi,
+                           first.data_ptr(), **shard_kw)
+        if recs.is_cuda:
+            torch.cuda.synchronize(recs.device)  # the engine's stream -> the collective's
+        keys = first[: ds.G]
+        keys[keys == -1] = _I64_MAX  # unselected (all ones) sorts last under a signed MIN
+        first[-1] = -st  # the status rides along: MIN = minus the largest error code
+        dist.all_reduce_min_(first)
+        _raise_if([-int(first[-1].item())], msg)
+        keys[keys == _I64_MAX] = -1
+        if keys.is_cuda:
+            torch.cuda.synchronize(keys.device)
+        union = eng.de_union_first_occ(keys.data_ptr(), ds.G)
+        return nat.DeResult(nat.SCC_DE_FAST, K, P, union, np.zeros(0, np.int32))
     return eng.de_finish_records(ds, code, K, recs.data_ptr(), counts, stride, fetch=fetch, **shard_kw)
 
 

@@ -103,6 +103,31 @@ def test_records_range_ingest_matches_full(eng, cfg_a, bounds, monkeypatch):
     _same(ref, runs[1][2])
 
 
+@pytest.mark.parametrize("pair_cuts", [[0, 28], [0, 10, 20, 28], [0, 0, 1, 27, 28]])
+def test_pair_split_selection_union(eng, cfg_a, pair_cuts):
+    """FAST selection split by pairs (scc_de_finish_records_pairs on each block
+    of pairs, first-occurrence keys MIN-combined, scc_de_union_first_occ):
+    deGeneUnion identical, in order, to the unsharded scc_de_run's."""
+    d, names, code = cfg_a
+    K = len(names)
+    P = K * (K - 1) // 2
+    assert pair_cuts[-1] == P
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    ref = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")
+    allr, counts, stride = _records(eng, ds, code, K, [(0, 900), (900, 2000)])
+    big = (1 << 63) - 1
+    comb = torch.full((d.G,), big, dtype=torch.int64, device="cuda:0")
+    for lo, hi in zip(pair_cuts[:-1], pair_cuts[1:]):
+        first = torch.empty(d.G, dtype=torch.int64, device="cuda:0")
+        eng.de_finish_records_pairs(ds, code, K, allr.data_ptr(), counts, stride, lo, hi, first.data_ptr())
+        torch.cuda.synchronize()
+        first[first == -1] = big
+        comb = torch.minimum(comb, first)
+    comb[comb == big] = -1
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(eng.de_union_first_occ(comb.data_ptr(), d.G), ref.union)
+
+
 def test_records_t_and_slow_match_unsharded(eng, cfg_a):
     d, names, code = cfg_a
     K = len(names)

@@ -55,6 +55,21 @@ class Stand:
             blk = view(ptr + 64 * b * stride, int(c), REC)
             got += [(int(r["pair"]), int(r["gene"]), int(r["u2"])) for r in blk]
         return sorted(got)
+    def de_finish_records_pairs(self, ds, code, K, ptr, counts, stride, plo, phi, first_ptr, **kw):
+        if self.fail == "select":
+            raise nat.SccError(7, "selection failed on this rank")
+        self.pairs_seen = [plo, phi]
+        got = self.de_finish_records(ds, code, K, ptr, counts, stride, "union")
+        first = view(first_ptr, ds.G, np.int64)
+        first[:] = -1
+        for p in range(plo, phi):  # "selected": the pair's first three tested genes; key (pair, rank)
+            for rank, g in enumerate(sorted(g for pp, g, _ in got if pp == p)[:3]):
+                key = (p << 32) | rank
+                if first[g] == -1 or key < first[g]:
+                    first[g] = key
+    def de_union_first_occ(self, first_ptr, G):
+        first = view(first_ptr, G, np.int64)
+        return np.array([g for _, g in sorted((int(first[g]), g) for g in range(G) if first[g] != -1)], np.int32)
     def pca_shard_colsum(self, ds, genes, lo, hi, part_ptr):
         if self.fail == "pca":
             raise nat.SccError(3, "out of memory on this rank")
@@ -98,8 +113,17 @@ eng = Stand(fail.split(":")[1] if fail and int(fail.split(":")[0]) == d.rank els
 res = {"rank": d.rank}
 try:
     w = np.arange(1, ds.G + 1, dtype=float)  # stored values per gene: later genes heavier
-    got = sharded.de_sharded(eng, ds, None, 4, d, torch.device("cpu"), fetch="union", weights=w)
+    got = sharded.de_sharded(eng, ds, None, 4, d, torch.device("cpu"), fetch="union", weights=w, pair_split=False)
     res["de_ok"] = got == sorted((p, g, 2 * g) for p, g in eng.tested(4, ds.G))
+    # pair-split selection: each rank selects its pairs, first occurrences MIN-combined
+    r2 = sharded.de_sharded(eng, ds, None, 4, d, torch.device("cpu"), fetch="union", weights=w)
+    want = []
+    for p in range(6):
+        for g in sorted(g for pp, g in eng.tested(4, ds.G) if pp == p)[:3]:
+            if g not in want:
+                want.append(g)
+    res["union_ok"] = [int(g) for g in r2.union] == want
+    res["pairs_seen"] = eng.pairs_seen
     res["genes"] = list(sharded.gene_shard(ds.G, d.rank, d.world, w))
     genes = np.arange(0, 40, 2)
     S = sharded.pca_sharded(eng, ds, genes, d, torch.device("cpu")).numpy().reshape(ds.N, 16)
@@ -152,12 +176,15 @@ def test_sharded_job_two_ranks():
     assert res[0]["genes"][1] > 20  # weights 1..40: the lighter genes make the bigger block
     # one eigensolve (rank 0), its vectors broadcast to every rank
     assert [r["eigen_calls"] for r in res] == [1, 0]
+    # pair-split selection: pairs [0, 3) and [3, 6), the union equals the all-pairs one
+    assert all(r["union_ok"] for r in res), res
+    assert [r["pairs_seen"] for r in res] == [[0, 3], [3, 6]]
 
 
 def test_error_on_one_rank_raises_everywhere():
     """a failure one rank alone sees (an R stop() on its genes, an
     OOM) must raise on every rank, not leave the other blocked in a collective."""
-    for rank, stage, code in ((1, "de", 5), (1, "pca", 3), (0, "eigen", 6)):
+    for rank, stage, code in ((1, "de", 5), (1, "pca", 3), (0, "eigen", 6), (1, "select", 7)):
         res = _run({"SCC_FAIL_RANK_STAGE": f"{rank}:{stage}"})
         assert [r.get("error") for r in res] == [code, code], (stage, res)
 
