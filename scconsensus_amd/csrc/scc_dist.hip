@@ -25,19 +25,32 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 // ------------------------------------------------------------------ gather
 // One wave per cell: its row indices stream in with 8 loads per lane in
 // flight; the value is fetched only for the union genes (a few per cent of
-// the nnz).  Row-index and union-map loads are clamped and unconditional, the
-// bounds applied by selects afterwards: a load under a lane condition is a
-// branch with its own wait, which issued the batch one load at a time.  Rows
-// outside [0, G) (invalid input, reported by the DE's ingest) map to no slot.
+// the nnz).  The cell's row of X[U,] (ld doubles, zero for absent genes and
+// the padding columns) is assembled in LDS and leaves as whole coalesced
+// lines, so the output needs no memset pass and no partial-line stores.
+// Row-index and union-map loads are clamped and unconditional, the bounds
+// applied by selects afterwards (a load under a lane condition is a branch
+// with its own wait).  Rows outside [0, G) (invalid input, reported by the
+// DE's ingest) map to no slot.
+// LDSROW false (ld > GATHER_LDS_LD: a union too wide for four LDS rows): the
+// values go straight to Xc, which the caller has zeroed.
+#define GATHER_LDS_LD 2048
+template <bool LDSROW>
 __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                     const double* __restrict__ vals, int N, int G,
                                                     const int* __restrict__ umap, int ld, double* __restrict__ Xc)
 {
-    const int lane = threadIdx.x & 63;
-    const int c = blockIdx.x * (blockDim.x >> 6) + scc_wave_id();
-    if (c >= N) return;
+    extern __shared__ __attribute__((aligned(16))) double grow[];  // [4 waves][ld]
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    const int c = blockIdx.x * (blockDim.x >> 6) + wv;
+    if (c >= N) return;  // whole waves: no workgroup barrier below
+    double* row = LDSROW ? grow + (size_t)wv * ld : Xc + (size_t)c * ld;
+    if (LDSROW)
+        for (int u = lane; u < ld; u += 64) row[u] = 0.0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // LDS stores drained (s_waitcnt lgkmcnt(0))
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const i64 b = indptr[c], e = indptr[c + 1];
-    if (e <= b) return;
     for (i64 k0 = b + lane; k0 < e; k0 += 512) {
         int r[8];
 #pragma unroll
@@ -54,9 +67,19 @@ __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indp
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-            if (u[q] >= 0) Xc[(size_t)c * ld + u[q]] = vals[k0 + 64 * q];
+            if (u[q] >= 0) row[u[q]] = vals[k0 + 64 * q];
     }
+    if (!LDSROW) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double* out = Xc + (size_t)c * ld;
+    for (int u = lane; u < ld; u += 64) out[u] = row[u];
 }
+
+// true when the CSC gather writes every element of its rows (the caller then
+// clears only the padding rows)
+extern "C" int scc_gather_writes_rows(int ld) { return ld <= GATHER_LDS_LD; }
 
 __global__ void __launch_bounds__(256) k_gather_dense(const double* __restrict__ X, int G, int N,
                                                       const int* __restrict__ genes, int nu, int ld,
@@ -813,8 +836,12 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
 {
     if (dense)
         hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
+    else if (ld <= GATHER_LDS_LD)
+        hipLaunchKernelGGL(k_gather_csc<true>, dim3((N + 3) / 4), dim3(256), sizeof(double) * 4 * (size_t)ld, st,
+                           indptr, rows, vals, N, G, umap, ld, Xc);
     else
-        hipLaunchKernelGGL(k_gather_csc, dim3((N + 3) / 4), dim3(256), 0, st, indptr, rows, vals, N, G, umap, ld, Xc);
+        hipLaunchKernelGGL(k_gather_csc<false>, dim3((N + 3) / 4), dim3(256), 0, st, indptr, rows, vals, N, G, umap,
+                           ld, Xc);
     return hipGetLastError();
 }
 

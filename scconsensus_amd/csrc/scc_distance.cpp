@@ -18,6 +18,7 @@ using namespace scc_rt;
 
 extern "C" {
 hipError_t scc_launch_union_map(int* umap, int G, const int* genes, int nu, hipStream_t st);
+int scc_gather_writes_rows(int ld);
 hipError_t scc_launch_gather(const long long* indptr, const int* rows, const double* vals, const double* dense,
                              int G, int N, const int* umap, const int* genes, int nu, int ld, double* Xc,
                              hipStream_t st);
@@ -213,7 +214,9 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
     {
         Scope sc(c, "gather", s0);
-        HIPCHK(c, hipMemsetAsync(d_X, 0, sizeof(double) * (size_t)Npad * ld, s0));
+        // the CSC gather writes whole rows (zeros included): only the padding rows need clearing
+        const size_t r0 = (ds->dense || !scc_gather_writes_rows(ld)) ? 0 : (size_t)N;
+        HIPCHK(c, hipMemsetAsync(d_X + r0 * ld, 0, sizeof(double) * ((size_t)Npad - r0) * ld, s0));
         HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
         HIPCHK(c, scc_launch_gather(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, N, d_umap, d_genes, nu, ld,
                                     d_X, s0));
@@ -383,7 +386,8 @@ extern "C" int scc_pca_shard_colsum(scc_ctx* c, const scc_dataset* ds, const int
     HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
     {
         Scope sc(c, "gather", s0);
-        HIPCHK(c, hipMemsetAsync(d_X, 0, sizeof(double) * (size_t)npad * ld, s0));
+        const size_t r0 = (ds->dense || !scc_gather_writes_rows(ld)) ? 0 : (size_t)n;  // CSC: whole rows written
+        HIPCHK(c, hipMemsetAsync(d_X + r0 * ld, 0, sizeof(double) * ((size_t)npad - r0) * ld, s0));
         HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
         if (n > 0)
             HIPCHK(c, scc_launch_gather(ds->dense ? nullptr : ds->d_indptr + cell_lo, ds->d_rows, ds->d_vals,

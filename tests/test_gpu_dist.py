@@ -342,3 +342,21 @@ def test_subspace_iteration_falls_back(eng, case, monkeypatch, capfd):
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
 
+
+
+def test_gather_wide_union_fallback(eng):
+    """A union wider than four LDS rows (|U| > 2048: the CSC gather's direct
+    store path, whole matrix zeroed first) and a narrow one (rows assembled in
+    LDS, only padding rows zeroed) both give the exact-SVD distance."""
+    import scipy.sparse as sp
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(5)
+    G, N = 2100, 300
+    X = sp.random(G, N, density=0.05, random_state=6, format="csc") * 4.0
+    X.data = np.log1p(X.data)
+    Xd = X.toarray()
+    ds = eng.dataset_csc(X.indptr.astype(np.int64), X.indices.astype(np.int32), X.data, G, N)
+    for g in (np.arange(G), np.sort(rng.choice(G, 150, replace=False))):
+        d = eng.distance(ds, g.astype(np.int32), nat.SCC_DIST_PCA_EUCLID)
+        ref = O.dist_euclidean(O.pca_scores(Xd, g))
+        assert np.max(np.abs(d - ref)) < 1e-5
