@@ -93,7 +93,11 @@ SCC_API void scc_ctx_reset_timers(scc_ctx* ctx);
 
 /* ---- dataset: the genes x cells matrix as R holds it ------------------- */
 /* dgCMatrix (CSC over cells): indptr[N+1] (R @p), rows[nnz] (R @i, 0-based
- * gene rows), vals[nnz] (R @x).  Replaces as.matrix(dataMatrix) (Fast:368). */
+ * gene rows), vals[nnz] (R @x).  Replaces as.matrix(dataMatrix) (Fast:368).
+ * SCC_PTR_HOST copies the arrays; SCC_PTR_DEVICE borrows them, and their
+ * contents must not change while the dataset lives: the first error-free DE
+ * run that reads every entry marks the dataset validated (rows in range and
+ * sorted) and caches nodg, and later gene-shard runs read only their genes. */
 SCC_API int scc_dataset_create_csc(scc_ctx* ctx, const int64_t* indptr, const int32_t* rows, const double* vals,
                            int64_t n_genes, int64_t n_cells, int64_t nnz, int32_t ptr_kind,
                            scc_dataset** out);
