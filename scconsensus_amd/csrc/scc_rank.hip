@@ -838,7 +838,7 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 
 #define RW_SLOTS_MAX 16  // tested pairs per gene the wave kernel holds: 64 * slots (2, 4, 8 or 16)
 #define RW_PAIRS_MAX (8 * 64 * RW_SLOTS_MAX)  // genes past 1024 tested pairs: one 16-slot pass per 1024
-#define RS_ACC_MAX 2048   // re-split: tested pairs of a gene whose in-parent cross terms sum in LDS
+#define RS_ACC_MAX (SCC_MAX_K * (SCC_MAX_K - 1) / 2)  // re-split: in-parent cross terms of every tested pair sum in LDS
 #define RS_T 256          // re-split: threads per workgroup
 #define RS_SLICES 8       // re-split: workgroups sharing one gene's large parents
 #define RS_KPT 8          // keys per thread (held in registers: the scatter is in place)
@@ -1145,7 +1145,6 @@ struct ResplitLds {
     u64 rmn[RS_T / 64], rmx[RS_T / 64];
     u32 hs[RS_HCAP];  // [sub-bucket][cluster] counts (in-parent cross term), when nb * K fits
     u32 bs[RS_HCAP];  // [sub-bucket][cluster] elements of the cluster in lower sub-buckets
-    u64 acc[RS_ACC_MAX];  // the gene's in-parent cross terms per tested pair (genes with <= RS_ACC_MAX)
     int nb, bk0, next, ovf, nw, w0;
 };
 
@@ -1159,7 +1158,7 @@ __device__ inline bool push_fat2(const ScRankLaunch& A, const ScRankItem& itm)
     return true;
 }
 
-__device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitLds& L)
+__device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitLds& L, u64* __restrict__ acc)
 {
     constexpr int W = RS_T / 64, BPT = RS_BINS / RS_T;
     const int K = A.K, g = it.gene, n = it.n;
@@ -1384,7 +1383,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
     }
     __syncthreads();
     const int ntp = A.gene_nt[g];
-    const bool lds_acc = ntp <= RS_ACC_MAX;
+    const bool lds_acc = ntp <= A.P;  // always: the dynamic LDS array holds P entries
     for (int j = tid; j < ntp; j += RS_T) {
         const u32 v = A.gene_tp[(size_t)g * A.P + j];
         const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
@@ -1393,7 +1392,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
 #pragma unroll 4
         for (int q = 0; q < nb; ++q) sacc += (u64)L.hs[q * K + a] * L.bs[q * K + b];
         if (lds_acc)
-            L.acc[j] += sacc;  // thread j owns tested pair j for the whole gene
+            acc[j] += sacc;  // thread j owns tested pair j for the whole gene
         else if (sacc)
             atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)sacc);
     }
@@ -1405,6 +1404,10 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
 __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
 {
     __shared__ ResplitLds L;
+    // the gene's in-parent cross terms per tested pair: P entries of dynamic LDS
+    // (8 B x 66 at config B, x 4950 at E), so no gene falls back to one global
+    // atomic per (parent, pair)
+    extern __shared__ __attribute__((aligned(16))) u64 racc[];
     const int ng = A.counts[11];
     // work items from a queue: slice sl of gene i takes the gene's parents
     // ge.y + sl, ge.y + sl + RS_SLICES, ... (a contiguous run of fatbk), so the
@@ -1420,19 +1423,19 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
         const int i = wi / RS_SLICES, sl = wi - i * RS_SLICES;
         const int4 ge = A.fatg[i];
         const int g = ge.x;
-        const int ntp = A.gene_nt[g] <= RS_ACC_MAX ? A.gene_nt[g] : 0;  // larger: atomics per parent
-        for (int j = threadIdx.x; j < ntp; j += RS_T) L.acc[j] = 0;
+        const int ntp = A.gene_nt[g];
+        for (int j = threadIdx.x; j < ntp; j += RS_T) racc[j] = 0;
         __syncthreads();
         for (int f = ge.y + sl; f < ge.y + ge.z; f += RS_SLICES) {
             const ScRankItem it = A.fatbk[f];
             if (it.n <= RSW_CAP) continue;  // k_rank_resplit_w (one wave per parent)
-            resplit_one(A, it, L);
+            resplit_one(A, it, L, racc);
             __syncthreads();
         }
         for (int j = threadIdx.x; j < ntp; j += RS_T) {
-            if (L.acc[j]) {
+            if (racc[j]) {
                 const u32 v = A.gene_tp[(size_t)g * A.P + j];
-                atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)L.acc[j]);
+                atomicAdd((unsigned long long*)&A.accS[(size_t)(v & 0xffffu) * A.G + g], (unsigned long long)racc[j]);
             }
         }
         __syncthreads();
@@ -2338,7 +2341,9 @@ extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, h
     W.rsw_chunk = (int)std::max(8LL, std::min(128LL, (long long)L->bucket_cap / (16 * waves)));
     W.rs_level = 0;
     hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
-    hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), 0, st, *L);
+    const size_t acc_lds = sizeof(u64) * (size_t)std::max(L->P, 1);
+    hipFuncSetAttribute((const void*)k_rank_resplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_lds);
+    hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), acc_lds, st, *L);
     if (L->fat2) {  // sub-buckets the first level left with > 64 distinct values
         W.rs_level = 1;
         hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
