@@ -949,13 +949,21 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     const char* ke = getenv("SCC_DIST_KERNEL");
     const int kind = (ke && *ke) ? atoi(ke) : 1;
     const char* env = getenv("SCC_DIST_COLS");  // 64 or 256 columns per tile
-    const int cols = (env && *env) ? atoi(env) : ((kind == 0 && N >= 65536) ? 256 : 64);
+    // default 64 columns; 128 for the aligned kernel from 64k cells (config D: 32.3 -> 31.5 ms; 16 / 32 columns
+    // 43.8 / 34.3 ms; config B: 64 columns 0.515 ms, 32: 0.535, 128: 0.525) -- all widths bit-identical
+    const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? (kind == 0 ? 256 : (kind == 1 ? 128 : 64)) : 64);
     if (kind == 1) {
         const char* nte = getenv("SCC_DIST_NT");  // nontemporal stores (default on)
         const bool nt = !(nte && *nte && atoi(nte) == 0);
         if (cols == 256)
             nt ? launch_dist_aligned<256, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
                : launch_dist_aligned<256, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
+        else if (cols == 32)
+            launch_dist_aligned<32, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st);
+        else if (cols == 16)
+            launch_dist_aligned<16, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st);
+        else if (cols == 128)
+            launch_dist_aligned<128, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st);
         else
             nt ? launch_dist_aligned<64, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
                : launch_dist_aligned<64, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);

@@ -251,7 +251,7 @@ def test_one_cu_rank_deficient_and_repeated(eng, n, monkeypatch):
     assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
 
 
-@pytest.mark.parametrize("cols", ["64", "256"])
+@pytest.mark.parametrize("cols", ["16", "32", "64", "128", "256"])
 @pytest.mark.parametrize("f32", [False, True])
 def test_distance_kernels_agree(eng, cols, f32, monkeypatch):
     """The three distance store kernels (SCC_DIST_KERNEL 1 = workgroup-staged
