@@ -152,14 +152,30 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     const int kr = lane >> 4, cc = lane & 15;
-    for (int c = c0; c < c1; c += 4) {
-        const double* row = Xc + (size_t)(c + kr) * ld;
-        const double a0 = row[i0 + cc], a1 = row[i0 + 16 + cc];
-        const double b0 = row[j0 + cc], b1 = row[j0 + 16 + cc];
-        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    // 16 rows (four 4-row k-steps) per round: all 16 loads of a round issued
+    // before its 16 MFMAs (clamped row, masked value past the chunk), so a
+    // round waits on memory once instead of four times
+    for (int c = c0; c < c1; c += 16) {
+        double a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int rr = c + 4 * u + kr;
+            const double* row = Xc + (size_t)min(rr, c1 - 1) * ld;
+            const double x0 = row[i0 + cc], x1 = row[i0 + 16 + cc];
+            const double y0 = row[j0 + cc], y1 = row[j0 + 16 + cc];
+            const bool ok = rr < c1;
+            a0[u] = ok ? x0 : 0.0;
+            a1[u] = ok ? x1 : 0.0;
+            b0[u] = ok ? y0 : 0.0;
+            b1[u] = ok ? y1 : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b0[u], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b1[u], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], b0[u], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], b1[u], acc[1][1], 0, 0, 0);
+        }
     }
     double* S = slabs + (size_t)chunk * ld * ld;
 #pragma unroll
