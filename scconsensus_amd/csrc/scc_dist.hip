@@ -117,17 +117,23 @@ __global__ void __launch_bounds__(256) k_colmean(const dd* __restrict__ part, in
     if (lane == 0) mean[u] = dd_div_n(s, (double)N);
 }
 
+// two elements per thread (ld is a multiple of 64): 16-byte loads and stores
 __global__ void __launch_bounds__(256) k_center(double* __restrict__ Xc, int N, int nu, int ld,
                                                 const double* __restrict__ mean)
 {
-    const size_t total = (size_t)N * ld;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
-        const int u = (int)(e % ld);
-        if (u < nu) Xc[e] -= mean[u];
+    const size_t total2 = (size_t)N * ld / 2;
+    double2* X2 = (double2*)Xc;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total2; e += (size_t)gridDim.x * blockDim.x) {
+        const int u = (int)((2 * e) % ld);
+        double2 x = X2[e];
+        if (u < nu) x.x -= mean[u];
+        if (u + 1 < nu) x.y -= mean[u + 1];
+        X2[e] = x;
     }
 }
 
 // ------------------------------------------------------------------ Gram (fp64 MFMA)
+#define GR_U 4  // 4-row k-steps whose loads are issued together (8: B 0.13, C 0.88, D 4.51 ms)
 // WG = 4 waves -> 64x64 tile of C (upper tiles only); wave -> 32x32 = 2x2 MFMA
 // 16x16x4 tiles.  Lane l holds A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15];
 // accumulator reg r is C[row = (l>>4) + 4r][col = l&15] (f64 layout).
@@ -152,13 +158,13 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     const int kr = lane >> 4, cc = lane & 15;
-    // 16 rows (four 4-row k-steps) per round: all 16 loads of a round issued
-    // before its 16 MFMAs (clamped row, masked value past the chunk), so a
-    // round waits on memory once instead of four times
-    for (int c = c0; c < c1; c += 16) {
-        double a0[4], a1[4], b0[4], b1[4];
+    // 4 GR_U rows per round: all loads of a round issued before its MFMAs
+    // (clamped row, masked value past the chunk), so a round waits on memory
+    // once instead of GR_U times (GR_U 4: B 0.14, C 0.89, D 4.35 ms; 1: 0.18 / 1.43 / 5.22)
+    for (int c = c0; c < c1; c += 4 * GR_U) {
+        double a0[GR_U], a1[GR_U], b0[GR_U], b1[GR_U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GR_U; ++u) {
             const int rr = c + 4 * u + kr;
             const double* row = Xc + (size_t)min(rr, c1 - 1) * ld;
             const double x0 = row[i0 + cc], x1 = row[i0 + 16 + cc];
@@ -170,7 +176,7 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
             b1[u] = ok ? y1 : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GR_U; ++u) {
             acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b0[u], acc[0][0], 0, 0, 0);
             acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b1[u], acc[0][1], 0, 0, 0);
             acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], b0[u], acc[1][0], 0, 0, 0);
