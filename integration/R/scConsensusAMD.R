@@ -60,7 +60,9 @@
     grp <- dynamicTreeCut::cutreeDynamic(dendro = tree, distM = dm, deepSplit = dsv,
                                          pamStage = FALSE, minClusterSize = minClusterSize)
     colors[[paste("deepsplit:", dsv)]] <- WGCNA::labels2colors(grp)
-    if (with_si) invisible(cluster::silhouette(grp, dmatrix = dm))
+    # deepSplitInfo's SI (Fast:433, computed and discarded by the reference):
+    # the engine's silhouette on its HBM-resident copy of d (no N x N matrix)
+    if (with_si) invisible(.Call("C_scc_si", as.integer(grp)))
   }
   names(colors) <- paste("deepsplit:", deepSplitValues)
   list(tree = tree, colors = colors)

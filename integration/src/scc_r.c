@@ -203,12 +203,32 @@ SEXP C_scc_distance(SEXP h, SEXP genes, SEXP metric, SEXP ncomp)
     return d;
 }
 
+/* mean(summary(cluster::silhouette(groups, as.matrix(d)))$clus.avg.widths)
+ * (Fast:433) on the engine-kept output of the last C_scc_distance call; NA
+ * when R's silhouette returns NA (fewer than 2 or as many groups as cells). */
+SEXP C_scc_si(SEXP groups)
+{
+    ensure_ctx();
+    const int N = LENGTH(groups);
+    int32_t* g = (int32_t*)R_alloc((size_t)N, sizeof(int32_t));
+    for (int k = 0; k < N; ++k) g[k] = INTEGER(groups)[k];
+    double* avg = (double*)R_alloc((size_t)N, sizeof(double));
+    int32_t ng = 0;
+    int rc = scc_silhouette(g_ctx, N, g, NULL, 0, NULL, avg, &ng);
+    if (rc == SCC_ERR_INVALID) return Rf_ScalarReal(NA_REAL);
+    check(rc);
+    double s = 0.0;
+    for (int k = 0; k < ng; ++k) s += avg[k];
+    return Rf_ScalarReal(ng > 0 ? s / ng : NA_REAL);
+}
+
 static const R_CallMethodDef call_methods[] = {
     {"C_scc_dataset", (DL_FUNC)&C_scc_dataset, 4},
     {"C_scc_release", (DL_FUNC)&C_scc_release, 1},
     {"C_scc_de_fast", (DL_FUNC)&C_scc_de_fast, 8},
     {"C_scc_de_slow", (DL_FUNC)&C_scc_de_slow, 6},
     {"C_scc_distance", (DL_FUNC)&C_scc_distance, 4},
+    {"C_scc_si", (DL_FUNC)&C_scc_si, 1},
     {NULL, NULL, 0}};
 
 /* the package is scConsensus (NAMESPACE: useDynLib(scConsensus, .registration = TRUE)) */

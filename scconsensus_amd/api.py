@@ -135,13 +135,23 @@ def _hclust_ward_d2(dist_packed, N):
     return {"merge": merge, "height": height, "order": order, "method": "ward.D2", "dist.method": "euclidean"}
 
 
-def _dynamic_colors(tree, dist_packed, deepSplitValues, minClusterSize):
+def _dynamic_colors(tree, dist_packed, deepSplitValues, minClusterSize, eng=None, info=None):
     """Fast:418-431: cutreeDynamic(dendro, distM = as.matrix(d), deepSplit = dsv,
-    pamStage = FALSE, minClusterSize) -> labels2colors, named "deepsplit: dsv"."""
+    pamStage = FALSE, minClusterSize) -> labels2colors, named "deepsplit: dsv".
+    With ``eng`` and a list ``info``: the reference's deepSplitInfo rows
+    (Fast:433: DeepSplit, NumbersOfClusters, SI = mean of
+    summary(cluster::silhouette(groups, as.matrix(d)))$clus.avg.widths), the
+    silhouette computed by the engine on its HBM-resident copy of d."""
     out = {}
+    N = len(tree["order"])
     for dsv in deepSplitValues:
         lab, _ = nat.cutree_hybrid(tree["merge"], tree["height"], dist_packed, int(dsv), int(minClusterSize))
         out[f"deepsplit: {dsv}"] = labels2colors(lab)
+        if eng is not None and info is not None:
+            lab = np.asarray(lab, np.int32)
+            k = len(np.unique(lab))
+            si = float(np.mean(eng.silhouette(N, lab)[1])) if 2 <= k < N else float("nan")  # R: NA otherwise
+            info.append({"DeepSplit": dsv, "NumbersOfClusters": k, "SI": si})
     return out
 
 
@@ -185,12 +195,14 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
         raise RuntimeError("no DE genes (R fails on an empty deGenes data frame, Fast:386)")
     d = eng.distance(ds, uni, nat.SCC_DIST_PCA_EUCLID)
     tree = _hclust_ward_d2(d, N)
+    info = [] if return_details else None  # deepSplitInfo: computed by the reference, never returned (Fast:433)
     ret = {"deGeneUnion": list(gnames[uni]), "cellTree": tree,
-           "dynamicColors": _dynamic_colors(tree, d, deepSplitValues, minClusterSize)}
+           "dynamicColors": _dynamic_colors(tree, d, deepSplitValues, minClusterSize, eng, info)}
     if save:
         _save(ret, filename)
     if return_details:
-        ret["_details"] = {"clusters": names, "code": code, "de": res, "dist": d, "union_idx": uni}
+        ret["_details"] = {"clusters": names, "code": code, "de": res, "dist": d, "union_idx": uni,
+                           "deepSplitInfo": info}
     ds.close()
     return ret
 

@@ -63,3 +63,27 @@ def test_api_mirror_returns_dynamic_colors(cfg_a):
     assert np.array_equal(tree["merge"], mg)
     lab, _ = nat.cutree_hybrid(mg, hg, gpu, 2, 10)
     assert out["dynamicColors"]["deepsplit: 2"] == api.labels2colors(lab)
+
+
+def test_api_deepsplit_info_silhouette(cfg_a):
+    """The reference's deepSplitInfo (Fast:433): per deepSplit the number of
+    clusters and SI = mean of summary(cluster::silhouette(groups,
+    as.matrix(d)))$clus.avg.widths, here from the engine's silhouette on the
+    HBM-resident distance; checked against sklearn's silhouette_samples on the
+    same distance (per-cluster means, singletons 0 as in cluster::silhouette)."""
+    from sklearn.metrics import silhouette_samples
+    d, gpu, _ = cfg_a
+    out = api.reclusterDEConsensusFast(d, d.labels, deepSplitValues=(1, 2), minClusterSize=10, return_details=True)
+    info = out["_details"]["deepSplitInfo"]
+    dist = out["_details"]["dist"]
+    M = squareform(dist)
+    tree = out["cellTree"]
+    assert [r["DeepSplit"] for r in info] == [1, 2]
+    for r in info:
+        lab, _ = nat.cutree_hybrid(tree["merge"], tree["height"], dist, int(r["DeepSplit"]), 10)
+        lab = np.asarray(lab)
+        ks = np.unique(lab)
+        assert r["NumbersOfClusters"] == len(ks)
+        s = silhouette_samples(M, lab, metric="precomputed")
+        ref = np.mean([s[lab == k].mean() for k in ks])
+        assert abs(r["SI"] - ref) < 1e-9, (r, ref)
