@@ -20,8 +20,6 @@
   colLabels <- consensusClusterLabels[colnames(dataMatrix)]
   code <- match(as.character(colLabels), keep) - 1L
   code[is.na(code)] <- -1L
-  if (length(keep) > 128L)
-    stop("scConsensus engine: ", length(keep), " clusters; one engine run holds at most 128")
   list(clusters = keep, code = as.integer(code))
 }
 

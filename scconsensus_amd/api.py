@@ -178,14 +178,10 @@ def reclusterDEConsensusFast(dataMatrix, consensusClusterLabels, method="wilcox"
     if len(names) < 2:
         raise ValueError("need at least two clusters with > minClusterSize cells")
     ds = _upload(eng, m)
-    if len(names) > 128:  # one engine run holds <= 128 clusters: group-pair runs (grouped.py)
-        from . import grouped
-        res = grouped.de_fast_grouped(eng, ds, code, len(names), q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
-                                      min_per_cent=float(minPerCent), top_n=NumbertopDEGenes, test=method)
-    else:
-        res = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
-                         min_per_cent=float(minPerCent), top_n=NumbertopDEGenes,
-                         fetch="rows" if return_details else "union", test=method)
+    # any K: more than 128 clusters run as group-pair runs inside libscc (scc_de_run)
+    res = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, q_val_thrs=qValThrs, log_fc_thrs=logFCThrs,
+                     min_per_cent=float(minPerCent), top_n=NumbertopDEGenes,
+                     fetch="rows" if return_details else "union", test=method)
     if res.status == nat.SCC_ERR_RSTOP:
         raise RuntimeError(res.message)
     uni = res.union

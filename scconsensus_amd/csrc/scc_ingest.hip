@@ -65,13 +65,24 @@ __device__ inline i64 wave_lower_bound(const int* __restrict__ rows, i64 lo, i64
 }
 
 // err bits: 1 non-finite value, 2 row index out of range, 4 rows not sorted
+//
+// The chunk's gene histogram lives in LDS as 8-bit counters (a count chunk has
+// <= kCountChunk = 32 cells, so a (chunk, gene) count is <= 32): gene l of the
+// window goes to byte l / nwq of word l % nwq (nwq = ceil(window / 4)), so the
+// consecutive genes of one cell's entries hit consecutive words (no two lanes
+// of a wave add to one word unless their genes are nwq apart).  One window
+// holds up to 4 * 40960 genes in 160 KB; a larger G is counted in windows of
+// `hw` genes: the first pass reads every entry (nodg, expm1, input checks,
+// tile boundaries, counts of window 0), later passes read each cell's entries
+// of their window only (two wave-parallel binary searches; dense: the range).
 template <bool DENSE>
 __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                     const double* __restrict__ vals, int G, const int* __restrict__ perm,
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
                                                     int* __restrict__ nodg, dd* __restrict__ wave_expm1,
-                                                    int want_expm1, int glo, int ghi, int rng, int* __restrict__ err)
+                                                    int want_expm1, int glo, int ghi, int rng, int hw,
+                                                    int* __restrict__ err)
 {
     // genes outside [glo, ghi) (a shard of the gene rows) are not counted; nodg
     // and the expm1 sum still see every entry -- unless rng (a validated CSC
@@ -82,86 +93,113 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int ch = blockIdx.x;
     const int a = cc_code[ch];
-    if (a >= 0)
-        for (int g = threadIdx.x; g < G; g += IH_T) hist[g] = 0;
-    __syncthreads();
     const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
     const int t0r = glo / gt, t1r = min(ntile, (ghi + gt - 1) / gt);  // rng: the tiles [t0r, t1r) cover [glo, ghi)
+    const int nwin = (G + hw - 1) / hw;
     dd se{0.0, 0.0};
     int bad = 0;
-    for (int p = p0 + wv; p < p1; p += IH_T / 64) {
-        const int c = perm[p];
-        i64 b, e;
-        cell_range<DENSE>(indptr, c, G, b, e);
-        u32 pos = 0;
-        i64* bp = bnd + (size_t)p * (ntile + 1);
-        i64 kb = b, ke = e;
-        if (!DENSE && rng) {
-            kb = wave_lower_bound(rows, b, e, t0r * gt);
-            ke = wave_lower_bound(rows, kb, e, t1r * gt);
-        }
-        for (i64 k0 = kb; k0 < ke; k0 += 4 * 64) {  // four loads in flight per lane
-            double xs[4];
-            int gs[4], gps[4];
-            // clamped unconditional loads + select (a load under a lane
-            // condition becomes a branch with its own wait, one load at a time)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const i64 k = k0 + u * 64 + lane;
-                const i64 kc = k < ke ? k : ke - 1;  // k0 < ke, so ke - 1 >= b
-                const double x = vals[kc];
-                xs[u] = k < ke ? x : 0.0;
+    for (int win = 0; win < nwin; ++win) {
+        const int wlo = win * hw, whi = min(G, wlo + hw);
+        const int clo = max(glo, wlo), chi = min(ghi, whi);  // genes this pass counts
+        const u32 nwq = (u32)(whi - wlo + 3) >> 2;
+        const u64 mq = ((1ull << 40) + nwq - 1) / nwq;  // l / nwq = (l * mq) >> 40 for l < 2^18
+        if (win > 0 && (a < 0 || clo >= chi)) continue;  // block-uniform
+        if (a >= 0)
+            for (u32 q = threadIdx.x; q < nwq; q += IH_T) hist[q] = 0;
+        __syncthreads();
+        for (int p = p0 + wv; p < p1; p += IH_T / 64) {
+            const int c = perm[p];
+            i64 b, e;
+            cell_range<DENSE>(indptr, c, G, b, e);
+            u32 pos = 0;
+            i64* bp = bnd + (size_t)p * (ntile + 1);
+            i64 kb = b, ke = e;
+            if (win > 0) {  // counting only: this window's entries
                 if (DENSE) {
-                    gs[u] = k < ke ? (int)(k - b) : -1;
-                    gps[u] = -1;
+                    kb = b + clo;
+                    ke = b + chi;
                 } else {
-                    const int r = rows[kc];
-                    const int rp = rows[kc > b ? kc - 1 : b];
-                    gs[u] = k < ke ? r : -1;
-                    gps[u] = (k < ke && k > b) ? rp : -1;
+                    kb = wave_lower_bound(rows, b, e, clo);
+                    ke = wave_lower_bound(rows, kb, e, chi);
                 }
+            } else if (!DENSE && rng) {
+                kb = wave_lower_bound(rows, b, e, t0r * gt);
+                ke = wave_lower_bound(rows, kb, e, t1r * gt);
             }
+            for (i64 k0 = kb; k0 < ke; k0 += 4 * 64) {  // four loads in flight per lane
+                double xs[4];
+                int gs[4], gps[4];
+                // clamped unconditional loads + select (a load under a lane
+                // condition becomes a branch with its own wait, one load at a time)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const i64 k = k0 + u * 64 + lane;
-                if (k >= ke) break;
-                const double x = xs[u];
-                const int g = gs[u];
-                const bool gok = (g >= 0) & (g < G);
-                bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
-                pos += (x > 0.0);
-                if (want_expm1) se = dd_add_d(se, expm1(x));
-                if (a >= 0 && x != 0.0 && g >= glo && g < ghi) atomicAdd(&hist[g], 1u);
-                if (!DENSE && a >= 0) {
-                    // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
-                    const int gp = gps[u];
-                    if (k > b && gp >= g) bad |= 4;
-                    const int tp = (gp < 0) ? -1 : min(gp / gt, ntile - 1);
-                    const int tg = gok ? g / gt : (g < 0 ? -1 : ntile - 1);
-                    for (int t = tp + 1; t <= tg; ++t) bp[t] = k;
+                for (int u = 0; u < 4; ++u) {
+                    const i64 k = k0 + u * 64 + lane;
+                    const i64 kc = k < ke ? k : ke - 1;  // k0 < ke, so ke - 1 >= b
+                    const double x = vals[kc];
+                    xs[u] = k < ke ? x : 0.0;
+                    if (DENSE) {
+                        gs[u] = k < ke ? (int)(k - b) : -1;
+                        gps[u] = -1;
+                    } else {
+                        const int r = rows[kc];
+                        const int rp = rows[kc > b ? kc - 1 : b];
+                        gs[u] = k < ke ? r : -1;
+                        gps[u] = (k < ke && k > b) ? rp : -1;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const i64 k = k0 + u * 64 + lane;
+                    if (k >= ke) break;
+                    const double x = xs[u];
+                    const int g = gs[u];
+                    if (a >= 0 && x != 0.0 && g >= clo && g < chi) {
+                        const u32 l = (u32)(g - wlo);
+                        const u32 q = (u32)(((u64)l * mq) >> 40);
+                        atomicAdd(&hist[l - q * nwq], 1u << (8 * q));
+                    }
+                    if (win > 0) continue;
+                    const bool gok = (g >= 0) & (g < G);
+                    bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
+                    pos += (x > 0.0);
+                    if (want_expm1) se = dd_add_d(se, expm1(x));
+                    if (!DENSE && a >= 0) {
+                        // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
+                        const int gp = gps[u];
+                        if (k > b && gp >= g) bad |= 4;
+                        const int tp = (gp < 0) ? -1 : min(gp / gt, ntile - 1);
+                        const int tg = gok ? g / gt : (g < 0 ? -1 : ntile - 1);
+                        for (int t = tp + 1; t <= tg; ++t) bp[t] = k;
+                    }
                 }
             }
+            if (win > 0) continue;
+            if (!DENSE && a >= 0) {
+                // tiles after the last entry read (and every tile of an empty cell) end
+                // at ke (= e, or in rng mode the first entry past tile t1r - 1)
+                const int gl = (ke > b) ? rows[ke - 1] : -1;
+                const int tl = (gl < 0) ? -1 : min(gl / gt, ntile - 1);
+                const int tend = rng ? t1r : ntile;
+                for (int t = tl + 1 + lane; t <= tend; t += 64) bp[t] = ke;
+            }
+            pos = u32_wave_sum(pos);
+            if (lane == 0 && !rng) nodg[c] = (int)pos;
         }
-        if (!DENSE && a >= 0) {
-            // tiles after the last entry read (and every tile of an empty cell) end
-            // at ke (= e, or in rng mode the first entry past tile t1r - 1)
-            const int gl = (ke > b) ? rows[ke - 1] : -1;
-            const int tl = (gl < 0) ? -1 : min(gl / gt, ntile - 1);
-            const int tend = rng ? t1r : ntile;
-            for (int t = tl + 1 + lane; t <= tend; t += 64) bp[t] = ke;
+        if (a < 0) break;  // unkept chunk: side work only (one pass)
+        __syncthreads();
+        u32* row = cnt + (size_t)ch * G;
+        for (int g = wlo + threadIdx.x; g < whi; g += IH_T) {
+            const u32 l = (u32)(g - wlo);
+            const u32 q = (u32)(((u64)l * mq) >> 40);
+            row[g] = (hist[l - q * nwq] >> (8 * q)) & 0xFFu;  // genes outside [glo, ghi) count 0
         }
-        pos = u32_wave_sum(pos);
-        if (lane == 0 && !rng) nodg[c] = (int)pos;
+        __syncthreads();
     }
     if (want_expm1) {
         se = dd_wave_sum(se);
         if (lane == 0) wave_expm1[blockIdx.x * (IH_T / 64) + wv] = se;
     }
     if (bad) atomicOr(err, bad);
-    if (a < 0) return;
-    __syncthreads();
-    u32* row = cnt + (size_t)ch * G;
-    for (int g = threadIdx.x; g < G; g += IH_T) row[g] = hist[g];
 }
 
 // per gene: exclusive prefix over the count chunks (in place); rows >= nc_kept
@@ -490,21 +528,32 @@ __global__ void k_reduce_dd(const dd* __restrict__ parts, int n, dd* __restrict_
 // ------------------------------------------------------------ host launchers
 extern "C" int scc_ingest_gene_tile(void) { return SC_GT; }
 
+// genes per histogram window: 4 per LDS word, at most 160 KB of words
+// (SCC_HIST_WINDOW overrides it, a test knob for the windowed path)
+extern "C" int scc_ingest_hist_window(int G)
+{
+    const char* v = getenv("SCC_HIST_WINDOW");
+    const int forced = (v && *v) ? atoi(v) : 0;
+    const int cap = forced > 0 ? std::min(forced, 4 * 40960) : 4 * 40960;
+    return std::max(1, std::min(G, cap));
+}
+
 extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows, const double* vals,
                                              const double* dense, int G, const int* perm, const int* cc_p0,
                                              const int* cc_code, int nc, int ntile, u32* cnt, i64* bnd, int* nodg,
                                              dd* wave_expm1, int want_expm1, int glo, int ghi, int rng, int* err,
                                              hipStream_t st)
 {
-    const size_t lds = sizeof(u32) * (size_t)G;
+    const int hw = scc_ingest_hist_window(G);
+    const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
     if (dense) {
         hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw, err);
     } else {
         hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, err);
     }
     return hipGetLastError();
 }

@@ -26,10 +26,10 @@ constexpr int kCapMedium = 16384;  // rank work item in LDS, 1024 threads (cappe
                                    // larger genes are split into value buckets
 constexpr int kCountChunk = 32;    // cells per ingest count chunk (one cluster each)
 constexpr int kScatterCC = 4;      // count chunks per ingest scatter chunk
-constexpr int kMaxGenesLds = 40960;  // ingest histogram of one chunk lives in LDS
 constexpr int kSelectCap = 2048;   // per-pair records sorted in LDS
 constexpr int kUnionCap = 4096;
-constexpr int kMaxK = SCC_MAX_K;  // 7-bit cluster codes in the rank kernels
+constexpr int kMaxK = SCC_MAX_K;  // 7-bit cluster codes in the rank kernels: clusters per engine run
+constexpr int kGroupMax = 64;     // K > 2 * kGroupMax: group-pair runs of <= 2 * kGroupMax clusters
 
 struct Timer {
     double ms = 0.0;
@@ -121,6 +121,7 @@ struct scc_de_result {
     const double *d_p = nullptr, *d_q = nullptr, *d_lfc = nullptr;
     const long long* d_u2 = nullptr;
     const uint8_t* d_de = nullptr;
+    bool vectors = true;  // d_p / d_lfc / d_u2 hold the [P][G] vectors (a FAST group-pair run: test_all only)
 };
 
 namespace scc_rt {
@@ -158,6 +159,36 @@ inline int ws_get(scc_ctx* c, const char* name, size_t bytes, void** out)
     if (hipMalloc(&p, grow) != hipSuccess) {
         hipGetLastError();
         return fail(c, SCC_ERR_OOM, std::string("hipMalloc failed for workspace ") + name);
+    }
+    c->ws[name] = {p, grow};
+    *out = p;
+    return SCC_OK;
+}
+
+// grow-only named workspace buffer whose first `used` bytes survive a growth
+inline int ws_keep(scc_ctx* c, const char* name, size_t bytes, size_t used, void** out)
+{
+    auto it = c->ws.find(name);
+    if (it != c->ws.end() && it->second.second >= bytes) {
+        *out = it->second.first;
+        return SCC_OK;
+    }
+    const size_t grow = std::max<size_t>(256, bytes + bytes / 2);
+    void* p = nullptr;
+    if (hipMalloc(&p, grow) != hipSuccess) {
+        hipGetLastError();
+        return fail(c, SCC_ERR_OOM, std::string("hipMalloc failed for workspace ") + name);
+    }
+    if (it != c->ws.end()) {
+        if (used && hipMemcpyAsync(p, it->second.first, used, hipMemcpyDeviceToDevice, c->s0) != hipSuccess) {
+            hipGetLastError();
+            hipFree(p);
+            return fail(c, SCC_ERR_HIP, std::string("workspace growth copy failed for ") + name);
+        }
+        hipStreamSynchronize(c->s0);
+        hipStreamSynchronize(c->s1);
+        hipFree(it->second.first);
+        c->ws.erase(it);
     }
     c->ws[name] = {p, grow};
     *out = p;

@@ -154,6 +154,7 @@ struct ScSelectLaunch {
 
 extern "C" {
 int scc_ingest_gene_tile(void);
+int scc_ingest_hist_window(int G);
 hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
                                   int G, const int* perm, const int* cc_p0, const int* cc_code, int nc, int ntile,
                                   uint32_t* cnt, long long* bnd, int* nodg, dd* wave_expm1, int want_expm1, int glo,
@@ -204,4 +205,8 @@ size_t scc_select_key_bytes(void);
 hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_t st);
 hipError_t scc_launch_union(const unsigned long long* first_occ, int G, void* scratch, int cap, int* out,
                             int* n_out, hipStream_t st);
+hipError_t scc_launch_seg_copy(const void* src, void* dst, int elem_bytes, const long long* seg, long long nseg,
+                               hipStream_t st);
+hipError_t scc_launch_first_remap(const unsigned long long* local, int G, const long long* lp2gp,
+                                  unsigned long long* global, hipStream_t st);
 }

@@ -9,6 +9,7 @@
 #include "scc_internal.hpp"
 
 #include <cstring>
+#include <memory>
 
 using namespace scc_rt;
 
@@ -355,7 +356,10 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (prm->test != SCC_TEST_WILCOX && (prm->test != SCC_TEST_T || prm->mode != SCC_DE_FAST))
         return fail(c, SCC_ERR_INVALID, "test: SCC_TEST_WILCOX, or SCC_TEST_T with SCC_DE_FAST");
     if (K < 2) return fail(c, SCC_ERR_INVALID, "need at least two clusters");
-    if (K > kMaxK) return fail(c, SCC_ERR_UNSUPPORTED, "K > 128 clusters is not supported by this build");
+    if (K > kMaxK)
+        return fail(c, SCC_ERR_UNSUPPORTED,
+                    "K > 128 clusters: one engine run holds 128 (scc_de_run cuts larger K into group-pair runs; "
+                    "the gene-shard entry points do not)");
     hipSetDevice(c->device);
     const int G = (int)ds->G, N = (int)ds->N, P = K * (K - 1) / 2;
     const bool fast = prm->mode == SCC_DE_FAST;
@@ -371,7 +375,6 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         // ComputePairWiseDE: min.cells.group = 3 (Fast:76,208-213)
         if (fast && nclu[a] < 3) return fail(c, SCC_ERR_RSTOP, "cluster has fewer than 3 cells (R stop())");
     }
-    if (G > kMaxGenesLds) return fail(c, SCC_ERR_UNSUPPORTED, "more than 40960 genes is not supported by this build");
     if (glo64 < 0 || ghi64 > G || glo64 > ghi64) return fail(c, SCC_ERR_INVALID, "gene shard out of range");
     const int glo = (int)glo64, ghi = (int)ghi64;
     const int64_t GK = (int64_t)G * K;
@@ -981,10 +984,279 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
 #undef WS
 }
 
+// ---------------------------------------------------------------- any K
+// More clusters than one engine run ranks (7-bit codes, 128): the K clusters
+// are cut into ng = ceil(K / gmax) groups of balanced size (gmax = 64, or
+// SCC_GROUP_SIZE), and the engine runs once per group pair (u < v) on the cells
+// of those <= 128 clusters (the others get code -1).  Every per-pair quantity
+// of both DE paths depends on the pair's two clusters alone (FAST: pct,
+// log-mean logFC, filters, test, BH over the pair's own rows, top_n,
+// Fast:229-392; SLOW: test, mean difference, gate with the GLOBAL threshold of
+// every entry -- the same in every run, since the ingest sums expm1 over all
+// cells whatever their code --, BH with n = G, first 30, slow:36,90-227), so a
+// global pair (i, j) is taken from exactly one run: the run of its two groups,
+// or for a pair inside one group the first run holding that group.  A run's
+// clusters keep the global order, so Cluster1 / Cluster2 orientation and the
+// within-run pair order are the global ones.  Rows (FAST) and per-pair vectors
+// are moved into the global (i, j) order on the device (k_seg_copy); the
+// union is unique() over the pairs' top lists in (i, j) order, i.e. genes by
+// their smallest (pair, rank) key: each run's keys are renumbered to global
+// pairs and MIN-folded (k_first_remap), then ordered once (k_union).
+static int de_run_grouped(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
+                          int gmax, scc_de_result** out)
+{
+    *out = nullptr;
+    const bool fast = prm->mode == SCC_DE_FAST;
+    if (prm->mode != SCC_DE_FAST && prm->mode != SCC_DE_SLOW) return fail(c, SCC_ERR_INVALID, "bad mode");
+    const int64_t G = ds->G, N = ds->N;
+    const int64_t P = (int64_t)K * (K - 1) / 2;
+    if (P >= ((int64_t)1 << 31)) return fail(c, SCC_ERR_UNSUPPORTED, "more than 2^31 cluster pairs");
+    {
+        std::vector<int64_t> n(K, 0);
+        for (int64_t i = 0; i < N; ++i) {
+            const int a = code[i];
+            if (a < -1 || a >= K) return fail(c, SCC_ERR_INVALID, "code out of range");
+            if (a >= 0) n[a]++;
+        }
+        for (int a = 0; a < K; ++a) {
+            if (n[a] == 0) return fail(c, SCC_ERR_INVALID, "empty cluster");
+            if (fast && n[a] < 3) return fail(c, SCC_ERR_RSTOP, "cluster has fewer than 3 cells (R stop())");
+        }
+    }
+    hipSetDevice(c->device);
+    hipStream_t s0 = c->s0;
+    const int ng = (K + gmax - 1) / gmax;
+    std::vector<int> gid(K);
+    std::vector<std::vector<int>> grp(ng);
+    for (int u = 0; u < ng; ++u)
+        for (int a = (int)((int64_t)u * K / ng); a < (int)((int64_t)(u + 1) * K / ng); ++a) {
+            grp[u].push_back(a);
+            gid[a] = u;
+        }
+    const bool vectors = !fast || prm->test_all;  // the dense [P][G] per-pair vectors
+    const size_t PG = (size_t)P * (size_t)G;
+    int rc;
+    double *g_p = nullptr, *g_lfc = nullptr, *g_q = nullptr;
+    long long* g_u2 = nullptr;
+    uint8_t* g_de = nullptr;
+    unsigned long long* g_first = nullptr;
+#define WSG(name, n, ptr)                                       \
+    do {                                                        \
+        if ((rc = ws(c, name, (size_t)(n), &(ptr)))) return rc; \
+    } while (0)
+    WSG("grp_first", G, g_first);
+    if (vectors) {
+        WSG("grp_p", PG, g_p);
+        WSG("grp_lfc", PG, g_lfc);
+        WSG("grp_u2", PG, g_u2);
+        if (!fast) {
+            WSG("grp_q", PG, g_q);
+            WSG("grp_de", PG, g_de);
+        }
+    }
+    HIPCHK(c, hipMemsetAsync(g_first, 0xFF, sizeof(unsigned long long) * G, s0));
+    // FAST rows: staged in run order (grow-preserving buffers), then gathered
+    // into the global pair order at the end
+    struct RowField {
+        const char* stage;
+        const char* fin;
+        int es;
+    };
+    static const RowField rf[9] = {{"grp_s_gene", "grp_row_gene", 4}, {"grp_s_p", "grp_row_p", 8},
+                                   {"grp_s_q", "grp_row_q", 8},       {"grp_s_lfc", "grp_row_lfc", 8},
+                                   {"grp_s_pct1", "grp_row_pct1", 8}, {"grp_s_pct2", "grp_row_pct2", 8},
+                                   {"grp_s_u2", "grp_row_u2", 8},     {"grp_s_t", "grp_row_t", 8},
+                                   {"grp_s_flags", "grp_row_flags", 1}};
+    int64_t staged = 0;
+    std::vector<int64_t> st_off(fast ? P : 0, 0), st_cnt(fast ? P : 0, 0);
+    std::vector<char> covered(ng, 0);
+    std::vector<int32_t> sub(N);
+    std::vector<long long> lp2gp, seg;
+    bool rstop = false;
+    std::string rstop_msg;
+    double log_thr = 0.0;
+    for (int u = 0; u < ng; ++u)
+        for (int v = u + 1; v < ng; ++v) {
+            std::vector<int> cl(grp[u]);
+            cl.insert(cl.end(), grp[v].begin(), grp[v].end());
+            const int Kl = (int)cl.size();
+            std::vector<int> lut(K, -1);
+            for (int l = 0; l < Kl; ++l) lut[cl[l]] = l;
+            for (int64_t i = 0; i < N; ++i) sub[i] = code[i] >= 0 ? lut[code[i]] : -1;
+            scc_de_result* r = nullptr;
+            rc = de_run_impl(c, ds, sub.data(), Kl, prm, DE_FULL, 0, G, nullptr, &r);
+            if (rc) {
+                if (rc != SCC_ERR_RSTOP || !r) {
+                    scc_de_result_destroy(r);
+                    return rc;
+                }
+                rstop = true;
+                rstop_msg = c->err;
+            }
+            log_thr = r->log_thr;
+            const int Pl = Kl * (Kl - 1) / 2;
+            lp2gp.assign(Pl, 0);
+            std::vector<char> take(Pl, 0);
+            {
+                int lp = 0;
+                for (int li = 0; li < Kl; ++li)
+                    for (int lj = li + 1; lj < Kl; ++lj, ++lp) {
+                        const int64_t gi = cl[li], gj = cl[lj];
+                        lp2gp[lp] = gi * K - gi * (gi + 1) / 2 + (gj - gi - 1);
+                        take[lp] = gid[gi] != gid[gj] || !covered[gid[gi]];
+                    }
+            }
+            covered[u] = covered[v] = 1;
+            long long *d_lp2gp = nullptr, *d_seg = nullptr;
+            unsigned long long* d_first = nullptr;
+            WSG("grp_lp2gp", Pl, d_lp2gp);
+            WSG("first", G, d_first);  // the run's per-gene first-occurrence keys
+            HIPCHK(c, hipMemcpyAsync(d_lp2gp, lp2gp.data(), sizeof(long long) * Pl, hipMemcpyHostToDevice, s0));
+            HIPCHK(c, scc_launch_first_remap(d_first, (int)G, d_lp2gp, g_first, s0));
+            if (vectors) {  // per-pair [G] vectors: one segment per taken pair
+                seg.clear();
+                for (int lp = 0; lp < Pl; ++lp)
+                    if (take[lp]) {
+                        seg.push_back((long long)lp * G);
+                        seg.push_back(lp2gp[lp] * G);
+                        seg.push_back(G);
+                    }
+                const long long ns = (long long)seg.size() / 3;
+                WSG("grp_seg", seg.size(), d_seg);
+                HIPCHK(c, hipMemcpyAsync(d_seg, seg.data(), sizeof(long long) * seg.size(), hipMemcpyHostToDevice, s0));
+                HIPCHK(c, scc_launch_seg_copy(r->d_p, g_p, 8, d_seg, ns, s0));
+                HIPCHK(c, scc_launch_seg_copy(r->d_lfc, g_lfc, 8, d_seg, ns, s0));
+                HIPCHK(c, scc_launch_seg_copy(r->d_u2, g_u2, 8, d_seg, ns, s0));
+                if (!fast) {
+                    HIPCHK(c, scc_launch_seg_copy(r->d_q, g_q, 8, d_seg, ns, s0));
+                    HIPCHK(c, scc_launch_seg_copy(r->d_de, g_de, 1, d_seg, ns, s0));
+                }
+                HIPCHK(c, hipStreamSynchronize(s0));  // d_seg is rewritten by the next segment table
+            }
+            if (fast) {  // the taken pairs' rows, appended to the staging buffers
+                seg.clear();
+                int64_t lo = 0, add = 0;
+                for (int lp = 0; lp < Pl; ++lp) {
+                    const int64_t n = r->pair_tested[lp];
+                    if (take[lp] && n > 0) {
+                        seg.push_back(lo);
+                        seg.push_back(staged + add);
+                        seg.push_back(n);
+                    }
+                    if (take[lp]) {
+                        st_off[lp2gp[lp]] = staged + add;
+                        st_cnt[lp2gp[lp]] = n;
+                        add += n;
+                    }
+                    lo += n;
+                }
+                const long long ns = (long long)seg.size() / 3;
+                if (ns > 0) {
+                    WSG("grp_seg", seg.size(), d_seg);
+                    HIPCHK(c, hipMemcpyAsync(d_seg, seg.data(), sizeof(long long) * seg.size(), hipMemcpyHostToDevice,
+                                             s0));
+                    const void* src[9] = {r->d_row_gene, r->d_row_p,  r->d_row_q,  r->d_row_lfc, r->d_row_pct1,
+                                          r->d_row_pct2, r->d_row_u2, r->d_row_t, r->d_row_flags};
+                    for (int f = 0; f < 9; ++f) {
+                        void* dst = nullptr;
+                        if ((rc = ws_keep(c, rf[f].stage, (size_t)(staged + add) * rf[f].es, (size_t)staged * rf[f].es,
+                                          &dst)))
+                            return rc;
+                        HIPCHK(c, scc_launch_seg_copy(src[f], dst, rf[f].es, d_seg, ns, s0));
+                    }
+                    HIPCHK(c, hipStreamSynchronize(s0));
+                }
+                staged += add;
+            }
+            scc_de_result_destroy(r);
+        }
+    scc_de_result* r = new scc_de_result();
+    r->ctx = c;
+    r->mode = prm->mode;
+    r->K = K;
+    r->P = (int)P;
+    r->G = G;
+    r->N = N;
+    r->log_thr = log_thr;
+    std::unique_ptr<scc_de_result> hold(r);
+    if (fast) {  // staged rows -> the global (i, j) order
+        r->pair_tested.resize(P);
+        seg.clear();
+        int64_t row = 0;
+        for (int64_t p = 0; p < P; ++p) {
+            r->pair_tested[p] = (int32_t)st_cnt[p];
+            if (st_cnt[p] > 0) {
+                seg.push_back(st_off[p]);
+                seg.push_back(row);
+                seg.push_back(st_cnt[p]);
+            }
+            row += st_cnt[p];
+        }
+        r->n_rows = row;
+        const long long ns = (long long)seg.size() / 3;
+        long long* d_seg = nullptr;
+        WSG("grp_seg", std::max<size_t>(seg.size(), 3), d_seg);
+        if (ns > 0)
+            HIPCHK(c, hipMemcpyAsync(d_seg, seg.data(), sizeof(long long) * seg.size(), hipMemcpyHostToDevice, s0));
+        void* fin[9];
+        for (int f = 0; f < 9; ++f) {
+            if ((rc = ws_get(c, rf[f].fin, (size_t)std::max<int64_t>(row, 1) * rf[f].es, &fin[f]))) return rc;
+            void* stg = nullptr;
+            if ((rc = ws_keep(c, rf[f].stage, (size_t)std::max<int64_t>(staged, 1) * rf[f].es, (size_t)staged * rf[f].es,
+                              &stg)))
+                return rc;
+            HIPCHK(c, scc_launch_seg_copy(stg, fin[f], rf[f].es, d_seg, ns, s0));
+        }
+        r->d_row_gene = (const int*)fin[0];
+        r->d_row_p = (const double*)fin[1];
+        r->d_row_q = (const double*)fin[2];
+        r->d_row_lfc = (const double*)fin[3];
+        r->d_row_pct1 = (const double*)fin[4];
+        r->d_row_pct2 = (const double*)fin[5];
+        r->d_row_u2 = (const long long*)fin[6];
+        r->d_row_t = (const long long*)fin[7];
+        r->d_row_flags = (const uint8_t*)fin[8];
+    }
+    r->d_p = g_p;
+    r->d_lfc = g_lfc;
+    r->d_u2 = g_u2;
+    r->d_q = g_q;
+    r->d_de = g_de;
+    r->vectors = vectors;
+    {  // the union: genes ordered by their smallest global (pair, rank) key
+        void* d_key = nullptr;
+        int *d_union = nullptr, *d_nu = nullptr, *d_nodg = nullptr;
+        if ((rc = ws_get(c, "key_scratch", (size_t)G * scc_select_key_bytes(), &d_key))) return rc;
+        WSG("union", G, d_union);
+        WSG("nu", 4, d_nu);
+        WSG("nodg", N, d_nodg);  // every run wrote the same nodg (clustering-independent)
+        HIPCHK(c, scc_launch_union(g_first, (int)G, d_key, env_int("SCC_UNION_CAP", kUnionCap), d_union, d_nu, s0));
+        int nu = 0;
+        HIPCHK(c, hipMemcpyAsync(&nu, d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
+        HIPCHK(c, hipStreamSynchronize(s0));
+        if (nu < 0 || nu > G) return fail(c, SCC_ERR_HIP, "union size out of range");
+        r->union_genes.resize(nu);
+        if (nu) HIPCHK(c, hipMemcpy(r->union_genes.data(), d_union, sizeof(int) * nu, hipMemcpyDeviceToHost));
+        r->d_nodg = d_nodg;
+    }
+    r->generation = c->generation;
+    *out = hold.release();
+    if (rstop) return fail(c, SCC_ERR_RSTOP, rstop_msg);
+    return SCC_OK;
+#undef WSG
+}
+
 extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
                           const scc_de_params* prm, scc_de_result** out)
 {
-    return de_run_impl(c, ds, code, K, prm, DE_FULL, 0, ds ? ds->G : 0, nullptr, out);
+    if (!c || !ds || !code || !prm || !out) return fail(c, SCC_ERR_INVALID, "scc_de_run: null argument");
+    *out = nullptr;
+    if (ds->ctx != c) return fail(c, SCC_ERR_INVALID, "dataset belongs to another context");
+    // SCC_GROUP_SIZE (test knob): group-pair runs of groups <= this size as
+    // soon as K exceeds two groups (default 64: K > 128)
+    const int gmax = std::min(std::max(env_int("SCC_GROUP_SIZE", kGroupMax), 1), kGroupMax);
+    if (K > 2 * gmax) return de_run_grouped(c, ds, code, K, prm, gmax, out);
+    return de_run_impl(c, ds, code, K, prm, DE_FULL, 0, ds->G, nullptr, out);
 }
 
 extern "C" int64_t scc_de_shard_bytes(int32_t K, int64_t n_genes)
@@ -1147,6 +1419,8 @@ extern "C" int scc_de_result_pair_vectors(const scc_de_result* r, double* p, dou
     if (rc) return rc;
     scc_ctx* c = r->ctx;
     const size_t n = (size_t)r->P * (size_t)r->G;
+    if (!r->vectors && (p || lfc || u2))
+        return fail(c, SCC_ERR_INVALID, "per-pair vectors of a FAST group-pair run exist with test_all = 1 only");
     if ((rc = d2h(c, p, r->d_p, n))) return rc;
     if ((rc = d2h(c, lfc, r->d_lfc, n))) return rc;
     if ((rc = d2h(c, (long long*)u2, r->d_u2, n))) return rc;

@@ -89,9 +89,7 @@ def _de_large(name, n_genes_sample, seed, dist_pairs=0):
     K = len(names)
     eng = nat.Engine(0)
     ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
-    from scconsensus_amd import grouped
-    assert grouped.runs_for(K) == 1  # K <= 128: ONE engine run (config E included)
-    g = grouped.de_fast_grouped(eng, ds, code, K)
+    g = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows")  # K <= 128: ONE engine run (config E included)
     r = g.rows
     P = K * (K - 1) // 2
     n = np.bincount(code[code >= 0], minlength=K).astype(np.int64)

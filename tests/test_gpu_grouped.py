@@ -1,6 +1,8 @@
-"""More than 64 clusters on the GPU in ONE engine run (7-bit cluster codes;
-BASELINE config E has K = 100), against one oracle run over all K; and the
-group-pair orchestration (grouped.py, for K > 128) against the native run.
+"""Many clusters on the GPU, each through ONE scc_de_run call: up to 128 in
+one engine run (7-bit cluster codes; BASELINE config E has K = 100), and any
+K beyond that through the group-pair runs inside libscc (de_run_grouped),
+against one oracle run over all K; plus gene counts past one LDS histogram
+window (G = 50,000 and forced small windows).
 
 Covered routes: the wave kernel's second mask register (clusters 64..127)
 and its 1024-pair windows (genes tested by > 1024 pairs), the items'
@@ -11,7 +13,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from scconsensus_amd import api, grouped, synth
+from scconsensus_amd import api, synth
 from test_gpu_de import _dense_stretch_matrix, _fast_compare, _slow_compare
 
 pytestmark = pytest.mark.gpu
@@ -54,33 +56,84 @@ def test_many_clusters_dense_value_stretch(eng, frac):
     _fast_compare(eng, ds, X, code, len(names), min_per_cent=1.0, log_fc_thrs=0.0)
 
 
-def test_128_clusters_and_the_limit(eng):
-    from scconsensus_amd import _native as nat
+def test_129_clusters_one_call(eng):
+    """K = 129: the smallest K past one engine run (3 group-pair runs)."""
     d = synth.generate("A", G=60, N=9000, K=129, seed=29)
     names, code = api.select_clusters(d.labels, 10)
     assert len(names) == 129
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
-    with pytest.raises(nat.SccError) as e:
-        eng.de_run(ds, code, 129, nat.SCC_DE_FAST, fetch="rows")
-    assert e.value.code == nat.SCC_ERR_UNSUPPORTED
-    c128 = np.where(code == 128, -1, code).astype(np.int32)  # drop the last cluster: K = 128
+    _fast_compare(eng, ds, d.dense(), code, 129)
+    c128 = np.where(code == 128, -1, code).astype(np.int32)  # drop the last cluster: K = 128, one run
     _fast_compare(eng, ds, d.dense(), c128, 128, min_per_cent=5.0, log_fc_thrs=0.2)
-    # K = 129 through the group-pair runs (3 runs of <= 128 clusters)
-    g = grouped.de_fast_grouped(eng, ds, code, 129)
-    o = O.de_fast(d.dense(), code, 129)
-    np.testing.assert_array_equal(g.rows.gene, o.row_gene)
-    np.testing.assert_array_equal(g.rows.u2, np.round(2 * o.row_W).astype(np.int64))
-    np.testing.assert_array_equal(g.union, o.union)
 
 
-def test_grouped_runs_equal_native(eng):
-    d = synth.generate("A", G=160, N=5000, K=70, seed=17)
+def test_fast_150_clusters_one_call(eng):
+    d = synth.generate("A", G=60, N=12000, K=150, seed=31)
+    names, code = api.select_clusters(d.labels, 10)
+    assert len(names) == 150
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g, o = _fast_compare(eng, ds, d.dense(), code, 150, min_per_cent=5.0, log_fc_thrs=0.2)
+    assert len(o.row_gene) > 100_000 and len(o.union) > 30
+
+
+def test_slow_150_clusters_one_call(eng):
+    d = synth.generate("A", G=24, N=12000, K=150, seed=37)
+    names, code = api.select_clusters(d.labels, 10)
+    assert len(names) == 150
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g, o = _slow_compare(eng, ds, d.dense(), code, 150)
+    assert g.p.shape == (150 * 149 // 2, 24) and len(o.union) > 0
+
+
+@pytest.mark.parametrize("mode", ["fast", "slow"])
+def test_grouped_runs_equal_native(eng, mode, monkeypatch):
+    """SCC_GROUP_SIZE=32 forces group-pair runs at K = 70 (3 groups): bit for
+    bit the one-run result."""
+    from scconsensus_amd import _native as nat
+    d = synth.generate("A", G=160 if mode == "fast" else 40, N=5000, K=70, seed=17)
     names, code = api.select_clusters(d.labels, 10)
     K = len(names)
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
-    from scconsensus_amd import _native as nat
-    nat_r = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows")
-    g = grouped.de_fast_grouped(eng, ds, code, K, group=32, min_k=0)
-    for f in ("pair_tested", "gene", "p", "q", "u2", "ties", "top"):
-        np.testing.assert_array_equal(getattr(g.rows, f), getattr(nat_r.rows, f), err_msg=f)
-    np.testing.assert_array_equal(g.union, nat_r.union)
+    m = nat.SCC_DE_FAST if mode == "fast" else nat.SCC_DE_SLOW
+    kw = dict(min_per_cent=5.0, log_fc_thrs=0.1) if mode == "fast" else dict(q_val_thrs=0.05, fc_thrs=1.5)
+    one = eng.de_run(ds, code, K, m, fetch="all", **kw)
+    monkeypatch.setenv("SCC_GROUP_SIZE", "32")
+    grp = eng.de_run(ds, code, K, m, fetch="all", **kw)
+    np.testing.assert_array_equal(grp.union, one.union)
+    np.testing.assert_array_equal(grp.nodg, one.nodg)
+    for f in ("p", "logfc", "u2") + (("q", "de") if mode == "slow" else ()):
+        np.testing.assert_array_equal(getattr(grp, f), getattr(one, f), err_msg=f)
+    if mode == "fast":
+        for f in ("pair_tested", "gene", "p", "q", "avg_logfc", "pct1", "pct2", "u2", "ties", "de", "top"):
+            np.testing.assert_array_equal(getattr(grp.rows, f), getattr(one.rows, f), err_msg=f)
+        u = eng.de_run(ds, code, K, m, fetch="union", **kw)  # no per-pair vectors kept
+        np.testing.assert_array_equal(u.union, one.union)
+    else:
+        assert grp.log_thr == one.log_thr
+
+
+def test_50000_genes(eng):
+    """G = 50,000 (was refused past 40,960: one LDS histogram window per
+    chunk; now 8-bit counters, 163,840 genes per window)."""
+    d = synth.generate("A", G=50_000, N=1200, K=6, seed=41)
+    names, code = api.select_clusters(d.labels, 10)
+    X = d.dense()
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    g, o = _fast_compare(eng, ds, X, code, len(names))
+    assert len(o.union) > 30
+    np.testing.assert_array_equal(g.nodg, O.nodg(X))
+    _slow_compare(eng, ds, X, code, len(names))
+
+
+@pytest.mark.parametrize("window", ["100", "777"])
+def test_histogram_windows(eng, window, monkeypatch):
+    """Forced small gene windows (several histogram passes per count chunk),
+    CSC and dense input, FAST and SLOW: the oracle's results."""
+    monkeypatch.setenv("SCC_HIST_WINDOW", window)
+    d = synth.generate("A", G=1000, N=1500, K=6, seed=43)
+    names, code = api.select_clusters(d.labels, 10)
+    X = d.dense()
+    for ds in (eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N), eng.dataset_dense(X)):
+        g, _ = _fast_compare(eng, ds, X, code, len(names))
+        np.testing.assert_array_equal(g.nodg, O.nodg(X))
+        _slow_compare(eng, ds, X, code, len(names))
