@@ -45,7 +45,7 @@ extern "C" {
 #define SCC_ERR_OOM 3         /* device allocation failed */
 #define SCC_ERR_NONFINITE 4   /* input holds NaN/Inf or out-of-range row index */
 #define SCC_ERR_RSTOP 5       /* the reference R code would stop() on this input */
-#define SCC_ERR_UNSUPPORTED 6 /* valid input outside this build's limits (e.g. K > 64) */
+#define SCC_ERR_UNSUPPORTED 6 /* valid input outside this build's limits (e.g. ncomp > 16) */
 
 #define SCC_DE_FAST 0 /* reclusterDEConsensusFast(method = "wilcox") */
 #define SCC_DE_SLOW 1 /* reclusterDEConsensus(method = "Wilcoxon") */
@@ -63,9 +63,13 @@ typedef struct scc_dataset scc_dataset;
 typedef struct scc_de_result scc_de_result;
 
 typedef struct {
-    int32_t device;      /* HIP device ordinal */
+    int32_t device;      /* HIP device ordinal (the context's only device when n_devices <= 1) */
     int32_t profile;     /* 1: time the dominant kernels with HIP events */
-    int32_t reserved[6];
+    int32_t n_devices;   /* > 1: ONE job over the devices devices[0 .. n_devices) (SURVEY 8b's device
+                            list; replaces the reference's nCores PSOCK workers, Fast:61-65,384) */
+    int32_t reserved[5];
+    const int32_t* devices; /* n_devices HIP ordinals, devices[0] the primary (a repeated ordinal runs
+                               several engines on one device: the sharded path on one GPU) */
 } scc_opts;
 
 typedef struct {
@@ -82,10 +86,36 @@ typedef struct {
 } scc_de_params;
 
 /* ---- context ---------------------------------------------------------- */
+/* With a device list (opts.n_devices > 1) the context drives every device of
+ * the list from this one host process (one host thread per device inside
+ * each call; peer copies over xGMI between them):
+ *   scc_dataset_create_*  uploads to devices[0] and replicates the matrix on
+ *                         the others (peer copies; a repeated ordinal shares it)
+ *   scc_de_run            gene row-blocks balanced by stored values, one per
+ *                         device, their tested-cell records gathered on
+ *                         devices[0], which runs the per-pair selection: the
+ *                         result equals the one-device run bit for bit
+ *                         (K > 128: every group-pair run is sharded this way)
+ *   scc_distance(_cols)   the PCA on devices[0], its N x 16 scores copied to
+ *                         every device, each device the packed columns of an
+ *                         equal share of the entries, streamed straight to
+ *                         the caller's host buffer or copied into its device
+ *                         buffer (bit for bit the one-device output; the
+ *                         Pearson metric runs on devices[0] only)
+ * Every other entry point works on devices[0].  Results and outputs live on
+ * devices[0]. */
 SCC_API int scc_ctx_create(const scc_opts* opts, scc_ctx** out);
+/* number of visible HIP devices (0 when none) */
+SCC_API int scc_device_count(int32_t* n);
 SCC_API void scc_ctx_destroy(scc_ctx* ctx);
 SCC_API const char* scc_ctx_last_error(const scc_ctx* ctx);
 SCC_API int scc_ctx_synchronize(scc_ctx* ctx);
+/* Launch the engine's work on the caller's stream (a hipStream_t of the
+ * context's device; external = 1, the legacy default stream NULL included)
+ * instead of its own non-blocking one (external = 0: back to its own).  A
+ * caller whose buffers come from a framework stream (torch) then needs no host
+ * synchronisation between its own work, its collectives and the engine. */
+SCC_API int scc_ctx_set_stream(scc_ctx* ctx, void* stream, int32_t external);
 /* Kernel timing (opts.profile = 1): total ms and launch count of a named
  * kernel family since the last reset ("gene_rank", "dist", "gram", ...). */
 SCC_API int scc_ctx_kernel_time(const scc_ctx* ctx, const char* name, double* total_ms, int64_t* launches);

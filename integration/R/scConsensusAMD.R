@@ -75,6 +75,8 @@ reclusterDEConsensusFast <- function(dataMatrix, consensusClusterLabels, method 
   # "roc" need Seurat helpers the reference never loads
   if (!(method %in% c("wilcox", "t"))) stop("Unknown test: ", method)
   sel <- .scc_codes(consensusClusterLabels, dataMatrix, minClusterSize)
+  # nCores PSOCK workers (Fast:61-65) -> min(nCores, GPUs) devices of ONE sharded job
+  .Call("C_scc_devices", as.integer(nCores))
   h <- .scc_dataset(dataMatrix)
   on.exit(.Call("C_scc_release", h), add = TRUE)
   res <- .Call("C_scc_de_fast", h, sel$code, length(sel$clusters),

@@ -13,6 +13,7 @@
  *   C_scc_de_slow   R/reclusterDEConsensus.R:32-227
  *   C_scc_distance  R/reclusterDEConsensusFast.R:398-400 (prcomp_irlba + dist), :403 (1 - cor)
  *   C_scc_release   frees the device copy early (the finalizer does it otherwise)
+ *   C_scc_devices   nCores (Fast:33,61-65) -> the context's device list
  */
 #include <R.h>
 #include <Rinternals.h>
@@ -23,13 +24,43 @@
 #include "scc.h"
 
 static scc_ctx* g_ctx = NULL;
+static int g_ndev = 1;  /* devices of g_ctx: 0 .. g_ndev - 1 */
 
 static void ensure_ctx(void)
 {
     if (g_ctx) return;
     scc_opts o;
     memset(&o, 0, sizeof(o));
+    int32_t devs[64];
+    if (g_ndev > 1) {
+        for (int k = 0; k < g_ndev; ++k) devs[k] = k;
+        o.n_devices = g_ndev;
+        o.devices = devs;
+    }
     if (scc_ctx_create(&o, &g_ctx) != SCC_OK) Rf_error("scConsensus engine: no MI355X (HIP) device available");
+}
+
+/* nCores (Fast:33, the PSOCK workers of Fast:61-65) -> the engine's device
+ * list: min(nCores, visible GPUs) devices, ONE job sharded over them (gene
+ * blocks for the DE, column slices for dist).  Recreates the context when
+ * the count changes (datasets of the old context must be released first:
+ * the wrappers hold one only inside a call). */
+SEXP C_scc_devices(SEXP n_cores)
+{
+    int32_t nvis = 0;
+    scc_device_count(&nvis);
+    if (nvis < 1) Rf_error("scConsensus engine: no MI355X (HIP) device available");
+    int want = Rf_asInteger(n_cores);
+    if (want == NA_INTEGER || want < 1) want = 1;
+    if (want > nvis) want = nvis;
+    if (want > 64) want = 64;
+    if (g_ctx && want != g_ndev) {
+        scc_ctx_destroy(g_ctx);
+        g_ctx = NULL;
+    }
+    g_ndev = want;
+    ensure_ctx();
+    return Rf_ScalarInteger(want);
 }
 
 static void check(int rc)
@@ -204,8 +235,11 @@ SEXP C_scc_distance(SEXP h, SEXP genes, SEXP metric, SEXP ncomp)
 }
 
 /* mean(summary(cluster::silhouette(groups, as.matrix(d)))$clus.avg.widths)
- * (Fast:433) on the engine-kept output of the last C_scc_distance call; NA
- * when R's silhouette returns NA (fewer than 2 or as many groups as cells). */
+ * (Fast:433) on the engine-kept output of the last C_scc_distance call.
+ * R's silhouette() returns NA for fewer than 2 groups or as many groups as
+ * cells, and summary(NA)$clus.avg.widths then stops ("$ operator is invalid
+ * for atomic vectors"): the same stop here.  Any other failure (no kept
+ * distance of this size, a HIP error) is an error too, never a silent NA. */
 SEXP C_scc_si(SEXP groups)
 {
     ensure_ctx();
@@ -215,11 +249,12 @@ SEXP C_scc_si(SEXP groups)
     double* avg = (double*)R_alloc((size_t)N, sizeof(double));
     int32_t ng = 0;
     int rc = scc_silhouette(g_ctx, N, g, NULL, 0, NULL, avg, &ng);
-    if (rc == SCC_ERR_INVALID) return Rf_ScalarReal(NA_REAL);
+    if (rc == SCC_ERR_INVALID && ng > 0 && (ng < 2 || ng >= N))
+        Rf_error("$ operator is invalid for atomic vectors");
     check(rc);
     double s = 0.0;
     for (int k = 0; k < ng; ++k) s += avg[k];
-    return Rf_ScalarReal(ng > 0 ? s / ng : NA_REAL);
+    return Rf_ScalarReal(s / ng);
 }
 
 static const R_CallMethodDef call_methods[] = {
@@ -229,6 +264,7 @@ static const R_CallMethodDef call_methods[] = {
     {"C_scc_de_slow", (DL_FUNC)&C_scc_de_slow, 6},
     {"C_scc_distance", (DL_FUNC)&C_scc_distance, 4},
     {"C_scc_si", (DL_FUNC)&C_scc_si, 1},
+    {"C_scc_devices", (DL_FUNC)&C_scc_devices, 1},
     {NULL, NULL, 0}};
 
 /* the package is scConsensus (NAMESPACE: useDynLib(scConsensus, .registration = TRUE)) */

@@ -34,7 +34,8 @@ SCC_PTR_DEVICE = 1
 
 # every symbol include/scc.h declares (tests check the library exports them all)
 EXPORTS = [
-    "scc_ctx_create", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_kernel_time",
+    "scc_ctx_create", "scc_device_count", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_set_stream",
+    "scc_ctx_kernel_time",
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_csr", "scc_dataset_create_dense", "scc_dataset_destroy",
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_run_shard_records",
     "scc_de_finish_records", "scc_de_finish_records_pairs", "scc_de_union_first_occ", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
@@ -52,7 +53,8 @@ class SccError(RuntimeError):
 
 
 class Opts(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int32), ("profile", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+    _fields_ = [("device", ctypes.c_int32), ("profile", ctypes.c_int32), ("n_devices", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5), ("devices", ctypes.POINTER(ctypes.c_int32))]
 
 
 class DeParams(ctypes.Structure):
@@ -92,9 +94,11 @@ def load():
     i32, i64, dbl, u8 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_uint8
     sig = {
         "scc_ctx_create": (ctypes.c_int, [P(Opts), P(vp)]),
+        "scc_device_count": (ctypes.c_int, [P(i32)]),
         "scc_ctx_destroy": (None, [vp]),
         "scc_ctx_last_error": (ctypes.c_char_p, [vp]),
         "scc_ctx_synchronize": (ctypes.c_int, [vp]),
+        "scc_ctx_set_stream": (ctypes.c_int, [vp, vp, i32]),
         "scc_ctx_kernel_time": (ctypes.c_int, [vp, ctypes.c_char_p, P(dbl), P(i64)]),
         "scc_ctx_reset_timers": (None, [vp]),
         "scc_dataset_create_csc": (ctypes.c_int, [vp, vp, vp, vp, i64, i64, i64, i32, P(vp)]),
@@ -192,13 +196,24 @@ class Dataset:
             pass
 
 
-class Engine:
-    """One MI355X device (``device`` = HIP ordinal)."""
+def device_count() -> int:
+    n = ctypes.c_int32()
+    load().scc_device_count(ctypes.byref(n))
+    return n.value
 
-    def __init__(self, device: int = 0, profile: bool = False):
+
+class Engine:
+    """One MI355X device (``device`` = HIP ordinal), or ONE job over a device
+    list (``devices``: HIP ordinals, devices[0] the primary; scc_opts.devices)."""
+
+    def __init__(self, device: int = 0, profile: bool = False, devices=None):
         self.lib = load()
         h = ctypes.c_void_p()
         o = Opts(device, 1 if profile else 0)
+        if devices is not None and len(devices) > 1:
+            self._devs = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+            o.n_devices = len(devices)
+            o.devices = self._devs
         rc = self.lib.scc_ctx_create(ctypes.byref(o), ctypes.byref(h))
         if rc != SCC_OK:
             raise SccError(rc, "scc_ctx_create failed (no HIP device?)")
@@ -510,6 +525,27 @@ class Engine:
 
     def synchronize(self):
         self._check(self.lib.scc_ctx_synchronize(self.ctx))
+
+    def set_stream(self, stream_handle):
+        """Launch on the caller's HIP stream (an int handle, e.g. torch's
+        ``torch.cuda.current_stream().cuda_stream``; 0 is the legacy default
+        stream); ``None``: back to the engine's own stream."""
+        self._check(self.lib.scc_ctx_set_stream(self.ctx, ctypes.c_void_p(stream_handle or None),
+                                                0 if stream_handle is None else 1))
+
+    def on_stream(self, stream_handle):
+        """Context manager: the engine's work goes on ``stream_handle`` inside."""
+        eng = self
+
+        class _On:
+            def __enter__(self):
+                eng.set_stream(stream_handle)
+                return eng
+
+            def __exit__(self, *exc):
+                eng.set_stream(None)
+                return False
+        return _On()
 
 
 # ---------------------------------------------------------------- host clustering

@@ -138,7 +138,9 @@ def _hclust_ward_d2(dist_packed, N):
 def _dynamic_colors(tree, dist_packed, deepSplitValues, minClusterSize, eng=None, info=None):
     """Fast:418-431: cutreeDynamic(dendro, distM = as.matrix(d), deepSplit = dsv,
     pamStage = FALSE, minClusterSize) -> labels2colors, named "deepsplit: dsv".
-    With ``eng`` and a list ``info``: the reference's deepSplitInfo rows
+    With ``eng`` (FAST, which computes the silhouette for every deepSplit):
+    R's stop when a deepSplit yields < 2 groups; with a list ``info`` too, the
+    reference's deepSplitInfo rows
     (Fast:433: DeepSplit, NumbersOfClusters, SI = mean of
     summary(cluster::silhouette(groups, as.matrix(d)))$clus.avg.widths), the
     silhouette computed by the engine on its HBM-resident copy of d."""
@@ -147,11 +149,16 @@ def _dynamic_colors(tree, dist_packed, deepSplitValues, minClusterSize, eng=None
     for dsv in deepSplitValues:
         lab, _ = nat.cutree_hybrid(tree["merge"], tree["height"], dist_packed, int(dsv), int(minClusterSize))
         out[f"deepsplit: {dsv}"] = labels2colors(lab)
-        if eng is not None and info is not None:
+        if eng is not None:
             lab = np.asarray(lab, np.int32)
             k = len(np.unique(lab))
-            si = float(np.mean(eng.silhouette(N, lab)[1])) if 2 <= k < N else float("nan")  # R: NA otherwise
-            info.append({"DeepSplit": dsv, "NumbersOfClusters": k, "SI": si})
+            if not 2 <= k < N:
+                # silhouette() returns NA and summary(NA)$clus.avg.widths stops (Fast:433)
+                raise RuntimeError("$ operator is invalid for atomic vectors (silhouette of "
+                                   f"{k} group(s) at deepSplit {dsv}, Fast:433)")
+            if info is not None:  # the SI the reference computes and discards
+                info.append({"DeepSplit": dsv, "NumbersOfClusters": k,
+                             "SI": float(np.mean(eng.silhouette(N, lab)[1]))})
     return out
 
 

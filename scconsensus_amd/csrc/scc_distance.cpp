@@ -171,6 +171,88 @@ static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi,
     return SCC_OK;
 }
 
+// Device list (scc_opts.n_devices > 1): the packed columns [col_lo, col_hi)
+// cut into one slice of equal entry count per device (distance
+// row/column blocks per GPU).  Every device gets the N x 16 scores (xGMI peer
+// copy) and writes its slice with the same kernel, so the output is the
+// one-device output bit for bit: straight into the caller's host buffer
+// (each device streams its own slice through its own staging), or into the
+// device output on devices[0] (peer copies of the other slices).  With host
+// output devices[0] keeps only its own slice of the engine-kept copy; the
+// others stay on their devices until scc_silhouette needs them
+// (last_dist_pending).
+static int dist_multi(scc_ctx* c, const double* d_P, int N, int64_t col_lo, int64_t col_hi, void* d_out,
+                      void* dist_out, int32_t out_kind, int32_t out_f32)
+{
+    const int D = 1 + (int)c->peers.size();
+    const size_t es = out_f32 ? 4 : 8;
+    auto colbase = [&](int64_t j) { return (size_t)j * (2 * (size_t)N - j - 1) / 2; };
+    const size_t base0 = colbase(col_lo), total = colbase(col_hi) - base0;
+    std::vector<int64_t> cut(D + 1, col_lo);
+    cut[D] = col_hi;
+    for (int d = 1; d < D; ++d) {  // first column whose packed start reaches d/D of the entries
+        int64_t j = cut[d - 1];
+        while (j < col_hi && colbase(j) - base0 < total * d / D) ++j;
+        cut[d] = j;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->s0));  // the scores exist before the peers copy them
+    std::vector<int> rcs(D, SCC_OK);
+    std::vector<void*> slice(D, nullptr);
+    std::vector<std::thread> th;
+    for (int d = 0; d < D; ++d)
+        th.emplace_back([&, d] {
+            scc_ctx* x = d ? c->peers[d - 1] : c;
+            hipSetDevice(x->device);
+            const int64_t a = cut[d], b = cut[d + 1];
+            const size_t off = colbase(a) - base0, n = colbase(b) - colbase(a);
+            const double* P = d_P;
+            auto run = [&]() -> int {
+                int rc;
+                if (d) {  // the scores on this device
+                    double* xp = nullptr;
+                    if ((rc = ws(x, "d_P", (size_t)N * 16, &xp))) return rc;
+                    if (x->device == c->device)
+                        HIPCHK(x, hipMemcpyAsync(xp, d_P, sizeof(double) * N * 16, hipMemcpyDeviceToDevice, x->s0));
+                    else
+                        HIPCHK(x, hipMemcpyPeerAsync(xp, x->device, d_P, c->device, sizeof(double) * N * 16, x->s0));
+                    P = xp;
+                }
+                if (a == b) return SCC_OK;
+                auto emit = [&](int64_t ca, int64_t cb, void* dst) {
+                    return scc_launch_dist_euclid(P, N, (int)ca, (int)cb, dst, out_f32, x->s0);
+                };
+                Scope sc(x, "dist", x->s0);
+                void* mine = (char*)d_out + off * es;  // devices[0]: straight into the output / kept copy
+                if (d) {
+                    if ((rc = ws_get(x, "d_dist", std::max<size_t>(n, 1) * es, &mine))) return rc;
+                    slice[d] = mine;
+                }
+                if (out_kind == SCC_PTR_HOST)
+                    return stream_to_host(x, N, a, b, es, (char*)mine, (char*)dist_out + off * es, emit);
+                HIPCHK(x, emit(a, b, mine));
+                if (d) {  // device output on devices[0]
+                    if (x->device == c->device)
+                        HIPCHK(x, hipMemcpyAsync((char*)d_out + off * es, mine, n * es, hipMemcpyDeviceToDevice, x->s0));
+                    else
+                        HIPCHK(x, hipMemcpyPeerAsync((char*)d_out + off * es, c->device, mine, x->device, n * es, x->s0));
+                }
+                HIPCHK(x, hipStreamSynchronize(x->s0));
+                return SCC_OK;
+            };
+            rcs[d] = run();
+        });
+    for (auto& t : th) t.join();
+    hipSetDevice(c->device);
+    for (int d = 0; d < D; ++d)
+        if (rcs[d]) return d ? fail(c, rcs[d], c->peers[d - 1]->err) : rcs[d];
+    if (out_kind == SCC_PTR_HOST)
+        for (int d = 1; d < D; ++d)
+            if (cut[d + 1] > cut[d])
+                c->last_dist_pending.push_back({c->peers[d - 1]->device, slice[d], colbase(cut[d]) - base0,
+                                                colbase(cut[d + 1]) - colbase(cut[d])});
+    return SCC_OK;
+}
+
 // columns [col_lo, col_hi) of the packed output (the whole matrix: [0, N))
 static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
                      int32_t ncomp, int64_t col_lo, int64_t col_hi, void* dist_out, int32_t out_kind, int32_t out_f32)
@@ -188,6 +270,8 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
     hipSetDevice(c->device);
     hipStream_t s0 = c->s0;
+    c->d_last_dist = nullptr;  // set again only when this call succeeds (the workspace may move)
+    c->last_dist_pending.clear();
     const int ld = (nu + 63) & ~63;
     const int Npad = (N + 15) & ~15;
     if (col_lo < 0 || col_hi > N || col_lo > col_hi) return fail(c, SCC_ERR_INVALID, "column slice out of range");
@@ -292,7 +376,9 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         auto emit = [&](int64_t a, int64_t b, void* dst) {
             return scc_launch_dist_euclid(d_P, N, (int)a, (int)b, dst, out_f32, s0);
         };
-        {
+        if (!c->peers.empty()) {
+            if ((rc = dist_multi(c, d_P, N, col_lo, col_hi, d_out, dist_out, out_kind, out_f32))) return rc;
+        } else {
             Scope sc(c, "dist", s0);
             if (out_kind == SCC_PTR_HOST) {
                 if ((rc = stream_to_host(c, N, col_lo, col_hi, out_f32 ? 4 : 8, (char*)d_out, (char*)dist_out, emit)))
@@ -327,13 +413,13 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     }
     // what scc_silhouette(dist = NULL) reads: only an output the engine owns
     // (a caller's device buffer may be freed or reused after this call)
+    HIPCHK(c, hipStreamSynchronize(s0));
+    if (metric == SCC_DIST_PCA_EUCLID && c->eig_err)
+        return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
     const bool own = out_kind == SCC_PTR_HOST || !dist_out;
     c->d_last_dist = (own && col_lo == 0 && col_hi == N) ? d_out : nullptr;
     c->last_dist_n = N;
     c->last_dist_f32 = out_f32 ? 1 : 0;
-    HIPCHK(c, hipStreamSynchronize(s0));
-    if (metric == SCC_DIST_PCA_EUCLID && c->eig_err)
-        return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
     return SCC_OK;
 #undef WS
 }
@@ -522,6 +608,8 @@ extern "C" int scc_distance_scores(scc_ctx* c, const void* scores, int64_t N64, 
     if (col_lo < 0 || col_hi > N || col_lo > col_hi) return fail(c, SCC_ERR_INVALID, "column slice out of range");
     hipSetDevice(c->device);
     hipStream_t s0 = c->s0;
+    c->d_last_dist = nullptr;  // set again only when this call succeeds
+    c->last_dist_pending.clear();
     auto colbase = [&](int64_t j) { return (size_t)j * (2 * (size_t)N - j - 1) / 2; };
     const size_t npairs = colbase(col_hi) - colbase(col_lo);
     const size_t es = out_f32 ? 4 : 8;
@@ -539,11 +627,11 @@ extern "C" int scc_distance_scores(scc_ctx* c, const void* scores, int64_t N64, 
             HIPCHK(c, emit(col_lo, col_hi, d_out));
         }
     }
+    HIPCHK(c, hipStreamSynchronize(s0));
     const bool own = out_kind == SCC_PTR_HOST || !dist_out;
     c->d_last_dist = (own && col_lo == 0 && col_hi == N) ? d_out : nullptr;
     c->last_dist_n = N;
     c->last_dist_f32 = out_f32 ? 1 : 0;
-    HIPCHK(c, hipStreamSynchronize(s0));
     return SCC_OK;
 }
 
@@ -560,6 +648,16 @@ extern "C" int scc_silhouette(scc_ctx* c, int64_t n_cells, const int32_t* groups
             return fail(c, SCC_ERR_INVALID, "scc_silhouette: no full scc_distance output of this size is kept");
         D = c->d_last_dist;
         f32 = c->last_dist_f32;
+        const size_t es = f32 ? 4 : 8;
+        hipSetDevice(c->device);
+        for (const auto& sl : c->last_dist_pending) {  // peer slices of a device-list distance
+            char* dst = (char*)c->d_last_dist + sl.off * es;
+            if (sl.dev == c->device)
+                HIPCHK(c, hipMemcpyAsync(dst, sl.ptr, sl.n * es, hipMemcpyDeviceToDevice, c->s0));
+            else
+                HIPCHK(c, hipMemcpyPeerAsync(dst, c->device, sl.ptr, sl.dev, sl.n * es, c->s0));
+        }
+        c->last_dist_pending.clear();
     }
     // cluster codes in increasing id order (silhouette's sorted clusters)
     std::vector<int32_t> ids(groups, groups + N);

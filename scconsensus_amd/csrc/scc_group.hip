@@ -40,6 +40,25 @@ __global__ void __launch_bounds__(256) k_first_remap(const u64* __restrict__ loc
     if (gk < global[g]) atomicMin((unsigned long long*)&global[g], (unsigned long long)gk);
 }
 
+// stored values per gene row of a CSC (the device list's gene-block weights)
+__global__ void __launch_bounds__(256) k_row_hist(const int* __restrict__ rows, long long nnz, int G,
+                                                  unsigned int* __restrict__ cnt)
+{
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < nnz; k += (long long)gridDim.x * 256) {
+        const int r = rows[k];
+        if (r >= 0 && r < G) atomicAdd(&cnt[r], 1u);
+    }
+}
+
+extern "C" hipError_t scc_launch_row_hist(const int* rows, long long nnz, int G, unsigned int* cnt, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(unsigned int) * (size_t)G, st);
+    if (e != hipSuccess || nnz <= 0) return e;
+    const unsigned grid = (unsigned)std::min<long long>((nnz + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_row_hist, dim3(grid), dim3(256), 0, st, rows, nnz, G, cnt);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t scc_launch_seg_copy(const void* src, void* dst, int elem_bytes, const long long* seg,
                                           long long nseg, hipStream_t st)
 {

@@ -47,6 +47,7 @@ struct scc_ctx {
     int device = 0;
     int n_cu = 256;
     hipStream_t s0 = nullptr, s1 = nullptr;
+    hipStream_t own_s0 = nullptr;  // the context's own stream (s0 unless scc_ctx_set_stream)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     // workspace slots (grow-only)
@@ -82,6 +83,18 @@ struct scc_ctx {
     int pca_nu = 0, pca_ld = 0;
     int64_t pca_N = 0, pca_clo = 0, pca_chi = 0;
     int pca_stage = 0;  // 1 after colsum, 2 after gram
+    // device list (scc_opts.n_devices > 1): the engines of devices[1..], each
+    // with its own streams and workspace; this context is devices[0]'s
+    std::vector<scc_ctx*> peers;
+    // the last full distance kept on this device when its columns were
+    // written by several devices: peer slices not yet copied in (entries
+    // [off, off + n) of d_last_dist live at ptr on device dev)
+    struct Slice {
+        int dev;
+        const void* ptr;
+        size_t off, n;
+    };
+    std::vector<Slice> last_dist_pending;
 };
 
 struct scc_dataset {
@@ -100,6 +113,11 @@ struct scc_dataset {
     // from this device cache.  The data must not change while the dataset lives.
     mutable bool validated = false;
     mutable int* d_nodg = nullptr;  // [N], always owned
+    // device list: the replica on each peer engine of the context (same order
+    // as scc_ctx::peers), and the stored values per gene that balance the
+    // gene row-blocks (computed on the first sharded run)
+    std::vector<scc_dataset*> reps;
+    mutable std::vector<int64_t> gene_w;
 };
 
 struct scc_de_result {

@@ -207,6 +207,7 @@ hipError_t scc_launch_union(const unsigned long long* first_occ, int G, void* sc
                             int* n_out, hipStream_t st);
 hipError_t scc_launch_seg_copy(const void* src, void* dst, int elem_bytes, const long long* seg, long long nseg,
                                hipStream_t st);
+hipError_t scc_launch_row_hist(const int* rows, long long nnz, int G, unsigned int* cnt, hipStream_t st);
 hipError_t scc_launch_first_remap(const unsigned long long* local, int G, const long long* lp2gp,
                                   unsigned long long* global, hipStream_t st);
 }

@@ -10,26 +10,23 @@
 
 #include <cstring>
 #include <memory>
+#include <thread>
 
 using namespace scc_rt;
 
 // ====================================================================== ctx
-extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
+static int ctx_create_one(int device, bool profile, scc_ctx** out)
 {
-    if (!out) return SCC_ERR_INVALID;
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         hipGetLastError();
         return SCC_ERR_HIP;
     }
+    if (device < 0 || device >= ndev) return SCC_ERR_INVALID;
     scc_ctx* c = new scc_ctx();
-    c->device = opts ? opts->device : 0;
-    c->profile = opts ? (opts->profile != 0) : false;
-    if (c->device < 0 || c->device >= ndev) {
-        delete c;
-        return SCC_ERR_INVALID;
-    }
+    c->device = device;
+    c->profile = profile;
     if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->s0, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s1, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -38,6 +35,7 @@ extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
         delete c;
         return SCC_ERR_HIP;
     }
+    c->own_s0 = c->s0;
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) {
         hipGetLastError();
         c->n_cu = 256;
@@ -46,11 +44,55 @@ extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
     return SCC_OK;
 }
 
+extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
+{
+    if (!out) return SCC_ERR_INVALID;
+    *out = nullptr;
+    const bool profile = opts ? (opts->profile != 0) : false;
+    const int nd = (opts && opts->n_devices > 1) ? opts->n_devices : 1;
+    if (nd > 1 && !opts->devices) return SCC_ERR_INVALID;
+    const int dev0 = nd > 1 ? opts->devices[0] : (opts ? opts->device : 0);
+    scc_ctx* c = nullptr;
+    int rc = ctx_create_one(dev0, profile, &c);
+    if (rc) return rc;
+    for (int i = 1; i < nd; ++i) {
+        scc_ctx* p = nullptr;
+        if ((rc = ctx_create_one(opts->devices[i], profile, &p))) {
+            scc_ctx_destroy(c);
+            return rc;
+        }
+        c->peers.push_back(p);
+        if (p->device != c->device) {  // xGMI peer access both ways (already enabled is fine)
+            hipSetDevice(c->device);
+            if (hipDeviceEnablePeerAccess(p->device, 0) != hipSuccess) hipGetLastError();
+            hipSetDevice(p->device);
+            if (hipDeviceEnablePeerAccess(c->device, 0) != hipSuccess) hipGetLastError();
+        }
+    }
+    hipSetDevice(c->device);
+    *out = c;
+    return SCC_OK;
+}
+
+extern "C" int scc_device_count(int32_t* n)
+{
+    if (!n) return SCC_ERR_INVALID;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess) {
+        hipGetLastError();
+        nd = 0;
+    }
+    *n = nd;
+    return SCC_OK;
+}
+
 extern "C" void scc_distance_release(scc_ctx* c);
 
 extern "C" void scc_ctx_destroy(scc_ctx* c)
 {
     if (!c) return;
+    for (scc_ctx* p : c->peers) scc_ctx_destroy(p);
+    c->peers.clear();
     hipSetDevice(c->device);
     scc_distance_release(c);
     hipStreamSynchronize(c->s0);
@@ -65,7 +107,8 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     if (c->h_dstage) hipHostFree(c->h_dstage);
     hipEventDestroy(c->ev_fork);
     hipEventDestroy(c->ev_join);
-    hipStreamDestroy(c->s0);
+    hipStreamSynchronize(c->s0);
+    hipStreamDestroy(c->own_s0);
     hipStreamDestroy(c->s1);
     delete c;
 }
@@ -78,6 +121,20 @@ extern "C" int scc_ctx_synchronize(scc_ctx* c)
     hipSetDevice(c->device);
     HIPCHK(c, hipStreamSynchronize(c->s0));
     HIPCHK(c, hipStreamSynchronize(c->s1));
+    for (scc_ctx* p : c->peers) {
+        int rc = scc_ctx_synchronize(p);
+        if (rc) return fail(c, rc, p->err);
+    }
+    hipSetDevice(c->device);
+    return SCC_OK;
+}
+
+extern "C" int scc_ctx_set_stream(scc_ctx* c, void* stream, int32_t external)
+{
+    if (!c) return SCC_ERR_INVALID;
+    hipSetDevice(c->device);
+    HIPCHK(c, hipStreamSynchronize(c->s0));  // work already queued on the old stream first
+    c->s0 = external ? (hipStream_t)stream : c->own_s0;
     return SCC_OK;
 }
 
@@ -102,6 +159,70 @@ extern "C" void scc_ctx_reset_timers(scc_ctx* c)
 }
 
 // ====================================================================== dataset
+// device list: the dataset's replica on every peer engine (the same device:
+// its buffers borrowed; another device: owned copies over xGMI)
+static int replicate(scc_ctx* c, scc_dataset* d)
+{
+    for (scc_ctx* p : c->peers) {
+        scc_dataset* r = new scc_dataset();
+        r->ctx = p;
+        r->device = p->device;
+        r->G = d->G;
+        r->N = d->N;
+        r->nnz = d->nnz;
+        r->dense = d->dense;
+        d->reps.push_back(r);
+        if (p->device == c->device) {
+            r->d_indptr = d->d_indptr;
+            r->d_rows = d->d_rows;
+            r->d_vals = d->d_vals;
+            r->d_dense = d->d_dense;
+            r->owned = false;
+            continue;
+        }
+        r->owned = true;
+        hipSetDevice(p->device);
+        auto peer = [&](void** dst, const void* src, size_t bytes) {
+            if (hipMalloc(dst, std::max<size_t>(bytes, 8)) != hipSuccess) {
+                hipGetLastError();
+                *dst = nullptr;
+                return false;
+            }
+            if (bytes && hipMemcpyPeerAsync(*dst, p->device, src, c->device, bytes, p->s0) != hipSuccess) {
+                hipGetLastError();
+                return false;
+            }
+            return true;
+        };
+        bool ok = true;
+        if (d->dense) {
+            ok = peer((void**)&r->d_dense, d->d_dense, sizeof(double) * (size_t)d->G * d->N);
+        } else {
+            ok = peer((void**)&r->d_indptr, d->d_indptr, sizeof(long long) * (d->N + 1)) &&
+                 peer((void**)&r->d_rows, d->d_rows, sizeof(int) * d->nnz) &&
+                 peer((void**)&r->d_vals, d->d_vals, sizeof(double) * d->nnz);
+        }
+        if (!ok || hipStreamSynchronize(p->s0) != hipSuccess) {
+            hipGetLastError();
+            hipSetDevice(c->device);
+            return fail(c, SCC_ERR_OOM, "dataset replication to a peer device failed");
+        }
+    }
+    hipSetDevice(c->device);
+    return SCC_OK;
+}
+
+static int finish_create(scc_ctx* c, scc_dataset* d, scc_dataset** out)
+{
+    int rc = replicate(c, d);
+    if (rc) {
+        scc_dataset_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return SCC_OK;
+}
+
 extern "C" int scc_dataset_create_csc(scc_ctx* c, const int64_t* indptr, const int32_t* rows, const double* vals,
                                       int64_t G, int64_t N, int64_t nnz, int32_t kind, scc_dataset** out)
 {
@@ -140,8 +261,7 @@ extern "C" int scc_dataset_create_csc(scc_ctx* c, const int64_t* indptr, const i
             return fail(c, SCC_ERR_HIP, "dataset upload failed");
         }
     }
-    *out = d;
-    return SCC_OK;
+    return finish_create(c, d, out);
 }
 
 extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const int32_t* cols, const double* vals,
@@ -250,8 +370,7 @@ extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const i
         scc_dataset_destroy(d);
         return fail(c, SCC_ERR_HIP, std::string("CSR transpose failed: ") + hipGetErrorString(e));
     }
-    *out = d;
-    return SCC_OK;
+    return finish_create(c, d, out);
 }
 
 extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, int64_t N, int32_t kind,
@@ -282,13 +401,14 @@ extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, 
             return fail(c, SCC_ERR_HIP, "dataset upload failed");
         }
     }
-    *out = d;
-    return SCC_OK;
+    return finish_create(c, d, out);
 }
 
 extern "C" void scc_dataset_destroy(scc_dataset* d)
 {
     if (!d) return;
+    for (scc_dataset* r : d->reps) scc_dataset_destroy(r);
+    d->reps.clear();
     if (d->owned || d->d_nodg) {
         hipSetDevice(d->device);
         hipDeviceSynchronize();
@@ -984,6 +1104,109 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
 #undef WS
 }
 
+// ---------------------------------------------------------------- device list
+// ONE DE job over the context's devices (scc_opts.n_devices > 1; SURVEY 8e:
+// gene row-blocks, then a gather of compact per-(pair, tested gene) records):
+// each device runs the per-(pair, gene) stage of its gene block and packs its
+// tested cells (scc_de_record, 64 B) -- one host thread per device --, the
+// records are copied to devices[0] (xGMI peer copies) and the per-pair BH,
+// filters, top-N and union run there: the scc_de_finish_records result, equal
+// to the one-device run bit for bit.  Blocks are balanced by the genes'
+// stored values (a CSC row histogram, computed once per dataset).
+static int gene_blocks(scc_ctx* c, const scc_dataset* ds, int D, std::vector<int64_t>& cut)
+{
+    const int64_t G = ds->G;
+    cut.assign(D + 1, 0);
+    cut[D] = G;
+    if (!ds->dense && ds->gene_w.empty() && ds->nnz > 0) {
+        unsigned int* d_h = nullptr;
+        int rc = ws(c, "row_hist", (size_t)G, &d_h);
+        if (rc) return rc;
+        HIPCHK(c, scc_launch_row_hist(ds->d_rows, ds->nnz, (int)G, d_h, c->s0));
+        std::vector<unsigned int> h(G);
+        HIPCHK(c, hipMemcpyAsync(h.data(), d_h, sizeof(unsigned int) * G, hipMemcpyDeviceToHost, c->s0));
+        HIPCHK(c, hipStreamSynchronize(c->s0));
+        ds->gene_w.assign(h.begin(), h.end());
+    }
+    std::vector<double> cw(G + 1, 0.0);
+    for (int64_t g = 0; g < G; ++g) cw[g + 1] = cw[g] + (ds->gene_w.empty() ? 1.0 : 1.0 + (double)ds->gene_w[g]);
+    for (int d = 1; d < D; ++d) {
+        const double share = cw[G] * d / D;
+        int64_t g = std::lower_bound(cw.begin(), cw.end(), share) - cw.begin();
+        // non-empty blocks while genes last
+        g = std::max<int64_t>(g, std::min<int64_t>(G, cut[d - 1] + 1));
+        cut[d] = std::min<int64_t>(g, G);
+    }
+    return SCC_OK;
+}
+
+static int de_run_multi(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
+                        scc_de_result** out)
+{
+    *out = nullptr;
+    if (ds->reps.size() != c->peers.size()) return fail(c, SCC_ERR_INVALID, "dataset has no replica on every device");
+    const int D = 1 + (int)c->peers.size();
+    std::vector<scc_ctx*> eng{c};
+    std::vector<const scc_dataset*> dsr{ds};
+    for (size_t i = 0; i < c->peers.size(); ++i) {
+        eng.push_back(c->peers[i]);
+        dsr.push_back(ds->reps[i]);
+    }
+    hipSetDevice(c->device);
+    std::vector<int64_t> cut;
+    int rc = gene_blocks(c, ds, D, cut);
+    if (rc) return rc;
+    const int64_t P = (int64_t)K * (K - 1) / 2;
+    std::vector<int> rcs(D, SCC_OK);
+    std::vector<int64_t> nrec(D, 0);
+    std::vector<void*> rbuf(D, nullptr);
+    {
+        std::vector<std::thread> th;
+        for (int d = 0; d < D; ++d)
+            th.emplace_back([&, d] {
+                scc_ctx* x = eng[d];
+                hipSetDevice(x->device);
+                const int64_t cap = std::max<int64_t>(1, P * (cut[d + 1] - cut[d]));
+                if ((rcs[d] = ws_get(x, "mrec", (size_t)cap * sizeof(scc_de_record), &rbuf[d]))) return;
+                RecIO io;
+                io.out = rbuf[d];
+                io.cap = cap;
+                io.n_out = &nrec[d];
+                rcs[d] = de_run_impl(x, dsr[d], code, K, prm, DE_SHARD_REC, cut[d], cut[d + 1], nullptr, nullptr, &io);
+            });
+        for (auto& t : th) t.join();
+    }
+    hipSetDevice(c->device);
+    for (int d = 0; d < D; ++d)
+        if (rcs[d]) return d ? fail(c, rcs[d], eng[d]->err) : rcs[d];
+    const int64_t stride = std::max<int64_t>(1, *std::max_element(nrec.begin(), nrec.end()));
+    void* all = nullptr;
+    if ((rc = ws_get(c, "mrec_all", (size_t)D * stride * sizeof(scc_de_record), &all))) return rc;
+    for (int d = 0; d < D; ++d) {
+        if (!nrec[d]) continue;
+        char* dst = (char*)all + (size_t)d * stride * sizeof(scc_de_record);
+        const size_t bytes = (size_t)nrec[d] * sizeof(scc_de_record);
+        if (eng[d]->device == c->device)
+            HIPCHK(c, hipMemcpyAsync(dst, rbuf[d], bytes, hipMemcpyDeviceToDevice, c->s0));
+        else
+            HIPCHK(c, hipMemcpyPeerAsync(dst, c->device, rbuf[d], eng[d]->device, bytes, c->s0));
+    }
+    RecIO io;
+    io.in = all;
+    io.counts = nrec.data();
+    io.nblocks = D;
+    io.stride = stride;
+    return de_run_impl(c, ds, code, K, prm, DE_FINISH_REC, 0, ds->G, nullptr, out, &io);
+}
+
+// one engine run of <= 128 clusters: on the context's device, or sharded over its device list
+static int de_run_one(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
+                      scc_de_result** out)
+{
+    if (!c->peers.empty() && K <= kMaxK) return de_run_multi(c, ds, code, K, prm, out);
+    return de_run_impl(c, ds, code, K, prm, DE_FULL, 0, ds->G, nullptr, out);
+}
+
 // ---------------------------------------------------------------- any K
 // More clusters than one engine run ranks (7-bit codes, 128): the K clusters
 // are cut into ng = ceil(K / gmax) groups of balanced size (gmax = 64, or
@@ -1084,7 +1307,7 @@ static int de_run_grouped(scc_ctx* c, const scc_dataset* ds, const int32_t* code
             for (int l = 0; l < Kl; ++l) lut[cl[l]] = l;
             for (int64_t i = 0; i < N; ++i) sub[i] = code[i] >= 0 ? lut[code[i]] : -1;
             scc_de_result* r = nullptr;
-            rc = de_run_impl(c, ds, sub.data(), Kl, prm, DE_FULL, 0, G, nullptr, &r);
+            rc = de_run_one(c, ds, sub.data(), Kl, prm, &r);
             if (rc) {
                 if (rc != SCC_ERR_RSTOP || !r) {
                     scc_de_result_destroy(r);
@@ -1256,7 +1479,7 @@ extern "C" int scc_de_run(scc_ctx* c, const scc_dataset* ds, const int32_t* code
     // soon as K exceeds two groups (default 64: K > 128)
     const int gmax = std::min(std::max(env_int("SCC_GROUP_SIZE", kGroupMax), 1), kGroupMax);
     if (K > 2 * gmax) return de_run_grouped(c, ds, code, K, prm, gmax, out);
-    return de_run_impl(c, ds, code, K, prm, DE_FULL, 0, ds->G, nullptr, out);
+    return de_run_one(c, ds, code, K, prm, out);
 }
 
 extern "C" int64_t scc_de_shard_bytes(int32_t K, int64_t n_genes)

@@ -15,7 +15,7 @@ and owns:
 * PCA (Fast:398): a block of cells.  Column sums of X[U, block] (all-gather,
   combined in rank order), the centred partial Gram (all-reduce of |U| x |U|
   fp64), the eigensolve of the summed Gram on rank 0 (its vectors broadcast),
-  the block's scores (all-reduce of the disjoint N x 16 rows).
+  the block's scores (all-gather of the ranks' N/world x 16 row blocks).
 * dist (Fast:400): a packed-column slice of equal entry count, kept in its HBM
   (or streamed to pinned host memory).
 
@@ -24,7 +24,10 @@ follows it, so an error one rank alone sees (an R stop() on its genes, an
 OOM) raises on every rank instead of leaving the others blocked.
 
 The buffers are torch tensors: import torch (and let it load its HIP runtime)
-before ``scconsensus_amd._native`` loads ``libscc.so``.
+before ``scconsensus_amd._native`` loads ``libscc.so``.  The engine launches on
+torch's current stream while a sharded stage runs (``scc_ctx_set_stream``), so
+torch's fills and copies, the RCCL collectives and the engine's kernels are
+ordered by the stream alone, with no host synchronisation between them.
 """
 from __future__ import annotations
 
@@ -70,6 +73,17 @@ def _call(fn, *a, **kw):
         return None, int(e.code), str(e)
 
 
+def _on_stream(eng, device):
+    """The engine's work on torch's current stream of ``device`` (a GPU
+    engine; the CPU stand-ins of the gloo tests have no streams)."""
+    import contextlib
+
+    import torch
+    if getattr(device, "type", "cpu") != "cuda" or not hasattr(eng, "on_stream"):
+        return contextlib.nullcontext()
+    return eng.on_stream(torch.cuda.current_stream(device).cuda_stream)
+
+
 def _raise_if(codes, msg=""):
     codes = [int(c) for c in codes]
     if any(codes):
@@ -85,6 +99,11 @@ def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weig
     FAST with fetch="union" over > 1 rank (``pair_split``): each rank runs the
     selection of a block of pairs and the union comes from the MIN-combined
     first-occurrence keys (the result then carries the union only)."""
+    with _on_stream(eng, device):
+        return _de_sharded(eng, ds, code, K, dist, device, fetch, weights, exchange, pair_split, **params)
+
+
+def _de_sharded(eng, ds, code, K, dist, device, fetch, weights, exchange, pair_split, **params):
     import torch
 
     shard_kw = {k: v for k, v in params.items() if k in _SHARD_KEYS}
@@ -95,8 +114,6 @@ def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weig
         buf = torch.empty(nbytes // 8 + 1, dtype=torch.int64, device=device)
         _, st, msg = _call(eng.de_run_shard, ds, code, K, lo, hi, buf.data_ptr(), **shard_kw)
         buf[-1] = st  # the status rides in the last word: summed, nonzero iff some rank failed
-        if not st:
-            eng.synchronize()  # the engine's streams -> the collective's stream
         dist.all_reduce_sum_(buf)
         st_all = int(buf[-1].item())
         _raise_if([st_all], msg)
@@ -114,8 +131,6 @@ def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weig
         big[: cap * REC_WORDS] = buf
         buf = big
     recs = dist.all_gather_cat(buf[: stride * REC_WORDS])
-    if recs.is_cuda:
-        torch.cuda.synchronize(recs.device)
     if fetch == "union" and params.get("mode", 0) == 0 and dist.world > 1 and pair_split:
         # the pairs are independent until the union: each rank selects its
         # pairs; the genes' first-occurrence keys are combined by MIN
@@ -124,16 +139,12 @@ def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weig
         first = torch.empty(ds.G + 1, dtype=torch.int64, device=device)
         _, st, msg = _call(eng.de_finish_records_pairs, ds, code, K, recs.data_ptr(), counts, stride, plo, phi,
                            first.data_ptr(), **shard_kw)
-        if recs.is_cuda:
-            torch.cuda.synchronize(recs.device)  # the engine's stream -> the collective's
         keys = first[: ds.G]
         keys[keys == -1] = _I64_MAX  # unselected (all ones) sorts last under a signed MIN
         first[-1] = -st  # the status rides along: MIN = minus the largest error code
         dist.all_reduce_min_(first)
         _raise_if([-int(first[-1].item())], msg)
         keys[keys == _I64_MAX] = -1
-        if keys.is_cuda:
-            torch.cuda.synchronize(keys.device)
         union = eng.de_union_first_occ(keys.data_ptr(), ds.G)
         return nat.DeResult(nat.SCC_DE_FAST, K, P, union, np.zeros(0, np.int32))
     return eng.de_finish_records(ds, code, K, recs.data_ptr(), counts, stride, fetch=fetch, **shard_kw)
@@ -142,41 +153,56 @@ def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weig
 def pca_sharded(eng, ds, genes, dist: parallel.Dist, device, ncomp=0):
     """prcomp_irlba(t(X[genes, ]), n = min(|U|, 15), center = TRUE)$x (Fast:398)
     of one job over the ranks: returns the full N x 16 score matrix (torch,
-    float64, on ``device``; columns >= ncomp zero), identical on every rank."""
+    float64, on ``device``; columns >= ncomp zero), identical on every rank.
+    Every stage's status word rides in its collective; they are read back
+    once, at the end (one host round trip)."""
+    with _on_stream(eng, device):
+        return _pca_sharded(eng, ds, genes, dist, device, ncomp)
+
+
+def _pca_sharded(eng, ds, genes, dist, device, ncomp):
     import torch
 
     genes = np.ascontiguousarray(genes, np.int32)
     nu, N = len(genes), ds.N
     lo, hi = cell_shard(N, dist.rank, dist.world)
     f64 = dict(dtype=torch.float64, device=device)
+    msgs = []
+
+    def call(fn, *a):
+        _, st, m = _call(fn, *a)
+        if st:
+            msgs.append(m)
+        return st
+
     part = torch.zeros(2 * nu + 1, **f64)  # dd column sums + the status word
-    _, st, msg = _call(eng.pca_shard_colsum, ds, genes, lo, hi, part.data_ptr())
-    part[-1] = st
+    part[-1] = call(eng.pca_shard_colsum, ds, genes, lo, hi, part.data_ptr())
     parts = dist.all_gather_cat(part).view(dist.world, 2 * nu + 1)
-    _raise_if(parts[:, -1].cpu().numpy(), msg)
-    parts = parts[:, : 2 * nu].contiguous()
+    pcs = parts[:, : 2 * nu].contiguous()
     gram = torch.zeros(nu * nu + 1, **f64)
-    _, st, msg = _call(eng.pca_shard_gram, parts.data_ptr(), dist.world, gram.data_ptr())
-    gram[-1] = st
+    gram[-1] = call(eng.pca_shard_gram, pcs.data_ptr(), dist.world, gram.data_ptr())
     dist.all_reduce_sum_(gram)
-    _raise_if([gram[-1].item()], msg)
-    # the eigenvectors of rank 0, broadcast (a sum with zeros elsewhere): the
-    # hand-off eigensolver's partial sums follow how many workgroups joined, so
-    # per-rank eigensolves could differ in the last bits
+    # the eigenvectors of rank 0, broadcast (a sum with zeros elsewhere): ONE
+    # eigensolve, so every rank's score block comes from the same vectors
     vecs = torch.zeros(nu * 16 + 1, **f64)
     if dist.rank == 0:
-        _, st, msg = _call(eng.pca_shard_eigen, gram.data_ptr(), vecs.data_ptr(), ncomp)
-        vecs[-1] = st
+        vecs[-1] = call(eng.pca_shard_eigen, gram.data_ptr(), vecs.data_ptr(), ncomp)
     dist.all_reduce_sum_(vecs)
-    _raise_if([vecs[-1].item()], msg if dist.rank == 0 else "rank 0's eigensolve failed")
-    scores = torch.zeros(N * 16 + 1, **f64)
-    _, st, msg = _call(eng.pca_shard_project, vecs.data_ptr(), scores.data_ptr(), ncomp)
-    scores[-1] = st
-    dist.all_reduce_sum_(scores)  # disjoint row blocks: the sum is the exact union
-    _raise_if([scores[-1].item()], msg)
-    if scores.is_cuda:
-        torch.cuda.synchronize(scores.device)
-    return scores[: N * 16]
+    # this rank's rows, then an all-gather of equal-size blocks (a block holds
+    # at most `rows` cells: N / world rounded up) and the status word
+    rows = -(-N // dist.world)
+    full = torch.zeros(N * 16, **f64)
+    st = call(eng.pca_shard_project, vecs.data_ptr(), full.data_ptr(), ncomp)
+    blk = torch.zeros(rows * 16 + 1, **f64)
+    blk[: (hi - lo) * 16] = full[lo * 16: hi * 16]
+    blk[-1] = st
+    allb = dist.all_gather_cat(blk).view(dist.world, rows * 16 + 1)
+    status = torch.stack([parts[:, -1].max(), gram[-1], vecs[-1], allb[:, -1].max()]).cpu().numpy()
+    _raise_if(status, msgs[0] if msgs else "another rank's PCA stage failed")
+    for r in range(dist.world):
+        a, b = cell_shard(N, r, dist.world)
+        full[a * 16: b * 16] = allb[r, : (b - a) * 16]
+    return full
 
 
 def column_shard(N: int, rank: int, world: int) -> tuple[int, int]:
@@ -213,5 +239,6 @@ def distance_sharded(eng, ds, genes, dist: parallel.Dist, device=None, f32=False
     if scores is None:
         scores = pca_sharded(eng, ds, genes, dist, device, ncomp)
     lo, hi = column_shard(ds.N, dist.rank, dist.world)
-    out = eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, f32=f32, device_out_ptr=device_out_ptr)
+    with _on_stream(eng, device):
+        out = eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, f32=f32, device_out_ptr=device_out_ptr)
     return lo, hi, out

@@ -79,12 +79,16 @@ class Stand:
         part[0::2] = s
         part[1::2] = 0.0
     def pca_shard_gram(self, parts_ptr, world, gram_ptr):
+        if not hasattr(self, "genes"):  # the engine: SCC_ERR_INVALID "call scc_pca_shard_colsum first"
+            raise nat.SccError(1, "scc_pca_shard_gram: call scc_pca_shard_colsum first")
         nu = len(self.genes)
         parts = view(parts_ptr, world * 2 * nu, np.float64).reshape(world, 2 * nu)
         mean = (parts[:, 0::2] + parts[:, 1::2]).sum(axis=0) / self.ds.N
         self.Xc = self.ds.X[self.genes][:, self.lo:self.hi].T - mean
         view(gram_ptr, nu * nu, np.float64)[:] = (self.Xc.T @ self.Xc).ravel()
     def pca_shard_eigen(self, gram_ptr, vecs_ptr, ncomp):
+        if not hasattr(self, "Xc"):
+            raise nat.SccError(1, "scc_pca_shard_eigen: call scc_pca_shard_gram first")
         nu = len(self.genes)
         self.eigen_calls = getattr(self, "eigen_calls", 0) + 1
         if self.fail == "eigen":
@@ -95,6 +99,8 @@ class Stand:
         Z = view(vecs_ptr, nu * 16, np.float64).reshape(nu, 16)
         Z[:, :k] = V[:, ::-1][:, :k]
     def pca_shard_project(self, vecs_ptr, scores_ptr, ncomp):
+        if not hasattr(self, "Xc"):
+            raise nat.SccError(1, "scc_pca_shard_project: call scc_pca_shard_gram first")
         nu = len(self.genes)
         k = ncomp or min(nu, 15)
         Z = view(vecs_ptr, nu * 16, np.float64).reshape(nu, 16)
