@@ -124,3 +124,63 @@ def sample_cell_pairs(N, n, seed):
     b = rng.integers(0, N - 1, n)
     b = np.where(b >= a, b + 1, b)
     return np.maximum(a, b), np.minimum(a, b)
+
+
+def slow_gate(Xs, code, K, log_thr):
+    """The SLOW expression gate of genes ``Xs`` (dense rows over all cells),
+    [P][len(Xs)] bool: mean(x_i) > log(thr) | mean(x_j) > log(thr) with R's
+    long-double two-pass mean (slow:109-113)."""
+    m = np.array([[O.r_mean(x[code == a]) for a in range(K)] for x in Xs])  # [genes][K]
+    up = m > log_thr
+    return np.array([up[:, i] | up[:, j] for i, j in pair_list(K)])
+
+
+def slow_log_threshold(vals, G, N, mean_scaling_factor):
+    """log(meanScalingFactor * mean(expm1(X))) (slow:36) from the stored values
+    (zeros add expm1(0) = 0), R's LDOUBLE two-pass mean."""
+    e = np.expm1(np.asarray(vals, np.float64)).astype(np.longdouble)
+    tot = np.longdouble(G) * np.longdouble(N)
+    s = e.sum() / tot
+    t = (e - s).sum() + (tot - len(e)) * (-s)
+    s = s + t / tot
+    return float(np.log(np.longdouble(mean_scaling_factor) * np.longdouble(float(s))))
+
+
+def check_slow_selection(g, q_val_thrs, fc_thrs, gate=None, gate_genes=None):
+    """SLOW selection at FULL size from the engine's per-pair vectors [P][G]:
+    BH with n = G, NaN counted (slow:116-121); every DE flag implies q <
+    qValThrs & |logfc| > log(fcThrs) (slow:165-170) and, where ``gate`` is
+    given (for ``gate_genes``, default all), equals it exactly; the union of
+    the first 30 of sort(|logfc|, decreasing) per pair in (i, j) order
+    (slow:209-227)."""
+    P, G = g.p.shape
+    cut = np.log(fc_thrs)
+    cols = np.arange(G) if gate_genes is None else np.asarray(gate_genes)
+    union, seen = [], set()
+    for p in range(P):
+        q = O.p_adjust_bh(g.p[p], n=G)
+        np.testing.assert_allclose(g.q[p], q, rtol=1e-12, atol=0, equal_nan=True, err_msg=f"pair {p}: BH q (n = G)")
+        must = ~np.isnan(q) & (q < q_val_thrs) & (np.abs(g.logfc[p]) > cut)
+        de = g.de[p] == 1
+        assert not np.any(de & ~must), f"pair {p}: DE flag without q / logFC"
+        if gate is not None:
+            np.testing.assert_array_equal(de[cols], must[cols] & gate[p], err_msg=f"pair {p}: DE flags")
+        idx = np.flatnonzero(de)
+        o = np.argsort(-np.abs(g.logfc[p][idx]), kind="stable")
+        for gene in idx[o][:30]:
+            if gene not in seen:
+                seen.add(gene)
+                union.append(gene)
+    np.testing.assert_array_equal(g.union, np.array(union, np.int32))
+
+
+def check_slow_against_oracle_subset(g, Xs, genes, code, K, q_val_thrs, fc_thrs, msf):
+    """The oracle (orc_de_slow, slow:69-187) on a gene subset over ALL cells
+    and pairs: exact W, p and logFC within the bar (q and the gate depend on
+    all genes: check_slow_selection).  Returns the number of cells compared."""
+    o = O.de_slow(Xs, code, K, q_val_thrs, fc_thrs, msf)
+    genes = np.asarray(genes)
+    np.testing.assert_array_equal(g.u2[:, genes], np.round(2 * o.W).astype(np.int64), err_msg="2U")
+    np.testing.assert_allclose(g.p[:, genes], o.p, rtol=P_RTOL, atol=0, equal_nan=True, err_msg="p")
+    np.testing.assert_allclose(g.logfc[:, genes], o.lfc, rtol=1e-12, atol=5e-14, err_msg="logFC")
+    return o.p.size

@@ -13,11 +13,16 @@ import pytest
 import torch  # before the engine loads (torch's HIP runtime first)
 
 import oracle as O
-from parity_helpers import (check_rows_against_oracle_subset, check_selection, packed_index, rows_of_gene_major,
-                            sample_cell_pairs)
+from parity_helpers import (check_rows_against_oracle_subset, check_selection, check_slow_against_oracle_subset,
+                            check_slow_selection, packed_index, rows_of_gene_major, sample_cell_pairs, slow_gate,
+                            slow_log_threshold)
 from scconsensus_amd import api, synth
 
 pytestmark = pytest.mark.gpu
+
+
+def _say(*a):  # progress in the GPU log (long tests)
+    print("[progress]", *a, flush=True)
 
 
 def test_config_d_parity(monkeypatch):
@@ -76,5 +81,37 @@ def test_config_d_parity(monkeypatch):
     assert np.max(np.abs(tail - ref_tail[order])) < 1e-5
     assert float(out.min()) >= 0.0
     del out
+    ds.close()
+    eng.close()
+
+
+def test_config_d_slow():
+    """reclusterDEConsensus (SLOW: every gene x every pair, slow:69-227) at
+    config D: the oracle on 60 genes over all 200k cells and 1225 pairs (exact
+    U, p / logFC within the bar), the global threshold restated from all 463 M
+    stored values, and the full-size selection from the engine's [1225][20000]
+    vectors: BH with n = G, DE flags (the gate restated on the subset genes),
+    the first-30 union."""
+    from scconsensus_amd import _native as nat
+    d = synth.generate_device("D", "cuda:0", layout="csr")
+    torch.cuda.synchronize()
+    eng = nat.Engine(0)
+    ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
+    names, code = api.select_clusters(d.labels, 10)
+    K, qthr, fc, msf = len(names), 0.05, 1.5, 5.0
+    assert K == 50
+    g = eng.de_run(ds, code, K, nat.SCC_DE_SLOW, q_val_thrs=qthr, fc_thrs=fc, mean_scaling_factor=msf, fetch="all")
+    assert g.p.shape == (1225, d.G)
+    _say("SLOW D engine done")
+    assert g.log_thr == pytest.approx(slow_log_threshold(d.data.cpu().numpy(), d.G, d.N, msf), rel=1e-13)
+    ip = d.indptr.cpu().numpy()
+    rng = np.random.default_rng(12)
+    genes = np.sort(rng.choice(d.G, 60, replace=False))
+    Xs = rows_of_gene_major(ip, d.indices, d.data, genes, d.N)
+    _say("SLOW D threshold / rows done")
+    assert check_slow_against_oracle_subset(g, Xs, genes, code, K, qthr, fc, msf) == 1225 * 60
+    _say("SLOW D subset oracle done")
+    check_slow_selection(g, qthr, fc, gate=slow_gate(Xs, code, K, g.log_thr), gate_genes=genes)
+    assert len(g.union) > 30
     ds.close()
     eng.close()
