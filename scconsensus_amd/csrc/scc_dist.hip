@@ -12,7 +12,7 @@
 //                   cell chunks into slabs reduced in a fixed order (deterministic)
 //   k_scores        P = Xc V_k (N x 16, zero padded components)
 //   k_dist_euclid   packed lower triangle in R `dist` order; per element the
-//                   sum of squared differences (FMA) + correctly rounded sqrt
+//                   sum of squared differences (FMA) + Newton-refined sqrt
 //   k_zscore / k_pearson_mfma  Pearson: per-cell centring/scaling, then an
 //                   LDS-pipelined FP32 MFMA (v_mfma_f32_32x32x2_f32) Gram with the
 //                   1 - r epilogue fused into coalesced packed-column stores.
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
 // one column are contiguous in the packed R order out[j*(2N-j-1)/2 + i-j-1].
 // Column j's scores are uniform across the tile (LDS broadcast); per element
 // |p_i|^2 + |p_j|^2 - 2 p_i.p_j over the k <= 15 components (the difference
-// form where that cancels) and a correctly rounded sqrt (the hardware
+// form where that cancels) and a Newton-refined sqrt (scc_sqrt_nr; the hardware
 // v_sqrt_f64 alone is ~1e-8 relative: 5e-7 absolute at B); the contract is
 // 1e-5 absolute (BASELINE north_star).  Line-aligned variants (a wave or a
 // workgroup walking a run of rows and storing 128-byte-aligned windows through
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restric
                 s = fma(dv, dv, s);
             }
         }
-        const double d = sqrt(s);
+        const double d = scc_sqrt_nr(s);
         if (F32)
             ((float*)out)[B + i] = (float)d;
         else
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
                     s = fma(dv, dv, s);
                 }
             }
-            stage[c][t] = sqrt(s);
+            stage[c][t] = scc_sqrt_nr(s);
         }
         __syncthreads();
 #pragma unroll
@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(DA_T) k_dist_wave(const double* __restrict__ P
                 s = fma(dv, dv, s);
             }
         }
-        const double d = sqrt(s);
+        const double d = scc_sqrt_nr(s);
         const int delta = (int)((B + R) & (HALO - 1));
         const double v = __shfl(d, min(lane + HALO - delta, 63), 64);
         const int i2 = R - delta + lane;
