@@ -169,8 +169,6 @@ __device__ inline u32 u32_wave_sum_dpp(u32 x)
     return x + scc_xor_lane<1>(x);
 }
 
-// wave index inside the workgroup, as a wave-uniform (SGPR) value: loops
-// bounded by it stay scalar instead of being treated as divergent
 // sqrt for s >= 0 from the hardware reciprocal square root (~2^-26
 // relative) and two Newton-Raphson / Goldschmidt corrections: within 1 ulp of
 // the correctly rounded result (the libm sequence adds denormal scaling and a
@@ -188,6 +186,8 @@ __device__ inline double scc_sqrt_nr(double s)
     return s > 0.0 ? y : 0.0;
 }
 
+// wave index inside the workgroup, as a wave-uniform (SGPR) value: loops
+// bounded by it stay scalar instead of being treated as divergent
 __device__ inline int scc_wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 __host__ __device__ inline int scc_next_pow2(int n)

@@ -685,7 +685,7 @@ __device__ __forceinline__ long long pearson_next(long long t, long long tend, l
 // order.  The last K chunk of a tile prefetches chunk 0 of the workgroup's
 // next tile, so the epilogue's stores and the next tile's first loads overlap
 // instead of paying a workgroup launch and a cold first chunk per tile.
-template <bool F32>
+template <bool F32, bool NT>
 __global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict__ Z, int N, int ldz, int nt, long long ntri,
                                                          long long per_xcd, int c_lo, int c_hi, long long obase,
                                                          void* __restrict__ out, int diag_nostore)
@@ -818,10 +818,17 @@ __global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict
                         const int i = I0 + wi + 32 * b + r32;
                         if (i < N && j < i) {
                             const float d = 1.0f - acc[a][b][r];
-                            if (F32)
-                                __builtin_nontemporal_store(d, (float*)out + (col + i));
-                            else
-                                __builtin_nontemporal_store((double)d, (double*)out + (col + i));
+                            if (F32) {
+                                if (NT)
+                                    __builtin_nontemporal_store(d, (float*)out + (col + i));
+                                else
+                                    ((float*)out)[col + i] = d;
+                            } else {
+                                if (NT)
+                                    __builtin_nontemporal_store((double)d, (double*)out + (col + i));
+                                else
+                                    ((double*)out)[col + i] = (double)d;
+                            }
                         }
                     }
                 }
@@ -1027,11 +1034,15 @@ extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld
     const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
     const char* ns = getenv("SCC_PEARSON_NOSTORE");
     const int nostore = ns && ns[0] == '1';
-    if (f32)
-        hipLaunchKernelGGL(k_pearson_mfma<true>, dim3((unsigned)(8 * nwg_xcd)), dim3(256), 0, st, Z, N, ldz, nt, ntri, per,
-                           c_lo, c_hi, obase, out, nostore);
-    else
-        hipLaunchKernelGGL(k_pearson_mfma<false>, dim3((unsigned)(8 * nwg_xcd)), dim3(256), 0, st, Z, N, ldz, nt, ntri, per,
-                           c_lo, c_hi, obase, out, nostore);
+    const char* nte = getenv("SCC_PEARSON_NT");  // nontemporal epilogue stores (default on)
+    const bool ntst = !(nte && *nte && atoi(nte) == 0);
+    const dim3 grid((unsigned)(8 * nwg_xcd));
+    const void* fn = f32 ? (ntst ? (const void*)k_pearson_mfma<true, true> : (const void*)k_pearson_mfma<true, false>)
+                         : (ntst ? (const void*)k_pearson_mfma<false, true> : (const void*)k_pearson_mfma<false, false>);
+    int nti = nt;
+    void* args[] = {(void*)&Z, (void*)&N, (void*)&ldz, (void*)&nti, (void*)&ntri, (void*)&per, (void*)&c_lo,
+                    (void*)&c_hi, (void*)&obase, (void*)&out, (void*)&nostore};
+    const hipError_t e = hipLaunchKernel(fn, grid, dim3(256), args, 0, st);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
