@@ -122,6 +122,8 @@ struct TriArgs {
     u32* counter;     // (unused)
     u64* stamps;      // diagnostic: WG 0 per-phase cycle sums (nullptr normally)
     u32* err;         // 1: a hand-off timed out
+    int stop;         // columns [0, stop) only; stop < n - 1: then the trailing block
+    double* tail;     // A^(stop)[stop:, stop:] (lower part, row-major, ld n - stop) for k_tridiag_tail
 };
 
 // Householder reflector from y[lo..n-1] (alpha = y[lo], x = y[lo+1..]), LAPACK
@@ -257,7 +259,8 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     __syncthreads();
     u64 t_b = 0, t_w = 0, t_c = 0, t_r = 0, t0 = 0;
     const bool stmp = a.stamps && me == 0 && tid == 0;
-    for (int i = 0; i <= n - 2; ++i) {
+    const int ilast = min(n - 2, a.stop - 1);
+    for (int i = 0; i <= ilast; ++i) {
         const int par = i & 1;
         const u32 tag = (u32)(i + 1);
         if (stmp) t0 = __builtin_amdgcn_s_memtime();
@@ -427,9 +430,12 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
             t_w += t1 - t0;
             t0 = t1;
         }
-        double pdt = 0.0;  // fixed-shape butterfly: identical in every wave of every workgroup
-        for (int q = lane; q < nwg; q += 64) pdt += part[q];
-        pdt = wave_sum_d(pdt);
+        // p.v over the handed-off p of every row, in a fixed order (a block sum
+        // over j): identical in every workgroup AND independent of how many
+        // workgroups joined (the per-workgroup partials part[] are not)
+        double pdl = 0.0;
+        for (int j = i + 1 + tid; j < n; j += TRI_T) pdl = fma(pp[j], vc[j], pdl);
+        const double pdt = block_sum<TRI_W>(pdl, red);
         const double a2 = -0.5 * tc * pdt;
         const double v1 = vc[i + 1];
         const double w1 = (tc != 0.0) ? fma(a2, v1, pp[i + 1]) : 0.0;
@@ -478,6 +484,42 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         __syncthreads();
         if (stmp) t_c += __builtin_amdgcn_s_memtime() - t0;
     }
+    if (a.stop < n - 1) {
+        // hand the trailing block A^(stop)[stop:, stop:] to k_tridiag_tail: row
+        // `stop` is y (updated in phase C); the other own rows still owe the
+        // update of column stop - 1 (v = vp, w = wp, applied lazily in phase B)
+        const int i0 = a.stop, mt = n - i0;
+        const bool prev = tp != 0.0;
+        if (me == 0 && tid == 0) a.tail[0] = y[i0];
+        const int l0 = (i0 + 1 > me) ? (i0 + 1 - me + nwg - 1) / nwg : 0;
+        if (nreg > 0) {
+#pragma unroll
+            for (int m = 0; m < TRI_MR; ++m) {
+                const int l = wv + TRI_W * m;
+                if (l >= nreg || l < l0) continue;
+                const int r = me + nwg * l;
+                const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
+#pragma unroll
+                for (int t = 0; t < NJA; ++t) {
+                    const int j = lane + 64 * t;
+                    if (j >= i0 && j <= r) {
+                        const double x = prev ? fma(-vr, wp[j], fma(-wr, vp[j], rr[m][t])) : rr[m][t];
+                        a.tail[(size_t)(r - i0) * mt + (j - i0)] = x;
+                    }
+                }
+            }
+        }
+        for (int l = max(l0, nreg) + wv; l < nown; l += TRI_W) {
+            const int r = me + nwg * l;
+            const double* row = rows + (size_t)(l - nreg) * n;
+            const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
+            for (int j = i0 + lane; j <= r; j += 64) {
+                double x = row[j];
+                if (prev) x = fma(-vr, wp[j], fma(-wr, vp[j], x));
+                a.tail[(size_t)(r - i0) * mt + (j - i0)] = x;
+            }
+        }
+    }
     if (stmp) {
         a.stamps[0] = t_b;
         a.stamps[1] = t_w;
@@ -485,6 +527,127 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         a.stamps[7] = t_r;
     }
 }
+
+// ---------------------------------------------------------------------------
+// 1b. the tail of the tridiagonalisation in ONE workgroup (dsytd2, lower):
+// columns [i0, n - 1) of A^(i0)[i0:, i0:], whose lower triangle (m = n - i0
+// <= TT_MMAX rows) is resident in LDS, packed by rows.  No cross-workgroup
+// hand-off: a column costs a few workgroup barriers.  Every reduction has a
+// fixed shape (block sums, 4-lane butterflies), so the result does not depend
+// on scheduling.  Outputs as k_tridiag (d, e, tau, reflector rows).
+#define TT_T 1024
+#define TT_W (TT_T / 64)
+#define TT_MMAX 196  // m(m+1)/2 + 3m + 32 doubles <= 160 KB
+__host__ __device__ __forceinline__ int tt_tri(int r) { return r * (r + 1) / 2; }
+
+__global__ void __launch_bounds__(TT_T) k_tridiag_tail(const double* __restrict__ src, int lds, int n, int i0,
+                                                       double* __restrict__ d, double* __restrict__ e,
+                                                       double* __restrict__ tau, double* __restrict__ refl, int lda)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int m = n - i0;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double* L = sm;                          // (r, c), c <= r, at r(r+1)/2 + c
+    double* v = L + (size_t)tt_tri(m);       // [m] reflector of the current column
+    double* p = v + m;                       // [m] tau A22 v
+    double* xc = p + m;                      // [m] the current column below the diagonal
+    double* red_x = xc + m;                  // [TT_W] partial |x|^2
+    double* red_p = red_x + TT_W;            // [TT_W] partial p.v
+    for (int r = wv; r < m; r += TT_W) {
+        const int b = tt_tri(r);
+        for (int c = lane; c <= r; c += 64) L[b + c] = src[(size_t)r * lds + c];
+    }
+    __syncthreads();
+    {  // column 0 and its |x|^2 past the first entry
+        double part = 0.0;
+        for (int a = 1 + tid; a < m; a += TT_T) {
+            const double x = L[tt_tri(a)];
+            xc[a] = x;
+            if (a >= 2) part = fma(x, x, part);
+        }
+        part = wave_sum_d(part);
+        if (lane == 0) red_x[wv] = part;
+    }
+    __syncthreads();
+    // 4 threads per row of the trailing block (row o + 1 + (tid >> 2)), each a
+    // quarter of its columns (b = o + 1 + q + 4 s); two barriers per column:
+    //   [reflector + p = tau A22 v + p.v partials] B1 [update + next column + its |x|^2] B2
+    const int q = tid & 3, rl = tid >> 2;
+    for (int o = 0; o <= m - 2; ++o) {
+        const int i = i0 + o;
+        double xn2 = 0.0;
+#pragma unroll
+        for (int w = 0; w < TT_W; ++w) xn2 += red_x[w];  // fixed order: identical in every thread
+        const double alpha = xc[o + 1];
+        double beta = alpha, tv = 0.0, scal = 0.0;
+        if (xn2 > 0.0) {
+            beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+            tv = (beta - alpha) / beta;
+            scal = 1.0 / (alpha - beta);
+        }
+        if (tid == 0) {
+            d[i] = L[tt_tri(o) + o];
+            e[i] = beta;
+            tau[i] = tv;
+        }
+        const int a = o + 1 + rl;
+        const bool live = a < m;
+        double s = 0.0;
+        if (live) {
+            const int ba = tt_tri(a);
+            for (int b = o + 1 + q; b < m; b += 4) {
+                const double x = b <= a ? L[ba + b] : L[tt_tri(b) + a];
+                const double vb = b == o + 1 ? 1.0 : xc[b] * scal;
+                s = fma(x, vb, s);
+            }
+        }
+        s += scc_xor_lane_f64<1>(s);
+        s += scc_xor_lane_f64<2>(s);
+        double pv = 0.0;
+        if (live && q == 0) {
+            const double va = a == o + 1 ? 1.0 : xc[a] * scal;
+            const double pa = tv * s;
+            v[a] = va;
+            p[a] = pa;
+            refl[(size_t)i * lda + i0 + a] = va;
+            pv = pa * va;
+        }
+        pv = wave_sum_d(pv);
+        if (lane == 0) red_p[wv] = pv;
+        __syncthreads();  // B1
+        double pvt = 0.0;
+#pragma unroll
+        for (int w = 0; w < TT_W; ++w) pvt += red_p[w];
+        const double a2 = -0.5 * tv * pvt;
+        // A22 -= v w^T + w v^T with w = p + a2 v; column o + 1 (the next
+        // reflector's) is kept aside with its |x|^2 past its first entry
+        double part = 0.0;
+        if (live) {
+            const int ba = tt_tri(a);
+            const double va = v[a], wa = fma(a2, va, p[a]);
+            for (int b = o + 1 + q; b <= a; b += 4) {
+                const double wb = fma(a2, v[b], p[b]);
+                const double x = fma(-va, wb, fma(-wa, v[b], L[ba + b]));
+                L[ba + b] = x;
+                if (b == o + 1) {
+                    xc[a] = x;
+                    if (a >= o + 3) part = fma(x, x, part);
+                }
+            }
+        }
+        part = wave_sum_d(part);
+        if (lane == 0) red_x[wv] = part;
+        __syncthreads();  // B2
+    }
+    if (tid == 0) {
+        d[n - 1] = L[tt_tri(m - 1) + m - 1];
+        e[n - 1] = 0.0;
+        tau[n - 1] = 0.0;
+    }
+}
+
+extern "C" int scc_tridiag_tail_max(void) { return TT_MMAX; }
+static size_t tt_lds_bytes(int m) { return sizeof(double) * ((size_t)tt_tri(m) + 3 * (size_t)m + 2 * TT_W); }
 
 // XCD registration shared by both tridiagonalisation kernels: the first
 // workgroup to arrive picks its XCD; up to a.nwg workgroups found on that XCD
@@ -692,7 +855,8 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag_wa(TriArgs a)
     }
     u64 t_b = 0, t_w = 0, t_c = 0, t0 = 0;
     const bool stmp = a.stamps && ag == 0 && lane == 0;
-    for (int i = 0; i <= n - 2; ++i) {
+    const int ilast = min(n - 2, a.stop - 1);
+    for (int i = 0; i <= ilast; ++i) {
         const int par = i & 1;
         const u32 tag = (u32)(i + 1);
         u64* pg = a.pg + (size_t)par * 2 * lda;
@@ -1562,7 +1726,7 @@ static int eig_local_env()
 }
 
 struct EigLayout {
-    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, tf, lu, work, total;
+    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, tf, lu, work, tail, total;
 };
 
 static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool lu_lds)
@@ -1589,6 +1753,7 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     const int R = (n + nwg - 1) / nwg;
     // XCD-local mode: fewer workgroups may register than planned -> room for all rows
     L.work = take(((size_t)n + 4 * 64) * n);  // row store of the HBM fall-backs (any participant count)
+    L.tail = take((size_t)TT_MMAX * TT_MMAX);  // the trailing block k_tridiag hands to k_tridiag_tail
     L.total = o;
     (void)k;
     return L;
@@ -1791,6 +1956,8 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.xcd_local = eig_local(n) ? 1 : 0;
     t.stamps = stamps;
     t.err = flags + 1;
+    t.stop = n;
+    t.tail = scratch + L.tail;
     const int R = (n + nwg - 1) / nwg;
     // at least 82 KB so that every workgroup has a CU of its own
     size_t lds = tri_lds_bytes(n, std::max(R - tri_reg_rows(n), 0), rows_lds);
@@ -1815,7 +1982,15 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     const bool wave_agents = (wa_env && *wa_env) ? atoi(wa_env) != 0 : false;  // measured slower (polling load)
     // wave agents: the planned participants' rows in LDS (HBM fall-back in the kernel)
     const size_t wa_lds = sizeof(double) * (size_t)TRI_W * ((n + TRI_W * nwg - 1) / (TRI_W * nwg)) * n;
-    if (one_cu) {
+    // the last TT_MMAX columns (all of them when n <= TT_MMAX) in ONE
+    // workgroup with the trailing block in LDS (k_tridiag_tail): no hand-off
+    // there; SCC_EIG_TAIL=0 keeps the hand-off kernel for every column
+    const char* tail_env = getenv("SCC_EIG_TAIL");
+    const bool use_tail = !one_cu && !wave_agents && n > 2 && !(tail_env && *tail_env && atoi(tail_env) == 0);
+    if (use_tail) t.stop = std::max(0, n - TT_MMAX);
+    if (use_tail && t.stop == 0) {
+        // nothing for the hand-off kernel
+    } else if (one_cu) {
         e = scc_launch_tridiag_cu(A, n, lda, t.work, t.d, t.e, t.tau, t.refl, t.reg, stamps, st);
         if (e != hipSuccess) return e;
     } else if (wave_agents && n <= 64 * TW_NJ && wa_lds <= EIG_LDS_MAX && nwg * TRI_W <= TW_MAXA) {
@@ -1851,6 +2026,14 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         if (e != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (use_tail) {
+        const int m = n - t.stop;
+        const size_t tlds = tt_lds_bytes(m);
+        hipFuncSetAttribute((const void*)k_tridiag_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds);
+        hipLaunchKernelGGL(k_tridiag_tail, dim3(1), dim3(TT_T), tlds, st, t.stop > 0 ? t.tail : A,
+                           t.stop > 0 ? m : lda, n, t.stop, t.d, t.e, t.tau, t.refl, lda);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (marks) hipEventRecord(marks[1], st);
     VecArgs v{};
     v.d = t.d;
@@ -1873,7 +2056,8 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     const char* pin_env = getenv("SCC_EIG_PIN");
     const int pin_mode = pin_env ? atoi(pin_env) : 2;
     // (measured at config B: eig_vec 0.37 ms anywhere, 0.42 claim loop, 0.32 wait)
-    const bool pin = t.xcd_local != 0 && pin_mode != 0;
+    // (the tail's reflectors come from another workgroup: no XCD to pin to)
+    const bool pin = t.xcd_local != 0 && pin_mode != 0 && !use_tail;
     v.wait = pin_mode == 2;
     v.xcd = pin && (pin_mode == 1 || 8 * k <= 256) ? t.reg : nullptr;  // wait needs co-residency
     v.vcount = flags + 5;
