@@ -244,7 +244,9 @@ SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* gen
  * vector, a contiguous slice.  Ranks that split [0, N) into column ranges of
  * equal entry counts each compute and keep their slice (the
  * distance tiles stay HBM-resident per GPU); the PCA is recomputed on every
- * rank (deterministic, identical scores). */
+ * rank.  The eigensolver's reductions have a fixed shape (no dependence on how
+ * many workgroups joined a hand-off), so every rank gets the same scores bit
+ * for bit on the same device type. */
 SCC_API int scc_distance_cols(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */,
                       int32_t n_union, int32_t metric, int32_t ncomp, int64_t col_lo, int64_t col_hi,
                       void* dist_out, int32_t out_kind, int32_t out_f32);

@@ -170,20 +170,18 @@ __device__ inline u32 u32_wave_sum_dpp(u32 x)
 }
 
 // sqrt for s >= 0 from the hardware reciprocal square root (~2^-26
-// relative) and two Newton-Raphson / Goldschmidt corrections: within 1 ulp of
-// the correctly rounded result (the libm sequence adds denormal scaling and a
-// third correction; distance entries are far from the denormal range, and 0
-// maps to 0).  v_sqrt_f64 alone is only ~1e-8 relative.
+// relative) and one Newton correction y += (s - y^2) / (2 y), with 1 / (2 y)
+// taken as g / 2: the error is ~delta^2 = 2^-52 relative plus the roundings,
+// i.e. within ~2 ulp (the libm sequence adds denormal scaling and two more
+// corrections; distance entries are far from the denormal range, and 0 maps
+// to 0).  v_sqrt_f64 alone is only ~1e-8 relative.
 __device__ inline double scc_sqrt_nr(double s)
 {
     const double g = __builtin_amdgcn_rsq(s);  // s = 0: +inf, handled below
-    double y = s * g, h = 0.5 * g;
-    const double r = fma(-h, y, 0.5);
-    y = fma(y, r, y);
-    h = fma(h, r, h);
+    const double y = s * g;
     const double e = fma(-y, y, s);
-    y = fma(e, h, y);
-    return s > 0.0 ? y : 0.0;
+    const double r = fma(e, 0.5 * g, y);
+    return s > 0.0 ? r : 0.0;
 }
 
 // wave index inside the workgroup, as a wave-uniform (SGPR) value: loops

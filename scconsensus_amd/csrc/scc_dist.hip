@@ -11,8 +11,9 @@
 //   k_gram_f64      C = Xc^T Xc, fp64 MFMA (v_mfma_f64_16x16x4_f64), split over
 //                   cell chunks into slabs reduced in a fixed order (deterministic)
 //   k_scores        P = Xc V_k (N x 16, zero padded components)
-//   k_dist_euclid   packed lower triangle in R `dist` order; per element the
-//                   sum of squared differences (FMA) + Newton-refined sqrt
+//   k_dist_aligned  packed lower triangle in R `dist` order, line-aligned
+//                   windows staged in LDS; per element the squared distance
+//                   (FMA) + Newton-refined sqrt
 //   k_zscore / k_pearson_mfma  Pearson: per-cell centring/scaling, then an
 //                   LDS-pipelined FP32 MFMA (v_mfma_f32_32x32x2_f32) Gram with the
 //                   1 - r epilogue fused into coalesced packed-column stores.
@@ -247,114 +248,12 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
 }
 
 // ------------------------------------------------------------------ Euclidean dist
-// Tile = DT_ROWS rows (i, one per thread) x DT_COLS columns (j); the stores of
-// one column are contiguous in the packed R order out[j*(2N-j-1)/2 + i-j-1].
-// Column j's scores are uniform across the tile (LDS broadcast); per element
-// |p_i|^2 + |p_j|^2 - 2 p_i.p_j over the k <= 15 components (the difference
-// form where that cancels) and a Newton-refined sqrt (scc_sqrt_nr; the hardware
-// v_sqrt_f64 alone is ~1e-8 relative: 5e-7 absolute at B); the contract is
-// 1e-5 absolute (BASELINE north_star).  Line-aligned variants (a wave or a
-// workgroup walking a run of rows and storing 128-byte-aligned windows through
-// an LDS ring) measured slower at config B (0.74-1.34 ms vs 0.69 ms).  The kernel is bound by the HBM
-// write stream (practical ceiling ~5.1 TB/s: scripts/write_bw.py).  Only
-// lower-triangle tiles are enumerated (column blocks in order, row blocks
-// rb >= cb / DT_RATIO), dealt to the XCDs in runs of DT_RUN consecutive tiles:
-// neighbouring row blocks of one column block share a cache line at every
-// column boundary, and a run keeps those lines in one XCD's L2 instead of two
-// partial write-backs.
-#define DT_ROWS 256
-// columns per tile: 64, or 256 when the scores outgrow the L2 (N >= 64k):
-// every tile reloads its rows' scores (128 B per row), 4x less often with
-// 256 columns (config D: 40 GB of score fetches at 64)
-#define DT_RUN 8
-
-template <int DT_RATIO>
-__device__ inline void dist_tile_of(long long t, int nrb, int& cb, int& rb)
-{
-    // column blocks come in groups Q = cb / DT_RATIO of DT_RATIO * (nrb - Q) tiles
-    auto before = [&](long long q) { return (long long)DT_RATIO * (q * nrb - q * (q - 1) / 2); };
-    const double h = nrb + 0.5;
-    long long Q = (long long)(h - sqrt(fmax(h * h - 2.0 * (double)t / DT_RATIO, 0.0)));
-    while (Q > 0 && before(Q) > t) --Q;
-    while (before(Q + 1) <= t) ++Q;
-    const long long rem = t - before(Q), per = nrb - Q;
-    cb = (int)(DT_RATIO * Q + rem / per);
-    rb = (int)(Q + rem % per);
-}
-
-// Columns [c_lo, c_hi) only (a rank's slice of the packed output, which
-// starts at packed index obase); t0 = the tiles of the column blocks before.
-template <bool F32, int DT_COLS>
-__global__ void __launch_bounds__(DT_ROWS) k_dist_euclid(const double* __restrict__ P, int N, int nrb, long long ntiles,
-                                                         long long t0, int c_lo, int c_hi, long long obase,
-                                                         void* __restrict__ out)
-{
-    // dispatch slot -> logical tile (slot x runs on XCD x % 8)
-    const long long lin = blockIdx.x, k = lin >> 3, x = lin & 7;
-    const long long t = ((k / DT_RUN) * 8 + x) * DT_RUN + k % DT_RUN;
-    if (t >= ntiles) return;
-    int cb, rb;
-    dist_tile_of<DT_ROWS / DT_COLS>(t0 + t, nrb, cb, rb);
-    // the tile's column scores in LDS, |p_j|^2 in the zero padding slot 15;
-    // every lane reads a column at the same address (broadcast), and LDS
-    // returns in order, so the next column's reads overlap this column's
-    // arithmetic (scalar loads cannot: their counter is waited to zero)
-    __shared__ __attribute__((aligned(16))) double cs[DT_COLS][16];
-    const int jb = cb * DT_COLS;
-    for (int e = threadIdx.x; e < DT_COLS * 16; e += DT_ROWS) {
-        const int jj = jb + e / 16;
-        cs[e / 16][e % 16] = (jj < N) ? P[(size_t)jj * 16 + e % 16] : 0.0;
-    }
-    __syncthreads();
-    if (threadIdx.x < DT_COLS) {
-        double nn = 0.0;
-#pragma unroll
-        for (int q = 0; q < 15; ++q) nn = fma(cs[threadIdx.x][q], cs[threadIdx.x][q], nn);
-        cs[threadIdx.x][15] = nn;
-    }
-    __syncthreads();
-    const int i = rb * DT_ROWS + (int)threadIdx.x;
-    const int j0 = max(jb, c_lo), j1 = min(min(N, jb + DT_COLS), c_hi);
-    if (i >= N) return;
-    double pi[15];
-#pragma unroll
-    for (int q = 0; q < 15; ++q) pi[q] = P[(size_t)i * 16 + q];
-    const int jend = min(j1, i);  // columns j < i only
-    // o(j, i) = B(j) + i with B(j) = j(2N - j - 1)/2 - j - 1, B(j + 1) = B(j) + N - j - 2
-    long long B = (long long)j0 * (2LL * N - j0 - 1) / 2 - j0 - 1 - obase;
-    double ni = 0.0;
-#pragma unroll
-    for (int q = 0; q < 15; ++q) ni = fma(pi[q], pi[q], ni);
-    for (int j = j0; j < jend; ++j) {
-        const double* pc = cs[j - jb];
-        // |p_i - p_j|^2 = |p_i|^2 + |p_j|^2 - 2 p_i.p_j: 15 FMAs instead of 15
-        // subtractions + 15 FMAs.  Its rounding error is below 20 eps (|p_i|^2 +
-        // |p_j|^2); where the result is under 2^-20 of that (near-identical
-        // cells: cancellation) the difference form is evaluated instead, so
-        // every entry is within ~1e-9 relative of the exact distance.
-        double dot = 0.0;
-#pragma unroll
-        for (int q = 0; q < 15; ++q) dot = fma(pi[q], pc[q], dot);
-        const double nsum = ni + pc[15];
-        double s = fma(-2.0, dot, nsum);
-        if (s < 0x1p-20 * nsum) {
-            s = 0.0;
-#pragma unroll
-            for (int q = 0; q < 15; ++q) {
-                const double dv = pi[q] - pc[q];
-                s = fma(dv, dv, s);
-            }
-        }
-        const double d = scc_sqrt_nr(s);
-        if (F32)
-            ((float*)out)[B + i] = (float)d;
-        else
-            ((double*)out)[B + i] = d;
-        B += N - j - 2;
-    }
-}
-
-// Line-aligned variant with a workgroup stage (SCC_DIST_KERNEL=1).
+// Per element |p_i|^2 + |p_j|^2 - 2 p_i.p_j over the k <= 15 components (the
+// difference form where that cancels) and a Newton-refined sqrt (scc_sqrt_nr;
+// the hardware v_sqrt_f64 alone is ~1e-8 relative: 5e-7 absolute at B); the
+// contract is 1e-5 absolute (BASELINE north_star).  The kernel is bound by the
+// HBM write stream (practical ceiling ~5.1 TB/s: scripts/write_bw.py).
+//
 // In R's packed order a column's entries are contiguous but start at any
 // offset, so a fixed row partition leaves two partial 128-B lines per (column,
 // tile) that the neighbouring tile completes later: read-modify-writes in HBM
@@ -465,110 +364,6 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
         }
         __syncthreads();
     }
-}
-
-// Wave-window variant (default): no workgroup barrier at all.  Each wave
-// computes 64 consecutive rows [R - HALO, R + WR) of every column (WR = 64 -
-// HALO, R a multiple of one line) and stores the WR-row window [R - delta_j,
-// R + WR - delta_j), which is line-aligned: the shift is a lane rotation of
-// the computed values (ds_bpermute, no LDS storage), and the first HALO rows
-// are computed twice (by this wave and the one below).  Four waves per tile,
-// tiles of 4 WR rows; column scores as wave-uniform (scalar) loads.
-template <bool F32, int DC>
-__global__ void __launch_bounds__(DA_T) k_dist_wave(const double* __restrict__ P, int N, int nrb, int cb_lo,
-                                                    int ncbl, int c_lo, int c_hi, long long obase,
-                                                    void* __restrict__ out)
-{
-    constexpr int HALO = F32 ? 32 : 16;  // outputs per 128-B line
-    constexpr int WR = 64 - HALO;        // rows stored per wave
-    constexpr int TR = (DA_T / 64) * WR; // rows per tile
-    __shared__ double cn[DC];
-    const int y = blockIdx.y;
-    int x = blockIdx.x;
-    int cb = cb_lo + y;
-    const int cntA = nrb - da_rbmin<TR, DC>(cb);
-    if (x >= cntA) {
-        x -= cntA;
-        const int cb2 = cb_lo + ncbl - 1 - y;
-        if (cb2 <= cb) return;
-        cb = cb2;
-        if (x >= nrb - da_rbmin<TR, DC>(cb)) return;
-    }
-    const int r0 = (da_rbmin<TR, DC>(cb) + x) * TR;
-    const int jb = max(cb * DC, c_lo);
-    const int je = min(min(cb * DC + DC, c_hi), min(N - 1, r0 + TR - 1));
-    if (jb >= je) return;
-    const int t = threadIdx.x, lane = t & 63;
-    for (int e = t; e < DC; e += DA_T) {
-        const int jj = min(cb * DC + e, N - 1);
-        double nn = 0.0;
-#pragma unroll
-        for (int q = 0; q < 15; ++q) nn = fma(P[(size_t)jj * 16 + q], P[(size_t)jj * 16 + q], nn);
-        cn[e] = nn;
-    }
-    __syncthreads();
-    const int R = r0 + WR * scc_wave_id();
-    const int wje = min(je, R + WR - 1);  // this wave's columns with a row in its window
-    const int i = R - HALO + lane;
-    const int ic = min(max(i, 0), N - 1);
-    double pi[15];
-#pragma unroll
-    for (int q = 0; q < 15; ++q) pi[q] = P[(size_t)ic * 16 + q];
-    double ni = 0.0;
-#pragma unroll
-    for (int q = 0; q < 15; ++q) ni = fma(pi[q], pi[q], ni);
-    long long B = (long long)jb * (2LL * N - jb - 1) / 2 - jb - 1 - obase;  // out index of (i, j) = B + i
-    for (int j = jb; j < wje; ++j) {
-        const double* pj = P + (size_t)j * 16;
-        double dot = 0.0;
-#pragma unroll
-        for (int q = 0; q < 15; ++q) dot = fma(pi[q], pj[q], dot);
-        const double nsum = ni + cn[j - cb * DC];
-        double s = fma(-2.0, dot, nsum);
-        if (s < 0x1p-20 * nsum) {  // near-identical cells: the difference form
-            s = 0.0;
-#pragma unroll
-            for (int q = 0; q < 15; ++q) {
-                const double dv = pi[q] - pj[q];
-                s = fma(dv, dv, s);
-            }
-        }
-        const double d = scc_sqrt_nr(s);
-        const int delta = (int)((B + R) & (HALO - 1));
-        const double v = __shfl(d, min(lane + HALO - delta, 63), 64);
-        const int i2 = R - delta + lane;
-        if (lane < WR && i2 > j && i2 < N) {
-            if (F32)
-                ((float*)out)[B + i2] = (float)v;
-            else
-                ((double*)out)[B + i2] = v;
-        }
-        B += N - j - 2;
-    }
-}
-
-template <int DC>
-static void launch_dist_wave(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
-{
-    const int HALO = f32 ? 32 : 16, TR = (DA_T / 64) * (64 - HALO);
-    const int nrb = (N + HALO - 1) / TR + 1;
-    const int cb_lo = c_lo / DC, cb_hi = (c_hi + DC - 1) / DC, ncbl = cb_hi - cb_lo;
-    const int npair = (ncbl + 1) / 2;
-    int gx = 1;
-    for (int y = 0; y < npair; ++y) {
-        const int a = cb_lo + y, b = cb_lo + ncbl - 1 - y;
-        const int ra = f32 ? da_rbmin<(DA_T / 64) * 32, DC>(a) : da_rbmin<(DA_T / 64) * 48, DC>(a);
-        const int rbb = f32 ? da_rbmin<(DA_T / 64) * 32, DC>(b) : da_rbmin<(DA_T / 64) * 48, DC>(b);
-        gx = std::max(gx, (nrb - ra) + (b > a ? nrb - rbb : 0));
-    }
-    const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
-    const dim3 grid((unsigned)gx, (unsigned)npair);
-    if (f32)
-        hipLaunchKernelGGL((k_dist_wave<true, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
-                           obase, out);
-    else
-        hipLaunchKernelGGL((k_dist_wave<false, DC>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
-                           obase, out);
 }
 
 template <int DC, int NB, bool NT>
@@ -949,67 +744,26 @@ extern "C" hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld,
     return hipGetLastError();
 }
 
-template <int DT_COLS>
-static void launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
-{
-    constexpr int DT_RATIO = DT_ROWS / DT_COLS;
-    const int nrb = (N + DT_ROWS - 1) / DT_ROWS;
-    const int cb0 = c_lo / DT_COLS, cb1 = (c_hi + DT_COLS - 1) / DT_COLS;
-    long long t0 = 0, ntiles = 0;
-    for (int cb = 0; cb < cb1; ++cb) (cb < cb0 ? t0 : ntiles) += nrb - cb / DT_RATIO;
-    const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
-    const long long ngrp = (ntiles + DT_RUN - 1) / DT_RUN;
-    const dim3 grid((unsigned)(((ngrp + 7) / 8) * 8 * DT_RUN));
-    if (f32)
-        hipLaunchKernelGGL((k_dist_euclid<true, DT_COLS>), grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo,
-                           c_hi, obase, out);
-    else
-        hipLaunchKernelGGL((k_dist_euclid<false, DT_COLS>), grid, dim3(DT_ROWS), 0, st, P, N, nrb, ntiles, t0, c_lo,
-                           c_hi, obase, out);
-}
-
 extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, void* out, int f32,
                                              hipStream_t st)
 {
     if (N < 2 || c_hi <= c_lo) return hipSuccess;
-    // SCC_DIST_KERNEL: 1 = workgroup-staged line windows (default), 2 = wave
-    // windows, 0 = the unaligned tiles (k_dist_euclid).  Measured at config B:
-    // 0.51 (nontemporal stores) / 0.54 / 0.59 / 0.69 ms; config D: 33.2 (64
-    // columns per tile, nontemporal) / 35.0 (64) / 36.2 (256) / 38.5 / 38.1 ms.
-    const char* ke = getenv("SCC_DIST_KERNEL");
-    const int kind = (ke && *ke) ? atoi(ke) : 1;
-    const char* env = getenv("SCC_DIST_COLS");  // 64 or 256 columns per tile
-    // default 64 columns; 128 for the aligned kernel from 64k cells (config D: 32.3 -> 31.5 ms; 16 / 32 columns
-    // 43.8 / 34.3 ms; config B: 64 columns 0.515 ms, 32: 0.535, 128: 0.525) -- all widths bit-identical
-    const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? (kind == 0 ? 256 : (kind == 1 ? 128 : 64)) : 64);
-    if (kind == 1) {
-        const char* nte = getenv("SCC_DIST_NT");  // nontemporal stores (default on)
-        const bool nt = !(nte && *nte && atoi(nte) == 0);
-        if (cols == 256)
-            nt ? launch_dist_aligned<256, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
-               : launch_dist_aligned<256, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
-        else if (cols == 32)
-            launch_dist_aligned<32, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st);
-        else if (cols == 16)
-            launch_dist_aligned<16, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st);
-        else if (cols == 128)
-            launch_dist_aligned<128, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st);
-        else
-            nt ? launch_dist_aligned<64, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
-               : launch_dist_aligned<64, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
-        return hipGetLastError();
-    }
-    if (kind == 2) {
-        if (cols == 256)
-            launch_dist_wave<256>(P, N, c_lo, c_hi, out, f32, st);
-        else
-            launch_dist_wave<64>(P, N, c_lo, c_hi, out, f32, st);
-        return hipGetLastError();
-    }
-    if (cols == 256)
-        launch_dist_euclid<256>(P, N, c_lo, c_hi, out, f32, st);
+    // columns per tile: 64, 128 from 64k cells (config D: 32.3 -> 31.5 ms; 16 / 32
+    // columns 43.8 / 34.3 ms; config B: 64 columns 0.515 ms, 32: 0.535, 128:
+    // 0.525); SCC_DIST_COLS forces either (bit-identical).  Nontemporal stores
+    // (SCC_DIST_NT=0: plain; B 0.51 vs 0.54 ms).  Removed after measuring slower
+    // at B / D: unaligned row tiles (0.69 / 38.1 ms), barrier-free wave windows
+    // (0.59 ms), 256-column tiles (0.78 / 36.2 ms).
+    const char* env = getenv("SCC_DIST_COLS");
+    const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? 128 : 64);
+    const char* nte = getenv("SCC_DIST_NT");
+    const bool nt = !(nte && *nte && atoi(nte) == 0);
+    if (cols == 128)
+        nt ? launch_dist_aligned<128, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
+           : launch_dist_aligned<128, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
     else
-        launch_dist_euclid<64>(P, N, c_lo, c_hi, out, f32, st);
+        nt ? launch_dist_aligned<64, DA_NB, true>(P, N, c_lo, c_hi, out, f32, st)
+           : launch_dist_aligned<64, DA_NB, false>(P, N, c_lo, c_hi, out, f32, st);
     return hipGetLastError();
 }
 

@@ -530,55 +530,111 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
 
 // ---------------------------------------------------------------------------
 // 1b. the tail of the tridiagonalisation in ONE workgroup (dsytd2, lower):
-// columns [i0, n - 1) of A^(i0)[i0:, i0:], whose lower triangle (m = n - i0
-// <= TT_MMAX rows) is resident in LDS, packed by rows.  No cross-workgroup
-// hand-off: a column costs a few workgroup barriers.  Every reduction has a
-// fixed shape (block sums, 4-lane butterflies), so the result does not depend
-// on scheduling.  Outputs as k_tridiag (d, e, tau, reflector rows).
-#define TT_T 1024
-#define TT_W (TT_T / 64)
-#define TT_MMAX 196  // m(m+1)/2 + 3m + 32 doubles <= 160 KB
-__host__ __device__ __forceinline__ int tt_tri(int r) { return r * (r + 1) / 2; }
-
-__global__ void __launch_bounds__(TT_T) k_tridiag_tail(const double* __restrict__ src, int lds, int n, int i0,
-                                                       double* __restrict__ d, double* __restrict__ e,
-                                                       double* __restrict__ tau, double* __restrict__ refl, int lda)
+// columns [i0, n - 1) of A^(i0)[i0:, i0:] (m = n - i0 <= TT_MMAX), the lower
+// triangle of the trailing block resident in REGISTERS.  Wave w owns rows
+// r = w + 8 s (row slot s); lane l holds columns l + 64 t of each (column slot
+// t <= r / 64, a compile-time triangle: 80 doubles per lane at m = 256).  A
+// column costs three workgroup barriers and two passes over the registers:
+//   pass 1  y = A22 v: row sums (a 4-row lane transpose-reduce per wave) and
+//           per-wave column partials (the symmetric half) into LDS     | B1
+//   reduce  thread x: y_x in a fixed order, p_x = tau y_x, p.v partials  | B2
+//   pass 2  A22 -= v w^T + w v^T; the owners of the next column keep its
+//           updated entries and |x|^2 partials for the next reflector    | B3
+// Every sum has a fixed shape, so the bits do not depend on scheduling.  No
+// hand-off latency, and no LDS traffic for the matrix: the old LDS-resident
+// tail (4 threads per row, dependent LDS chains) took 6.8 us per column.
+// Outputs as k_tridiag (d, e, tau, reflector rows).
+#define TR_W 8
+#define TR_T (TR_W * 64)
+#define TT_MMAX 256
+#define TR_S (TT_MMAX / TR_W)  // row slots per wave
+#define TR_CS (TT_MMAX / 64)   // column slots
+#define TR_P (64 / TR_W)  // row slots per step of the column-slot count
+// column slots of row slot s (rows w + 8 s <= 8 s + 7), and the register offset
+// of slot s: closed forms, so unrolled loops index the array with constants
+__host__ __device__ constexpr int tr_ts(int s) { return s / TR_P + 1; }
+__host__ __device__ constexpr int tr_off(int s)
 {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+    return s + TR_P * (s / TR_P) * (s / TR_P - 1) / 2 + (s - TR_P * (s / TR_P)) * (s / TR_P);
+}
+static_assert(TR_S <= 64 && (TR_S & (TR_S - 1)) == 0, "row slots fit the lanes");
+static_assert(tr_off(1) == 1 && tr_off(8) == 8 && tr_off(9) == 10 && tr_off(16) == 24 && tr_off(TR_S) == 80,
+              "register triangle layout");
+
+struct TrLds {
+    double xcol[2][TT_MMAX];   // the captured column below its diagonal (double-buffered)
+    double pp[TT_MMAX];        // p = tau A22 v
+    double rows[TT_MMAX];      // row sums of pass 1
+    double colp[TR_W][TT_MMAX];  // per-wave column partials of pass 1
+    double redx[TR_W], redp[TR_W];
+    double diag;
+};
+
+__global__ void __launch_bounds__(TR_T) k_tridiag_tail(const double* __restrict__ src, int lds, int n, int i0,
+                                                       double* __restrict__ d, double* __restrict__ e,
+                                                       double* __restrict__ tau, double* __restrict__ refl, int lda,
+                                                       unsigned long long* __restrict__ stamps)
+{
+    __shared__ TrLds S;
+    // diagnostic (stamps != nullptr): wave 0's cycles per phase, summed over the columns
+    const bool stmp = stamps && threadIdx.x == 0;
+    unsigned long long ts0 = 0, tp1 = 0, tpr = 0, tp2 = 0, tpc = 0;
     const int m = n - i0;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    double* L = sm;                          // (r, c), c <= r, at r(r+1)/2 + c
-    double* v = L + (size_t)tt_tri(m);       // [m] reflector of the current column
-    double* p = v + m;                       // [m] tau A22 v
-    double* xc = p + m;                      // [m] the current column below the diagonal
-    double* red_x = xc + m;                  // [TT_W] partial |x|^2
-    double* red_p = red_x + TT_W;            // [TT_W] partial p.v
-    for (int r = wv; r < m; r += TT_W) {
-        const int b = tt_tri(r);
-        for (int c = lane; c <= r; c += 64) L[b + c] = src[(size_t)r * lds + c];
+    const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    // xcol entries at or above the current subdiagonal and past m stay 0, and
+    // pp is 0 outside the trailing block, so v and w vanish there and dead
+    // rows / columns need no masks (only the upper part of each diagonal slot)
+    for (int x = tid; x < TT_MMAX; x += TR_T) {
+        S.xcol[0][x] = 0.0;
+        S.xcol[1][x] = 0.0;
+        S.pp[x] = 0.0;
     }
-    __syncthreads();
-    {  // column 0 and its |x|^2 past the first entry
-        double part = 0.0;
-        for (int a = 1 + tid; a < m; a += TT_T) {
-            const double x = L[tt_tri(a)];
-            xc[a] = x;
-            if (a >= 2) part = fma(x, x, part);
+    double a[tr_off(TR_S)];
+    // the lower triangle (clamped loads, then a select: the whole batch in flight)
+#pragma unroll
+    for (int s = 0; s < TR_S; ++s) {
+        const int r = w + TR_W * s;
+        const int rc = r < m ? r : m - 1;
+#pragma unroll
+        for (int t = 0; t < tr_ts(s); ++t) {
+            const int c = lane + 64 * t;
+            const double x = src[(size_t)rc * lds + (c <= rc ? c : rc)];
+            a[tr_off(s) + t] = (r < m && c <= r) ? x : 0.0;
         }
-        part = wave_sum_d(part);
-        if (lane == 0) red_x[wv] = part;
     }
     __syncthreads();
-    // 4 threads per row of the trailing block (row o + 1 + (tid >> 2)), each a
-    // quarter of its columns (b = o + 1 + q + 4 s); two barriers per column:
-    //   [reflector + p = tau A22 v + p.v partials] B1 [update + next column + its |x|^2] B2
-    const int q = tid & 3, rl = tid >> 2;
+    {  // column 0: its diagonal, the entries below and their |x|^2 past the first
+        double part = 0.0;
+        if (lane == 0) {
+#pragma unroll
+            for (int s = 0; s < TR_S; ++s) {
+                const int r = w + TR_W * s;
+                const double x = a[tr_off(s)];
+                if (r == 0) S.diag = x;
+                else if (r < m) {
+                    S.xcol[0][r] = x;
+                    if (r >= 2) part = fma(x, x, part);
+                }
+            }
+            S.redx[w] = part;
+        }
+    }
+    __syncthreads();
+    int buf = 0;
     for (int o = 0; o <= m - 2; ++o) {
         const int i = i0 + o;
         double xn2 = 0.0;
 #pragma unroll
-        for (int w = 0; w < TT_W; ++w) xn2 += red_x[w];  // fixed order: identical in every thread
+        for (int v = 0; v < TR_W; ++v) xn2 += S.redx[v];  // fixed order: identical in every thread
+        const double* xc = S.xcol[buf];
+        // every LDS value this column needs, in one batch: alpha, the 4 column
+        // entries of this lane and (lane s < TR_S) the entry of row slot s
         const double alpha = xc[o + 1];
+        double xcl[TR_CS];
+#pragma unroll
+        for (int t = 0; t < TR_CS; ++t) xcl[t] = xc[lane + 64 * t];
+        const int rl = w + TR_W * (lane & (TR_S - 1));  // this lane's row slot (lanes >= TR_S repeat)
+        const double xrl = xc[rl];
         double beta = alpha, tv = 0.0, scal = 0.0;
         if (xn2 > 0.0) {
             beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
@@ -586,68 +642,179 @@ __global__ void __launch_bounds__(TT_T) k_tridiag_tail(const double* __restrict_
             scal = 1.0 / (alpha - beta);
         }
         if (tid == 0) {
-            d[i] = L[tt_tri(o) + o];
+            d[i] = S.diag;
             e[i] = beta;
             tau[i] = tv;
         }
-        const int a = o + 1 + rl;
-        const bool live = a < m;
-        double s = 0.0;
-        if (live) {
-            const int ba = tt_tri(a);
-            for (int b = o + 1 + q; b < m; b += 4) {
-                const double x = b <= a ? L[ba + b] : L[tt_tri(b) + a];
-                const double vb = b == o + 1 ? 1.0 : xc[b] * scal;
-                s = fma(x, vb, s);
-            }
-        }
-        s += scc_xor_lane_f64<1>(s);
-        s += scc_xor_lane_f64<2>(s);
-        double pv = 0.0;
-        if (live && q == 0) {
-            const double va = a == o + 1 ? 1.0 : xc[a] * scal;
-            const double pa = tv * s;
-            v[a] = va;
-            p[a] = pa;
-            refl[(size_t)i * lda + i0 + a] = va;
-            pv = pa * va;
-        }
-        pv = wave_sum_d(pv);
-        if (lane == 0) red_p[wv] = pv;
-        __syncthreads();  // B1
-        double pvt = 0.0;
+        double vc[TR_CS];
 #pragma unroll
-        for (int w = 0; w < TT_W; ++w) pvt += red_p[w];
+        for (int t = 0; t < TR_CS; ++t) vc[t] = lane + 64 * t == o + 1 ? 1.0 : xcl[t] * scal;
+        const double vrl = rl == o + 1 ? 1.0 : xrl * scal;  // v of this lane's row slot
+        // a row slot's value, wave-uniform, from the lane that holds it
+        auto slot_val = [&](double x, int s) {
+            const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
+            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, s);
+            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), s);
+            return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+        };
+        // ---- pass 1: y = A22 v (row sums per 4-slot batch, column partials).
+        // Dead rows and columns carry v = 0; only whole dead batches are skipped.
+        double cacc[TR_CS];
+#pragma unroll
+        for (int t = 0; t < TR_CS; ++t) cacc[t] = 0.0;
+#pragma unroll
+        for (int sb = 0; sb < TR_S; sb += 4) {
+            if (w + TR_W * (sb + 3) <= o || w + TR_W * sb >= m) continue;  // no live row in the batch
+            double rb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int s = sb + j, r = w + TR_W * s;
+                const double vr = slot_val(vrl, s);
+                double rs = 0.0;
+#pragma unroll
+                for (int t = 0; t < tr_ts(s); ++t) {
+                    const double x = a[tr_off(s) + t];
+                    rs = fma(x, vc[t], rs);
+                    if (t == tr_ts(s) - 1)  // diagonal slot: the strictly lower part feeds the columns
+                        cacc[t] = fma(lane + 64 * t < r ? x : 0.0, vr, cacc[t]);
+                    else
+                        cacc[t] = fma(x, vr, cacc[t]);
+                }
+                rb[j] = rs;
+            }
+            // 4 row sums across the 64 lanes: halve by lane^32 and lane^16, then a butterfly
+            const bool h32 = (lane & 32) != 0, h16 = (lane & 16) != 0;
+            double k0 = h32 ? rb[2] : rb[0], k1 = h32 ? rb[3] : rb[1];
+            const double g0 = h32 ? rb[0] : rb[2], g1 = h32 ? rb[1] : rb[3];
+            k0 += scc_xor_lane_f64<32>(g0);
+            k1 += scc_xor_lane_f64<32>(g1);
+            double c = h16 ? k1 : k0;
+            c += scc_xor_lane_f64<16>(h16 ? k0 : k1);
+            c += scc_xor_lane_f64<8>(c);
+            c += scc_xor_lane_f64<4>(c);
+            c += scc_xor_lane_f64<2>(c);
+            c += scc_xor_lane_f64<1>(c);
+            if ((lane & 15) == 0) S.rows[w + TR_W * (sb + (lane >> 4))] = c;
+        }
+#pragma unroll
+        for (int t = 0; t < TR_CS; ++t) S.colp[w][lane + 64 * t] = cacc[t];
+        __syncthreads();  // B1
+        if (stmp) {
+            const unsigned long long tn = clock64();
+            tp1 += tn - ts0;
+            ts0 = tn;
+        }
+        // ---- reduce: y, p = tau y (0 outside the trailing block), p.v; the reflector row
+        {
+            double pv = 0.0;
+            const int x = tid;
+            if (x < TT_MMAX) {
+                const bool live = x > o && x < m;
+                double px = 0.0;
+                if (live) {
+                    double y = S.rows[x];
+#pragma unroll
+                    for (int v = 0; v < TR_W; ++v) y += S.colp[v][x];
+                    px = tv * y;
+                    const double vx = x == o + 1 ? 1.0 : xc[x] * scal;
+                    pv = px * vx;
+                    refl[(size_t)i * lda + i0 + x] = vx;
+                }
+                S.pp[x] = px;
+            }
+            pv = wave_sum_d(pv);
+            if (lane == 0) S.redp[w] = pv;
+        }
+        __syncthreads();  // B2
+        if (stmp) {
+            const unsigned long long tn = clock64();
+            tpr += tn - ts0;
+            ts0 = tn;
+        }
+        double pvt = 0.0;
+        double ppc[TR_CS];
+#pragma unroll
+        for (int t = 0; t < TR_CS; ++t) ppc[t] = S.pp[lane + 64 * t];
+        const double ppr = S.pp[rl];
+#pragma unroll
+        for (int v = 0; v < TR_W; ++v) pvt += S.redp[v];
         const double a2 = -0.5 * tv * pvt;
-        // A22 -= v w^T + w v^T with w = p + a2 v; column o + 1 (the next
-        // reflector's) is kept aside with its |x|^2 past its first entry
-        double part = 0.0;
-        if (live) {
-            const int ba = tt_tri(a);
-            const double va = v[a], wa = fma(a2, va, p[a]);
-            for (int b = o + 1 + q; b <= a; b += 4) {
-                const double wb = fma(a2, v[b], p[b]);
-                const double x = fma(-va, wb, fma(-wa, v[b], L[ba + b]));
-                L[ba + b] = x;
-                if (b == o + 1) {
-                    xc[a] = x;
-                    if (a >= o + 3) part = fma(x, x, part);
+        double wc[TR_CS];
+#pragma unroll
+        for (int t = 0; t < TR_CS; ++t) wc[t] = fma(a2, vc[t], ppc[t]);
+        const double wrl = fma(a2, vrl, ppr);  // w of this lane's row slot
+        // ---- pass 2: A22 -= v w^T + w v^T (v = w = 0 on dead rows and columns)
+#pragma unroll
+        for (int sb = 0; sb < TR_S; sb += 4) {
+            if (w + TR_W * (sb + 3) <= o || w + TR_W * sb >= m) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int s = sb + j, r = w + TR_W * s;
+                const double vr = slot_val(vrl, s);
+                const double wr = slot_val(wrl, s);
+#pragma unroll
+                for (int t = 0; t < tr_ts(s); ++t) {
+                    const double x = a[tr_off(s) + t];
+                    const double xn = fma(-vr, wc[t], fma(-wr, vc[t], x));
+                    if (t == tr_ts(s) - 1)
+                        a[tr_off(s) + t] = lane + 64 * t > r ? 0.0 : xn;  // the upper part stays 0
+                    else
+                        a[tr_off(s) + t] = xn;
                 }
             }
         }
-        part = wave_sum_d(part);
-        if (lane == 0) red_x[wv] = part;
-        __syncthreads();  // B2
+        if (stmp) {
+            const unsigned long long tn = clock64();
+            tp2 += tn - ts0;
+            ts0 = tn;
+        }
+        // ---- column q = o + 1 for the next reflector: the entries below its
+        // diagonal (rows above it written as 0), the diagonal, and |x|^2 past
+        // the first entry; lane q % 64 of every wave holds the column
+        const int q = o + 1, tq = q >> 6, lq = q & 63, nb = buf ^ 1;
+        double part = 0.0;
+#pragma unroll
+        for (int t = 0; t < TR_CS; ++t) {
+            if (t != tq) continue;
+            if (lane == lq) {
+#pragma unroll
+                for (int s = 0; s < TR_S; ++s) {
+                    if (tr_ts(s) <= t) continue;  // compile-time: rows < 64 t
+                    // a batch of rows all < q (zero already) or all >= m (never read)
+                    if (w + TR_W * ((s & ~3) + 3) < q || w + TR_W * (s & ~3) >= m) continue;
+                    const int r = w + TR_W * s;
+                    const double x = a[tr_off(s) + t];
+                    S.xcol[nb][r] = r > q ? x : 0.0;
+                    if (r == q) S.diag = x;
+                    part = fma(r >= q + 2 ? x : 0.0, x, part);
+                }
+                S.redx[w] = part;
+            }
+        }
+        // rows q - 1 and q of that buffer may still hold an older column (slots
+        // this capture does not cover): at or above the next subdiagonal they read 0
+        if (tid == 0) {
+            S.xcol[nb][q] = 0.0;
+            if (q >= 1) S.xcol[nb][q - 1] = 0.0;
+        }
+        buf = nb;
+        __syncthreads();  // B3
+        if (stmp) tpc += clock64() - ts0;
+    }
+    if (stmp) {
+        stamps[17] = tp1;
+        stamps[18] = tpr;
+        stamps[19] = tp2;
+        stamps[20] = tpc;
     }
     if (tid == 0) {
-        d[n - 1] = L[tt_tri(m - 1) + m - 1];
+        d[n - 1] = S.diag;
         e[n - 1] = 0.0;
         tau[n - 1] = 0.0;
     }
 }
 
 extern "C" int scc_tridiag_tail_max(void) { return TT_MMAX; }
-static size_t tt_lds_bytes(int m) { return sizeof(double) * ((size_t)tt_tri(m) + 3 * (size_t)m + 2 * TT_W); }
 
 // XCD registration shared by both tridiagonalisation kernels: the first
 // workgroup to arrive picks its XCD; up to a.nwg workgroups found on that XCD
@@ -756,279 +923,6 @@ __device__ inline int xcd_item_wait(const u32* xcd_pick, u32* vc, int items, u32
     }
     __syncthreads();
     return s_item;
-}
-
-// Wave-agent tridiagonalisation for n <= 64 * TW_NJ.  Every wave of every
-// participating workgroup is an independent agent: it owns rows r with
-// r % NA == agent, keeps v_i, v_{i-1}, w_{i-1} in registers (lane-strided,
-// j = lane + 64 t), polls every granule it needs itself and computes w_i,
-// row i+1 and the next reflector redundantly.  The main loop has no
-// workgroup barrier at all; agents only meet through the tagged granules.
-#define TW_NJ 8
-#define TW_MAXA 256  // agents (64 workgroups of 4 waves)
-template <bool LOCAL>
-__global__ void __launch_bounds__(TRI_T) k_tridiag_wa(TriArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    __shared__ int s_rank, s_nwg;
-    const int n = a.n, lda = a.lda;
-    const int lane = threadIdx.x & 63, wv = scc_wave_id();
-    int me = blockIdx.x, nwg = a.nwg;
-    if (LOCAL) {
-        xcd_register(a, n, &s_rank, &s_nwg);
-        if (s_rank < 0) return;
-        me = s_rank;
-        nwg = s_nwg;
-    }
-    const int NA = nwg * TRI_W;         // agents
-    const int ag = me * TRI_W + wv;     // this wave's agent id
-    const int RA = (n + NA - 1) / NA;   // rows per agent
-    // rows in LDS when the participants' share fits (fewer workgroups than
-    // planned may register on the XCD: then the rows live in HBM scratch)
-    const bool in_lds = (size_t)TRI_W * RA * n <= (size_t)a.lds_rows_cap;
-    double* rows = in_lds ? sm + (size_t)wv * RA * n : a.work + (size_t)ag * RA * n;
-    const int nown = (ag < n) ? (n - ag + NA - 1) / NA : 0;
-    for (int l = 0; l < nown; ++l) {
-        const double* src = a.A + (size_t)(ag + NA * l) * lda;
-        for (int j = lane; j < n; j += 64) rows[(size_t)l * n + j] = src[j];
-    }
-    double vc[TW_NJ], vp[TW_NJ], wp[TW_NJ];
-    // row 0 -> reflector 0 (every agent)
-    double y[TW_NJ];
-#pragma unroll
-    for (int t = 0; t < TW_NJ; ++t) {
-        const int j = lane + 64 * t;
-        y[t] = (j < n) ? a.A[j] : 0.0;
-        vp[t] = 0.0;
-        wp[t] = 0.0;
-    }
-    auto bcast = [&](const double* r, int j) -> double {  // element j of a lane-strided register vector
-        double v = 0.0;
-#pragma unroll
-        for (int t = 0; t < TW_NJ; ++t)
-            if (t == (j >> 6)) v = r[t];
-        return __shfl(v, j & 63, 64);
-    };
-    const double d0 = bcast(y, 0);
-    if (n == 1) {
-        if (ag == 0 && lane == 0) {
-            a.d[0] = d0;
-            a.e[0] = 0.0;
-            a.tau[0] = 0.0;
-        }
-        return;
-    }
-    double tc, tp = 0.0;
-    {
-        double part = 0.0;
-#pragma unroll
-        for (int t = 0; t < TW_NJ; ++t) {
-            const int j = lane + 64 * t;
-            if (j >= 2 && j < n) part += y[t] * y[t];
-        }
-        const double xn2 = wave_sum_d(part);
-        const double alpha = bcast(y, 1);
-        double beta = alpha, scal = 0.0;
-        tc = 0.0;
-        if (xn2 > 0.0) {
-            beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-            tc = (beta - alpha) / beta;
-            scal = 1.0 / (alpha - beta);
-        }
-#pragma unroll
-        for (int t = 0; t < TW_NJ; ++t) {
-            const int j = lane + 64 * t;
-            vc[t] = (j == 1) ? 1.0 : ((j > 1 && j < n) ? y[t] * scal : 0.0);
-        }
-        if (ag == 0) {
-            if (lane == 0) {
-                a.d[0] = d0;
-                a.e[0] = beta;
-                a.tau[0] = tc;
-            }
-#pragma unroll
-            for (int t = 0; t < TW_NJ; ++t) {
-                const int j = lane + 64 * t;
-                if (j >= 1 && j < n) a.refl[j] = vc[t];
-            }
-        }
-    }
-    u64 t_b = 0, t_w = 0, t_c = 0, t0 = 0;
-    const bool stmp = a.stamps && ag == 0 && lane == 0;
-    const int ilast = min(n - 2, a.stop - 1);
-    for (int i = 0; i <= ilast; ++i) {
-        const int par = i & 1;
-        const u32 tag = (u32)(i + 1);
-        u64* pg = a.pg + (size_t)par * 2 * lda;
-        u64* rg = a.rg + (size_t)par * 2 * lda;
-        u64* dg = a.dg + (size_t)par * 2 * EIG_MAX_WG * TRI_W;
-        const bool prev = (i >= 1) && (tp != 0.0);
-        if (stmp) t0 = __builtin_amdgcn_s_memtime();
-        // ---- phase B: own rows r >= i+1
-        double pd = 0.0;
-        const int l0 = (i + 1 > ag) ? (i + 1 - ag + NA - 1) / NA : 0;
-        for (int l = l0; l < nown; ++l) {
-            const int r = ag + NA * l;
-            double* row = rows + (size_t)l * n;
-            const double vr = prev ? bcast(vp, r) : 0.0, wr = prev ? bcast(wp, r) : 0.0;
-            const bool pub = (r == i + 1);
-            double s = 0.0;
-#pragma unroll
-            for (int t = 0; t < TW_NJ; ++t) {
-                const int j = lane + 64 * t;
-                if (j > i && j < n) {
-                    double x = row[j];
-                    if (prev) {
-                        x = x - vr * wp[t] - wr * vp[t];
-                        row[j] = x;
-                    }
-                    if (pub) put_g<LOCAL>(rg + 2 * j, x, tag);
-                    s += x * vc[t];
-                }
-            }
-            s = wave_sum_d(s);
-            const double p = tc * s;
-            if (lane == 0) put_g<LOCAL>(pg + 2 * r, p, tag);
-            pd += p * bcast(vc, r);
-        }
-        if (lane == 0) put_g<LOCAL>(dg + 2 * ag, pd, tag);
-        if (stmp) {
-            const u64 t1 = __builtin_amdgcn_s_memtime();
-            t_b += t1 - t0;
-            t0 = t1;
-        }
-        // ---- phase C: poll p, row i+1 and the agents' partials; all loads in flight
-        double pj[TW_NJ];
-        double pdt = 0.0;
-        {
-            u64 g[TW_NJ][4];
-            constexpr int DPL = TW_MAXA / 64;  // partial slots per lane
-            u64 gd[DPL][2];
-#pragma unroll
-            for (int t = 0; t < TW_NJ; ++t) {
-                const int j = lane + 64 * t;
-                if (j > i && j < n) {
-                    g[t][0] = get_g(pg + 2 * j);
-                    g[t][1] = get_g(pg + 2 * j + 1);
-                    g[t][2] = get_g(rg + 2 * j);
-                    g[t][3] = get_g(rg + 2 * j + 1);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < DPL; ++q) {
-                const int ax = lane + 64 * q;
-                if (ax < NA) {
-                    gd[q][0] = get_g(dg + 2 * ax);
-                    gd[q][1] = get_g(dg + 2 * ax + 1);
-                }
-            }
-            u32 spins = 0;
-            for (;;) {
-                bool ok = true;
-#pragma unroll
-                for (int t = 0; t < TW_NJ; ++t) {
-                    const int j = lane + 64 * t;
-                    if (j > i && j < n) {
-#pragma unroll
-                        for (int h = 0; h < 4; ++h)
-                            if ((u32)(g[t][h] >> 32) != tag) {
-                                ok = false;
-                                g[t][h] = get_g((h < 2 ? pg : rg) + 2 * j + (h & 1));
-                            }
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < DPL; ++q) {
-                    const int ax = lane + 64 * q;
-                    if (ax < NA) {
-#pragma unroll
-                        for (int h = 0; h < 2; ++h)
-                            if ((u32)(gd[q][h] >> 32) != tag) {
-                                ok = false;
-                                gd[q][h] = get_g(dg + 2 * ax + h);
-                            }
-                    }
-                }
-                if (__all(ok)) break;
-                if (++spins > EIG_SPIN_LIMIT) {
-                    __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    return;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-#pragma unroll
-            for (int t = 0; t < TW_NJ; ++t) {
-                const int j = lane + 64 * t;
-                const bool act = j > i && j < n;
-                pj[t] = act ? g_val(g[t][0], g[t][1]) : 0.0;
-                y[t] = act ? g_val(g[t][2], g[t][3]) : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < DPL; ++q)
-                if (lane + 64 * q < NA) pdt += g_val(gd[q][0], gd[q][1]);
-            pdt = wave_sum_d(pdt);
-        }
-        if (stmp) {
-            const u64 t1 = __builtin_amdgcn_s_memtime();
-            t_w += t1 - t0;
-            t0 = t1;
-        }
-        const double a2 = -0.5 * tc * pdt;
-        const double v1 = bcast(vc, i + 1);
-        const double w1 = (tc != 0.0) ? bcast(pj, i + 1) + a2 * v1 : 0.0;
-        double xp = 0.0;
-#pragma unroll
-        for (int t = 0; t < TW_NJ; ++t) {
-            const int j = lane + 64 * t;
-            const bool act = j > i && j < n;
-            const double wj = (act && tc != 0.0) ? pj[t] + a2 * vc[t] : 0.0;
-            const double yj = act ? y[t] - v1 * wj - w1 * vc[t] : 0.0;
-            wp[t] = wj;
-            y[t] = yj;
-            if (j >= i + 3 && j < n) xp += yj * yj;
-        }
-        const double dnext = bcast(y, i + 1);
-        if (i + 1 <= n - 2) {
-            const double xn2 = wave_sum_d(xp);
-            const double alpha = bcast(y, i + 2);
-            double bn = alpha, tn = 0.0, scal = 0.0;
-            if (xn2 > 0.0) {
-                bn = -copysign(sqrt(alpha * alpha + xn2), alpha);
-                tn = (bn - alpha) / bn;
-                scal = 1.0 / (alpha - bn);
-            }
-#pragma unroll
-            for (int t = 0; t < TW_NJ; ++t) {
-                const int j = lane + 64 * t;
-                vp[t] = vc[t];  // v_i becomes the previous reflector
-                vc[t] = (j == i + 2) ? 1.0 : ((j > i + 2 && j < n) ? y[t] * scal : 0.0);
-            }
-            if (ag == 0) {
-                if (lane == 0) {
-                    a.d[i + 1] = dnext;
-                    a.e[i + 1] = bn;
-                    a.tau[i + 1] = tn;
-                }
-#pragma unroll
-                for (int t = 0; t < TW_NJ; ++t) {
-                    const int j = lane + 64 * t;
-                    if (j >= i + 2 && j < n) a.refl[(size_t)(i + 1) * lda + j] = vc[t];
-                }
-            }
-            tp = tc;
-            tc = tn;
-        } else if (ag == 0 && lane == 0) {
-            a.d[n - 1] = dnext;
-            a.e[n - 1] = 0.0;
-            a.tau[n - 1] = 0.0;
-        }
-        if (stmp) t_c += __builtin_amdgcn_s_memtime() - t0;
-    }
-    if (stmp) {
-        a.stamps[0] = t_b;
-        a.stamps[1] = t_w;
-        a.stamps[2] = t_c;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1810,16 +1704,6 @@ static void eig_plan(int n, int& nwg, bool& rows_lds, bool& lu_lds)
     lu_lds = sizeof(double) * 10 * (size_t)n <= EIG_LDS_MAX;
 }
 
-extern "C" int scc_sbr_band(int n);
-extern "C" int scc_tridiag_cu_fits(int n);
-extern "C" hipError_t scc_launch_tridiag_cu(const double* A, int n, int lda, double* grows, double* d, double* e,
-                                            double* tau, double* refl, unsigned int* reg, unsigned long long* stamps,
-                                            hipStream_t st);
-extern "C" size_t scc_sbr_scratch_doubles(int n, int lda);
-extern "C" hipError_t scc_launch_sbr_reduce(const double* A, int n, int lda, double* scr, double* d, double* e,
-                                            unsigned long long* stamps, hipStream_t st);
-extern "C" hipError_t scc_launch_sbr_back(double* Zq, int n, int lda, int k, const double* scr, hipStream_t st);
-
 // A non-blocking side stream (and fork / join events) per device for work
 // that overlaps the eigensolver's main chain; created once, never destroyed
 // (process lifetime, like the HIP runtime's own streams).
@@ -1857,7 +1741,7 @@ extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k)
     int nwg;
     bool rl, ll;
     eig_plan(n, nwg, rl, ll);
-    return eig_layout(n, lda, k, nwg, rl, ll).total + scc_sbr_scratch_doubles(n, lda);
+    return eig_layout(n, lda, k, nwg, rl, ll).total;
 }
 
 // direct solver + (for large n) the subspace iteration tried first (scc_subspace.hip)
@@ -1898,42 +1782,6 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
             return hipSuccess;
         }
     }
-    if (scc_sbr_band(n)) {
-        // two-stage reduction (scc_sbr.hip): dense -> band -> tridiagonal, no
-        // per-column hand-off; eigenvectors of the tridiagonal as below, then
-        // the two back-transformations
-        double* sbr = scratch + L.total;
-        if (marks) hipEventRecord(marks[0], st);
-        if ((e = scc_launch_sbr_reduce(A, n, lda, sbr, scratch + L.d, scratch + L.e, stamps, st)) != hipSuccess) return e;
-        if (marks) hipEventRecord(marks[1], st);
-        VecArgs v{};
-        v.d = scratch + L.d;
-        v.e = scratch + L.e;
-        v.n = n;
-        v.lda = lda;
-        v.k = k;
-        v.lu_lds = lu_lds ? 1 : 0;
-        v.lu = scratch + L.lu;
-        v.Zq = scratch + L.zq;
-        v.W = W;
-        v.tnorm = scratch + L.tnorm;
-        v.stamps = stamps;
-        v.xcd = nullptr;
-        v.vcount = flags + 5;
-        v.err = flags + 1;
-        v.bt_none = 1;
-        const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
-        hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
-        if (marks) hipEventRecord(marks[2], st);
-        hipLaunchKernelGGL(k_tri_vectors, dim3(k), dim3(VEC_T), vlds, st, v);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if ((e = scc_launch_sbr_back(v.Zq, n, lda, k, sbr, st)) != hipSuccess) return e;
-        if (marks) hipEventRecord(marks[3], st);
-        if (marks) hipEventRecord(marks[4], st);
-        launch_eig_finish(v.Zq, n, lda, k, W, v.tnorm, Z, st);
-        if (marks) hipEventRecord(marks[5], st);
-        return hipGetLastError();
-    }
     // granule tags restart at 1 every launch
     e = hipMemsetAsync(scratch + L.pg, 0, sizeof(double) * (L.zq - L.pg), st);
     if (e != hipSuccess) return e;
@@ -1971,39 +1819,16 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 64;
     }
-    // opt-in (SCC_EIG_CU=1, n <= 336): the whole matrix resident in ONE compute
-    // unit (scc_tridiag_cu.hip), no cross-CU hand-off, fixed reduction order
-    // (bit-reproducible).  Measured 4x SLOWER than the kernels below (n = 323:
-    // 4.48 vs 1.07 ms; n = 64: 0.35 vs 0.20 ms): the per-row latency chains of
-    // one workgroup cost more than the per-column hand-off they remove.
-    const char* cu_env = getenv("SCC_EIG_CU");
-    const bool one_cu = scc_tridiag_cu_fits(n) && cu_env && *cu_env && atoi(cu_env) != 0;
-    const char* wa_env = getenv("SCC_EIG_WAVE");
-    const bool wave_agents = (wa_env && *wa_env) ? atoi(wa_env) != 0 : false;  // measured slower (polling load)
-    // wave agents: the planned participants' rows in LDS (HBM fall-back in the kernel)
-    const size_t wa_lds = sizeof(double) * (size_t)TRI_W * ((n + TRI_W * nwg - 1) / (TRI_W * nwg)) * n;
-    // the last TT_MMAX columns (all of them when n <= TT_MMAX) in ONE
-    // workgroup with the trailing block in LDS (k_tridiag_tail): no hand-off
-    // there; SCC_EIG_TAIL=0 keeps the hand-off kernel for every column
+    // opt-in (SCC_EIG_TAIL=1): the last TT_MMAX columns (all of them when n <=
+    // TT_MMAX) in ONE workgroup with the trailing block in registers
+    // (k_tridiag_tail): no hand-off there, but measured slower than the
+    // hand-off kernel at every n (one workgroup's per-column
+    // latency chain exceeds the hand-off it removes)
     const char* tail_env = getenv("SCC_EIG_TAIL");
-    const bool use_tail = !one_cu && !wave_agents && n > 2 && !(tail_env && *tail_env && atoi(tail_env) == 0);
+    const bool use_tail = n > 2 && tail_env && *tail_env && atoi(tail_env) != 0;
     if (use_tail) t.stop = std::max(0, n - TT_MMAX);
     if (use_tail && t.stop == 0) {
         // nothing for the hand-off kernel
-    } else if (one_cu) {
-        e = scc_launch_tridiag_cu(A, n, lda, t.work, t.d, t.e, t.tau, t.refl, t.reg, stamps, st);
-        if (e != hipSuccess) return e;
-    } else if (wave_agents && n <= 64 * TW_NJ && wa_lds <= EIG_LDS_MAX && nwg * TRI_W <= TW_MAXA) {
-        size_t l2 = wa_lds < 82 * 1024 ? 82 * 1024 : wa_lds;
-        t.lds_rows_cap = (int)(l2 / sizeof(double));
-        if (t.xcd_local) {
-            const int grid = std::min(8 * nwg, cus);
-            hipFuncSetAttribute((const void*)k_tridiag_wa<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
-            hipLaunchKernelGGL(k_tridiag_wa<true>, dim3(grid), dim3(TRI_T), l2, st, t);
-        } else {
-            hipFuncSetAttribute((const void*)k_tridiag_wa<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2);
-            hipLaunchKernelGGL(k_tridiag_wa<false>, dim3(nwg), dim3(TRI_T), l2, st, t);
-        }
     } else {
         // register rows for n <= 896 (6, 8 or 14 column slots per lane; the rest
         // of a workgroup's rows in LDS), else LDS / HBM rows
@@ -2028,10 +1853,8 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (use_tail) {
         const int m = n - t.stop;
-        const size_t tlds = tt_lds_bytes(m);
-        hipFuncSetAttribute((const void*)k_tridiag_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tlds);
-        hipLaunchKernelGGL(k_tridiag_tail, dim3(1), dim3(TT_T), tlds, st, t.stop > 0 ? t.tail : A,
-                           t.stop > 0 ? m : lda, n, t.stop, t.d, t.e, t.tau, t.refl, lda);
+        hipLaunchKernelGGL(k_tridiag_tail, dim3(1), dim3(TR_T), 0, st, t.stop > 0 ? t.tail : A,
+                           t.stop > 0 ? m : lda, n, t.stop, t.d, t.e, t.tau, t.refl, lda, stamps);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (marks) hipEventRecord(marks[1], st);

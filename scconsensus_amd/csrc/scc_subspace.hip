@@ -20,7 +20,8 @@
 // ~ that / (lambda_15 - lambda_16)); otherwise — slow convergence (config B:
 // lambda_65 / lambda_15 = 0.88, the 15th eigenvalue inside the noise bulk), a
 // rank-deficient Gram (Cholesky breakdown) — the caller runs the direct solver.
-// Every reduction has a fixed order (deterministic, rank-identical in a
+// A deflated power check on the basis' complement (k_si_guard) rejects a
+// result that missed a top eigenpair.  Every reduction has a fixed order (deterministic, rank-identical in a
 // sharded job).  Output layout as scc_launch_eigen_topk: Z[u*16 + q], W[q],
 // largest-magnitude component of each vector positive.
 #include "scc_common.hpp"
@@ -194,15 +195,119 @@ __global__ void __launch_bounds__(64) k_si_apply(const double* __restrict__ W, c
 }
 
 // deterministic pseudo-random start block
-__global__ void k_si_init(int n, double* __restrict__ V)
+// (rows >= live are zero: a test hook, SCC_EIG_SI_INIT_ROWS, that lets a test
+// hide part of the spectrum from the iteration to exercise k_si_guard)
+__global__ void k_si_init(int n, int live, double* __restrict__ V)
 {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n * SI_B) return;
+    if (e / SI_B >= live) {
+        V[e] = 0.0;
+        return;
+    }
     unsigned h = (unsigned)e * 2654435761u ^ 0x9e3779b9u;
     h ^= h >> 13;
     h *= 0x5bd1e995u;
     h ^= h >> 15;
     V[e] = (double)(h & 0xffffff) / 16777216.0 - 0.5;
+}
+
+// Guard against a missed top eigenpair (residuals only prove that each Ritz
+// pair is close to SOME eigenpair): power iteration on the complement of the
+// final 64-column basis, (I - V V^T) C (I - V V^T), from a start vector
+// independent of the iteration's start block.  If the block holds the top 64
+// eigenvectors, its largest eigenvalue is ~lambda_65 < theta_k; a missed
+// eigenvalue above theta_k would dominate after SI_GUARD_IT products (its
+// share grows like (lambda / lambda_65)^it).  Flag bit 8 when the Rayleigh
+// quotient reaches theta_k.  One workgroup (n <= SI_GUARD_NMAX), fixed-order
+// sums.
+#define SI_GUARD_T 1024
+#define SI_GUARD_W (SI_GUARD_T / 64)
+#define SI_GUARD_IT 24
+#define SI_GUARD_NMAX 8192
+__device__ inline double si_wave_sum(double v)
+{
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ inline double si_block_sum(double v, double* red)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    v = si_wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int q = 0; q < SI_GUARD_W; ++q) t += red[q];
+    return t;
+}
+
+// x -= V (V^T x), twice
+__device__ inline void si_deflate(double* x, const double* __restrict__ V, int n, double* pr)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int j = w; j < SI_B; j += SI_GUARD_W) {
+            double sacc = 0.0;
+            for (int i = lane; i < n; i += 64) sacc = fma(V[(size_t)i * SI_B + j], x[i], sacc);
+            sacc = si_wave_sum(sacc);
+            if (lane == 0) pr[j] = sacc;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) {
+            double sacc = x[i];
+            for (int j = 0; j < SI_B; ++j) sacc = fma(-V[(size_t)i * SI_B + j], pr[j], sacc);
+            x[i] = sacc;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(SI_GUARD_T) k_si_guard(const double* __restrict__ C, int ldc, int n,
+                                                         const double* __restrict__ V,
+                                                         const double* __restrict__ theta, int k,
+                                                         u32* __restrict__ flag)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ double red[SI_GUARD_W];
+    __shared__ double pr[SI_B];
+    double* x = sm;
+    double* y = x + n;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < n; i += SI_GUARD_T) {
+        unsigned h = (unsigned)i * 0x85ebca6bu ^ 0xc2b2ae35u;
+        h ^= h >> 16;
+        h *= 0x27d4eb2du;
+        h ^= h >> 15;
+        x[i] = (double)(h & 0xffffff) / 16777216.0 - 0.5;
+    }
+    __syncthreads();
+    si_deflate(x, V, n, pr);
+    double rho = 0.0;
+    for (int it = 0; it < SI_GUARD_IT; ++it) {
+        double ss = 0.0;
+        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) ss = fma(x[i], x[i], ss);
+        ss = si_block_sum(ss, red);
+        if (!(ss > 0.0)) return;  // the complement is empty to working precision: nothing missed
+        const double inv = 1.0 / sqrt(ss);
+        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) x[i] *= inv;
+        __syncthreads();
+        for (int i = w; i < n; i += SI_GUARD_W) {  // y = C x, a wave per row
+            double sacc = 0.0;
+            for (int j = lane; j < n; j += 64) sacc = fma(C[(size_t)i * ldc + j], x[j], sacc);
+            sacc = si_wave_sum(sacc);
+            if (lane == 0) y[i] = sacc;
+        }
+        __syncthreads();
+        si_deflate(y, V, n, pr);
+        double xy = 0.0;
+        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) xy = fma(x[i], y[i], xy);
+        rho = si_block_sum(xy, red);
+        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) x[i] = y[i];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && !(rho < theta[k - 1])) atomicOr(flag, 8u);
 }
 
 // H = (V^T W + (V^T W)^T) / 2
@@ -367,7 +472,9 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     const int every = (oe && *oe) ? std::max(1, atoi(oe)) : 4;
     double* a = V;   // the current block
     double* b = Wm;  // the product
-    hipLaunchKernelGGL(k_si_init, dim3((n * SI_B + 255) / 256), dim3(256), 0, st, n, b);
+    const char* ie = getenv("SCC_EIG_SI_INIT_ROWS");
+    const int live = (ie && *ie) ? std::max(SI_B, std::min(n, atoi(ie))) : n;
+    hipLaunchKernelGGL(k_si_init, dim3((n * SI_B + 255) / 256), dim3(256), 0, st, n, live, b);
     orth(b, a);
     for (int it = 0; it < iters; ++it) {
         hipLaunchKernelGGL(k_si_mul, gmul, dim3(256), 0, st, C, ldc, n, a, b);
@@ -391,6 +498,12 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     hipLaunchKernelGGL(k_si_check, dim3(1), dim3(64), 0, st, rpart, mpart, nblk, theta, k, SI_TOL, sgn, Wout, flag);
     hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, st, Z, sgn, n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (n <= SI_GUARD_NMAX) {  // no top eigenpair missed (bit 8); beyond: the residual test alone
+        const size_t glds = sizeof(double) * 2 * (size_t)n;
+        hipFuncSetAttribute((const void*)k_si_guard, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds);
+        hipLaunchKernelGGL(k_si_guard, dim3(1), dim3(SI_GUARD_T), glds, st, C, ldc, n, a, theta, k, flag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     u32 h[2] = {0, 0};
     if ((e = hipMemcpyAsync(&h[0], flag, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if (inner_err && (e = hipMemcpyAsync(&h[1], inner_err, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess)

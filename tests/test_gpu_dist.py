@@ -80,14 +80,14 @@ def test_dist_packed_order_small(eng):
     np.testing.assert_allclose(dist, [1, 3, 6, 2, 5, 3], atol=1e-12)
 
 
-@pytest.mark.parametrize("sbr", ["0", "1"])
+@pytest.mark.parametrize("tail", ["0", "1"])
 @pytest.mark.parametrize("n", [2, 3, 5, 8, 17, 40, 130, 700])
-def test_eigensolver_sizes(eng, n, sbr, monkeypatch):
-    """Multi-workgroup tridiagonalisation + per-eigenpair vectors at many |U|
-    (workgroup counts 2..70, rows in LDS) against numpy's exact SVD; the
-    one-stage solver (default) and the opt-in two-stage path (48 <= n <= 1026)."""
+def test_eigensolver_sizes(eng, n, tail, monkeypatch):
+    """Tridiagonalisation + per-eigenpair vectors at many |U| against numpy's
+    exact SVD: the hand-off kernel for every column (the default, workgroup
+    counts 2..70, rows in LDS) and the opt-in register tail (SCC_EIG_TAIL=1)."""
     from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SBR", sbr)
+    monkeypatch.setenv("SCC_EIG_TAIL", tail)
     monkeypatch.setenv("SCC_EIG_SI", "0")  # the direct solvers (subspace iteration: its own tests)
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
@@ -132,66 +132,44 @@ def test_eigensolver_rows_beyond_lds(eng, monkeypatch):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
-@pytest.mark.parametrize("n", [48, 64, 97, 200, 323, 586, 587, 845, 1026])
-def test_two_stage_eigensolver(eng, n, monkeypatch):
-    """The two-stage reduction (scc_sbr.hip, SCC_EIG_SBR=1: dense -> band of 16
-    (n <= 586) or 8 columns -> tridiagonal) against numpy's exact SVD, and
-    against the one-stage solver on the PCA scores."""
+@pytest.mark.parametrize("tail", ["0", "1"])
+def test_rank_deficient_and_repeated(eng, tail, monkeypatch):
+    """Identical genes (zero-norm columns: tau = 0 reflectors) and exactly
+    repeated eigenvalues inside the top 15, n = 90 and 300, with and without
+    the register tail."""
     from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SBR", "1")
+    monkeypatch.setenv("SCC_EIG_TAIL", tail)
     monkeypatch.setenv("SCC_EIG_SI", "0")
-    rng = np.random.default_rng(300 + n)
-    X = rng.standard_normal((n, 1000)) * np.linspace(3.0, 0.5, n)[:, None]
-    X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 1000)) * 4.0
-    ds = eng.dataset_dense(X)
-    g = np.arange(n)
-    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    ref = O.dist_euclidean(O.pca_scores(X, g))
-    assert np.max(np.abs(dist - ref)) < 1e-5
-    S2 = eng.last_pca_scores(X.shape[1])
-    monkeypatch.setenv("SCC_EIG_SBR", "0")
-    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    S1 = eng.last_pca_scores(X.shape[1])
-    # two exact methods: they agree to rounding amplified by the 15/16 gap
-    assert np.max(np.abs(dist - d1)) < 1e-6
-    np.testing.assert_allclose(np.abs(S2), np.abs(S1), rtol=0, atol=1e-7 * np.abs(S1).max())
-
-
-def test_two_stage_rank_deficient_and_repeated(eng, monkeypatch):
-    """Identical genes (rank-deficient panels: zero-norm reflectors) and exactly
-    repeated eigenvalues inside the top 15, n = 90 (two-stage path)."""
-    from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SBR", "1")
-    rng = np.random.default_rng(8)
-    n, N = 90, 600
-    sv = np.array([9.0] * 3 + [7.0] * 4 + [5.0] * 2 + [4.0] * 6 + [1.0] * (n - 15))
-    Q, _ = np.linalg.qr(rng.standard_normal((N, n)))
-    Q -= Q.mean(axis=0)
-    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
-    X = (Q @ np.diag(sv) @ V.T).T
-    ds = eng.dataset_dense(X)
-    g = np.arange(n)
-    assert np.max(np.abs(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID) - O.dist_euclidean(O.pca_scores(X, g)))) < 1e-5
-    X2 = np.concatenate([X[:30], X[:30], X[:30]])  # 90 genes, rank <= 30
-    ds2 = eng.dataset_dense(X2)
-    dist = eng.distance(ds2, g, nat.SCC_DIST_PCA_EUCLID)
-    assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
+    for n in (90, 300):
+        rng = np.random.default_rng(8 + n)
+        N = 700
+        sv = np.array([9.0] * 3 + [7.0] * 4 + [5.0] * 2 + [4.0] * 6 + [1.0] * (n - 15))
+        Q, _ = np.linalg.qr(rng.standard_normal((N, n)))
+        Q -= Q.mean(axis=0)
+        V, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        X = (Q @ np.diag(sv) @ V.T).T
+        ds = eng.dataset_dense(X)
+        g = np.arange(n)
+        assert np.max(np.abs(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID) - O.dist_euclidean(O.pca_scores(X, g)))) < 1e-5
+        X2 = np.concatenate([X[: n // 3]] * 3)  # rank <= n / 3
+        ds2 = eng.dataset_dense(X2)
+        dist = eng.distance(ds2, g, nat.SCC_DIST_PCA_EUCLID)
+        assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
 
 
 @pytest.mark.parametrize("xcd", ["0", "1"])
-@pytest.mark.parametrize("wave", ["0", "1"])
+@pytest.mark.parametrize("tail", ["0", "1"])
 @pytest.mark.parametrize("n,nwg", [(323, 8), (323, 32), (323, 64), (500, 48), (700, 70), (700, 256), (1500, 40),
                                    (1500, 150), (2100, 210)])
-def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, wave, monkeypatch):
+def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, tail, monkeypatch):
     """Same eigenpairs for any number of tridiagonalisation workgroups, either
-    hand-off (cross-XCD write-through or one-XCD L2), either kernel (wave
-    agents or workgroup barriers), rows in LDS or in HBM."""
+    hand-off (cross-XCD write-through or one-XCD L2), with or without the
+    register tail, rows in LDS or in HBM."""
     from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SBR", "0")  # the one-stage solver
     monkeypatch.setenv("SCC_EIG_SI", "0")
     monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
     monkeypatch.setenv("SCC_EIG_XCD", xcd)
-    monkeypatch.setenv("SCC_EIG_WAVE", wave)
+    monkeypatch.setenv("SCC_EIG_TAIL", tail)
     rng = np.random.default_rng(11)
     X = rng.standard_normal((n, 900)) * np.linspace(3.0, 0.5, n)[:, None]
     X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 900)) * 4.0
@@ -202,62 +180,12 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, wave, monkeypatch):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
-@pytest.mark.parametrize("n", [2, 3, 17, 64, 65, 128, 150, 191, 200, 241, 250, 300, 323, 336])
-def test_one_cu_tridiagonalisation(eng, n, monkeypatch):
-    """Single-CU tridiagonalisation (scc_tridiag_cu.hip, n <= 336: rows in
-    registers, in LDS and, past n ~ 190, in a global scratch store) against the
-    exact SVD and the multi-workgroup kernel; bit-identical from run to run
-    (fixed reduction order)."""
-    from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SBR", "0")
-    rng = np.random.default_rng(500 + n)
-    N = 800
-    X = rng.standard_normal((n, N)) * np.linspace(3.0, 0.5, n)[:, None]
-    k = min(20, n)
-    X[:k] += rng.standard_normal((k, 1)) * rng.standard_normal((1, N)) * 4.0
-    ds = eng.dataset_dense(X)
-    g = np.arange(n)
-    monkeypatch.setenv("SCC_EIG_CU", "1")
-    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    d1b = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    assert np.array_equal(d1, d1b)
-    ref = O.dist_euclidean(O.pca_scores(X, g))
-    assert np.max(np.abs(d1 - ref)) < 1e-5
-    monkeypatch.setenv("SCC_EIG_CU", "0")
-    d0 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
-    assert np.max(np.abs(d1 - d0)) < 1e-6
-
-
-@pytest.mark.parametrize("n", [90, 300])
-def test_one_cu_rank_deficient_and_repeated(eng, n, monkeypatch):
-    """One-CU path: exactly repeated eigenvalues in the top 15, then identical
-    genes (zero-norm columns: tau = 0 reflectors), with rows in every store."""
-    from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_SBR", "0")
-    monkeypatch.setenv("SCC_EIG_CU", "1")
-    rng = np.random.default_rng(9 + n)
-    N = 700
-    sv = np.array([9.0] * 3 + [7.0] * 4 + [5.0] * 2 + [4.0] * 6 + [1.0] * (n - 15))
-    Q, _ = np.linalg.qr(rng.standard_normal((N, n)))
-    Q -= Q.mean(axis=0)
-    V, _ = np.linalg.qr(rng.standard_normal((n, n)))
-    X = (Q @ np.diag(sv) @ V.T).T
-    g = np.arange(n)
-    ds = eng.dataset_dense(X)
-    assert np.max(np.abs(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID) - O.dist_euclidean(O.pca_scores(X, g)))) < 1e-5
-    X2 = np.concatenate([X[: n // 3]] * 3)  # rank <= n / 3
-    ds2 = eng.dataset_dense(X2)
-    dist = eng.distance(ds2, g, nat.SCC_DIST_PCA_EUCLID)
-    assert np.max(np.abs(dist - O.dist_euclidean(O.pca_scores(X2, g)))) < 1e-5
-
-
-@pytest.mark.parametrize("cols", ["16", "32", "64", "128", "256"])
 @pytest.mark.parametrize("f32", [False, True])
-def test_distance_kernels_agree(eng, cols, f32, monkeypatch):
-    """The three distance store kernels (SCC_DIST_KERNEL 1 = workgroup-staged
-    windows, plain or nontemporal stores, 2 = wave windows, 0 = unaligned tiles) give bit-identical packed
-    output (same arithmetic, only the store pattern differs), over the full
-    vector and over column slices whose starts are not line-aligned."""
+def test_distance_kernels_agree(eng, f32, monkeypatch):
+    """The distance store kernel's tile widths (64 / 128 columns) and store
+    kinds (plain / nontemporal) give bit-identical packed output (same
+    arithmetic, only the store pattern differs), over the full vector and over
+    column slices whose starts are not line-aligned."""
     from scconsensus_amd import _native as nat
     rng = np.random.default_rng(41)
     G, N = 60, 1337
@@ -265,10 +193,9 @@ def test_distance_kernels_agree(eng, cols, f32, monkeypatch):
     X[:, 7] = X[:, 8]  # two identical cells: a zero distance (difference form)
     ds = eng.dataset_dense(X)
     g = np.arange(0, G, 2)
-    monkeypatch.setenv("SCC_DIST_COLS", cols)
     outs = []
-    for kind, nt in [("1", "1"), ("1", "0"), ("2", "1"), ("0", "1")]:
-        monkeypatch.setenv("SCC_DIST_KERNEL", kind)
+    for cols, nt in [("64", "1"), ("64", "0"), ("128", "1"), ("128", "0")]:
+        monkeypatch.setenv("SCC_DIST_COLS", cols)
         monkeypatch.setenv("SCC_DIST_NT", nt)
         outs.append(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID, f32=f32))
     monkeypatch.setenv("SCC_DIST_NT", "1")
@@ -279,8 +206,8 @@ def test_distance_kernels_agree(eng, cols, f32, monkeypatch):
     for c_lo, c_hi in [(5, 77), (700, 1336)]:
         lo = c_lo * (2 * N - c_lo - 1) // 2
         hi = c_hi * (2 * N - c_hi - 1) // 2
-        for kind in ["2", "1"]:
-            monkeypatch.setenv("SCC_DIST_KERNEL", kind)
+        for cols in ["64", "128"]:
+            monkeypatch.setenv("SCC_DIST_COLS", cols)
             part = eng.distance_cols(ds, g, c_lo, c_hi, nat.SCC_DIST_PCA_EUCLID, f32=f32)
             assert np.array_equal(part, outs[0][lo:hi])
 
@@ -342,6 +269,38 @@ def test_subspace_iteration_falls_back(eng, case, monkeypatch, capfd):
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
 
+
+def test_subspace_guard_catches_missed_eigenpair(eng, monkeypatch, capfd):
+    """the residual test alone accepts Ritz pairs that are exact
+    eigenpairs but not the TOP ones.  A block-diagonal Gram (genes 0..399 and
+    400..499 on disjoint cells, zero-mean rows: centring keeps the blocks
+    apart) whose second block holds the largest eigenvalue, with the start
+    block's rows >= 400 zeroed (test hook): the iteration never sees that
+    block, every residual passes, and the deflated power check (flag bit 8)
+    must reject the result so the direct solver answers."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(12)
+    n, N = 500, 3000
+    X = np.zeros((n, N))
+    X[:400, :1500] = _spiky(400, 1500, 30, 5)
+    X[400:, 1500:] = rng.standard_normal((100, 1500)) * 0.3
+    X[400:, 1500:] += rng.standard_normal((100, 1)) * rng.standard_normal((1, 1500)) * 40.0  # the top eigenvalue
+    X[:400, :1500] -= X[:400, :1500].mean(axis=1, keepdims=True)
+    X[400:, 1500:] -= X[400:, 1500:].mean(axis=1, keepdims=True)
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    monkeypatch.setenv("SCC_EIG_SI_LOG", "1")
+    monkeypatch.setenv("SCC_EIG_SI_INIT_ROWS", "400")
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    err = capfd.readouterr().err
+    assert f"[scc si] n={n}" in err, err
+    flag = int(err.split("flag=")[1].split()[0])
+    assert flag & 8 and not flag & 2, err  # residuals passed, the guard rejected
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
+    monkeypatch.delenv("SCC_EIG_SI_INIT_ROWS")
+    d2 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)  # the normal start (whichever path answers)
+    assert np.max(np.abs(d2 - ref)) < 1e-5
 
 
 def test_gather_wide_union_fallback(eng):

@@ -1,10 +1,10 @@
-"""The PCA eigensolver's one-workgroup tail (k_tridiag_tail: the last <= 196
-columns of the Householder tridiagonalisation with the trailing block in LDS,
-all columns when |U| <= 196) against the exact SVD, against the hand-off
-kernel alone (SCC_EIG_TAIL=0), and run to run: the tridiagonalisation's
-reductions now have a fixed shape (no dependence on how many workgroups
-joined the hand-off), so the distance is bit-identical across repeats
-(Fast:398-400)."""
+"""The PCA eigensolver's opt-in one-workgroup tail (SCC_EIG_TAIL=1,
+k_tridiag_tail: the last <= 256 columns of the Householder tridiagonalisation
+with the trailing block in registers, all columns when |U| <= 256) against the
+exact SVD and against the hand-off kernel alone (the default), and run to run:
+the tridiagonalisation's reductions have a fixed shape (no dependence on how
+many workgroups joined the hand-off), so the distance is bit-identical across
+repeats (Fast:398-400)."""
 import numpy as np
 import pytest
 
@@ -30,9 +30,10 @@ def _spiked(n, N, seed):
     return X
 
 
-@pytest.mark.parametrize("n", [3, 4, 17, 64, 195, 196, 197, 230, 323, 399])
+@pytest.mark.parametrize("n", [3, 4, 17, 64, 195, 196, 197, 230, 255, 256, 257, 323, 399])
 def test_tail_sizes(eng, n, monkeypatch):
     monkeypatch.setenv("SCC_EIG_SI", "0")  # the direct solver at every n
+    monkeypatch.setenv("SCC_EIG_TAIL", "1")
     X = _spiked(n, 700, 300 + n)
     ds = eng.dataset_dense(X)
     g = np.arange(n)
@@ -50,6 +51,7 @@ def test_tail_agrees_with_handoff_kernel(eng, n, monkeypatch):
     X = _spiked(n, 900, 7 + n)
     ds = eng.dataset_dense(X)
     g = np.arange(n)
+    monkeypatch.setenv("SCC_EIG_TAIL", "1")
     a = eng.distance(ds, g)
     monkeypatch.setenv("SCC_EIG_TAIL", "0")
     b = eng.distance(ds, g)
