@@ -21,9 +21,7 @@ for s in "$@"; do
     benchq) step benchq 600 python bench.py --no-cpu-baseline ;;
     stamps) SCC_STAMPS=1 step stamps 300 python scripts/diag_gpu.py B ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;
-    eigtail) step eigtail 300 python -u scripts/eig_tail_time.py 64,150,200,256,257,323 ;;
-    teig) step teig 600 python -u -m pytest tests/test_gpu_eigen_tail.py tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread ;;
-    tstamps) SCC_STAMPS=1 step tstamps 300 python -u scripts/eig_tail_stamps.py 64,128,256,323 ;;
+    tdist) step tdist 600 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

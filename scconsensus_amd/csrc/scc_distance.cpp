@@ -347,8 +347,6 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
                         h[8], h[9], h[10], h[11]);
                 fprintf(stderr, "[scc stamps] block back-transform: stage %llu, V^T Y %llu, T W %llu, Y update %llu, "
                         "load %llu cycles\n", h[12], h[13], h[14], h[15], h[16]);
-                fprintf(stderr, "[scc stamps] register tail (wave 0, all columns): pass 1 %llu, reduce %llu, "
-                        "pass 2 %llu, capture %llu cycles\n", h[17], h[18], h[19], h[20]);
             }
             if (marks) {
                 c->pending.push_back({"eig_tridiag", mk[0], mk[1]});

@@ -122,8 +122,6 @@ struct TriArgs {
     u32* counter;     // (unused)
     u64* stamps;      // diagnostic: WG 0 per-phase cycle sums (nullptr normally)
     u32* err;         // 1: a hand-off timed out
-    int stop;         // columns [0, stop) only; stop < n - 1: then the trailing block
-    double* tail;     // A^(stop)[stop:, stop:] (lower part, row-major, ld n - stop) for k_tridiag_tail
 };
 
 // Householder reflector from y[lo..n-1] (alpha = y[lo], x = y[lo+1..]), LAPACK
@@ -259,8 +257,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     __syncthreads();
     u64 t_b = 0, t_w = 0, t_c = 0, t_r = 0, t0 = 0;
     const bool stmp = a.stamps && me == 0 && tid == 0;
-    const int ilast = min(n - 2, a.stop - 1);
-    for (int i = 0; i <= ilast; ++i) {
+    for (int i = 0; i <= n - 2; ++i) {
         const int par = i & 1;
         const u32 tag = (u32)(i + 1);
         if (stmp) t0 = __builtin_amdgcn_s_memtime();
@@ -484,42 +481,6 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
         __syncthreads();
         if (stmp) t_c += __builtin_amdgcn_s_memtime() - t0;
     }
-    if (a.stop < n - 1) {
-        // hand the trailing block A^(stop)[stop:, stop:] to k_tridiag_tail: row
-        // `stop` is y (updated in phase C); the other own rows still owe the
-        // update of column stop - 1 (v = vp, w = wp, applied lazily in phase B)
-        const int i0 = a.stop, mt = n - i0;
-        const bool prev = tp != 0.0;
-        if (me == 0 && tid == 0) a.tail[0] = y[i0];
-        const int l0 = (i0 + 1 > me) ? (i0 + 1 - me + nwg - 1) / nwg : 0;
-        if (nreg > 0) {
-#pragma unroll
-            for (int m = 0; m < TRI_MR; ++m) {
-                const int l = wv + TRI_W * m;
-                if (l >= nreg || l < l0) continue;
-                const int r = me + nwg * l;
-                const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
-#pragma unroll
-                for (int t = 0; t < NJA; ++t) {
-                    const int j = lane + 64 * t;
-                    if (j >= i0 && j <= r) {
-                        const double x = prev ? fma(-vr, wp[j], fma(-wr, vp[j], rr[m][t])) : rr[m][t];
-                        a.tail[(size_t)(r - i0) * mt + (j - i0)] = x;
-                    }
-                }
-            }
-        }
-        for (int l = max(l0, nreg) + wv; l < nown; l += TRI_W) {
-            const int r = me + nwg * l;
-            const double* row = rows + (size_t)(l - nreg) * n;
-            const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
-            for (int j = i0 + lane; j <= r; j += 64) {
-                double x = row[j];
-                if (prev) x = fma(-vr, wp[j], fma(-wr, vp[j], x));
-                a.tail[(size_t)(r - i0) * mt + (j - i0)] = x;
-            }
-        }
-    }
     if (stmp) {
         a.stamps[0] = t_b;
         a.stamps[1] = t_w;
@@ -528,293 +489,6 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
     }
 }
 
-// ---------------------------------------------------------------------------
-// 1b. the tail of the tridiagonalisation in ONE workgroup (dsytd2, lower):
-// columns [i0, n - 1) of A^(i0)[i0:, i0:] (m = n - i0 <= TT_MMAX), the lower
-// triangle of the trailing block resident in REGISTERS.  Wave w owns rows
-// r = w + 8 s (row slot s); lane l holds columns l + 64 t of each (column slot
-// t <= r / 64, a compile-time triangle: 80 doubles per lane at m = 256).  A
-// column costs three workgroup barriers and two passes over the registers:
-//   pass 1  y = A22 v: row sums (a 4-row lane transpose-reduce per wave) and
-//           per-wave column partials (the symmetric half) into LDS     | B1
-//   reduce  thread x: y_x in a fixed order, p_x = tau y_x, p.v partials  | B2
-//   pass 2  A22 -= v w^T + w v^T; the owners of the next column keep its
-//           updated entries and |x|^2 partials for the next reflector    | B3
-// Every sum has a fixed shape, so the bits do not depend on scheduling.  No
-// hand-off latency, and no LDS traffic for the matrix: the old LDS-resident
-// tail (4 threads per row, dependent LDS chains) took 6.8 us per column.
-// Outputs as k_tridiag (d, e, tau, reflector rows).
-#define TR_W 8
-#define TR_T (TR_W * 64)
-#define TT_MMAX 256
-#define TR_S (TT_MMAX / TR_W)  // row slots per wave
-#define TR_CS (TT_MMAX / 64)   // column slots
-#define TR_P (64 / TR_W)  // row slots per step of the column-slot count
-// column slots of row slot s (rows w + 8 s <= 8 s + 7), and the register offset
-// of slot s: closed forms, so unrolled loops index the array with constants
-__host__ __device__ constexpr int tr_ts(int s) { return s / TR_P + 1; }
-__host__ __device__ constexpr int tr_off(int s)
-{
-    return s + TR_P * (s / TR_P) * (s / TR_P - 1) / 2 + (s - TR_P * (s / TR_P)) * (s / TR_P);
-}
-static_assert(TR_S <= 64 && (TR_S & (TR_S - 1)) == 0, "row slots fit the lanes");
-static_assert(tr_off(1) == 1 && tr_off(8) == 8 && tr_off(9) == 10 && tr_off(16) == 24 && tr_off(TR_S) == 80,
-              "register triangle layout");
-
-struct TrLds {
-    double xcol[2][TT_MMAX];   // the captured column below its diagonal (double-buffered)
-    double pp[TT_MMAX];        // p = tau A22 v
-    double rows[TT_MMAX];      // row sums of pass 1
-    double colp[TR_W][TT_MMAX];  // per-wave column partials of pass 1
-    double redx[TR_W], redp[TR_W];
-    double diag;
-};
-
-__global__ void __launch_bounds__(TR_T) k_tridiag_tail(const double* __restrict__ src, int lds, int n, int i0,
-                                                       double* __restrict__ d, double* __restrict__ e,
-                                                       double* __restrict__ tau, double* __restrict__ refl, int lda,
-                                                       unsigned long long* __restrict__ stamps)
-{
-    __shared__ TrLds S;
-    // diagnostic (stamps != nullptr): wave 0's cycles per phase, summed over the columns
-    const bool stmp = stamps && threadIdx.x == 0;
-    unsigned long long ts0 = 0, tp1 = 0, tpr = 0, tp2 = 0, tpc = 0;
-    const int m = n - i0;
-    const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
-    // xcol entries at or above the current subdiagonal and past m stay 0, and
-    // pp is 0 outside the trailing block, so v and w vanish there and dead
-    // rows / columns need no masks (only the upper part of each diagonal slot)
-    for (int x = tid; x < TT_MMAX; x += TR_T) {
-        S.xcol[0][x] = 0.0;
-        S.xcol[1][x] = 0.0;
-        S.pp[x] = 0.0;
-    }
-    double a[tr_off(TR_S)];
-    // the lower triangle (clamped loads, then a select: the whole batch in flight)
-#pragma unroll
-    for (int s = 0; s < TR_S; ++s) {
-        const int r = w + TR_W * s;
-        const int rc = r < m ? r : m - 1;
-#pragma unroll
-        for (int t = 0; t < tr_ts(s); ++t) {
-            const int c = lane + 64 * t;
-            const double x = src[(size_t)rc * lds + (c <= rc ? c : rc)];
-            a[tr_off(s) + t] = (r < m && c <= r) ? x : 0.0;
-        }
-    }
-    __syncthreads();
-    {  // column 0: its diagonal, the entries below and their |x|^2 past the first
-        double part = 0.0;
-        if (lane == 0) {
-#pragma unroll
-            for (int s = 0; s < TR_S; ++s) {
-                const int r = w + TR_W * s;
-                const double x = a[tr_off(s)];
-                if (r == 0) S.diag = x;
-                else if (r < m) {
-                    S.xcol[0][r] = x;
-                    if (r >= 2) part = fma(x, x, part);
-                }
-            }
-            S.redx[w] = part;
-        }
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int o = 0; o <= m - 2; ++o) {
-        const int i = i0 + o;
-        double xn2 = 0.0;
-#pragma unroll
-        for (int v = 0; v < TR_W; ++v) xn2 += S.redx[v];  // fixed order: identical in every thread
-        const double* xc = S.xcol[buf];
-        // every LDS value this column needs, in one batch: alpha, the 4 column
-        // entries of this lane and (lane s < TR_S) the entry of row slot s
-        const double alpha = xc[o + 1];
-        double xcl[TR_CS];
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) xcl[t] = xc[lane + 64 * t];
-        const int rl = w + TR_W * (lane & (TR_S - 1));  // this lane's row slot (lanes >= TR_S repeat)
-        const double xrl = xc[rl];
-        double beta = alpha, tv = 0.0, scal = 0.0;
-        if (xn2 > 0.0) {
-            beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-            tv = (beta - alpha) / beta;
-            scal = 1.0 / (alpha - beta);
-        }
-        if (tid == 0) {
-            d[i] = S.diag;
-            e[i] = beta;
-            tau[i] = tv;
-        }
-        double vc[TR_CS];
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) vc[t] = lane + 64 * t == o + 1 ? 1.0 : xcl[t] * scal;
-        const double vrl = rl == o + 1 ? 1.0 : xrl * scal;  // v of this lane's row slot
-        // a row slot's value, wave-uniform, from the lane that holds it
-        auto slot_val = [&](double x, int s) {
-            const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
-            const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, s);
-            const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), s);
-            return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-        };
-        // ---- pass 1: y = A22 v (row sums per 4-slot batch, column partials).
-        // Dead rows and columns carry v = 0; only whole dead batches are skipped.
-        double cacc[TR_CS];
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) cacc[t] = 0.0;
-#pragma unroll
-        for (int sb = 0; sb < TR_S; sb += 4) {
-            if (w + TR_W * (sb + 3) <= o || w + TR_W * sb >= m) continue;  // no live row in the batch
-            double rb[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int s = sb + j, r = w + TR_W * s;
-                const double vr = slot_val(vrl, s);
-                double rs = 0.0;
-#pragma unroll
-                for (int t = 0; t < tr_ts(s); ++t) {
-                    const double x = a[tr_off(s) + t];
-                    rs = fma(x, vc[t], rs);
-                    if (t == tr_ts(s) - 1)  // diagonal slot: the strictly lower part feeds the columns
-                        cacc[t] = fma(lane + 64 * t < r ? x : 0.0, vr, cacc[t]);
-                    else
-                        cacc[t] = fma(x, vr, cacc[t]);
-                }
-                rb[j] = rs;
-            }
-            // 4 row sums across the 64 lanes: halve by lane^32 and lane^16, then a butterfly
-            const bool h32 = (lane & 32) != 0, h16 = (lane & 16) != 0;
-            double k0 = h32 ? rb[2] : rb[0], k1 = h32 ? rb[3] : rb[1];
-            const double g0 = h32 ? rb[0] : rb[2], g1 = h32 ? rb[1] : rb[3];
-            k0 += scc_xor_lane_f64<32>(g0);
-            k1 += scc_xor_lane_f64<32>(g1);
-            double c = h16 ? k1 : k0;
-            c += scc_xor_lane_f64<16>(h16 ? k0 : k1);
-            c += scc_xor_lane_f64<8>(c);
-            c += scc_xor_lane_f64<4>(c);
-            c += scc_xor_lane_f64<2>(c);
-            c += scc_xor_lane_f64<1>(c);
-            if ((lane & 15) == 0) S.rows[w + TR_W * (sb + (lane >> 4))] = c;
-        }
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) S.colp[w][lane + 64 * t] = cacc[t];
-        __syncthreads();  // B1
-        if (stmp) {
-            const unsigned long long tn = clock64();
-            tp1 += tn - ts0;
-            ts0 = tn;
-        }
-        // ---- reduce: y, p = tau y (0 outside the trailing block), p.v; the reflector row
-        {
-            double pv = 0.0;
-            const int x = tid;
-            if (x < TT_MMAX) {
-                const bool live = x > o && x < m;
-                double px = 0.0;
-                if (live) {
-                    double y = S.rows[x];
-#pragma unroll
-                    for (int v = 0; v < TR_W; ++v) y += S.colp[v][x];
-                    px = tv * y;
-                    const double vx = x == o + 1 ? 1.0 : xc[x] * scal;
-                    pv = px * vx;
-                    refl[(size_t)i * lda + i0 + x] = vx;
-                }
-                S.pp[x] = px;
-            }
-            pv = wave_sum_d(pv);
-            if (lane == 0) S.redp[w] = pv;
-        }
-        __syncthreads();  // B2
-        if (stmp) {
-            const unsigned long long tn = clock64();
-            tpr += tn - ts0;
-            ts0 = tn;
-        }
-        double pvt = 0.0;
-        double ppc[TR_CS];
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) ppc[t] = S.pp[lane + 64 * t];
-        const double ppr = S.pp[rl];
-#pragma unroll
-        for (int v = 0; v < TR_W; ++v) pvt += S.redp[v];
-        const double a2 = -0.5 * tv * pvt;
-        double wc[TR_CS];
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) wc[t] = fma(a2, vc[t], ppc[t]);
-        const double wrl = fma(a2, vrl, ppr);  // w of this lane's row slot
-        // ---- pass 2: A22 -= v w^T + w v^T (v = w = 0 on dead rows and columns)
-#pragma unroll
-        for (int sb = 0; sb < TR_S; sb += 4) {
-            if (w + TR_W * (sb + 3) <= o || w + TR_W * sb >= m) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int s = sb + j, r = w + TR_W * s;
-                const double vr = slot_val(vrl, s);
-                const double wr = slot_val(wrl, s);
-#pragma unroll
-                for (int t = 0; t < tr_ts(s); ++t) {
-                    const double x = a[tr_off(s) + t];
-                    const double xn = fma(-vr, wc[t], fma(-wr, vc[t], x));
-                    if (t == tr_ts(s) - 1)
-                        a[tr_off(s) + t] = lane + 64 * t > r ? 0.0 : xn;  // the upper part stays 0
-                    else
-                        a[tr_off(s) + t] = xn;
-                }
-            }
-        }
-        if (stmp) {
-            const unsigned long long tn = clock64();
-            tp2 += tn - ts0;
-            ts0 = tn;
-        }
-        // ---- column q = o + 1 for the next reflector: the entries below its
-        // diagonal (rows above it written as 0), the diagonal, and |x|^2 past
-        // the first entry; lane q % 64 of every wave holds the column
-        const int q = o + 1, tq = q >> 6, lq = q & 63, nb = buf ^ 1;
-        double part = 0.0;
-#pragma unroll
-        for (int t = 0; t < TR_CS; ++t) {
-            if (t != tq) continue;
-            if (lane == lq) {
-#pragma unroll
-                for (int s = 0; s < TR_S; ++s) {
-                    if (tr_ts(s) <= t) continue;  // compile-time: rows < 64 t
-                    // a batch of rows all < q (zero already) or all >= m (never read)
-                    if (w + TR_W * ((s & ~3) + 3) < q || w + TR_W * (s & ~3) >= m) continue;
-                    const int r = w + TR_W * s;
-                    const double x = a[tr_off(s) + t];
-                    S.xcol[nb][r] = r > q ? x : 0.0;
-                    if (r == q) S.diag = x;
-                    part = fma(r >= q + 2 ? x : 0.0, x, part);
-                }
-                S.redx[w] = part;
-            }
-        }
-        // rows q - 1 and q of that buffer may still hold an older column (slots
-        // this capture does not cover): at or above the next subdiagonal they read 0
-        if (tid == 0) {
-            S.xcol[nb][q] = 0.0;
-            if (q >= 1) S.xcol[nb][q - 1] = 0.0;
-        }
-        buf = nb;
-        __syncthreads();  // B3
-        if (stmp) tpc += clock64() - ts0;
-    }
-    if (stmp) {
-        stamps[17] = tp1;
-        stamps[18] = tpr;
-        stamps[19] = tp2;
-        stamps[20] = tpc;
-    }
-    if (tid == 0) {
-        d[n - 1] = S.diag;
-        e[n - 1] = 0.0;
-        tau[n - 1] = 0.0;
-    }
-}
-
-extern "C" int scc_tridiag_tail_max(void) { return TT_MMAX; }
 
 // XCD registration shared by both tridiagonalisation kernels: the first
 // workgroup to arrive picks its XCD; up to a.nwg workgroups found on that XCD
@@ -1620,7 +1294,7 @@ static int eig_local_env()
 }
 
 struct EigLayout {
-    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, tf, lu, work, tail, total;
+    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, tf, lu, work, total;
 };
 
 static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool lu_lds)
@@ -1647,7 +1321,6 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     const int R = (n + nwg - 1) / nwg;
     // XCD-local mode: fewer workgroups may register than planned -> room for all rows
     L.work = take(((size_t)n + 4 * 64) * n);  // row store of the HBM fall-backs (any participant count)
-    L.tail = take((size_t)TT_MMAX * TT_MMAX);  // the trailing block k_tridiag hands to k_tridiag_tail
     L.total = o;
     (void)k;
     return L;
@@ -1804,8 +1477,6 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.xcd_local = eig_local(n) ? 1 : 0;
     t.stamps = stamps;
     t.err = flags + 1;
-    t.stop = n;
-    t.tail = scratch + L.tail;
     const int R = (n + nwg - 1) / nwg;
     // at least 82 KB so that every workgroup has a CU of its own
     size_t lds = tri_lds_bytes(n, std::max(R - tri_reg_rows(n), 0), rows_lds);
@@ -1819,17 +1490,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 64;
     }
-    // opt-in (SCC_EIG_TAIL=1): the last TT_MMAX columns (all of them when n <=
-    // TT_MMAX) in ONE workgroup with the trailing block in registers
-    // (k_tridiag_tail): no hand-off there, but measured slower than the
-    // hand-off kernel at every n (one workgroup's per-column
-    // latency chain exceeds the hand-off it removes)
-    const char* tail_env = getenv("SCC_EIG_TAIL");
-    const bool use_tail = n > 2 && tail_env && *tail_env && atoi(tail_env) != 0;
-    if (use_tail) t.stop = std::max(0, n - TT_MMAX);
-    if (use_tail && t.stop == 0) {
-        // nothing for the hand-off kernel
-    } else {
+    {
         // register rows for n <= 896 (6, 8 or 14 column slots per lane; the rest
         // of a workgroup's rows in LDS), else LDS / HBM rows
         const int nj = tri_nj(n);
@@ -1851,12 +1512,6 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         if (e != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (use_tail) {
-        const int m = n - t.stop;
-        hipLaunchKernelGGL(k_tridiag_tail, dim3(1), dim3(TR_T), 0, st, t.stop > 0 ? t.tail : A,
-                           t.stop > 0 ? m : lda, n, t.stop, t.d, t.e, t.tau, t.refl, lda, stamps);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     if (marks) hipEventRecord(marks[1], st);
     VecArgs v{};
     v.d = t.d;
@@ -1879,8 +1534,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     const char* pin_env = getenv("SCC_EIG_PIN");
     const int pin_mode = pin_env ? atoi(pin_env) : 2;
     // (measured at config B: eig_vec 0.37 ms anywhere, 0.42 claim loop, 0.32 wait)
-    // (the tail's reflectors come from another workgroup: no XCD to pin to)
-    const bool pin = t.xcd_local != 0 && pin_mode != 0 && !use_tail;
+    const bool pin = t.xcd_local != 0 && pin_mode != 0;
     v.wait = pin_mode == 2;
     v.xcd = pin && (pin_mode == 1 || 8 * k <= 256) ? t.reg : nullptr;  // wait needs co-residency
     v.vcount = flags + 5;

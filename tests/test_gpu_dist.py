@@ -80,14 +80,12 @@ def test_dist_packed_order_small(eng):
     np.testing.assert_allclose(dist, [1, 3, 6, 2, 5, 3], atol=1e-12)
 
 
-@pytest.mark.parametrize("tail", ["0", "1"])
-@pytest.mark.parametrize("n", [2, 3, 5, 8, 17, 40, 130, 700])
-def test_eigensolver_sizes(eng, n, tail, monkeypatch):
-    """Tridiagonalisation + per-eigenpair vectors at many |U| against numpy's
-    exact SVD: the hand-off kernel for every column (the default, workgroup
-    counts 2..70, rows in LDS) and the opt-in register tail (SCC_EIG_TAIL=1)."""
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 17, 40, 130, 255, 256, 257, 323, 700])
+def test_eigensolver_sizes(eng, n, monkeypatch):
+    """Multi-workgroup tridiagonalisation + per-eigenpair vectors at many |U|
+    (workgroup counts 2..70, rows in registers or LDS) against numpy's exact
+    SVD."""
     from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_TAIL", tail)
     monkeypatch.setenv("SCC_EIG_SI", "0")  # the direct solvers (subspace iteration: its own tests)
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
@@ -132,13 +130,10 @@ def test_eigensolver_rows_beyond_lds(eng, monkeypatch):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
-@pytest.mark.parametrize("tail", ["0", "1"])
-def test_rank_deficient_and_repeated(eng, tail, monkeypatch):
+def test_rank_deficient_and_repeated(eng, monkeypatch):
     """Identical genes (zero-norm columns: tau = 0 reflectors) and exactly
-    repeated eigenvalues inside the top 15, n = 90 and 300, with and without
-    the register tail."""
+    repeated eigenvalues inside the top 15, n = 90 and 300."""
     from scconsensus_amd import _native as nat
-    monkeypatch.setenv("SCC_EIG_TAIL", tail)
     monkeypatch.setenv("SCC_EIG_SI", "0")
     for n in (90, 300):
         rng = np.random.default_rng(8 + n)
@@ -158,18 +153,15 @@ def test_rank_deficient_and_repeated(eng, tail, monkeypatch):
 
 
 @pytest.mark.parametrize("xcd", ["0", "1"])
-@pytest.mark.parametrize("tail", ["0", "1"])
 @pytest.mark.parametrize("n,nwg", [(323, 8), (323, 32), (323, 64), (500, 48), (700, 70), (700, 256), (1500, 40),
                                    (1500, 150), (2100, 210)])
-def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, tail, monkeypatch):
+def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, monkeypatch):
     """Same eigenpairs for any number of tridiagonalisation workgroups, either
-    hand-off (cross-XCD write-through or one-XCD L2), with or without the
-    register tail, rows in LDS or in HBM."""
+    hand-off (cross-XCD write-through or one-XCD L2), rows in LDS or in HBM."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
     monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
     monkeypatch.setenv("SCC_EIG_XCD", xcd)
-    monkeypatch.setenv("SCC_EIG_TAIL", tail)
     rng = np.random.default_rng(11)
     X = rng.standard_normal((n, 900)) * np.linspace(3.0, 0.5, n)[:, None]
     X[:20] += rng.standard_normal((20, 1)) * rng.standard_normal((1, 900)) * 4.0
@@ -178,6 +170,23 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, tail, monkeypatch):
     dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+def test_workgroup_count_bitwise(eng, monkeypatch):
+    """The tridiagonalisation's reductions have a fixed shape: 8, 20 or 32
+    workgroups in the hand-off give the same distance bits."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SI", "0")
+    rng = np.random.default_rng(21)
+    n = 323
+    X = rng.standard_normal((n, 900)) * np.linspace(3.0, 0.5, n)[:, None]
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    outs = []
+    for nwg in (8, 20, 32):
+        monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
+        outs.append(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID))
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
 
 
 @pytest.mark.parametrize("f32", [False, True])
@@ -301,6 +310,22 @@ def test_subspace_guard_catches_missed_eigenpair(eng, monkeypatch, capfd):
     monkeypatch.delenv("SCC_EIG_SI_INIT_ROWS")
     d2 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)  # the normal start (whichever path answers)
     assert np.max(np.abs(d2 - ref)) < 1e-5
+
+
+def test_repeat_bitwise_config_b(eng):
+    """the same config-B job twice gives the same `dist` bits
+    (every reduction has a fixed order; the tridiagonalisation's sums do not
+    depend on how many workgroups joined its hand-off)."""
+    from scconsensus_amd import _native as nat
+    from scconsensus_amd import api, synth
+    d = synth.generate("B")
+    names, code = api.select_clusters(d.labels, 10)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    uni = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="union").union
+    first = eng.distance(ds, uni)
+    for _ in range(2):
+        again = eng.distance(ds, uni)
+        assert np.array_equal(first, again)
 
 
 def test_gather_wide_union_fallback(eng):
