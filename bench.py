@@ -53,6 +53,8 @@ def _args(argv=None):
     ap.add_argument("--no-pearson", action="store_true", help="skip the side measurement of the Pearson kernel")
     ap.add_argument("--no-transfers", action="store_true", help="skip the D2H / H2D side measurements")
     ap.add_argument("--cpu-sample-genes", type=int, default=1500)
+    ap.add_argument("--no-stage-events", action="store_true",
+                    help="no per-stage HIP events in the engine (diagnostic: their cost on the step)")
     ap.add_argument("--mode", choices=["shard", "jobs"], default="shard",
                     help="shard: ONE job over all ranks (strong scaling); jobs: one job per rank (weak scaling)")
     ap.add_argument("--dry-run", action="store_true",
@@ -248,7 +250,7 @@ def main():
     names, code = api.select_clusters(d.labels, 10)
     K = len(names)
     P = K * (K - 1) // 2
-    eng = nat.Engine(gpu, profile=True)
+    eng = nat.Engine(gpu, profile=not a.no_stage_events)
     if a.config == "E":
         ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
         return de_only(a, eng, ds, d, code, K, dist, world)
@@ -301,13 +303,20 @@ def main():
         dist.barrier()
         return r, dist.max_over_ranks(time.perf_counter() - t0) / nsteps * 1e3
 
-    for _ in range(a.warmup):
-        r = step()
-    eng.synchronize()
-    eng.reset_timers()
-    r, ms = timed(a.steps)
+    # Warm-up: the first step allocates; the others time every stage (HIP
+    # events around each stage: the per-stage table).  An event between two
+    # kernels leaves the GPU idle ~12 us (0.14 ms per config-B step with every
+    # stage timed), so the timed region then brackets only the dominant stage.
     fams = ["ingest", "gene_stats", "pair_filter", "gene_rank", "pair_test", "pair_select", "gather", "center", "gram",
             "eigen", "eig_tridiag", "eig_vec", "eig_fin", "scores", "dist"]
+    os.environ.pop("SCC_PROFILE_STAGES", None)
+    r = step()
+    eng.synchronize()
+    eng.reset_timers()
+    nprof = max(1, a.warmup - 1)
+    for _ in range(nprof):
+        r = step()
+    eng.synchronize()
     times = {f: eng.kernel_time(f) for f in fams}
     stage_ms = {f: (t[0] / max(t[1], 1)) for f, t in times.items()}
     # algorithmic work per launch of each timed kernel (family): what roofline.achieved divides
@@ -340,6 +349,14 @@ def main():
                               "eigen stage: block subspace iteration (k_si_mul/gram/cholinv/apply, "
                               "Rayleigh-Ritz through the direct solver at n = 64)")
     dom = max(alg, key=lambda f: stage_ms.get(f, 0.0))
+    # the timed region: HIP events around the dominant stage only
+    os.environ["SCC_PROFILE_STAGES"] = dom
+    eng.reset_timers()
+    r, ms = timed(a.steps)
+    t_dom = eng.kernel_time(dom)
+    stage_ms_warmup_dom = stage_ms[dom]
+    stage_ms[dom] = t_dom[0] / max(t_dom[1], 1)
+    os.environ["SCC_PROFILE_STAGES"] = "-"  # the side measurements below: no stage events
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
     if os.path.exists(tpath) and not multi:
@@ -350,6 +367,8 @@ def main():
     def roof(f):
         bound, work, kname = alg[f]
         t_s = stage_ms[f] / 1e3
+        if t_s <= 0.0:  # --no-stage-events: no per-kernel times
+            return {"bound": bound, "achieved": None, "kernel": kname}
         if bound == "hbm":
             ach = work / t_s / 1e9
             return {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
@@ -388,6 +407,7 @@ def main():
     # north_star's MFMA kernel: the Pearson 1 - cor distance (Fast:403) on the
     # same union, measured beside the step (not part of the reference's path)
     if not a.no_pearson and not multi:
+        os.environ["SCC_PROFILE_STAGES"] = "zscore,pearson"
         eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)  # warm-up (first launch, buffers)
         eng.synchronize()
         eng.reset_timers()
@@ -432,6 +452,10 @@ def main():
                    "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": nnz, "union": nu,
                    "parallelism": f"shard{world}" if shard else f"jobs{world}"},
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        "stage_ms_source": (f"{dom}: HIP events over the timed region (the only stage timed there); the others: "
+                            f"{nprof} warm-up step(s) with every stage timed (each event adds ~12 us of GPU idle, "
+                            f"so those steps are not the timed ones); {dom} in those steps: "
+                            f"{stage_ms_warmup_dom:.4f} ms"),
         "roofline": roof_dom,
         "kernels": kernels,
     }

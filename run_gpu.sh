@@ -22,6 +22,9 @@ for s in "$@"; do
     stamps) SCC_STAMPS=1 step stamps 300 python scripts/diag_gpu.py B ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 ;;
     tdist) step tdist 600 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 120 --timeout-method thread ;;
+    benchev) step benchev 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 && step benchnoev 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 --no-stage-events ;;
+    benchq2) step benchq2 600 python bench.py --no-cpu-baseline --no-transfers --steps 20 --warmup 5 ;;
+    profq) step profq 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 2 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

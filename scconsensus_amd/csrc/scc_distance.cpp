@@ -254,6 +254,31 @@ static int dist_multi(scc_ctx* c, const double* d_P, int N, int64_t col_lo, int6
 }
 
 // columns [col_lo, col_hi) of the packed output (the whole matrix: [0, N))
+
+// the gene list through a pinned buffer: an asynchronous DMA instead of the
+// staged copy a pageable source takes
+static int genes_h2d(scc_ctx* c, int* d_genes, const int32_t* genes, int nu, hipStream_t s0)
+{
+    if (c->h_genes_n < (size_t)nu) {
+        if (c->h_genes) hipHostFree(c->h_genes);
+        c->h_genes = nullptr;
+        c->h_genes_n = 0;
+        if (hipHostMalloc((void**)&c->h_genes, sizeof(int) * std::max(nu, 1024), hipHostMallocDefault) != hipSuccess) {
+            hipGetLastError();
+            c->h_genes = nullptr;
+            HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
+            return SCC_OK;
+        }
+        c->h_genes_n = (size_t)std::max(nu, 1024);
+    }
+    if (!c->ev_genes) HIPCHK(c, hipEventCreateWithFlags(&c->ev_genes, hipEventDisableTiming));
+    HIPCHK(c, hipEventSynchronize(c->ev_genes));  // the previous copy out of h_genes has completed
+    std::memcpy(c->h_genes, genes, sizeof(int) * nu);
+    HIPCHK(c, hipMemcpyAsync(d_genes, c->h_genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
+    HIPCHK(c, hipEventRecord(c->ev_genes, s0));
+    return SCC_OK;
+}
+
 static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
                      int32_t ncomp, int64_t col_lo, int64_t col_hi, void* dist_out, int32_t out_kind, int32_t out_f32)
 {
@@ -295,7 +320,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     if (out_kind == SCC_PTR_HOST || !dist_out) {  // NULL device output: keep it in the workspace
         if ((rc = ws_get(c, "d_dist", npairs * (out_f32 ? 4 : 8), &d_out))) return rc;
     }
-    HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
+    if ((rc = genes_h2d(c, d_genes, genes, nu, s0))) return rc;
     {
         Scope sc(c, "gather", s0);
         // the CSC gather writes whole rows (zeros included): only the padding rows need clearing
@@ -305,6 +330,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         HIPCHK(c, scc_launch_gather(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, N, d_umap, d_genes, nu, ld,
                                     d_X, s0));
     }
+    unsigned int* d_eig_err = nullptr;  // the hand-off's time-out flag, read back after the last launch
     if (metric == SCC_DIST_PCA_EUCLID) {
         double *d_slabs, *d_C, *d_W, *d_Z, *d_P, *d_escr;
         const int nchunk = std::max(1, std::min(32, Npad / 512));
@@ -322,14 +348,18 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
             Scope sc(c, "gram", s0);
             HIPCHK(c, scc_launch_gram(d_X, Npad, ld, nchunk, d_slabs, d_C, s0));
         }
-        unsigned int* d_eig_err = nullptr;
         {
             Scope sc(c, "eigen", s0);
             hipEvent_t mk[6];
             hipEvent_t* marks = nullptr;
-            if (c->profile) {  // per-kernel split of the eigensolve
-                for (auto& m : mk) m = ev_take(c);
-                marks = mk;
+            static const char* const mk_names[3] = {"eig_tridiag", "eig_vec", "eig_fin"};
+            for (int q = 0; q < 3; ++q) {  // per-kernel split of the eigensolve
+                mk[2 * q] = mk[2 * q + 1] = nullptr;
+                if (stage_timed(c, mk_names[q])) {
+                    mk[2 * q] = ev_take(c);
+                    mk[2 * q + 1] = ev_take(c);
+                    marks = mk;
+                }
             }
             unsigned long long* st_buf = nullptr;
             if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 24, st_buf);
@@ -348,14 +378,11 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
                 fprintf(stderr, "[scc stamps] block back-transform: stage %llu, V^T Y %llu, T W %llu, Y update %llu, "
                         "load %llu cycles\n", h[12], h[13], h[14], h[15], h[16]);
             }
-            if (marks) {
-                c->pending.push_back({"eig_tridiag", mk[0], mk[1]});
-                c->pending.push_back({"eig_vec", mk[2], mk[3]});
-                c->pending.push_back({"eig_fin", mk[4], mk[5]});
-            }
+            for (int q = 0; q < 3; ++q)
+                if (mk[2 * q]) c->pending.push_back({mk_names[q], mk[2 * q], mk[2 * q + 1]});
         }
-        HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
         if (env_int("SCC_EIG_DUMP", 0)) {  // debug: eigenvalues and vectors on stderr
+            HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
             std::vector<double> w(k), z((size_t)nu * 16);
             HIPCHK(c, hipMemcpyAsync(w.data(), d_W, sizeof(double) * k, hipMemcpyDeviceToHost, s0));
             HIPCHK(c, hipMemcpyAsync(z.data(), d_Z, sizeof(double) * z.size(), hipMemcpyDeviceToHost, s0));
@@ -412,7 +439,11 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         }
     }
     // what scc_silhouette(dist = NULL) reads: only an output the engine owns
-    // (a caller's device buffer may be freed or reused after this call)
+    // (a caller's device buffer may be freed or reused after this call).  The
+    // eigensolver's flag is read here, after the last launch (a copy between
+    // the eigensolve and the scores left the GPU idle ~30 us per call).
+    c->eig_err = 0;
+    if (d_eig_err) HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
     HIPCHK(c, hipStreamSynchronize(s0));
     if (metric == SCC_DIST_PCA_EUCLID && c->eig_err)
         return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
@@ -469,7 +500,7 @@ extern "C" int scc_pca_shard_colsum(scc_ctx* c, const scc_dataset* ds, const int
     if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
     const int nchunk_mean = 512;
     if ((rc = ws_get(c, "d_part", sizeof(double) * 2 * (size_t)nchunk_mean * ld, &d_part))) return rc;
-    HIPCHK(c, hipMemcpyAsync(d_genes, genes, sizeof(int) * nu, hipMemcpyHostToDevice, s0));
+    if ((rc = genes_h2d(c, d_genes, genes, nu, s0))) return rc;
     {
         Scope sc(c, "gather", s0);
         const size_t r0 = (ds->dense || !scc_gather_writes_rows(ld)) ? 0 : (size_t)n;  // CSC: whole rows written

@@ -1206,6 +1206,137 @@ __global__ void __launch_bounds__(TB_T) k_tri_back(double* __restrict__ Zq, int 
         for (int i = 0; i < 5; ++i) stamps[12 + i] = ph[i];
 }
 
+// Explicit Q = H_0 H_1 ... H_{n-3} = B_0 B_1 ... B_{m-1} (B_b = I - V_b T_b
+// V_b^T, the compact-WY blocks of k_refl_T), formed on the side stream while
+// k_tri_vectors finds the tridiagonal's eigenvectors: the rows of Q evolve
+// independently (q_r^T <- q_r^T B_b, block by block from e_r^T), so each
+// workgroup owns QF_R rows in LDS and needs no other workgroup.  Per block:
+// S = Q_rows V_b and Q_rows -= (S T_b) V_b^T, both on fp64 MFMA 16x16x4.
+// The back-transformation is then one product Z = Q Y (k_apply_q) instead
+// of the one-workgroup, block-sequential k_tri_back on the critical path.
+#define QF_R 16
+#define QF_T 256
+static_assert(8 * (QF_T / 64) == BT_NB, "k_form_q stages BT_NB reflector rows, QF_VB per wave");
+__global__ void __launch_bounds__(QF_T) k_form_q(const double* __restrict__ refl, const double* __restrict__ tf, int n,
+                                                 int lda, double* __restrict__ Q)
+{
+    typedef double d4v __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Qs = sm;                     // [QF_R][n]
+    double* Vs = Qs + (size_t)QF_R * n;  // [BT_NB][n]: v_i over all rows (zero at rows <= kb + i)
+    __shared__ double Sp[2][QF_R][BT_NB];  // K-halves of Q_rows V_b
+    __shared__ double S2[QF_R][BT_NB];     // (Q_rows V_b) T_b
+    __shared__ double Ts[BT_NB][BT_NB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int r0 = blockIdx.x * QF_R;
+    for (int r = wv; r < QF_R; r += QF_T / 64)
+        for (int j = lane; j < n; j += 64) Qs[(size_t)r * n + j] = (r0 + r == j) ? 1.0 : 0.0;
+    const int nr = n - 2, nblk = nr > 0 ? (nr + BT_NB - 1) / BT_NB : 0;
+    // V_b's rows: wave w stages rows i = w + 4 u, lanes over j, QF_VB loads of
+    // a row-chunk in flight at once (clamped, unconditional; masked on store)
+    constexpr int QF_VB = 8;
+    for (int b = 0; b < nblk; ++b) {
+        const int kb = b * BT_NB, nb = min(BT_NB, nr - kb), m0 = kb + 1;
+        __syncthreads();  // the previous block's update of Qs is complete before Vs is reused
+        for (int j0 = 0; j0 < n; j0 += 64) {
+            const int j = j0 + lane, jc = min(j, n - 1);
+            double vv[QF_VB];
+#pragma unroll
+            for (int u = 0; u < QF_VB; ++u) {
+                const int i = wv + (QF_T / 64) * u;
+                vv[u] = refl[(size_t)(kb + min(i, nb - 1)) * lda + jc];
+            }
+#pragma unroll
+            for (int u = 0; u < QF_VB; ++u) {
+                const int i = wv + (QF_T / 64) * u;
+                if (j < n) Vs[(size_t)i * n + j] = (i < nb && j > kb + i) ? vv[u] : 0.0;
+            }
+        }
+        for (int x = tid; x < BT_NB * BT_NB; x += QF_T) (&Ts[0][0])[x] = tf[(size_t)b * BT_NB * BT_NB + x];
+        __syncthreads();
+        {  // S = Q_rows V_b^T-side: 16 rows x 32 reflectors, K = the rows j >= m0; wave
+            // w: reflector tile w & 1, K half w >> 1
+            const int tile = wv & 1, half = wv >> 1;
+            const double* qa = Qs + (size_t)(lane & 15) * n;
+            const double* vb = Vs + (size_t)(tile * 16 + (lane & 15)) * n;
+            d4v acc = {0.0, 0.0, 0.0, 0.0};
+            for (int j0 = m0 + 4 * half; j0 < n; j0 += 8) {
+                const int j = j0 + (lane >> 4), jc = min(j, n - 1);
+                const double a = qa[jc], bq = vb[jc];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(j < n ? a : 0.0, j < n ? bq : 0.0, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Sp[half][(lane >> 4) + 4 * r][tile * 16 + (lane & 15)] = acc[r];
+        }
+        __syncthreads();
+        for (int x = tid; x < QF_R * BT_NB; x += QF_T) {  // S2 = S T (T upper triangular, zero past nb)
+            const int r = x / BT_NB, i = x % BT_NB;
+            double sacc = 0.0;
+#pragma unroll 8
+            for (int c = 0; c < BT_NB; ++c) sacc = fma(Sp[0][r][c] + Sp[1][r][c], Ts[c][i], sacc);
+            S2[r][i] = sacc;
+        }
+        __syncthreads();
+        // Q_rows[:, j] -= S2 V_b[:, j] for j >= m0: 16 x 16 tiles over j, K = 32 reflectors
+        for (int t = wv; t * 16 < n - m0; t += QF_T / 64) {
+            const int jb = m0 + t * 16;
+            d4v acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int i0 = 0; i0 < BT_NB; i0 += 4) {
+                const int i = i0 + (lane >> 4), j = jb + (lane & 15);
+                const double a = S2[lane & 15][i];  // A[row r][k i]
+                const double bv = Vs[(size_t)i * n + min(j, n - 1)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, j < n ? bv : 0.0, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = (lane >> 4) + 4 * r, j = jb + (lane & 15);
+                if (j < n) Qs[(size_t)row * n + j] -= acc[r];
+            }
+        }
+    }
+    __syncthreads();
+    for (int r = wv; r < QF_R; r += QF_T / 64)
+        if (r0 + r < n)
+            for (int j = lane; j < n; j += 64) Q[(size_t)(r0 + r) * lda + j] = Qs[(size_t)r * n + j];
+}
+
+// Z = Q Y: the back-transformed eigenvectors, Zt[q][r] = sum_j Q[r][j] Y[q][j]
+// (Y = the tridiagonal's eigenvectors, [16][lda]); one 16-row tile of Z^T per
+// workgroup (one wave), K = n in steps of 4
+__global__ void __launch_bounds__(64) k_apply_q(const double* __restrict__ Q, const double* __restrict__ Y, int n,
+                                                int lda, int k, double* __restrict__ Zt)
+{
+    typedef double d4v __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x, r0 = blockIdx.x * 16;
+    const int r = min(r0 + (lane & 15), n - 1), q = lane & 15;
+    d4v acc = {0.0, 0.0, 0.0, 0.0};
+    const double* qrow = Q + (size_t)r * lda;
+    const double* ycol = Y + (size_t)min(q, k - 1) * lda;
+    for (int j0 = 0; j0 < n; j0 += 32) {  // 8 MFMA steps, their 16 loads in flight together
+        double a[8], bq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int jc = min(j0 + 4 * u + (lane >> 4), n - 1);
+            a[u] = qrow[jc];
+            bq[u] = ycol[jc];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = j0 + 4 * u + (lane >> 4);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(j < n ? a[u] : 0.0, (j < n && q < k) ? bq[u] : 0.0, acc, 0,
+                                                       0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rr = r0 + (lane >> 4) + 4 * i;
+        if (rr < n && q < k) Zt[(size_t)q * lda + rr] = acc[i];
+    }
+}
+
+static size_t form_q_lds(int n) { return sizeof(double) * (size_t)(QF_R + BT_NB) * n; }
+
 // dynamic LDS of k_tri_back (its static arrays take 32 KB more)
 static size_t tri_back_lds(int n, int k) { return sizeof(double) * ((size_t)k + BT_NB) * n; }
 
@@ -1294,7 +1425,7 @@ static int eig_local_env()
 }
 
 struct EigLayout {
-    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, refl, tf, lu, work, total;
+    size_t d, e, tau, tnorm, flags, pg, rg, dg, zq, zt, refl, tf, lu, work, q, total;
 };
 
 static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool lu_lds)
@@ -1315,12 +1446,14 @@ static EigLayout eig_layout(int n, int lda, int k, int nwg, bool rows_lds, bool 
     L.rg = take(4 * (size_t)lda);
     L.dg = take(4 * EIG_MAX_WG * TRI_W);  // one partial per wave agent
     L.zq = take(16 * (size_t)lda);
+    L.zt = take(16 * (size_t)lda);
     L.refl = take((size_t)n * lda);
     L.tf = take((size_t)((n + BT_NB) / BT_NB) * BT_NB * BT_NB);
     L.lu = lu_lds ? o : take((size_t)16 * 6 * n);
     const int R = (n + nwg - 1) / nwg;
     // XCD-local mode: fewer workgroups may register than planned -> room for all rows
     L.work = take(((size_t)n + 4 * 64) * n);  // row store of the HBM fall-backs (any participant count)
+    L.q = take((size_t)n * lda);              // explicit Q of the reflectors (k_form_q)
     L.total = o;
     (void)k;
     return L;
@@ -1426,7 +1559,8 @@ extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 // A: n x n symmetric (full), row-major, lda (read only).  scratch: see
 // scc_eigen_scratch_doubles.  Z: n x 16 out, W: k out (descending).
 // *err_dev (device u32 inside scratch) is set to 1 if a hand-off timed out.
-// marks (optional): 6 events recorded before/after each of the three launches.
+// marks (optional): 6 events recorded before/after each of the three launches
+// (a null entry is skipped).
 extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
                                             double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
                                             unsigned long long* stamps, hipStream_t st)
@@ -1443,15 +1577,14 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if (scc_si_wanted(n)) {
         // large |U|: block subspace iteration first; accepted only when every
         // Ritz residual passes (else the direct solver below runs)
-        if (marks) hipEventRecord(marks[0], st);
+        if (marks && marks[0]) hipEventRecord(marks[0], st);
         int ok = 0;
         e = scc_eigen_si(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, st);
         if (e != hipSuccess) return e;
         if (ok) {
-            if (marks) {
-                hipEventRecord(marks[1], st);
-                for (int m = 2; m < 6; ++m) hipEventRecord(marks[m], st);
-            }
+            if (marks)
+                for (int m = 1; m < 6; ++m)
+                    if (marks[m]) hipEventRecord(marks[m], st);
             return hipSuccess;
         }
     }
@@ -1482,7 +1615,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     size_t lds = tri_lds_bytes(n, std::max(R - tri_reg_rows(n), 0), rows_lds);
     if (lds < 82 * 1024) lds = 82 * 1024;
     t.lds_rows_cap = rows_lds ? (int)((lds / sizeof(double) - (5 * (size_t)n + 64 + EIG_MAX_WG)) / n) : 0;
-    if (marks) hipEventRecord(marks[0], st);
+    if (marks && marks[0]) hipEventRecord(marks[0], st);
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -1512,7 +1645,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         if (e != hipSuccess) return e;
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (marks) hipEventRecord(marks[1], st);
+    if (marks && marks[1]) hipEventRecord(marks[1], st);
     VecArgs v{};
     v.d = t.d;
     v.e = t.e;
@@ -1541,19 +1674,23 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     v.err = flags + 1;
     const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
     hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
-    // one workgroup back-transforms all k vectors when they and a reflector
-    // block fit its LDS (SCC_EIG_BT=0: per-eigenpair back-transformation)
+    // Back-transformation: the explicit Q formed on a side stream beside
+    // k_tri_vectors, then Z = Q Y (SCC_EIG_BT=2, the default where its LDS
+    // fits); SCC_EIG_BT=1: one workgroup applying the reflector blocks to all
+    // k vectors after k_tri_vectors (k_tri_back); 0: per eigenpair, inside
+    // k_tri_vectors
     const char* bt_env = getenv("SCC_EIG_BT");
-    const bool bt_one = n > 2 && n - 1 <= 12 * TB_T / BT_NB && tri_back_lds(n, k) + 33 * 1024 <= EIG_LDS_MAX &&
-                        !(bt_env && *bt_env && atoi(bt_env) == 0);  // one fetch batch covers a block
-    v.bt_none = bt_one ? 1 : 0;
+    const int bt_mode = (bt_env && *bt_env) ? atoi(bt_env) : 2;
+    const bool back_fits = n > 2 && n - 1 <= 12 * TB_T / BT_NB && tri_back_lds(n, k) + 33 * 1024 <= EIG_LDS_MAX;
+    const bool q_form = n > 2 && bt_mode == 2 && form_q_lds(n) + 24 * 1024 <= EIG_LDS_MAX;  // + its static arrays
+    const bool bt_one = !q_form && back_fits && bt_mode != 0;  // one fetch batch covers a block
+    v.bt_none = (bt_one || q_form) ? 1 : 0;
     // k_refl_T (reflectors -> T factors) does not depend on the tridiagonal's
-    // eigenpairs: with the one-workgroup back-transformation it runs on a side
-    // stream beside k_tri_vectors, which then needs nothing from the
-    // reflectors' XCD either
+    // eigenpairs: it runs on a side stream beside k_tri_vectors (and k_form_q
+    // after it), so k_tri_vectors needs nothing from the reflectors' XCD
     hipStream_t side = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-    if (bt_one) {
+    if (bt_one || q_form) {
         v.xcd = nullptr;
         side_stream(&side, &fork_ev, &join_ev);
     }
@@ -1568,21 +1705,34 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         hipLaunchKernelGGL(k_refl_T, dim3(pin ? 8 * nblk : nblk), dim3(1024), 0, rs, t.refl, t.tau, n, lda,
                            scratch + L.tf, pin ? t.reg : nullptr, flags + 9);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (q_form) {
+            const size_t qlds = form_q_lds(n);
+            hipFuncSetAttribute((const void*)k_form_q, hipFuncAttributeMaxDynamicSharedMemorySize, (int)qlds);
+            hipLaunchKernelGGL(k_form_q, dim3((n + QF_R - 1) / QF_R), dim3(QF_T), qlds, rs, t.refl, scratch + L.tf, n,
+                               lda, scratch + L.q);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
         if (side) hipEventRecord(join_ev, side);
     }
-    if (marks) hipEventRecord(marks[2], st);
+    if (marks && marks[2]) hipEventRecord(marks[2], st);
     hipLaunchKernelGGL(k_tri_vectors, dim3(v.xcd ? 8 * k : k), dim3(VEC_T), vlds, st, v);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (side && n > 2) hipStreamWaitEvent(st, join_ev, 0);
-    if (bt_one) {
+    double* zfin = v.Zq;
+    if (q_form) {
+        hipLaunchKernelGGL(k_apply_q, dim3((n + 15) / 16), dim3(64), 0, st, scratch + L.q, v.Zq, n, lda, k,
+                           scratch + L.zt);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        zfin = scratch + L.zt;
+    } else if (bt_one) {
         const size_t blds = tri_back_lds(n, k);
         hipFuncSetAttribute((const void*)k_tri_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
         hipLaunchKernelGGL(k_tri_back, dim3(1), dim3(TB_T), blds, st, v.Zq, n, lda, k, v.refl, v.tf, stamps);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (marks) hipEventRecord(marks[3], st);
-    if (marks) hipEventRecord(marks[4], st);
-    launch_eig_finish(v.Zq, n, lda, k, W, v.tnorm, Z, st);
-    if (marks) hipEventRecord(marks[5], st);
+    if (marks && marks[3]) hipEventRecord(marks[3], st);
+    if (marks && marks[4]) hipEventRecord(marks[4], st);
+    launch_eig_finish(zfin, n, lda, k, W, v.tnorm, Z, st);
+    if (marks && marks[5]) hipEventRecord(marks[5], st);
     return hipGetLastError();
 }

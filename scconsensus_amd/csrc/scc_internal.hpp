@@ -65,6 +65,11 @@ struct scc_ctx {
     std::vector<int> host_tables;  // cell permutation + chunk tables of the last scc_de_run
     int* h_stage = nullptr;        // pinned: the DE result header, tested counts and union, one D2H
     size_t h_stage_n = 0;
+    int* h_tab = nullptr;          // pinned: a DE call's host tables (asynchronous H2D)
+    size_t h_tab_n = 0;
+    int* h_genes = nullptr;        // pinned: a distance call's gene list (asynchronous H2D)
+    size_t h_genes_n = 0;
+    hipEvent_t ev_genes = nullptr;  // recorded after the last copy out of h_genes
     // last PCA
     const double* d_last_scores = nullptr;  // N x 16 in the workspace
     int last_n = 0;
@@ -248,14 +253,32 @@ inline bool debug_sync()
     return v != 0;
 }
 
+// Whether a profiled context times the stage `name`: every stage, unless
+// SCC_PROFILE_STAGES holds a comma-separated list (read at each stage: a
+// caller may switch it between calls).  A timing event between two kernels
+// leaves the GPU idle ~12 us, ~0.14 ms per config-B step with every stage
+// timed, so a timed benchmark region brackets only the stage it reports.
+inline bool stage_timed(const scc_ctx* c, const char* name)
+{
+    if (!c->profile) return false;
+    const char* f = getenv("SCC_PROFILE_STAGES");
+    if (!f || !*f) return true;
+    const size_t n = strlen(name);
+    for (const char* q = f; (q = strstr(q, name)) != nullptr; q += n)
+        if ((q == f || q[-1] == ',') && (q[n] == ',' || q[n] == 0)) return true;
+    return false;
+}
+
 struct Scope {
     scc_ctx* c;
     const char* name;
     hipStream_t st;
     hipEvent_t a = nullptr;
+    bool on = false;
     Scope(scc_ctx* c_, const char* n, hipStream_t s) : c(c_), name(n), st(s)
     {
-        if (c->profile) {
+        on = stage_timed(c, name);
+        if (on) {
             a = ev_take(c);
             hipEventRecord(a, st);
         }
@@ -263,7 +286,7 @@ struct Scope {
     }
     ~Scope()
     {
-        if (c->profile) {
+        if (on) {
             hipEvent_t b = ev_take(c);
             hipEventRecord(b, st);
             c->pending.push_back({name, a, b});

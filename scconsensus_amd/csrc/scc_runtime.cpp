@@ -104,6 +104,9 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     }
     for (auto e : c->ev_pool) hipEventDestroy(e);
     if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->h_tab) hipHostFree(c->h_tab);
+    if (c->ev_genes) hipEventSynchronize(c->ev_genes), hipEventDestroy(c->ev_genes);
+    if (c->h_genes) hipHostFree(c->h_genes);
     if (c->h_dstage) hipHostFree(c->h_dstage);
     hipEventDestroy(c->ev_fork);
     hipEventDestroy(c->ev_join);
@@ -666,7 +669,23 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             return fail(c, SCC_ERR_INVALID, "scc_de_finish: this context ran no scc_de_run_shard for these inputs");
         log_thr = c->shard_log_thr;
     } else {
-    HIPCHK(c, hipMemcpyAsync(d_tab, H.data(), sizeof(int) * H.size(), hipMemcpyHostToDevice, s0));
+    // the tables through a pinned buffer (an asynchronous DMA; every earlier
+    // DE call ended with a synchronisation, so no copy out of it is pending)
+    const int* tab_src = H.data();
+    if (c->h_tab_n < H.size()) {
+        if (c->h_tab) hipHostFree(c->h_tab);
+        c->h_tab = nullptr;
+        c->h_tab_n = 0;
+        if (hipHostMalloc((void**)&c->h_tab, sizeof(int) * H.size(), hipHostMallocDefault) == hipSuccess)
+            c->h_tab_n = H.size();
+        else
+            hipGetLastError();
+    }
+    if (c->h_tab) {
+        std::memcpy(c->h_tab, H.data(), sizeof(int) * H.size());
+        tab_src = c->h_tab;
+    }
+    HIPCHK(c, hipMemcpyAsync(d_tab, tab_src, sizeof(int) * H.size(), hipMemcpyHostToDevice, s0));
     const char* ife = getenv("SCC_INGEST_FULL");
     hist_rng = !ds->dense && ds->validated && ds->d_nodg && fast && (glo > 0 || ghi < G) && !(ife && atoi(ife));
     hist_full = !hist_rng;
@@ -1039,7 +1058,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         if (c->h_stage) hipHostFree(c->h_stage);
         c->h_stage = nullptr;
         c->h_stage_n = 0;
-        if (hipHostMalloc((void**)&c->h_stage, sizeof(int) * stage_n, hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc((void**)&c->h_stage, sizeof(int) * stage_n, hipHostMallocMapped) != hipSuccess) {
             hipGetLastError();
             c->h_stage = nullptr;
             return fail(c, SCC_ERR_OOM, "pinned staging allocation failed");
@@ -1047,13 +1066,10 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         c->h_stage_n = stage_n;
     }
     int* hs = c->h_stage;
-    HIPCHK(c, hipMemcpyAsync(&hs[0], d_nu, sizeof(int), hipMemcpyDeviceToHost, s0));
-    HIPCHK(c, hipMemcpyAsync(&hs[1], d_err, sizeof(int), hipMemcpyDeviceToHost, s0));
-    if (fast) {
-        HIPCHK(c, hipMemcpyAsync(&hs[2], d_rowoff + P, sizeof(long long), hipMemcpyDeviceToHost, s0));
-        HIPCHK(c, hipMemcpyAsync(&hs[4], d_tested, sizeof(int) * P, hipMemcpyDeviceToHost, s0));
-    }
-    HIPCHK(c, hipMemcpyAsync(&hs[4 + P], d_union, sizeof(int) * G, hipMemcpyDeviceToHost, s0));
+    int* hs_dev = nullptr;  // the same pinned buffer as the device sees it
+    HIPCHK(c, hipHostGetDevicePointer((void**)&hs_dev, hs, 0));
+    HIPCHK(c, scc_launch_stage_pack(d_nu, d_err, fast ? d_rowoff + P : nullptr, fast ? d_tested : nullptr, P, d_union,
+                                    G, hs_dev, s0));
     HIPCHK(c, hipStreamSynchronize(s0));
     const int hdr[2] = {hs[0], hs[1]};
     if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");

@@ -172,6 +172,30 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, monkeypatch):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
+@pytest.mark.parametrize("n", [3, 17, 64, 150, 323, 354, 400])
+def test_back_transformations_agree(eng, n, monkeypatch):
+    """The three back-transformations of the tridiagonal's eigenvectors give
+    the same PCA: the explicit Q formed beside the eigenvector kernel, then
+    Z = Q Y (SCC_EIG_BT=2, default where it fits), the one-workgroup blocked
+    k_tri_back (1) and the per-eigenpair one (0); all against the exact SVD."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SI", "0")
+    rng = np.random.default_rng(600 + n)
+    X = rng.standard_normal((n, 800)) * np.linspace(3.0, 0.5, n)[:, None]
+    X[: min(n, 12)] += rng.standard_normal((min(n, 12), 1)) * rng.standard_normal((1, 800)) * 3.0
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    outs = []
+    for bt in ("2", "1", "0"):
+        monkeypatch.setenv("SCC_EIG_BT", bt)
+        d = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+        assert np.max(np.abs(d - ref)) < 1e-7, bt
+        outs.append(d)
+    assert np.max(np.abs(outs[0] - outs[1])) < 1e-9
+    assert np.max(np.abs(outs[0] - outs[2])) < 1e-9
+
+
 def test_workgroup_count_bitwise(eng, monkeypatch):
     """The tridiagonalisation's reductions have a fixed shape: 8, 20 or 32
     workgroups in the hand-off give the same distance bits."""
