@@ -282,12 +282,27 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                 vpr[t] = (live && prev) ? pv : 0.0;
                 wpr[t] = (live && prev) ? pw : 0.0;
             }
+            // the (up to) 3 register rows together: their v_r / w_r read at once,
+            // the rank-2 updates and dot products, then ONE transposed butterfly
+            // for the 3 row sums (per row the same additions in the same order as
+            // wave_sum_d: lanes l, l ^ 32, l ^ 16, ...; bit-identical)
+            static_assert(TRI_MR <= 4, "phase B reduces up to 4 register rows at once");
+            double sdm[4] = {0.0, 0.0, 0.0, 0.0};
+            double vrm[TRI_MR], wrm[TRI_MR];
+#pragma unroll
+            for (int m = 0; m < TRI_MR; ++m) {
+                const int l = wv + TRI_W * m;
+                const int rc = min(me + nwg * l, n - 1);  // clamped, unconditional loads
+                const double a = vp[rc], b = wp[rc];
+                vrm[m] = prev ? a : 0.0;
+                wrm[m] = prev ? b : 0.0;
+            }
 #pragma unroll
             for (int m = 0; m < TRI_MR; ++m) {
                 const int l = wv + TRI_W * m;
                 if (l >= nreg || l < l0) continue;
                 const int r = me + nwg * l;
-                const double vr = prev ? vp[r] : 0.0, wr = prev ? wp[r] : 0.0;
+                const double vr = vrm[m], wr = wrm[m];
                 double sd = 0.0;
 #pragma unroll
                 for (int t = 0; t < NJA; ++t) {
@@ -295,6 +310,7 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                     rr[m][t] = x;
                     sd = fma(x, vcr[t], sd);
                 }
+                sdm[m] = sd;
                 if (r == i + 1) {
 #pragma unroll
                     for (int t = 0; t < NJA; ++t) {
@@ -302,11 +318,32 @@ __global__ void __launch_bounds__(TRI_T) k_tridiag(TriArgs a)
                         if (j > i && j < n) put_g<LOCAL>(rg + 2 * j, rr[m][t], tag);
                     }
                 }
-                sd = wave_sum_d(sd);
-                const double p = tc * sd;
-                if (lane == 0) {
-                    put_g<LOCAL>(pg + 2 * r, p, tag);
-                    pd += p * vc[r];
+            }
+            {
+                const bool h32 = (lane & 32) != 0, h16 = (lane & 16) != 0;
+                double k0 = h32 ? sdm[2] : sdm[0], k1 = h32 ? sdm[3] : sdm[1];
+                const double g0 = h32 ? sdm[0] : sdm[2], g1 = h32 ? sdm[1] : sdm[3];
+                k0 += scc_xor_lane_f64<32>(g0);
+                k1 += scc_xor_lane_f64<32>(g1);
+                double c = h16 ? k1 : k0;
+                c += scc_xor_lane_f64<16>(h16 ? k0 : k1);
+                c += scc_xor_lane_f64<8>(c);
+                c += scc_xor_lane_f64<4>(c);
+                c += scc_xor_lane_f64<2>(c);
+                c += scc_xor_lane_f64<1>(c);
+                // lane 16 m holds row m's sum
+                const int m = lane >> 4;
+                const int l = wv + TRI_W * m;
+                const int rc = min(me + nwg * l, n - 1);
+                const double p = tc * c;
+                const double pv = p * vc[rc];
+                if ((lane & 15) == 0 && m < TRI_MR && l < nreg && l >= l0) put_g<LOCAL>(pg + 2 * rc, p, tag);
+                // the wave's p.v partial in row order (lane 0 adds them as before)
+#pragma unroll
+                for (int mm = 0; mm < TRI_MR; ++mm) {
+                    const int lm = wv + TRI_W * mm;
+                    const double x = __shfl(pv, 16 * mm, 64);
+                    if (lane == 0 && lm < nreg && lm >= l0) pd += x;
                 }
             }
         }

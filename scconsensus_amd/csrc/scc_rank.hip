@@ -876,6 +876,11 @@ struct SplitLds {
     int nb, bk0, next;
     int nfat, fat0, nwav, wav0;
 };
+// the split's LDS: its tables, then the bucket-order staging of a gene that
+// fits one register chunk (SP_CHUNK keys + codes)
+static constexpr size_t kSplitStageOff = (sizeof(SplitLds) + 15) & ~(size_t)15;
+static_assert(kSplitStageOff + (size_t)SP_CHUNK * 9 <= 160 * 1024, "split LDS");
+
 
 // One ranked gene: 2048-bin histogram of its key window, bins packed into
 // value buckets of < 2 * target elements (a bin of more than `target` is a
@@ -1028,7 +1033,13 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     }
     __syncthreads();
     // ---- 4. scatter into bucket order (keys2 / codes2 over the gene's own range);
-    // the order inside a bucket is arbitrary (its ranker sorts by key and cluster)
+    // the order inside a bucket is arbitrary (its ranker sorts by key and cluster).
+    // A gene of one register chunk is ordered in LDS and leaves as whole lines
+    // (scattered 8-byte / 1-byte stores wrote each line several times over:
+    // 3.8x the keys2 + codes2 bytes at config D); larger genes store directly.
+    const bool staged = n <= SP_CHUNK;
+    u64* stk = (u64*)((char*)&L + kSplitStageOff);
+    u8* stc = (u8*)(stk + SP_CHUNK);
     for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
         if (n > SP_CHUNK) load_chunk(c0);
         int a = 0;
@@ -1041,13 +1052,24 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
                 const u32 d = (u32)((k - kmn) >> sh);
                 const u32 bk = L.bid[d];
                 const u32 pos = atomicAdd(&L.bcur[bk], 1u);
-                A.keys2[base + pos] = k;
-                A.codes2[base + pos] = (u8)a;
+                if (staged) {
+                    stk[pos] = k;
+                    stc[pos] = (u8)a;
+                } else {
+                    A.keys2[base + pos] = k;
+                    A.codes2[base + pos] = (u8)a;
+                }
                 if (k != L.rep[d]) L.bdiff[bk] = 1;
             }
         }
     }
     __syncthreads();
+    if (staged) {
+        for (int i = tid; i < n; i += SP_T) {
+            A.keys2[base + i] = stk[i];
+            A.codes2[base + i] = stc[i];
+        }
+    }
     // ---- 5. one work unit per bucket (empty buckets: a zero histogram row).
     // Wave buckets and re-split parents are reserved once per gene (one global
     // atomic each, not one per bucket) and placed with LDS cursors.
@@ -2266,7 +2288,7 @@ extern "C" int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim)
 extern "C" size_t scc_rank_split_lds(int K)
 {
     (void)K;
-    return sizeof(SplitLds);
+    return kSplitStageOff + (size_t)SP_CHUNK * (sizeof(u64) + 1);
 }
 
 extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st)

@@ -32,6 +32,7 @@ for k in sorted(set(fe) | set(wr)):
     wb = w * 1024 / max(nw, 1)
     out[k] = {"fetch_bytes_per_launch_corrected": fb, "write_bytes_per_launch": wb,
               "traffic_bytes_per_launch": fb + wb, "launches": max(nf, nw)}
-print(json.dumps({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over "
-                            "`python3 bench.py --no-cpu-baseline --steps 3 --warmup 1`; FETCH_SIZE x2 (gfx950)",
+print(json.dumps({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over `python3 bench.py "
+                            "--config <cfg> --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 2` "
+                            "(scripts/pmc_traffic.sh); FETCH_SIZE x2 (gfx950)",
                   "kernels": out}, indent=1))

@@ -2,17 +2,21 @@
 # HBM traffic per kernel from rocprofv3 PMC counters (MI355X_MICROARCH.md
 # HBM section): FETCH_SIZE and WRITE_SIZE in separate passes (they cannot
 # share the 4 TCC slots), each pass its own process over the same bench
-# command.  Output: gpurun_out/pmc_traffic/{fetch,write}/run_counter_collection.csv
+# command.  Output: gpurun_out/pmc_traffic_<cfg>/{FETCH_SIZE,WRITE_SIZE}/...
+# Usage: scripts/pmc_traffic.sh [config=B]
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc_traffic
+cfg=${1:-B}
+out=gpurun_out/pmc_traffic_$cfg
+mkdir -p $out
 for ctr in FETCH_SIZE WRITE_SIZE; do
-  d=gpurun_out/pmc_traffic/$ctr
-  timeout -s KILL 180 rocprofv3 --pmc $ctr --output-format csv -d $d -o run -- \
-    python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/pmc_traffic/$ctr.log 2>&1
+  d=$out/$ctr
+  timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $d -o run -- \
+    python3 bench.py --config $cfg --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 2 \
+    > $out/$ctr.log 2>&1
   rc=$?; echo "pass $ctr rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done
-python3 scripts/pmc_summary.py gpurun_out/pmc_traffic > gpurun_out/pmc_traffic/summary.json
-cat gpurun_out/pmc_traffic/summary.json
+python3 scripts/pmc_summary.py $out > $out/summary.json
+cat $out/summary.json
