@@ -235,7 +235,10 @@ SCC_API void scc_de_result_destroy(scc_de_result* r);
  * (N-1,0),(2,1),...), length N(N-1)/2.  out_kind SCC_PTR_HOST copies to the
  * caller's host buffer; SCC_PTR_DEVICE writes a device buffer of the ctx
  * device (dist_out == NULL: the engine keeps it HBM-resident in its own
- * workspace, valid until the next call).  ncomp <= 0 means min(n_union, 15) (Fast:398).  out_f32 != 0 writes
+ * workspace, valid until the next call; that call returns as soon as its work
+ * is queued, and a failure of its eigensolver's cross-workgroup hand-off is
+ * reported by the next synchronising call: scc_ctx_synchronize, scc_de_run,
+ * or an scc_distance into a host or caller buffer).  ncomp <= 0 means min(n_union, 15) (Fast:398).  out_f32 != 0 writes
  * float instead of double. */
 SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */, int32_t n_union,
                  int32_t metric, int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32);

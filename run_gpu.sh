@@ -27,9 +27,12 @@ for s in "$@"; do
     profq) step profq 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 2 ;;
     pmcB) step pmcB 600 bash scripts/pmc_traffic.sh B ;;
     pmcD) step pmcD 900 bash scripts/pmc_traffic.sh D ;;
+    benchP1) SCC_PEARSON_NBUF=1 step benchP1 600 python bench.py --no-cpu-baseline --no-transfers --steps 5 --warmup 2 ;;
     benchD) step benchD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchC) step benchC 900 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchE) step benchE 900 python bench.py --config E --no-cpu-baseline --steps 3 --warmup 2 ;;
+    dbgx) AMD_LOG_LEVEL=1 step dbgx 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_exchange.py -x -v --timeout 120 --timeout-method thread ;;
+    sticky) AMD_LOG_LEVEL=2 step sticky 300 python -u scripts/dbg_sticky.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -78,6 +78,65 @@ __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indp
     for (int u = lane; u < ld; u += 64) out[u] = row[u];
 }
 
+// The same gather with the union map in LDS (u16 slots, 0xffff = not in the
+// union): persistent workgroups load the map once and walk cells, so a row
+// index costs one LDS lookup instead of a dependent global load of umap[row]
+// (three dependent global round trips per batch of 512 entries become two).
+// Used when the map and four LDS rows fit (G * 2 + 4 * ld * 8 bytes).
+__global__ void __launch_bounds__(256) k_gather_csc_lm(const i64* __restrict__ indptr, const int* __restrict__ rows,
+                                                       const double* __restrict__ vals, int N, int G,
+                                                       const int* __restrict__ umap, int ld, double* __restrict__ Xc)
+{
+    extern __shared__ __attribute__((aligned(16))) double grow[];  // [4 waves][ld], then the map
+    unsigned short* lmap = (unsigned short*)(grow + 4 * (size_t)ld);
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+        const int u = umap[g];
+        lmap[g] = (unsigned short)(u >= 0 ? u : 0xffff);
+    }
+    __syncthreads();
+    double* row = grow + (size_t)wv * ld;
+    for (int c = blockIdx.x * 4 + wv; c < N; c += gridDim.x * 4) {
+        for (int u = lane; u < ld; u += 64) row[u] = 0.0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const i64 b = indptr[c], e = indptr[c + 1];
+        for (i64 k0 = b + lane; k0 < e; k0 += 512) {
+            int r[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const i64 k = k0 + 64 * q;
+                r[q] = rows[k < e ? k : e - 1];
+            }
+            int u[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int rc = min(max(r[q], 0), G - 1);
+                const int x = lmap[rc];
+                u[q] = (k0 + 64 * q < e && r[q] == rc && x != 0xffff) ? x : -1;
+            }
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {  // the hits' values, all in flight together
+                const i64 k = k0 + 64 * q;
+                v[q] = vals[u[q] >= 0 ? k : b];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (u[q] >= 0) row[u[q]] = v[q];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        double* out = Xc + (size_t)c * ld;
+        for (int u = lane; u < ld; u += 64) out[u] = row[u];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the row is read out before the next clear
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
 // true when the CSC gather writes every element of its rows (the caller then
 // clears only the padding rows)
 extern "C" int scc_gather_writes_rows(int ld) { return ld <= GATHER_LDS_LD; }
@@ -480,8 +539,9 @@ __device__ __forceinline__ long long pearson_next(long long t, long long tend, l
 // order.  The last K chunk of a tile prefetches chunk 0 of the workgroup's
 // next tile, so the epilogue's stores and the next tile's first loads overlap
 // instead of paying a workgroup launch and a cold first chunk per tile.
-template <bool F32, bool NT>
-__global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict__ Z, int N, int ldz, int nt, long long ntri,
+//   NBUF = 1: one LDS buffer (two barriers per chunk) at 3 workgroups per CU
+template <bool F32, bool NT, int NBUF>
+__global__ void __launch_bounds__(256, NBUF == 2 ? 2 : 3) k_pearson_mfma(const float* __restrict__ Z, int N, int ldz, int nt, long long ntri,
                                                          long long per_xcd, int c_lo, int c_hi, long long obase,
                                                          void* __restrict__ out, int diag_nostore)
 {
@@ -493,8 +553,8 @@ __global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict
     int ti = tt.x, tj = tt.y;
     if (t >= tend) return;
 
-    __shared__ __attribute__((aligned(16))) float sA[2][PT * PLD];
-    __shared__ __attribute__((aligned(16))) float sB[2][PT * PLD];
+    __shared__ __attribute__((aligned(16))) float sA[NBUF][PT * PLD];
+    __shared__ __attribute__((aligned(16))) float sB[NBUF][PT * PLD];
     const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
     const int h = lane >> 5, r32 = lane & 31;
     const int wj = (w >> 1) * 64, wi = (w & 1) * 64;
@@ -589,9 +649,15 @@ __global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict
                 PEARSON_STEP(w);
 #undef PEARSON_STEP
             }
-            if (more) PEARSON_LSTORE(buf ^ 1);
-            __syncthreads();
-            buf ^= 1;
+            if constexpr (NBUF == 2) {
+                if (more) PEARSON_LSTORE(buf ^ 1);
+                __syncthreads();
+                buf ^= 1;
+            } else {
+                __syncthreads();
+                if (more) PEARSON_LSTORE(0);
+                __syncthreads();
+            }
         }
 
         if (diag_nostore) {  // diagnostic (SCC_PEARSON_NOSTORE=1): keep the result live, store nothing
@@ -661,7 +727,20 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
 {
     if (dense)
         hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
-    else if (ld <= GATHER_LDS_LD)
+    else if (ld <= GATHER_LDS_LD && sizeof(double) * 4 * (size_t)ld + 2 * (size_t)G <= 120 * 1024 &&
+             !(getenv("SCC_GATHER_LM") && atoi(getenv("SCC_GATHER_LM")) == 0)) {
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+        }
+        const size_t lds = sizeof(double) * 4 * (size_t)ld + ((2 * (size_t)G + 15) & ~(size_t)15);
+        hipFuncSetAttribute((const void*)k_gather_csc_lm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const int grid = std::max(1, std::min((N + 3) / 4, 2 * cus));
+        hipLaunchKernelGGL(k_gather_csc_lm, dim3(grid), dim3(256), lds, st, indptr, rows, vals, N, G, umap, ld, Xc);
+    } else if (ld <= GATHER_LDS_LD)
         hipLaunchKernelGGL(k_gather_csc<true>, dim3((N + 3) / 4), dim3(256), sizeof(double) * 4 * (size_t)ld, st,
                            indptr, rows, vals, N, G, umap, ld, Xc);
     else
@@ -790,9 +869,15 @@ extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld
     const int nostore = ns && ns[0] == '1';
     const char* nte = getenv("SCC_PEARSON_NT");  // nontemporal epilogue stores (default on)
     const bool ntst = !(nte && *nte && atoi(nte) == 0);
-    const dim3 grid((unsigned)(8 * nwg_xcd));
-    const void* fn = f32 ? (ntst ? (const void*)k_pearson_mfma<true, true> : (const void*)k_pearson_mfma<true, false>)
-                         : (ntst ? (const void*)k_pearson_mfma<false, true> : (const void*)k_pearson_mfma<false, false>);
+    const char* nbe = getenv("SCC_PEARSON_NBUF");  // 1: single LDS buffer, 3 workgroups per CU
+    const bool one = nbe && *nbe && atoi(nbe) == 1;
+    const long long nwg = one ? (per < 96 ? per : 96) : nwg_xcd;
+    const dim3 grid((unsigned)(8 * nwg));
+    const void* fn =
+        one ? (f32 ? (ntst ? (const void*)k_pearson_mfma<true, true, 1> : (const void*)k_pearson_mfma<true, false, 1>)
+                   : (ntst ? (const void*)k_pearson_mfma<false, true, 1> : (const void*)k_pearson_mfma<false, false, 1>))
+            : (f32 ? (ntst ? (const void*)k_pearson_mfma<true, true, 2> : (const void*)k_pearson_mfma<true, false, 2>)
+                   : (ntst ? (const void*)k_pearson_mfma<false, true, 2> : (const void*)k_pearson_mfma<false, false, 2>));
     int nti = nt;
     void* args[] = {(void*)&Z, (void*)&N, (void*)&ldz, (void*)&nti, (void*)&ntri, (void*)&per, (void*)&c_lo,
                     (void*)&c_hi, (void*)&obase, (void*)&out, (void*)&nostore};

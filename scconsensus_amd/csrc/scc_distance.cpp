@@ -242,7 +242,7 @@ static int dist_multi(scc_ctx* c, const double* d_P, int N, int64_t col_lo, int6
             rcs[d] = run();
         });
     for (auto& t : th) t.join();
-    hipSetDevice(c->device);
+    scc_enter(c);
     for (int d = 0; d < D; ++d)
         if (rcs[d]) return d ? fail(c, rcs[d], c->peers[d - 1]->err) : rcs[d];
     if (out_kind == SCC_PTR_HOST)
@@ -293,7 +293,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         if (genes[u] < 0 || genes[u] >= G) return fail(c, SCC_ERR_INVALID, "gene index out of range");
     int k = ncomp > 0 ? ncomp : std::min(nu, 15);
     if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     c->d_last_dist = nullptr;  // set again only when this call succeeds (the workspace may move)
     c->last_dist_pending.clear();
@@ -443,14 +443,52 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     // eigensolver's flag is read here, after the last launch (a copy between
     // the eigensolve and the scores left the GPU idle ~30 us per call).
     c->eig_err = 0;
-    if (d_eig_err) HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
-    HIPCHK(c, hipStreamSynchronize(s0));
-    if (metric == SCC_DIST_PCA_EUCLID && c->eig_err)
-        return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
+    unsigned int* hflag_dev = nullptr;
+    if (d_eig_err) {
+        if (!c->h_flag) {
+            // a page, not 4 bytes: a tiny pinned allocation came back without a
+            // device mapping (hipHostGetDevicePointer: "Cannot get amd_mem_obj")
+            if (hipHostMalloc((void**)&c->h_flag, 4096, hipHostMallocMapped) == hipSuccess)
+                *c->h_flag = 0;
+            else {
+                hipGetLastError();
+                c->h_flag = nullptr;
+            }
+        }
+        if (c->h_flag && hipHostGetDevicePointer((void**)&hflag_dev, c->h_flag, 0) != hipSuccess) {
+            hipGetLastError();
+            hflag_dev = nullptr;
+        }
+        if (hflag_dev)
+            HIPCHK(c, scc_launch_flag_copy(d_eig_err, hflag_dev, s0));
+        else
+            HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));
+    }
     const bool own = out_kind == SCC_PTR_HOST || !dist_out;
     c->d_last_dist = (own && col_lo == 0 && col_hi == N) ? d_out : nullptr;
     c->last_dist_n = N;
     c->last_dist_f32 = out_f32 ? 1 : 0;
+    if (hflag_dev && out_kind == SCC_PTR_DEVICE && !dist_out && c->peers.empty()) {
+        // the engine keeps the output (HBM-resident, read only by later calls
+        // on this context's stream): return once the work is queued, so the
+        // caller's next host work overlaps the distance kernels; the hand-off
+        // flag waits in h_flag for the next synchronising call (scc_de_run,
+        // scc_ctx_synchronize, a host- or caller-buffer scc_distance)
+        c->eig_flag_pending = true;
+        return SCC_OK;
+    }
+    HIPCHK(c, hipStreamSynchronize(s0));
+    if (hflag_dev) {
+        c->eig_flag_pending = true;
+        int rc2 = check_pending_eig(c);
+        if (rc2) {
+            c->d_last_dist = nullptr;
+            return rc2;
+        }
+    } else if (metric == SCC_DIST_PCA_EUCLID && c->eig_err) {
+        c->d_last_dist = nullptr;
+        return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
+    }
     return SCC_OK;
 #undef WS
 }
@@ -486,7 +524,7 @@ extern "C" int scc_pca_shard_colsum(scc_ctx* c, const scc_dataset* ds, const int
     if (cell_lo < 0 || cell_hi > N || cell_lo > cell_hi) return fail(c, SCC_ERR_INVALID, "cell shard out of range");
     for (int u = 0; u < nu; ++u)
         if (genes[u] < 0 || genes[u] >= G) return fail(c, SCC_ERR_INVALID, "gene index out of range");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     const int ld = (nu + 63) & ~63;
     const int n = (int)(cell_hi - cell_lo);
@@ -529,7 +567,7 @@ extern "C" int scc_pca_shard_gram(scc_ctx* c, const void* parts, int32_t world, 
 {
     if (!c || !parts || !gram || world < 1) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_gram: bad argument");
     if (c->pca_stage < 1) return fail(c, SCC_ERR_INVALID, "scc_pca_shard_gram: call scc_pca_shard_colsum first");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     const int nu = c->pca_nu, ld = c->pca_ld;
     const int n = (int)(c->pca_chi - c->pca_clo);
@@ -568,7 +606,7 @@ extern "C" int scc_pca_shard_eigen(scc_ctx* c, const void* gram_sum, int32_t nco
     const int nu = c->pca_nu, ld = c->pca_ld;
     const int k = ncomp > 0 ? ncomp : std::min(nu, 15);
     if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     int rc;
     double *d_C, *d_W, *d_Z, *d_escr;
@@ -601,7 +639,7 @@ extern "C" int scc_pca_shard_project(scc_ctx* c, const void* vecs, int32_t ncomp
     const int nu = c->pca_nu, ld = c->pca_ld;
     const int k = ncomp > 0 ? ncomp : std::min(nu, 15);
     if (k > 16 || k > nu) return fail(c, SCC_ERR_UNSUPPORTED, "ncomp must be <= min(16, |U|)");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     const int n = (int)(c->pca_chi - c->pca_clo);
     const int npad = std::max(16, (n + 15) & ~15);
@@ -637,7 +675,7 @@ extern "C" int scc_distance_scores(scc_ctx* c, const void* scores, int64_t N64, 
     if (N64 < 2 || N64 > INT32_MAX) return fail(c, SCC_ERR_INVALID, "scc_distance_scores: bad cell count");
     const int N = (int)N64;
     if (col_lo < 0 || col_hi > N || col_lo > col_hi) return fail(c, SCC_ERR_INVALID, "column slice out of range");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     c->d_last_dist = nullptr;  // set again only when this call succeeds
     c->last_dist_pending.clear();
@@ -702,7 +740,7 @@ extern "C" int scc_silhouette(scc_ctx* c, int64_t n_cells, const int32_t* groups
         lab[i] = (int)(std::lower_bound(ids.begin(), ids.end(), groups[i]) - ids.begin());
         cnt[lab[i]]++;
     }
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     int rc;
     int *d_lab, *d_cnt;

@@ -75,6 +75,8 @@ struct scc_ctx {
     int last_n = 0;
     int last_ncomp = 0;
     unsigned int eig_err = 0;  // hand-off timeout flag of the last eigensolve (host copy)
+    unsigned int* h_flag = nullptr;  // pinned, device-mapped: where a kernel ORs that flag in
+    bool eig_flag_pending = false;   // an unsynchronised scc_distance left its flag in h_flag
     const void* d_last_dist = nullptr;  // device copy of the last full scc_distance output
     int64_t last_dist_n = 0;
     int last_dist_f32 = 0;
@@ -238,6 +240,16 @@ inline hipEvent_t ev_take(scc_ctx* c)
     hipEventCreate(&e);
     return e;
 }
+
+// Entry of every C-ABI call: the context's device, and the thread's HIP
+// "last error" cleared (each of our runtime calls is checked where it is made;
+// a residue left by a call outside the engine or a deliberate probe must not
+// be reported by the next kernel launch's hipGetLastError()).
+void scc_enter(const scc_ctx* c);
+
+// after a synchronisation: the eigensolver flag an earlier device-output
+// scc_distance (which returns without synchronising) left in h_flag
+int check_pending_eig(scc_ctx* c);
 
 inline int env_int(const char* name, int dflt)
 {

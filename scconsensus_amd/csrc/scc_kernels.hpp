@@ -205,6 +205,7 @@ size_t scc_select_key_bytes(void);
 hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_t st);
 hipError_t scc_launch_union(const unsigned long long* first_occ, int G, void* scratch, int cap, int* out,
                             int* n_out, hipStream_t st);
+hipError_t scc_launch_flag_copy(const unsigned int* src, unsigned int* dst_dev, hipStream_t st);
 hipError_t scc_launch_stage_pack(const int* nu, const int* err, const long long* nrows, const int* tested, int P,
                                  const int* uni, int G, int* out_dev, hipStream_t st);
 hipError_t scc_launch_seg_copy(const void* src, void* dst, int elem_bytes, const long long* seg, long long nseg,

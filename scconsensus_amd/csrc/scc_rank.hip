@@ -1797,14 +1797,41 @@ __device__ inline u32 wave_sum_u32(u32 v)
     return (u32)__builtin_amdgcn_readlane(x, 63);
 }
 
-// The same merge on one combined key (key - gene minimum) << 6 | cluster.
-template <int ST>
-__device__ inline void bitonic_merge_ck(u64& ck, bool up, int lane)
+// The same merge on one combined key (key - gene minimum) << 7 | cluster.
+// The lanes that keep the minimum at stride ST of a merge whose direction
+// bit is UPBIT (0: ascending everywhere) form a compile-time lane mask KM, so
+// a compare-exchange is two lane moves, one 64-bit compare into a lane mask,
+// one scalar XNOR with KM and two selects (the min / max / direction selects
+// the compiler made of `keep_min ? min : max` took 14 instructions a step,
+// the per-lane direction masks spilled to SGPR lanes).  take = lt XNOR KM:
+// a keep-min lane takes the partner's key when it is smaller, a keep-max lane
+// when it is not smaller (equal keys: either is the same key).
+__host__ __device__ constexpr u64 bitonic_km(int ST, int UPBIT)
 {
-    const u64 o = ((u64)scc_xor_lane<ST>((u32)(ck >> 32)) << 32) | (u64)scc_xor_lane<ST>((u32)ck);
-    const bool keep_min = ((lane & ST) == 0) == up;
-    ck = keep_min ? (o < ck ? o : ck) : (o < ck ? ck : o);
-    if constexpr (ST > 1) bitonic_merge_ck<ST / 2>(ck, up, lane);
+    u64 m = 0;
+    for (int l = 0; l < 64; ++l)
+        if (((l & ST) == 0) == (UPBIT == 0 || (l & UPBIT) == 0)) m |= 1ull << l;
+    return m;
+}
+
+// per-lane select by a lane mask held in scalar registers (bit set: b)
+__device__ inline u32 lane_select(u64 mask, u32 a, u32 b)
+{
+    u32 r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+    return r;
+}
+
+template <int ST, int UPBIT>
+__device__ inline void bitonic_merge_ck(u64& ck)
+{
+    const u32 olo = scc_xor_lane<ST>((u32)ck), ohi = scc_xor_lane<ST>((u32)(ck >> 32));
+    const u64 o = ((u64)ohi << 32) | olo;
+    constexpr u64 KM = bitonic_km(ST, UPBIT);
+    const u64 lt = __ballot(o < ck);
+    const u64 take = ~(lt ^ KM);
+    ck = ((u64)lane_select(take, (u32)(ck >> 32), ohi) << 32) | lane_select(take, (u32)ck, olo);
+    if constexpr (ST > 1) bitonic_merge_ck<ST / 2, UPBIT>(ck);
 }
 
 __device__ inline u64 shfl_u64(u64 v, int src)
@@ -2006,12 +2033,12 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             } else if (gk != ~0ull) {  // one 64-bit sort key: (key - gene minimum) << 7 | cluster
                 u64 ck = vl ? (((key - gk) << SCC_CODE_BITS) | code) : ~0ull;
                 // levels up to the next power of two >= n (lanes past it hold only ~0)
-                if (n > 1) bitonic_merge_ck<1>(ck, (lane & 2) == 0, lane);
-                if (n > 2) bitonic_merge_ck<2>(ck, (lane & 4) == 0, lane);
-                if (n > 4) bitonic_merge_ck<4>(ck, (lane & 8) == 0, lane);
-                if (n > 8) bitonic_merge_ck<8>(ck, (lane & 16) == 0, lane);
-                if (n > 16) bitonic_merge_ck<16>(ck, (lane & 32) == 0, lane);
-                if (n > 32) bitonic_merge_ck<32>(ck, true, lane);
+                if (n > 1) bitonic_merge_ck<1, 2>(ck);
+                if (n > 2) bitonic_merge_ck<2, 4>(ck);
+                if (n > 4) bitonic_merge_ck<4, 8>(ck);
+                if (n > 8) bitonic_merge_ck<8, 16>(ck);
+                if (n > 16) bitonic_merge_ck<16, 32>(ck);
+                if (n > 32) bitonic_merge_ck<32, 0>(ck);
                 key = ck >> SCC_CODE_BITS;  // order-equivalent for the tie tests below
                 code = vl ? (u32)(ck & SCC_CODE_MASK) : 255u;
             } else {

@@ -69,7 +69,7 @@ extern "C" int scc_ctx_create(const scc_opts* opts, scc_ctx** out)
             if (hipDeviceEnablePeerAccess(c->device, 0) != hipSuccess) hipGetLastError();
         }
     }
-    hipSetDevice(c->device);
+    scc_enter(c);
     *out = c;
     return SCC_OK;
 }
@@ -93,7 +93,7 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     if (!c) return;
     for (scc_ctx* p : c->peers) scc_ctx_destroy(p);
     c->peers.clear();
-    hipSetDevice(c->device);
+    scc_enter(c);
     scc_distance_release(c);
     hipStreamSynchronize(c->s0);
     hipStreamSynchronize(c->s1);
@@ -105,6 +105,7 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     for (auto e : c->ev_pool) hipEventDestroy(e);
     if (c->h_stage) hipHostFree(c->h_stage);
     if (c->h_tab) hipHostFree(c->h_tab);
+    if (c->h_flag) hipHostFree(c->h_flag);
     if (c->ev_genes) hipEventSynchronize(c->ev_genes), hipEventDestroy(c->ev_genes);
     if (c->h_genes) hipHostFree(c->h_genes);
     if (c->h_dstage) hipHostFree(c->h_dstage);
@@ -118,24 +119,44 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
 
 extern "C" const char* scc_ctx_last_error(const scc_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+namespace scc_rt {
+void scc_enter(const scc_ctx* c)
+{
+    hipSetDevice(c->device);
+    (void)hipGetLastError();
+}
+
+int check_pending_eig(scc_ctx* c)
+{
+    if (!c->eig_flag_pending || !c->h_flag) return SCC_OK;
+    c->eig_flag_pending = false;
+    const unsigned int v = *(volatile unsigned int*)c->h_flag;
+    *(volatile unsigned int*)c->h_flag = 0;
+    c->eig_err = v;
+    if (v) return fail(c, SCC_ERR_HIP, "scc_distance: eigensolver workgroup hand-off timed out");
+    return SCC_OK;
+}
+
+}  // namespace scc_rt
+
 extern "C" int scc_ctx_synchronize(scc_ctx* c)
 {
     if (!c) return SCC_ERR_INVALID;
-    hipSetDevice(c->device);
+    scc_enter(c);
     HIPCHK(c, hipStreamSynchronize(c->s0));
     HIPCHK(c, hipStreamSynchronize(c->s1));
     for (scc_ctx* p : c->peers) {
         int rc = scc_ctx_synchronize(p);
         if (rc) return fail(c, rc, p->err);
     }
-    hipSetDevice(c->device);
-    return SCC_OK;
+    scc_enter(c);
+    return check_pending_eig(c);
 }
 
 extern "C" int scc_ctx_set_stream(scc_ctx* c, void* stream, int32_t external)
 {
     if (!c) return SCC_ERR_INVALID;
-    hipSetDevice(c->device);
+    scc_enter(c);
     HIPCHK(c, hipStreamSynchronize(c->s0));  // work already queued on the old stream first
     c->s0 = external ? (hipStream_t)stream : c->own_s0;
     return SCC_OK;
@@ -145,7 +166,7 @@ extern "C" int scc_ctx_kernel_time(const scc_ctx* cc, const char* name, double* 
 {
     scc_ctx* c = const_cast<scc_ctx*>(cc);
     if (!c || !name) return SCC_ERR_INVALID;
-    hipSetDevice(c->device);
+    scc_enter(c);
     resolve_timers(c);
     auto it = c->timers.find(name);
     if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.ms;
@@ -156,7 +177,7 @@ extern "C" int scc_ctx_kernel_time(const scc_ctx* cc, const char* name, double* 
 extern "C" void scc_ctx_reset_timers(scc_ctx* c)
 {
     if (!c) return;
-    hipSetDevice(c->device);
+    scc_enter(c);
     resolve_timers(c);
     c->timers.clear();
 }
@@ -211,7 +232,7 @@ static int replicate(scc_ctx* c, scc_dataset* d)
             return fail(c, SCC_ERR_OOM, "dataset replication to a peer device failed");
         }
     }
-    hipSetDevice(c->device);
+    scc_enter(c);
     return SCC_OK;
 }
 
@@ -232,7 +253,7 @@ extern "C" int scc_dataset_create_csc(scc_ctx* c, const int64_t* indptr, const i
     if (!c || !out || !indptr || G <= 0 || N <= 0 || nnz < 0 || (nnz > 0 && (!rows || !vals)))
         return fail(c, SCC_ERR_INVALID, "scc_dataset_create_csc: bad arguments");
     if (G > INT32_MAX || N > INT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "dimensions exceed int32");
-    hipSetDevice(c->device);
+    scc_enter(c);
     scc_dataset* d = new scc_dataset();
     d->ctx = c;
     d->device = c->device;
@@ -274,7 +295,7 @@ extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const i
         return fail(c, SCC_ERR_INVALID, "scc_dataset_create_csr: bad arguments");
     if (G > INT32_MAX || N > INT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "dimensions exceed int32");
     if (nnz > UINT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "more than 2^32 stored values");
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     // the CSR on the device (borrowed, or a temporary upload)
     long long* d_ip = nullptr;
@@ -381,7 +402,7 @@ extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, 
 {
     if (!c || !out || !x || G <= 0 || N <= 0) return fail(c, SCC_ERR_INVALID, "scc_dataset_create_dense: bad arguments");
     if (G > INT32_MAX || N > INT32_MAX) return fail(c, SCC_ERR_UNSUPPORTED, "dimensions exceed int32");
-    hipSetDevice(c->device);
+    scc_enter(c);
     scc_dataset* d = new scc_dataset();
     d->ctx = c;
     d->device = c->device;
@@ -483,7 +504,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         return fail(c, SCC_ERR_UNSUPPORTED,
                     "K > 128 clusters: one engine run holds 128 (scc_de_run cuts larger K into group-pair runs; "
                     "the gene-shard entry points do not)");
-    hipSetDevice(c->device);
+    scc_enter(c);
     const int G = (int)ds->G, N = (int)ds->N, P = K * (K - 1) / 2;
     const bool fast = prm->mode == SCC_DE_FAST;
     // cluster sizes (host: the codes are a host array at the R boundary)
@@ -674,6 +695,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     const int* tab_src = H.data();
     if (c->h_tab_n < H.size()) {
         if (c->h_tab) hipHostFree(c->h_tab);
+    if (c->h_flag) hipHostFree(c->h_flag);
         c->h_tab = nullptr;
         c->h_tab_n = 0;
         if (hipHostMalloc((void**)&c->h_tab, sizeof(int) * H.size(), hipHostMallocDefault) == hipSuccess)
@@ -1071,6 +1093,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     HIPCHK(c, scc_launch_stage_pack(d_nu, d_err, fast ? d_rowoff + P : nullptr, fast ? d_tested : nullptr, P, d_union,
                                     G, hs_dev, s0));
     HIPCHK(c, hipStreamSynchronize(s0));
+    if ((rc = check_pending_eig(c))) return rc;  // an earlier device-output scc_distance
     const int hdr[2] = {hs[0], hs[1]};
     if (hdr[1] & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
     if (hdr[1] & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
@@ -1168,7 +1191,7 @@ static int de_run_multi(scc_ctx* c, const scc_dataset* ds, const int32_t* code, 
         eng.push_back(c->peers[i]);
         dsr.push_back(ds->reps[i]);
     }
-    hipSetDevice(c->device);
+    scc_enter(c);
     std::vector<int64_t> cut;
     int rc = gene_blocks(c, ds, D, cut);
     if (rc) return rc;
@@ -1192,7 +1215,7 @@ static int de_run_multi(scc_ctx* c, const scc_dataset* ds, const int32_t* code, 
             });
         for (auto& t : th) t.join();
     }
-    hipSetDevice(c->device);
+    scc_enter(c);
     for (int d = 0; d < D; ++d)
         if (rcs[d]) return d ? fail(c, rcs[d], eng[d]->err) : rcs[d];
     const int64_t stride = std::max<int64_t>(1, *std::max_element(nrec.begin(), nrec.end()));
@@ -1262,7 +1285,7 @@ static int de_run_grouped(scc_ctx* c, const scc_dataset* ds, const int32_t* code
             if (fast && n[a] < 3) return fail(c, SCC_ERR_RSTOP, "cluster has fewer than 3 cells (R stop())");
         }
     }
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     const int ng = (K + gmax - 1) / gmax;
     std::vector<int> gid(K);
@@ -1577,7 +1600,7 @@ extern "C" int scc_de_union_first_occ(scc_ctx* c, const void* first_occ, int64_t
     if (!c || !first_occ || !genes || !n_union || G64 < 1 || G64 > INT32_MAX)
         return fail(c, SCC_ERR_INVALID, "scc_de_union_first_occ: bad arguments");
     const int G = (int)G64;
-    hipSetDevice(c->device);
+    scc_enter(c);
     hipStream_t s0 = c->s0;
     int rc;
     void* d_key = nullptr;

@@ -20,7 +20,7 @@
 // ~ that / (lambda_15 - lambda_16)); otherwise — slow convergence (config B:
 // lambda_65 / lambda_15 = 0.88, the 15th eigenvalue inside the noise bulk), a
 // rank-deficient Gram (Cholesky breakdown) — the caller runs the direct solver.
-// A deflated power check on the basis' complement (k_si_guard) rejects a
+// A deflated power check on the basis' complement (k_sig_norm/k_sig_step) rejects a
 // result that missed a top eigenpair.  Every reduction has a fixed order (deterministic, rank-identical in a
 // sharded job).  Output layout as scc_launch_eigen_topk: Z[u*16 + q], W[q],
 // largest-magnitude component of each vector positive.
@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(64) k_si_apply(const double* __restrict__ W, c
 
 // deterministic pseudo-random start block
 // (rows >= live are zero: a test hook, SCC_EIG_SI_INIT_ROWS, that lets a test
-// hide part of the spectrum from the iteration to exercise k_si_guard)
+// hide part of the spectrum from the iteration to exercise the guard)
 __global__ void k_si_init(int n, int live, double* __restrict__ V)
 {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -214,100 +214,123 @@ __global__ void k_si_init(int n, int live, double* __restrict__ V)
 
 // Guard against a missed top eigenpair (residuals only prove that each Ritz
 // pair is close to SOME eigenpair): power iteration on the complement of the
-// final 64-column basis, (I - V V^T) C (I - V V^T), from a start vector
+// final 64-column basis, P C P with P = I - V V^T, from a start vector
 // independent of the iteration's start block.  If the block holds the top 64
-// eigenvectors, its largest eigenvalue is ~lambda_65 < theta_k; a missed
-// eigenvalue above theta_k would dominate after SI_GUARD_IT products (its
-// share grows like (lambda / lambda_65)^it).  Flag bit 8 when the Rayleigh
-// quotient reaches theta_k.  One workgroup (n <= SI_GUARD_NMAX), fixed-order
-// sums.
-#define SI_GUARD_T 1024
-#define SI_GUARD_W (SI_GUARD_T / 64)
-#define SI_GUARD_IT 24
-#define SI_GUARD_NMAX 8192
-__device__ inline double si_wave_sum(double v)
+// eigenvectors, the complement's largest eigenvalue is ~lambda_65 < theta_k; a
+// missed eigenvalue above theta_k dominates after SI_GUARD_IT products (its
+// share grows like (lambda / lambda_65)^it).  Flag bit 8 when the last Rayleigh
+// quotient reaches theta_k.  For u in range(P), P C u = C u - V (W^T u) with
+// W = C V, the Rayleigh-Ritz product already in hand, so one product is two
+// launches: k_sig_norm (one workgroup: 1/|u|, z = W^T u / |u|, the Rayleigh
+// quotient of the previous vector) and k_sig_step (y = C u/|u| - V z over
+// n/16 workgroups, a wave per 4 rows, C and V read along rows).  Fixed-order
+// sums throughout.
+#define SI_GUARD_IT 12
+#define SI_GUARD_NMAX 65536
+#define SIG_T 1024
+#define SIG_W (SIG_T / 64)
+
+__device__ inline double sig_wave_sum(double v)
 {
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += scc_xor_lane_f64<32>(v);
+    v += scc_xor_lane_f64<16>(v);
+    v += scc_xor_lane_f64<8>(v);
+    v += scc_xor_lane_f64<4>(v);
+    v += scc_xor_lane_f64<2>(v);
+    return v + scc_xor_lane_f64<1>(v);
 }
 
-__device__ inline double si_block_sum(double v, double* red)
+__device__ inline double sig_block_sum(double v, double* red)
 {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    v = si_wave_sum(v);
+    v = sig_wave_sum(v);
     __syncthreads();
-    if (lane == 0) red[w] = v;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     double t = 0.0;
-    for (int q = 0; q < SI_GUARD_W; ++q) t += red[q];
+    for (int q = 0; q < SIG_W; ++q) t += red[q];
     return t;
 }
 
-// x -= V (V^T x), twice
-__device__ inline void si_deflate(double* x, const double* __restrict__ V, int n, double* pr)
+__global__ void k_sig_init(int n, double* __restrict__ x)
 {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int j = w; j < SI_B; j += SI_GUARD_W) {
-            double sacc = 0.0;
-            for (int i = lane; i < n; i += 64) sacc = fma(V[(size_t)i * SI_B + j], x[i], sacc);
-            sacc = si_wave_sum(sacc);
-            if (lane == 0) pr[j] = sacc;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned h = (unsigned)i * 0x85ebca6bu ^ 0xc2b2ae35u;
+    h ^= h >> 16;
+    h *= 0x27d4eb2du;
+    h ^= h >> 15;
+    x[i] = (double)(h & 0xffffff) / 16777216.0 - 0.5;
+}
+
+// u: the newest vector; uprev (null on the first call): the one it was made
+// from, normalised by sc[0] as found on entry.  Writes sc[0] = 1/|u| and
+// z = M^T u / |u| (M = V for the start vector, W after); with uprev,
+// rho = (uprev sc[0]) . u; last: flag bit 8 when !(rho < theta[k-1]).
+__global__ void __launch_bounds__(SIG_T) k_sig_norm(const double* __restrict__ M, int n, const double* __restrict__ u,
+                                                   const double* __restrict__ uprev, double* __restrict__ sc,
+                                                   double* __restrict__ z, const double* __restrict__ theta, int k,
+                                                   u32* __restrict__ flag, int last)
+{
+    __shared__ double red[SIG_W];
+    __shared__ double zp[SIG_W][SI_B];
+    const int lane = threadIdx.x & 63, w = scc_wave_id();
+    const double pin = uprev ? sc[0] : 0.0;
+    double ss = 0.0, xy = 0.0;
+    for (int i = threadIdx.x; i < n; i += SIG_T) {
+        const double ui = u[i];
+        ss = fma(ui, ui, ss);
+        if (uprev) xy = fma(uprev[i] * pin, ui, xy);
+    }
+    ss = sig_block_sum(ss, red);
+    xy = sig_block_sum(xy, red);
+    double zq = 0.0;
+    if (!last)
+        for (int i = w; i < n; i += SIG_W) zq = fma(M[(size_t)i * SI_B + lane], u[i], zq);
+    zp[w][lane] = zq;
+    __syncthreads();
+    if (threadIdx.x < SI_B) {
+        double t = 0.0;
+        for (int q = 0; q < SIG_W; ++q) t += zp[q][threadIdx.x];
+        const double inv = ss > 0.0 ? 1.0 / sqrt(ss) : 0.0;  // an empty complement: nothing missed
+        z[threadIdx.x] = t * inv;
+        if (threadIdx.x == 0) {
+            sc[0] = inv;
+            sc[1] = xy;
+            if (last && !(xy < theta[k - 1])) atomicOr(flag, 8u);
         }
-        __syncthreads();
-        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) {
-            double sacc = x[i];
-            for (int j = 0; j < SI_B; ++j) sacc = fma(-V[(size_t)i * SI_B + j], pr[j], sacc);
-            x[i] = sacc;
-        }
-        __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(SI_GUARD_T) k_si_guard(const double* __restrict__ C, int ldc, int n,
-                                                         const double* __restrict__ V,
-                                                         const double* __restrict__ theta, int k,
-                                                         u32* __restrict__ flag)
+// mode 1: y = C (u sc[0]) - V z;  mode 0: y = u sc[0] - V z (the start vector's deflation)
+__global__ void __launch_bounds__(256) k_sig_step(const double* __restrict__ C, int ldc, int n,
+                                                 const double* __restrict__ u, const double* __restrict__ sc,
+                                                 const double* __restrict__ V, const double* __restrict__ z,
+                                                 double* __restrict__ y, int mode)
 {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    __shared__ double red[SI_GUARD_W];
-    __shared__ double pr[SI_B];
-    double* x = sm;
-    double* y = x + n;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < n; i += SI_GUARD_T) {
-        unsigned h = (unsigned)i * 0x85ebca6bu ^ 0xc2b2ae35u;
-        h ^= h >> 16;
-        h *= 0x27d4eb2du;
-        h ^= h >> 15;
-        x[i] = (double)(h & 0xffffff) / 16777216.0 - 0.5;
-    }
-    __syncthreads();
-    si_deflate(x, V, n, pr);
-    double rho = 0.0;
-    for (int it = 0; it < SI_GUARD_IT; ++it) {
-        double ss = 0.0;
-        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) ss = fma(x[i], x[i], ss);
-        ss = si_block_sum(ss, red);
-        if (!(ss > 0.0)) return;  // the complement is empty to working precision: nothing missed
-        const double inv = 1.0 / sqrt(ss);
-        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) x[i] *= inv;
-        __syncthreads();
-        for (int i = w; i < n; i += SI_GUARD_W) {  // y = C x, a wave per row
-            double sacc = 0.0;
-            for (int j = lane; j < n; j += 64) sacc = fma(C[(size_t)i * ldc + j], x[j], sacc);
-            sacc = si_wave_sum(sacc);
-            if (lane == 0) y[i] = sacc;
+    const int lane = threadIdx.x & 63;
+    const int i0 = (blockIdx.x * 4 + scc_wave_id()) * 4;
+    if (i0 >= n) return;  // wave-uniform
+    const int nr = min(4, n - i0);
+    const double inv = sc[0];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (mode) {
+        for (int j = lane; j < n; j += 64) {
+            const double uj = u[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (r < nr) acc[r] = fma(C[(size_t)(i0 + r) * ldc + j], uj, acc[r]);
         }
-        __syncthreads();
-        si_deflate(y, V, n, pr);
-        double xy = 0.0;
-        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) xy = fma(x[i], y[i], xy);
-        rho = si_block_sum(xy, red);
-        for (int i = threadIdx.x; i < n; i += SI_GUARD_T) x[i] = y[i];
-        __syncthreads();
+    } else if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = u[min(i0 + r, n - 1)];
     }
-    if (threadIdx.x == 0 && !(rho < theta[k - 1])) atomicOr(flag, 8u);
+    const double zl = z[lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = min(i0 + r, n - 1);
+        acc[r] = sig_wave_sum(fma(-V[(size_t)i * SI_B + lane], zl, acc[r] * inv));
+    }
+    if (lane < nr) y[i0 + lane] = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
 }
 
 // H = (V^T W + (V^T W)^T) / 2
@@ -417,6 +440,7 @@ extern "C" size_t scc_si_scratch_doubles(int n)
 {
     const size_t np = si_npad(n), nblk = (np + 255) / 256;
     return 2 * np * SI_B + (size_t)SI_B * SI_B + 3 * SI_B * SI_B + SI_B * 16 + 64 + 3 * nblk * 16 + 64 +
+           2 * np + SI_B + 8 +
            scc_eigen_topk_scratch_direct(SI_B, SI_B, 16) + 256;
 }
 
@@ -453,7 +477,11 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     double* rpart = sgn + 16;
     double* mpart = rpart + (size_t)nblk * 32;
     u32* flag = (u32*)(mpart + (size_t)nblk * 16);
-    double* escr = (double*)(flag + 64);
+    double* gu = (double*)(flag + 64);  // the guard's two vectors, z and scalars
+    double* gy = gu + np;
+    double* gz = gy + np;
+    double* gsc = gz + SI_B;
+    double* escr = gsc + 8;
     hipError_t e;
     if ((e = hipMemsetAsync(flag, 0, sizeof(u32) * 4, st)) != hipSuccess) return e;
     const char* ite = getenv("SCC_EIG_SI_IT");
@@ -499,9 +527,19 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, st, Z, sgn, n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (n <= SI_GUARD_NMAX) {  // no top eigenpair missed (bit 8); beyond: the residual test alone
-        const size_t glds = sizeof(double) * 2 * (size_t)n;
-        hipFuncSetAttribute((const void*)k_si_guard, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds);
-        hipLaunchKernelGGL(k_si_guard, dim3(1), dim3(SI_GUARD_T), glds, st, C, ldc, n, a, theta, k, flag);
+        const dim3 gstep((n + 15) / 16);
+        hipLaunchKernelGGL(k_sig_init, dim3((n + 255) / 256), dim3(256), 0, st, n, gu);
+        hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, st, a, n, gu, nullptr, gsc, gz, theta, k, flag, 0);
+        hipLaunchKernelGGL(k_sig_step, gstep, dim3(256), 0, st, C, ldc, n, gu, gsc, a, gz, gy, 0);
+        double* u = gy;  // in range(P)
+        double* y = gu;
+        for (int it = 0; it < SI_GUARD_IT; ++it) {
+            hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, st, b, n, u, it ? y : nullptr, gsc, gz, theta, k,
+                               flag, 0);
+            hipLaunchKernelGGL(k_sig_step, gstep, dim3(256), 0, st, C, ldc, n, u, gsc, a, gz, y, 1);
+            std::swap(u, y);
+        }
+        hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, st, b, n, u, y, gsc, gz, theta, k, flag, 1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     u32 h[2] = {0, 0};

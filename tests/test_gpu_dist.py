@@ -71,6 +71,18 @@ def test_pearson_matches_numpy(eng, cfg_a):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
+def test_pearson_single_buffer_bitwise(eng, cfg_a, monkeypatch):
+    """The one-LDS-buffer variant (SCC_PEARSON_NBUF=1) runs the same MFMA
+    sequence: identical bits."""
+    from scconsensus_amd import _native as nat
+    d, X, uni = cfg_a
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    a = eng.distance(ds, uni, nat.SCC_DIST_PEARSON)
+    monkeypatch.setenv("SCC_PEARSON_NBUF", "1")
+    b = eng.distance(ds, uni, nat.SCC_DIST_PEARSON)
+    assert np.array_equal(a, b)
+
+
 def test_dist_packed_order_small(eng):
     """R dist order on a tiny hand case: (1,0),(2,0),(3,0),(2,1),(3,1),(3,2)."""
     from scconsensus_amd import _native as nat
