@@ -539,9 +539,8 @@ __device__ __forceinline__ long long pearson_next(long long t, long long tend, l
 // order.  The last K chunk of a tile prefetches chunk 0 of the workgroup's
 // next tile, so the epilogue's stores and the next tile's first loads overlap
 // instead of paying a workgroup launch and a cold first chunk per tile.
-//   NBUF = 1: one LDS buffer (two barriers per chunk) at 3 workgroups per CU
-template <bool F32, bool NT, int NBUF>
-__global__ void __launch_bounds__(256, NBUF == 2 ? 2 : 3) k_pearson_mfma(const float* __restrict__ Z, int N, int ldz, int nt, long long ntri,
+template <bool F32, bool NT>
+__global__ void __launch_bounds__(256, 2) k_pearson_mfma(const float* __restrict__ Z, int N, int ldz, int nt, long long ntri,
                                                          long long per_xcd, int c_lo, int c_hi, long long obase,
                                                          void* __restrict__ out, int diag_nostore)
 {
@@ -553,8 +552,8 @@ __global__ void __launch_bounds__(256, NBUF == 2 ? 2 : 3) k_pearson_mfma(const f
     int ti = tt.x, tj = tt.y;
     if (t >= tend) return;
 
-    __shared__ __attribute__((aligned(16))) float sA[NBUF][PT * PLD];
-    __shared__ __attribute__((aligned(16))) float sB[NBUF][PT * PLD];
+    __shared__ __attribute__((aligned(16))) float sA[2][PT * PLD];
+    __shared__ __attribute__((aligned(16))) float sB[2][PT * PLD];
     const int tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
     const int h = lane >> 5, r32 = lane & 31;
     const int wj = (w >> 1) * 64, wi = (w & 1) * 64;
@@ -630,14 +629,23 @@ __global__ void __launch_bounds__(256, NBUF == 2 ? 2 : 3) k_pearson_mfma(const f
             const float* A = sA[buf];
             const float* B = sB[buf];
             const int ng = min(PK, ldz - c * PK) / 8;  // 8-float groups of this chunk (the last may be short)
+            // fragments of group g + 1 are read from LDS while group g's MFMAs
+            // run (two waves per SIMD both waiting on LDS left the MFMA pipe idle)
+            float4 fa0[2], fa1[2], fb0[2], fb1[2];
+#define PEARSON_FRAG(S_, G_)                                                   \
+    do {                                                                       \
+        const int ko_ = 8 * (G_) + 4 * h;                                      \
+        fa0[S_] = *(const float4*)&A[(wj + r32) * PLD + ko_];                  \
+        fa1[S_] = *(const float4*)&A[(wj + 32 + r32) * PLD + ko_];             \
+        fb0[S_] = *(const float4*)&B[(wi + r32) * PLD + ko_];                  \
+        fb1[S_] = *(const float4*)&B[(wi + 32 + r32) * PLD + ko_];             \
+    } while (0)
+            PEARSON_FRAG(0, 0);
 #pragma unroll
             for (int g = 0; g < PK / 8; ++g) {
                 if (g >= ng) break;
-                const int ko = 8 * g + 4 * h;
-                const float4 a0 = *(const float4*)&A[(wj + r32) * PLD + ko];
-                const float4 a1 = *(const float4*)&A[(wj + 32 + r32) * PLD + ko];
-                const float4 b0 = *(const float4*)&B[(wi + r32) * PLD + ko];
-                const float4 b1 = *(const float4*)&B[(wi + 32 + r32) * PLD + ko];
+                if (g + 1 < PK / 8 && g + 1 < ng) PEARSON_FRAG((g + 1) & 1, g + 1);
+                const float4 a0 = fa0[g & 1], a1 = fa1[g & 1], b0 = fb0[g & 1], b1 = fb1[g & 1];
 #define PEARSON_STEP(SEL)                                                                       \
     acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.SEL, b0.SEL, acc[0][0], 0, 0, 0);          \
     acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.SEL, b1.SEL, acc[0][1], 0, 0, 0);          \
@@ -649,15 +657,10 @@ __global__ void __launch_bounds__(256, NBUF == 2 ? 2 : 3) k_pearson_mfma(const f
                 PEARSON_STEP(w);
 #undef PEARSON_STEP
             }
-            if constexpr (NBUF == 2) {
-                if (more) PEARSON_LSTORE(buf ^ 1);
-                __syncthreads();
-                buf ^= 1;
-            } else {
-                __syncthreads();
-                if (more) PEARSON_LSTORE(0);
-                __syncthreads();
-            }
+#undef PEARSON_FRAG
+            if (more) PEARSON_LSTORE(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
         }
 
         if (diag_nostore) {  // diagnostic (SCC_PEARSON_NOSTORE=1): keep the result live, store nothing
@@ -867,17 +870,15 @@ extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld
     const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
     const char* ns = getenv("SCC_PEARSON_NOSTORE");
     const int nostore = ns && ns[0] == '1';
-    const char* nte = getenv("SCC_PEARSON_NT");  // nontemporal epilogue stores (default on)
-    const bool ntst = !(nte && *nte && atoi(nte) == 0);
-    const char* nbe = getenv("SCC_PEARSON_NBUF");  // 1: single LDS buffer, 3 workgroups per CU
-    const bool one = nbe && *nbe && atoi(nbe) == 1;
-    const long long nwg = one ? (per < 96 ? per : 96) : nwg_xcd;
-    const dim3 grid((unsigned)(8 * nwg));
-    const void* fn =
-        one ? (f32 ? (ntst ? (const void*)k_pearson_mfma<true, true, 1> : (const void*)k_pearson_mfma<true, false, 1>)
-                   : (ntst ? (const void*)k_pearson_mfma<false, true, 1> : (const void*)k_pearson_mfma<false, false, 1>))
-            : (f32 ? (ntst ? (const void*)k_pearson_mfma<true, true, 2> : (const void*)k_pearson_mfma<true, false, 2>)
-                   : (ntst ? (const void*)k_pearson_mfma<false, true, 2> : (const void*)k_pearson_mfma<false, false, 2>));
+    // nontemporal epilogue stores: off by default (measured at B: WRITE_SIZE
+    // 3.04 GB/launch with them, 2.73 GB = 1.01x the 2.70 GB output without —
+    // the L2 merges the partial lines that neighbouring tiles of one XCD write —
+    // and 2.287 vs 2.267 ms); SCC_PEARSON_NT=1 turns them on
+    const char* nte = getenv("SCC_PEARSON_NT");
+    const bool ntst = nte && *nte && atoi(nte) != 0;
+    const dim3 grid((unsigned)(8 * nwg_xcd));
+    const void* fn = f32 ? (ntst ? (const void*)k_pearson_mfma<true, true> : (const void*)k_pearson_mfma<true, false>)
+                         : (ntst ? (const void*)k_pearson_mfma<false, true> : (const void*)k_pearson_mfma<false, false>);
     int nti = nt;
     void* args[] = {(void*)&Z, (void*)&N, (void*)&ldz, (void*)&nti, (void*)&ntri, (void*)&per, (void*)&c_lo,
                     (void*)&c_hi, (void*)&obase, (void*)&out, (void*)&nostore};

@@ -412,6 +412,7 @@ __global__ void k_si_check(const double* __restrict__ rpart, const double* __res
 {
     const int q = threadIdx.x;
     if (q >= 16) return;
+    double* rlog = (double*)(flag + 8);  // residual / |theta_1| per pair, for SCC_EIG_SI_LOG
     double s = 0.0, m = 0.0, nn = 0.0;
     for (int b = 0; b < nblk; ++b) {
         s += rpart[(size_t)b * 32 + q];
@@ -421,6 +422,7 @@ __global__ void k_si_check(const double* __restrict__ rpart, const double* __res
     sgn[q] = (m < 0.0) ? -1.0 : 1.0;
     if (q < k) {
         Wout[q] = theta[q];
+        rlog[q] = sqrt(s) / fabs(theta[0]);
         if (!(sqrt(s) <= tol * fabs(theta[0]))) atomicOr(flag, 2u);  // residual
         if (!(fabs(nn - 1.0) <= 1e-9)) atomicOr(flag, 4u);              // basis not orthonormal
     }
@@ -547,7 +549,14 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     if (inner_err && (e = hipMemcpyAsync(&h[1], inner_err, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess)
         return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc si] n=%d iters=%d flag=%u inner=%u\n", n, iters, h[0], h[1]);
+    if (getenv("SCC_EIG_SI_LOG")) {
+        double lg[16] = {0};
+        if (hipMemcpy(lg, flag + 8, sizeof(double) * 16, hipMemcpyDeviceToHost) == hipSuccess) {
+            double rmax = 0.0;
+            for (int q = 0; q < k; ++q) rmax = std::max(rmax, lg[q]);
+            fprintf(stderr, "[scc si] n=%d iters=%d flag=%u inner=%u maxres=%.3g\n", n, iters, h[0], h[1], rmax);
+        }
+    }
     *ok = (h[0] == 0 && h[1] == 0) ? 1 : 0;
     return hipSuccess;
 }

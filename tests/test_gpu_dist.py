@@ -71,14 +71,14 @@ def test_pearson_matches_numpy(eng, cfg_a):
     assert np.max(np.abs(dist - ref)) < 1e-5
 
 
-def test_pearson_single_buffer_bitwise(eng, cfg_a, monkeypatch):
-    """The one-LDS-buffer variant (SCC_PEARSON_NBUF=1) runs the same MFMA
-    sequence: identical bits."""
+def test_pearson_nontemporal_bitwise(eng, cfg_a, monkeypatch):
+    """Nontemporal epilogue stores (SCC_PEARSON_NT=1, off by default) store
+    the same values: identical bits."""
     from scconsensus_amd import _native as nat
     d, X, uni = cfg_a
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     a = eng.distance(ds, uni, nat.SCC_DIST_PEARSON)
-    monkeypatch.setenv("SCC_PEARSON_NBUF", "1")
+    monkeypatch.setenv("SCC_PEARSON_NT", "1")
     b = eng.distance(ds, uni, nat.SCC_DIST_PEARSON)
     assert np.array_equal(a, b)
 
