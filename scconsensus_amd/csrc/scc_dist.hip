@@ -871,7 +871,7 @@ extern "C" hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld
     const char* ns = getenv("SCC_PEARSON_NOSTORE");
     const int nostore = ns && ns[0] == '1';
     // nontemporal epilogue stores: off by default (measured at B: WRITE_SIZE
-    // 3.04 GB/launch with them, 2.73 GB = 1.01x the 2.70 GB output without —
+    // 3.11 GB/launch with them, 2.79 GB = 1.03x the 2.70 GB output without —
     // the L2 merges the partial lines that neighbouring tiles of one XCD write —
     // and 2.287 vs 2.267 ms); SCC_PEARSON_NT=1 turns them on
     const char* nte = getenv("SCC_PEARSON_NT");
