@@ -373,8 +373,8 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
                         "phase C %llu cycles\n", nu, nwg_used, h[0], h[7], h[1], h[2]);
                 fprintf(stderr, "[scc stamps] vectors (eigenpair 0): bisection %llu, LU %llu, inverse iteration %llu, "
                         "back-transform %llu cycles\n", h[3], h[4], h[5], h[6]);
-                fprintf(stderr, "[scc stamps] two-stage panel 0: load %llu, columns %llu, T %llu, rows %llu cycles\n",
-                        h[8], h[9], h[10], h[11]);
+                fprintf(stderr, "[scc stamps] twisted (eigenpair 0): chains %llu, vector %llu, second pass %llu cycles\n",
+                        h[8], h[9], h[10]);
                 fprintf(stderr, "[scc stamps] block back-transform: stage %llu, V^T Y %llu, T W %llu, Y update %llu, "
                         "load %llu cycles\n", h[12], h[13], h[14], h[15], h[16]);
             }

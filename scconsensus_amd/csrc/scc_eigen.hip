@@ -655,6 +655,7 @@ struct VecArgs {
     int wait;          // 1: xcd_item_wait (grid co-resident), 0: xcd_next
     u64* stamps;    // diagnostic: workgroup 0's phase boundaries at [3..7] (nullptr normally)
     int bt_none;    // 1: leave the tridiagonal's eigenvector (the two-stage path back-transforms it)
+    int twist;      // 1: twisted factorization for isolated eigenvalues (SCC_EIG_TWIST, default 1)
 };
 
 // numbers of eigenvalues of T (d, e^2) strictly below x[0..SP) (Sturm
@@ -670,9 +671,7 @@ __device__ inline void sturm_counts(const double* d, const double* e2, int n, co
         q[p] = fabs(q[p]) < pivmin ? -pivmin : q[p];
         c[p] = (q[p] < 0.0);
     }
-#pragma unroll 4
-    for (int i = 1; i < n; ++i) {
-        const double di = d[i], ei = e2[i - 1];
+    auto step = [&](double di, double ei) {
 #pragma unroll
         for (int p = 0; p < VEC_SP; ++p) {
             // e2 / q as the hardware reciprocal refined by one Newton step (a few
@@ -684,7 +683,191 @@ __device__ inline void sturm_counts(const double* d, const double* e2, int n, co
             q[p] = t;
             c[p] += (t < 0.0);
         }
+    };
+    // whole blocks of 8 steps with their inputs loaded ahead of the chain (a
+    // bound check per step costs a branch on the chain), then the remainder
+    int i0 = 1;
+    for (; i0 + 8 <= n; i0 += 8) {
+        double dv[8], ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            dv[u] = d[i0 + u];
+            ev[u] = e2[i0 + u - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) step(dv[u], ev[u]);
     }
+    for (; i0 < n; ++i0) step(d[i0], e2[i0 - 1]);
+}
+
+// Eigenvector of an isolated eigenvalue from the twisted factorization of
+// T - lam I (Parlett & Dhillon; LAPACK dlar1v without the representation
+// tree): the stationary forward (D+) and backward (D-) recurrences run on two
+// lanes of one wave in lockstep, gamma_r = D+_r + D-_r - (d_r - lam) picks the
+// twist index r = argmin |gamma_r| (smallest r on ties), z_r = 1 and the
+// entries on either side are products of ratios formed by all threads (two
+// lanes again).  The Rayleigh correction lam + gamma_r / |z|^2 then gives the
+// shift of a second pass.  Two dependent chains of n divisions and two of n
+// multiplies, where the LU and two inverse-iteration solves were five chains
+// of n steps on one thread.  Used when [lam - delta, lam + delta], delta =
+// 1e-7 ||T||, holds exactly one eigenvalue (so the vector's error, ~eps ||T|| /
+// gap, stays below ~1e-9); returns false (block-uniform) otherwise or when the
+// vector is not finite, and the caller runs inverse iteration.  y: the
+// normalised vector; wk: 4 n scratch doubles.
+__device__ __forceinline__ bool tri_twisted(const double* dl, const double* el, const double* e2l, int n, double lam, double tnorm,
+                            double pivmin, double* wk, double* y, double* red, int* ired, u64* stm)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    u64 c0 = stm ? clock64() : 0, c1 = 0, c2 = 0;
+    double* Dp = wk;
+    double* Dm = wk + n;
+    double* rl = wk + 2 * (size_t)n;  // -e_i / D+_i   (z_i from z_{i+1}, i < r)
+    double* rm = wk + 3 * (size_t)n;  // -e_{i-1} / D-_i (z_i from z_{i-1}, i > r)
+    __shared__ int s_cnt[4];
+    const double tiny = kEps * tnorm + 1e-300;
+    const double del = 1e-7 * tnorm + pivmin;
+    constexpr int SB = 8;
+    for (int pass = 0; pass < 2; ++pass) {
+        // lanes 0..3 of wave 0 in lockstep: D+ at lam from the top (0), D- at
+        // lam from the bottom (1), Sturm counts at lam - delta (2) and lam +
+        // delta (3, first pass only).  The recurrence is carried in determinant
+        // form, p_i = (d_i - x) p_{i-1} - e_{i-1}^2 p_{i-2}: one FMA on the
+        // dependent chain, no division (lanes 0 and 1 store p_i and p_{i-1},
+        // all threads form D_i = p_i / p_{i-1} afterwards; the counts are sign
+        // changes), the pair rescaled by a power of two once per SB steps
+        if (tid < (pass == 0 ? 4 : 2)) {
+            const bool fwd = tid != 1;
+            const double x = tid == 2 ? lam - del : (tid == 3 ? lam + del : lam);
+            // lanes 2 and 3 store into y (overwritten later): no branch per step
+            double* po = tid == 0 ? Dp : (tid == 1 ? Dm : y);  // p_i
+            double* qo = tid == 0 ? rl : (tid == 1 ? rm : y);  // p_{i-1}, same scale
+            double pp = 1.0;
+            double pc = dl[fwd ? 0 : n - 1] - x;
+            int neg = pc < 0.0;
+            po[fwd ? 0 : n - 1] = pc;
+            qo[fwd ? 0 : n - 1] = 1.0;
+            auto step = [&](int s, double av, double ev) {
+                const double pn = fma(av, pc, -ev * pp);
+                neg += (pn < 0.0) != (pc < 0.0);
+                const int i = fwd ? s : n - 1 - s;
+                po[i] = pn;
+                qo[i] = pc;
+                pp = pc;
+                pc = pn;
+            };
+            int s0 = 1;
+            for (; s0 + SB <= n; s0 += SB) {  // whole blocks: no bound check inside
+                double av[SB], ev[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {  // inputs loaded ahead of the chain
+                    const int s = s0 + u;
+                    const int i = fwd ? s : n - 1 - s;
+                    av[u] = dl[i] - x;
+                    ev[u] = e2l[fwd ? s - 1 : i];
+                }
+#pragma unroll
+                for (int u = 0; u < SB; ++u) step(s0 + u, av[u], ev[u]);
+                const int ex = ilogb(pc);
+                if (ex > 256 || ex < -256) {
+                    pc = ldexp(pc, -ex);
+                    pp = ldexp(pp, -ex);
+                }
+            }
+            for (; s0 < n; ++s0) {
+                const int i = fwd ? s0 : n - 1 - s0;
+                step(s0, dl[i] - x, e2l[fwd ? s0 - 1 : i]);
+            }
+            if (pass == 0 && tid >= 2) s_cnt[tid] = neg;
+        }
+        __syncthreads();
+        if (pass == 0 && stm) c1 = clock64();
+        if (pass == 0 && s_cnt[3] - s_cnt[2] != 1) return false;  // not isolated (or non-finite)
+        for (int i = tid; i < n; i += VEC_T) {  // D = p_i / p_{i-1}; an exact zero pivot -> tiny
+            const double dp = Dp[i] / rl[i], dm = Dm[i] / rm[i];
+            Dp[i] = (fabs(dp) < tiny) ? (dp < 0.0 ? -tiny : tiny) : dp;
+            Dm[i] = (fabs(dm) < tiny) ? (dm < 0.0 ? -tiny : tiny) : dm;
+        }
+        __syncthreads();
+        double best = INFINITY;
+        int br = n;
+        for (int r = tid; r < n; r += VEC_T) {
+            const double g = fabs(Dp[r] + Dm[r] - (dl[r] - lam));
+            if (g < best) {
+                best = g;
+                br = r;
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const double ob = __shfl_xor(best, m, 64);
+            const int orr = __shfl_xor(br, m, 64);
+            if (ob < best || (ob == best && orr < br)) {
+                best = ob;
+                br = orr;
+            }
+        }
+        if (lane == 0) {
+            red[wv] = best;
+            ired[wv] = br;
+        }
+        __syncthreads();
+        best = red[0];
+        br = ired[0];
+        for (int w = 1; w < VEC_W; ++w)
+            if (red[w] < best || (red[w] == best && ired[w] < br)) {
+                best = red[w];
+                br = ired[w];
+            }
+        __syncthreads();
+        if (br >= n) return false;  // every gamma NaN
+        const int r = br;
+        const double gam = Dp[r] + Dm[r] - (dl[r] - lam);
+        for (int i = tid; i < n; i += VEC_T) {
+            rl[i] = (i < n - 1) ? -el[i] / Dp[i] : 0.0;
+            rm[i] = (i > 0) ? -el[i - 1] / Dm[i] : 0.0;
+        }
+        __syncthreads();
+        if (tid < 2) {  // lane 0: z_{r-1} .. z_0, lane 1: z_{r+1} .. z_{n-1}
+            const bool up = tid == 0;
+            const int len = up ? r : n - 1 - r;
+            double z = 1.0;
+            if (up) y[r] = 1.0;
+            int s0 = 1;
+            for (; s0 + SB - 1 <= len; s0 += SB) {  // whole blocks: no bound check inside
+                double rv[SB];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) rv[u] = up ? rl[r - s0 - u] : rm[r + s0 + u];
+#pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    z *= rv[u];
+                    y[up ? r - s0 - u : r + s0 + u] = z;
+                }
+            }
+            for (; s0 <= len; ++s0) {
+                z *= up ? rl[r - s0] : rm[r + s0];
+                y[up ? r - s0 : r + s0] = z;
+            }
+        }
+        __syncthreads();
+        double ss = 0.0;
+        for (int i = tid; i < n; i += VEC_T) ss = fma(y[i], y[i], ss);
+        ss = block_sum<VEC_W>(ss, red);
+        if (!(ss >= 1.0) || !(ss < INFINITY)) return false;
+        if (pass == 0) {
+            if (stm) c2 = clock64();
+            lam += gam / ss;  // Rayleigh quotient of z
+        } else {
+            const double inv = 1.0 / sqrt(ss);
+            for (int i = tid; i < n; i += VEC_T) y[i] *= inv;
+            __syncthreads();
+        }
+    }
+    if (stm) {
+        stm[8] = c1 - c0;
+        stm[9] = c2 - c1;
+        stm[10] = clock64() - c2;
+    }
+    return true;
 }
 
 __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
@@ -777,134 +960,142 @@ __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
         a.W[q] = lam;
         if (q == 0) a.tnorm[0] = tnorm;
     }
-    // ---- inverse iteration (dgttrf / dgttrs) by thread 0: the factor's
-    // recurrence runs in registers (the next diagonal and super-diagonal are
-    // carried, the inputs are independent loads), pivots stored as reciprocals
-    double* fdr = lu;  // 1 / U diagonal
-    double* fu = fdr + n;
-    double* fu2 = fu + n;
-    double* fl = fu2 + n;
-    double* fp = fl + n;
-    double* w = fp + n;  // forward-solve result
-    const double tiny = kEps * tnorm + 1e-300;
-    if (tid == 0) {
-        // inputs of LU_B steps are loaded together ahead of the dependent chain
-        constexpr int LU_B = 8;
-        double dcur = dl[0] - lam, ucur = (n > 1) ? el[0] : 0.0;
-        for (int i0 = 0; i0 < n - 1; i0 += LU_B) {
-            double li[LU_B], dn[LU_B], un[LU_B];
-#pragma unroll
-            for (int u = 0; u < LU_B; ++u) {  // clamped unconditional loads
-                const int i = i0 + u;
-                const double e0 = el[min(i, n - 1)], d1 = dl[min(i + 1, n - 1)], e1 = el[min(i + 1, n - 1)];
-                li[u] = e0;
-                dn[u] = d1 - lam;
-                un[u] = (i < n - 2) ? e1 : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < LU_B; ++u) {  // branch-free step: one division on the chain
-                const int i = i0 + u;
-                if (i >= n - 1) break;
-                const bool piv = fabs(dcur) < fabs(li[u]);  // LAPACK dgttrf: swap rows i, i+1
-                const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
-                const double den = piv ? li[u] : dc;
-                // (piv ? dc : l) / den as a refined hardware reciprocal (a few ulp)
-                const double r0 = __builtin_amdgcn_rcp(den);
-                const double f = (piv ? dc : li[u]) * fma(fma(-den, r0, 1.0), r0, r0);
-                fl[i] = f;
-                fdr[i] = den;  // the pivot; its reciprocal is taken below, off the chain
-                // operands selected first, one FMA each on the chain (no branch)
-                const double ua = piv ? dn[u] : ucur, ub = piv ? ucur : dn[u];
-                fu[i] = ua;
-                fu2[i] = piv ? un[u] : 0.0;  // zero at i = n - 2
-                fp[i] = piv ? 1.0 : 0.0;
-                dcur = fma(-f, ua, ub);
-                ucur = piv ? -f * un[u] : un[u];
-            }
-        }
-        if (dcur == 0.0) dcur = tiny;
-        fdr[n - 1] = dcur;
-        fu[n - 1] = 0.0;
-        fu2[n - 1] = 0.0;
-    }
-    __syncthreads();
-    for (int i = tid; i < n; i += VEC_T) fdr[i] = 1.0 / fdr[i];
-    const u64 t2 = stmp ? clock64() : 0;
-    for (int i = tid; i < n; i += VEC_T) {  // deterministic pseudo-random start
-        unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)q * 40503u + 12345u);
-        h ^= h >> 13;
-        h *= 0x5bd1e995u;
-        h ^= h >> 15;
-        y[i] = 0.5 + (double)(h & 0xffff) / 65536.0;
-    }
-    __syncthreads();
-    for (int iter = 0; iter < 2; ++iter) {
+    // ---- twisted factorization for an isolated eigenvalue (tri_twisted);
+    // otherwise (a cluster closer than 1e-7 ||T||, a non-finite vector) inverse
+    // iteration below
+    u64 t2 = 0;
+    const bool twisted = a.twist && a.lu_lds && tri_twisted(dl, el, e2l, n, lam, tnorm, pivmin, y + n, y, red, ired, stmp ? a.stamps : nullptr);
+    if (!twisted) {
+        // ---- inverse iteration (dgttrf / dgttrs) by thread 0: the factor's
+        // recurrence runs in registers (the next diagonal and super-diagonal are
+        // carried, the inputs are independent loads), pivots stored as reciprocals
+        double* fdr = lu;  // 1 / U diagonal
+        double* fu = fdr + n;
+        double* fu2 = fu + n;
+        double* fl = fu2 + n;
+        double* fp = fl + n;
+        double* w = fp + n;  // forward-solve result
+        const double tiny = kEps * tnorm + 1e-300;
         if (tid == 0) {
-            constexpr int SB = 8;  // inputs of SB steps loaded ahead of the dependent chain
-            double bi = y[0];
-            for (int i0 = 0; i0 < n - 1; i0 += SB) {  // w = L^-1 P y
-                double bn[SB], f[SB], pv[SB];
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int i = min(i0 + u, n - 2);
-                    bn[u] = y[i + 1];
-                    f[u] = fl[i];
-                    pv[u] = fp[i];
+            // inputs of LU_B steps are loaded together ahead of the dependent chain
+            constexpr int LU_B = 8;
+            double dcur = dl[0] - lam, ucur = (n > 1) ? el[0] : 0.0;
+            for (int i0 = 0; i0 < n - 1; i0 += LU_B) {
+                double li[LU_B], dn[LU_B], un[LU_B];
+    #pragma unroll
+                for (int u = 0; u < LU_B; ++u) {  // clamped unconditional loads
+                    const int i = i0 + u;
+                    const double e0 = el[min(i, n - 1)], d1 = dl[min(i + 1, n - 1)], e1 = el[min(i + 1, n - 1)];
+                    li[u] = e0;
+                    dn[u] = d1 - lam;
+                    un[u] = (i < n - 2) ? e1 : 0.0;
                 }
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    if (i0 + u >= n - 1) break;
-                    // operands selected first, one FMA on the chain (no branch)
-                    const bool piv = pv[u] != 0.0;
-                    const double xa = piv ? bn[u] : bi, xb = piv ? bi : bn[u];
-                    w[i0 + u] = xa;
-                    bi = fma(-f[u], xa, xb);
-                }
-            }
-            w[n - 1] = bi;
-            double z1 = 0.0, z2 = 0.0;  // y = U^-1 w, from the bottom
-            for (int i1 = n - 1; i1 >= 0; i1 -= SB) {
-                double wv8[SB], u1[SB], u2[SB], r[SB];
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int i = max(i1 - u, 0);
-                    wv8[u] = w[i];
-                    u1[u] = fu[i];
-                    u2[u] = fu2[i];
-                    r[u] = fdr[i];
-                }
-#pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int i = i1 - u;
-                    if (i < 0) break;
-                    const double z0 = fma(-u1[u], z2, fma(-u2[u], z1, wv8[u])) * r[u];  // z2 = y[i+1], z1 = y[i+2]
-                    y[i] = z0;
-                    z1 = z2;
-                    z2 = z0;
+    #pragma unroll
+                for (int u = 0; u < LU_B; ++u) {  // branch-free step: one division on the chain
+                    const int i = i0 + u;
+                    if (i >= n - 1) break;
+                    const bool piv = fabs(dcur) < fabs(li[u]);  // LAPACK dgttrf: swap rows i, i+1
+                    const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
+                    const double den = piv ? li[u] : dc;
+                    // (piv ? dc : l) / den as a refined hardware reciprocal (a few ulp)
+                    const double r0 = __builtin_amdgcn_rcp(den);
+                    const double f = (piv ? dc : li[u]) * fma(fma(-den, r0, 1.0), r0, r0);
+                    fl[i] = f;
+                    fdr[i] = den;  // the pivot; its reciprocal is taken below, off the chain
+                    // operands selected first, one FMA each on the chain (no branch)
+                    const double ua = piv ? dn[u] : ucur, ub = piv ? ucur : dn[u];
+                    fu[i] = ua;
+                    fu2[i] = piv ? un[u] : 0.0;  // zero at i = n - 2
+                    fp[i] = piv ? 1.0 : 0.0;
+                    dcur = fma(-f, ua, ub);
+                    ucur = piv ? -f * un[u] : un[u];
                 }
             }
+            if (dcur == 0.0) dcur = tiny;
+            fdr[n - 1] = dcur;
+            fu[n - 1] = 0.0;
+            fu2[n - 1] = 0.0;
         }
         __syncthreads();
-        // scale by the largest magnitude first (a solve can grow y by 1/pivot ~ 1e300)
-        double mx = 0.0;
-        for (int i = tid; i < n; i += VEC_T) mx = fmax(mx, fabs(y[i]));
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) mx = fmax(mx, __shfl_xor(mx, m, 64));
-        if (lane == 0) red[8 + wv] = mx;
-        __syncthreads();
-        mx = red[8];
-        for (int w2 = 1; w2 < VEC_W; ++w2) mx = fmax(mx, red[8 + w2]);
-        const double sc = (mx > 0.0 && mx < INFINITY) ? 1.0 / mx : 1.0;
-        double s = 0.0;
-        for (int i = tid; i < n; i += VEC_T) {
-            const double v = y[i] * sc;
-            s += v * v;
+        for (int i = tid; i < n; i += VEC_T) fdr[i] = 1.0 / fdr[i];
+        t2 = stmp ? clock64() : 0;
+        for (int i = tid; i < n; i += VEC_T) {  // deterministic pseudo-random start
+            unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)q * 40503u + 12345u);
+            h ^= h >> 13;
+            h *= 0x5bd1e995u;
+            h ^= h >> 15;
+            y[i] = 0.5 + (double)(h & 0xffff) / 65536.0;
         }
-        s = block_sum<VEC_W>(s, red);
-        const double inv = sc / sqrt(s);
-        for (int i = tid; i < n; i += VEC_T) y[i] *= inv;
         __syncthreads();
+        for (int iter = 0; iter < 2; ++iter) {
+            if (tid == 0) {
+                constexpr int SB = 8;  // inputs of SB steps loaded ahead of the dependent chain
+                double bi = y[0];
+                for (int i0 = 0; i0 < n - 1; i0 += SB) {  // w = L^-1 P y
+                    double bn[SB], f[SB], pv[SB];
+    #pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        const int i = min(i0 + u, n - 2);
+                        bn[u] = y[i + 1];
+                        f[u] = fl[i];
+                        pv[u] = fp[i];
+                    }
+    #pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        if (i0 + u >= n - 1) break;
+                        // operands selected first, one FMA on the chain (no branch)
+                        const bool piv = pv[u] != 0.0;
+                        const double xa = piv ? bn[u] : bi, xb = piv ? bi : bn[u];
+                        w[i0 + u] = xa;
+                        bi = fma(-f[u], xa, xb);
+                    }
+                }
+                w[n - 1] = bi;
+                double z1 = 0.0, z2 = 0.0;  // y = U^-1 w, from the bottom
+                for (int i1 = n - 1; i1 >= 0; i1 -= SB) {
+                    double wv8[SB], u1[SB], u2[SB], r[SB];
+    #pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        const int i = max(i1 - u, 0);
+                        wv8[u] = w[i];
+                        u1[u] = fu[i];
+                        u2[u] = fu2[i];
+                        r[u] = fdr[i];
+                    }
+    #pragma unroll
+                    for (int u = 0; u < SB; ++u) {
+                        const int i = i1 - u;
+                        if (i < 0) break;
+                        const double z0 = fma(-u1[u], z2, fma(-u2[u], z1, wv8[u])) * r[u];  // z2 = y[i+1], z1 = y[i+2]
+                        y[i] = z0;
+                        z1 = z2;
+                        z2 = z0;
+                    }
+                }
+            }
+            __syncthreads();
+            // scale by the largest magnitude first (a solve can grow y by 1/pivot ~ 1e300)
+            double mx = 0.0;
+            for (int i = tid; i < n; i += VEC_T) mx = fmax(mx, fabs(y[i]));
+    #pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) mx = fmax(mx, __shfl_xor(mx, m, 64));
+            if (lane == 0) red[8 + wv] = mx;
+            __syncthreads();
+            mx = red[8];
+            for (int w2 = 1; w2 < VEC_W; ++w2) mx = fmax(mx, red[8 + w2]);
+            const double sc = (mx > 0.0 && mx < INFINITY) ? 1.0 / mx : 1.0;
+            double s = 0.0;
+            for (int i = tid; i < n; i += VEC_T) {
+                const double v = y[i] * sc;
+                s += v * v;
+            }
+            s = block_sum<VEC_W>(s, red);
+            const double inv = sc / sqrt(s);
+            for (int i = tid; i < n; i += VEC_T) y[i] *= inv;
+            __syncthreads();
+        }
     }
+    if (twisted) t2 = stmp ? clock64() : 0;
     // ---- back-transformation z = H_0 H_1 ... H_{n-3} y in blocks of BT_NB
     // reflectors, last block first: block b is I - V T V^T (compact WY, T from
     // k_refl_T), three barrier-separated steps per block
@@ -1692,6 +1883,10 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     v.lda = lda;
     v.k = k;
     v.lu_lds = lu_lds ? 1 : 0;
+    {
+        const char* te = getenv("SCC_EIG_TWIST");  // 0: inverse iteration for every eigenpair
+        v.twist = (te && *te && atoi(te) == 0) ? 0 : 1;
+    }
     v.lu = scratch + L.lu;
     v.Zq = scratch + L.zq;
     v.W = W;

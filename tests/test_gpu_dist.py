@@ -208,6 +208,28 @@ def test_back_transformations_agree(eng, n, monkeypatch):
     assert np.max(np.abs(outs[0] - outs[2])) < 1e-9
 
 
+@pytest.mark.parametrize("n", [2, 3, 17, 64, 150, 323, 400])
+def test_twisted_vectors_agree(eng, n, monkeypatch):
+    """Eigenvectors from the twisted factorization (isolated eigenvalues, the
+    default) and from inverse iteration (SCC_EIG_TWIST=0) give the same PCA,
+    both equal to the exact SVD; config B's bulk-edge spacing (relative gaps
+    ~3e-3 among eigenvalues 11..16) included."""
+    from scconsensus_amd import _native as nat
+    monkeypatch.setenv("SCC_EIG_SI", "0")
+    rng = np.random.default_rng(700 + n)
+    X = rng.standard_normal((n, 900)) * np.linspace(1.0, 0.97, n)[:, None]  # a near-flat bulk
+    X[: min(n, 10)] += rng.standard_normal((min(n, 10), 1)) * rng.standard_normal((1, 900)) * 3.0
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    d1 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    monkeypatch.setenv("SCC_EIG_TWIST", "0")
+    d0 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    assert np.max(np.abs(d1 - ref)) < 1e-5
+    assert np.max(np.abs(d0 - ref)) < 1e-5
+    assert np.max(np.abs(d1 - d0)) < 1e-7
+
+
 def test_workgroup_count_bitwise(eng, monkeypatch):
     """The tridiagonalisation's reductions have a fixed shape: 8, 20 or 32
     workgroups in the hand-off give the same distance bits."""
