@@ -1165,6 +1165,28 @@ __global__ void __launch_bounds__(VEC_T) k_tri_vectors(VecArgs a)
     for (int q; (q = xcd_next(a.xcd, a.vcount, a.k, &role)) >= 0;) tri_vector_item(a, q);
 }
 
+// T[0:i, i] = -tau_i T[0:i, 0:i] G[i, 0:i], T[i][i] = tau_i (G[i][j] = v_i .
+// v_j for j < i).  Row r of T only depends on row r (T[r][i] = -tau_i sum_{r <=
+// m < i} T[r][m] G[i][m]), so thread r < 32 keeps its row in registers and
+// runs all columns without a barrier; G is read as LDS broadcasts.
+__device__ __forceinline__ void refl_T_recur(const double (*G)[BT_NB + 1], const double* __restrict__ tau, int kb,
+                                             int nb, double* __restrict__ tf, int b)
+{
+    const int r = threadIdx.x;
+    if (r >= BT_NB) return;
+    double t[BT_NB];
+#pragma unroll
+    for (int i = 0; i < BT_NB; ++i) {
+        const double ti = i < nb ? tau[kb + min(i, nb - 1)] : 0.0;
+        double sacc = 0.0;
+#pragma unroll
+        for (int m = 0; m < i; ++m) sacc = fma(m >= r ? t[m] : 0.0, G[i][m], sacc);
+        t[i] = (i < nb) ? ((r < i) ? -ti * sacc : (r == i ? ti : 0.0)) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < BT_NB; ++i) tf[(size_t)b * BT_NB * BT_NB + r * BT_NB + i] = t[i];
+}
+
 // T factors of the compact WY form of the reflectors, one workgroup per block
 // of BT_NB (LAPACK dlarft, forward / columnwise): T[i][i] = tau_i,
 // T[0:i, i] = -tau_i T[0:i, 0:i] (V[:, 0:i]^T v_i).
@@ -1172,7 +1194,6 @@ __device__ __forceinline__ void refl_T_item(const double* __restrict__ refl, con
                                             int lda, double* __restrict__ tf, const int b)
 {
     __shared__ double G[BT_NB][BT_NB + 1];
-    __shared__ double T[BT_NB][BT_NB + 1];
     const int kb = b * BT_NB, nb = min(BT_NB, n - 2 - kb), tid = threadIdx.x;
     // G[i][j] = v_i . v_j for j < i (both nonzero from row kb + i + 1): wave wv
     // takes rows i = wv and wv + 16, every j < i in registers
@@ -1198,20 +1219,54 @@ __device__ __forceinline__ void refl_T_item(const double* __restrict__ refl, con
             if (lane == 0) G[i][j] = sj;
         }
     }
-    for (int e = tid; e < BT_NB * (BT_NB + 1); e += 1024) (&T[0][0])[e] = 0.0;
     __syncthreads();
-    for (int i = 0; i < nb; ++i) {
-        const double ti = tau[kb + i];
-        if (tid < i) {
-            double s = 0.0;
-            for (int m = tid; m < i; ++m) s += T[tid][m] * G[i][m];
-            T[tid][i] = -ti * s;
-        } else if (tid == i) {
-            T[i][i] = ti;
+    refl_T_recur(G, tau, kb, nb, tf, b);
+}
+
+// k_refl_T with the block's 32 reflector rows staged in LDS (32 n doubles,
+// coalesced), then G[i][j] = v_i . v_j by thread (i, j) from LDS: one pass over
+// the reflectors instead of 32 strided loads per row step and 32 wave sums per
+// row.  Grid: one workgroup per block.
+__global__ void __launch_bounds__(1024) k_refl_T_lds(const double* __restrict__ refl, const double* __restrict__ tau,
+                                                     int n, int lda, double* __restrict__ tf)
+{
+    extern __shared__ __attribute__((aligned(16))) double Vs[];  // [BT_NB][n]
+    __shared__ double G[BT_NB][BT_NB + 1];
+    const int b = blockIdx.x, kb = b * BT_NB, nb = min(BT_NB, n - 2 - kb), tid = threadIdx.x;
+    const int lane = tid & 63, wv = scc_wave_id();
+    // v_i: rows > kb + i (zero elsewhere and past nb); clamped unconditional
+    // loads, all of a lane's in flight before the first store
+    constexpr int SR = 8;  // row steps per batch
+    for (int i = wv; i < BT_NB; i += 16) {
+        const double* src = refl + (size_t)(kb + min(i, nb - 1)) * lda;
+        for (int r0 = lane; r0 < n; r0 += 64 * SR) {
+            double v[SR];
+#pragma unroll
+            for (int u = 0; u < SR; ++u) v[u] = src[min(r0 + 64 * u, n - 1)];
+#pragma unroll
+            for (int u = 0; u < SR; ++u) {
+                const int r = r0 + 64 * u;
+                if (r < n) Vs[(size_t)i * n + r] = (i < nb && r > kb + i) ? v[u] : 0.0;
+            }
         }
-        __syncthreads();
     }
-    tf[(size_t)b * BT_NB * BT_NB + tid] = T[tid >> 5][tid & 31];
+    __syncthreads();
+    if (wv < 4) {  // G = V V^T on fp64 MFMA: wave w the 16 x 16 tile (16 (w >> 1), 16 (w & 1))
+        const int i0 = 16 * (wv >> 1), j0 = 16 * (wv & 1), kr = lane >> 4, cc = lane & 15;
+        const double* va = Vs + (size_t)(i0 + cc) * n;
+        const double* vb = Vs + (size_t)(j0 + cc) * n;
+        typedef double d4v __attribute__((ext_vector_type(4)));
+        d4v acc = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = kb & ~3; k0 < n; k0 += 4) {  // rows <= kb are zero in every v of the block
+            const int r = min(k0 + kr, n - 1);
+            const bool ok = k0 + kr < n;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ok ? va[r] : 0.0, ok ? vb[r] : 0.0, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) G[i0 + kr + 4 * q][j0 + cc] = acc[q];
+    }
+    __syncthreads();
+    refl_T_recur(G, tau, kb, nb, tf, b);
 }
 
 __global__ void __launch_bounds__(1024) k_refl_T(const double* __restrict__ refl, const double* __restrict__ tau, int n,
@@ -1934,8 +1989,15 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
             hipStreamWaitEvent(side, fork_ev, 0);
             rs = side;
         }
-        hipLaunchKernelGGL(k_refl_T, dim3(pin ? 8 * nblk : nblk), dim3(1024), 0, rs, t.refl, t.tau, n, lda,
-                           scratch + L.tf, pin ? t.reg : nullptr, flags + 9);
+        const size_t rlds = sizeof(double) * BT_NB * (size_t)n;
+        if (rlds + 20 * 1024 <= EIG_LDS_MAX) {  // + the static G, T (one coalesced read: no XCD pinning)
+            hipFuncSetAttribute((const void*)k_refl_T_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds);
+            hipLaunchKernelGGL(k_refl_T_lds, dim3(nblk), dim3(1024), rlds, rs, t.refl, t.tau, n, lda,
+                               scratch + L.tf);
+        } else {
+            hipLaunchKernelGGL(k_refl_T, dim3(pin ? 8 * nblk : nblk), dim3(1024), 0, rs, t.refl, t.tau, n, lda,
+                               scratch + L.tf, pin ? t.reg : nullptr, flags + 9);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (q_form) {
             const size_t qlds = form_q_lds(n);
