@@ -1499,6 +1499,7 @@ __global__ void __launch_bounds__(TB_T) k_tri_back(double* __restrict__ Zq, int 
 // of the one-workgroup, block-sequential k_tri_back on the critical path.
 #define QF_R 16
 #define QF_T 256
+#define QF_MAXC 6  // 64-column chunks of a reflector row held in registers (n <= 384)
 static_assert(8 * (QF_T / 64) == BT_NB, "k_form_q stages BT_NB reflector rows, QF_VB per wave");
 __global__ void __launch_bounds__(QF_T) k_form_q(const double* __restrict__ refl, const double* __restrict__ tf, int n,
                                                  int lda, double* __restrict__ Q)
@@ -1515,28 +1516,38 @@ __global__ void __launch_bounds__(QF_T) k_form_q(const double* __restrict__ refl
     for (int r = wv; r < QF_R; r += QF_T / 64)
         for (int j = lane; j < n; j += 64) Qs[(size_t)r * n + j] = (r0 + r == j) ? 1.0 : 0.0;
     const int nr = n - 2, nblk = nr > 0 ? (nr + BT_NB - 1) / BT_NB : 0;
-    // V_b's rows: wave w stages rows i = w + 4 u, lanes over j, QF_VB loads of
-    // a row-chunk in flight at once (clamped, unconditional; masked on store)
+    // V_b's rows: wave w stages rows i = w + 4 u, lanes over j.  Block b + 1's
+    // values are loaded into registers (clamped, unconditional) while block b
+    // is applied, and stored to LDS (masked) at the top of the next iteration,
+    // so the reflector fetch latency is paid once instead of once per block
     constexpr int QF_VB = 8;
+    double pf[QF_MAXC][QF_VB];
+    auto fetch = [&](int b) {
+        const int kb = b * BT_NB, nb = min(BT_NB, nr - kb);
+#pragma unroll
+        for (int c = 0; c < QF_MAXC; ++c) {
+            const int jc = min(c * 64 + lane, n - 1);
+#pragma unroll
+            for (int u = 0; u < QF_VB; ++u)
+                pf[c][u] = refl[(size_t)(kb + min(wv + (QF_T / 64) * u, nb - 1)) * lda + jc];
+        }
+    };
+    if (nblk > 0) fetch(0);
     for (int b = 0; b < nblk; ++b) {
         const int kb = b * BT_NB, nb = min(BT_NB, nr - kb), m0 = kb + 1;
         __syncthreads();  // the previous block's update of Qs is complete before Vs is reused
-        for (int j0 = 0; j0 < n; j0 += 64) {
-            const int j = j0 + lane, jc = min(j, n - 1);
-            double vv[QF_VB];
+#pragma unroll
+        for (int c = 0; c < QF_MAXC; ++c) {
+            const int j = c * 64 + lane;
 #pragma unroll
             for (int u = 0; u < QF_VB; ++u) {
                 const int i = wv + (QF_T / 64) * u;
-                vv[u] = refl[(size_t)(kb + min(i, nb - 1)) * lda + jc];
-            }
-#pragma unroll
-            for (int u = 0; u < QF_VB; ++u) {
-                const int i = wv + (QF_T / 64) * u;
-                if (j < n) Vs[(size_t)i * n + j] = (i < nb && j > kb + i) ? vv[u] : 0.0;
+                if (j < n) Vs[(size_t)i * n + j] = (i < nb && j > kb + i) ? pf[c][u] : 0.0;
             }
         }
         for (int x = tid; x < BT_NB * BT_NB; x += QF_T) (&Ts[0][0])[x] = tf[(size_t)b * BT_NB * BT_NB + x];
         __syncthreads();
+        if (b + 1 < nblk) fetch(b + 1);
         {  // S = Q_rows V_b^T-side: 16 rows x 32 reflectors, K = the rows j >= m0; wave
             // w: reflector tile w & 1, K half w >> 1
             const int tile = wv & 1, half = wv >> 1;
@@ -1969,7 +1980,8 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     const char* bt_env = getenv("SCC_EIG_BT");
     const int bt_mode = (bt_env && *bt_env) ? atoi(bt_env) : 2;
     const bool back_fits = n > 2 && n - 1 <= 12 * TB_T / BT_NB && tri_back_lds(n, k) + 33 * 1024 <= EIG_LDS_MAX;
-    const bool q_form = n > 2 && bt_mode == 2 && form_q_lds(n) + 24 * 1024 <= EIG_LDS_MAX;  // + its static arrays
+    const bool q_form = n > 2 && bt_mode == 2 && form_q_lds(n) + 24 * 1024 <= EIG_LDS_MAX &&  // + its static arrays
+                        n <= 64 * QF_MAXC;
     const bool bt_one = !q_form && back_fits && bt_mode != 0;  // one fetch batch covers a block
     v.bt_none = (bt_one || q_form) ? 1 : 0;
     // k_refl_T (reflectors -> T factors) does not depend on the tridiagonal's
