@@ -706,14 +706,16 @@ __device__ inline void sturm_counts(const double* d, const double* e2, int n, co
 // lanes of one wave in lockstep, gamma_r = D+_r + D-_r - (d_r - lam) picks the
 // twist index r = argmin |gamma_r| (smallest r on ties), z_r = 1 and the
 // entries on either side are products of ratios formed by all threads (two
-// lanes again).  The Rayleigh correction lam + gamma_r / |z|^2 then gives the
-// shift of a second pass.  Two dependent chains of n divisions and two of n
+// lanes again).  The shift comes from a bisection closed to 4 eps ||T||, so
+// one solve suffices (TW_PASSES = 2 adds a pass at the Rayleigh-corrected
+// shift lam + gamma_r / |z|^2).  Two dependent chains of n divisions and two of n
 // multiplies, where the LU and two inverse-iteration solves were five chains
 // of n steps on one thread.  Used when [lam - delta, lam + delta], delta =
 // 1e-7 ||T||, holds exactly one eigenvalue (so the vector's error, ~eps ||T|| /
 // gap, stays below ~1e-9); returns false (block-uniform) otherwise or when the
 // vector is not finite, and the caller runs inverse iteration.  y: the
 // normalised vector; wk: 4 n scratch doubles.
+#define TW_PASSES 1  // twisted solves (a second one after a Rayleigh correction of the shift)
 __device__ __forceinline__ bool tri_twisted(const double* dl, const double* el, const double* e2l, int n, double lam, double tnorm,
                             double pivmin, double* wk, double* y, double* red, int* ired, u64* stm)
 {
@@ -727,7 +729,7 @@ __device__ __forceinline__ bool tri_twisted(const double* dl, const double* el, 
     const double tiny = kEps * tnorm + 1e-300;
     const double del = 1e-7 * tnorm + pivmin;
     constexpr int SB = 8;
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < TW_PASSES; ++pass) {
         // lanes 0..3 of wave 0 in lockstep: D+ at lam from the top (0), D- at
         // lam from the bottom (1), Sturm counts at lam - delta (2) and lam +
         // delta (3, first pass only).  The recurrence is carried in determinant
@@ -853,7 +855,7 @@ __device__ __forceinline__ bool tri_twisted(const double* dl, const double* el, 
         for (int i = tid; i < n; i += VEC_T) ss = fma(y[i], y[i], ss);
         ss = block_sum<VEC_W>(ss, red);
         if (!(ss >= 1.0) || !(ss < INFINITY)) return false;
-        if (pass == 0) {
+        if (pass + 1 < TW_PASSES) {
             if (stm) c2 = clock64();
             lam += gam / ss;  // Rayleigh quotient of z
         } else {
@@ -863,6 +865,7 @@ __device__ __forceinline__ bool tri_twisted(const double* dl, const double* el, 
         }
     }
     if (stm) {
+        if (!c2) c2 = c1;
         stm[8] = c1 - c0;
         stm[9] = c2 - c1;
         stm[10] = clock64() - c2;
@@ -948,11 +951,13 @@ __device__ __forceinline__ void tri_vector_item(const VecArgs& a, const int q)
         if (nlo == lo && nhi == hi) break;
         lo = nlo;
         hi = nhi;
-        // 1e-11 relative (or 2 eps ||T||) is enough: the eigenvector comes from
-        // inverse iteration, whose error does not depend on the shift's last
-        // digits (two solves gain (shift error / gap)^2), and the eigenvalue
-        // itself only feeds the 1e-3 ||T|| cluster rule of the finish
-        if (hi - lo <= fmax(1e-11 * fmax(fabs(lo), fabs(hi)), 2.0 * kEps * tnorm) + pivmin) break;
+        // 1e-11 relative (or 2 eps ||T||) is enough for inverse iteration (two
+        // solves gain (shift error / gap)^2); the twisted factorization takes
+        // the shift as it is, so with a.twist the bracket closes to 4 eps ||T||
+        // (its vector error ~ shift error / gap)
+        if (hi - lo <= (a.twist ? 4.0 * kEps * tnorm
+                                : fmax(1e-11 * fmax(fabs(lo), fabs(hi)), 2.0 * kEps * tnorm)) + pivmin)
+            break;
     }
     const double lam = 0.5 * (lo + hi);
     const u64 t1 = stmp ? clock64() : 0;
