@@ -835,7 +835,8 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     // 0.525); SCC_DIST_COLS forces either (bit-identical).  Nontemporal stores
     // (SCC_DIST_NT=0: plain; B 0.51 vs 0.54 ms).  Removed after measuring slower
     // at B / D: unaligned row tiles (0.69 / 38.1 ms), barrier-free wave windows
-    // (0.59 ms), 256-column tiles (0.78 / 36.2 ms).
+    // (0.59 ms), 256-column tiles (0.78 / 36.2 ms).  Columns per LDS stage (DA_NB):
+    // B 8: 0.57-0.58 ms, 4: 0.566, 16: 0.69.
     const char* env = getenv("SCC_DIST_COLS");
     const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? 128 : 64);
     const char* nte = getenv("SCC_DIST_NT");
