@@ -55,6 +55,8 @@ def _args(argv=None):
     ap.add_argument("--cpu-sample-genes", type=int, default=1500)
     ap.add_argument("--no-stage-events", action="store_true",
                     help="no per-stage HIP events in the engine (diagnostic: their cost on the step)")
+    ap.add_argument("--split-calls", action="store_true",
+                    help="scc_de_run then scc_distance (two C calls) instead of the fused scc_de_distance")
     ap.add_argument("--mode", choices=["shard", "jobs"], default="shard",
                     help="shard: ONE job over all ranks (strong scaling); jobs: one job per rank (weak scaling)")
     ap.add_argument("--dry-run", action="store_true",
@@ -285,11 +287,18 @@ def main():
                 eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, out=dist_out[: hi * (2 * ds.N - hi - 1) // 2
                                                                                  - lo * (2 * ds.N - lo - 1) // 2])
             return r
-        r = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")
+        if a.split_calls:  # scc_de_run, then scc_distance on the returned union
+            r = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")
+            if isinstance(dist_out, int):
+                eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
+            else:
+                eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, out=dist_out)
+            return r
+        # scc_de_distance: the same two stages in one C call
         if isinstance(dist_out, int):
-            eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
+            r, _ = eng.de_distance(ds, code, K, nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
         else:
-            eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, out=dist_out)
+            r, _ = eng.de_distance(ds, code, K, nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID, out=dist_out)
         return r
 
     def timed(nsteps, **kw):

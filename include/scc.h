@@ -242,6 +242,15 @@ SCC_API void scc_de_result_destroy(scc_de_result* r);
  * float instead of double. */
 SCC_API int scc_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* genes /* host */, int32_t n_union,
                  int32_t metric, int32_t ncomp, void* dist_out, int32_t out_kind, int32_t out_f32);
+/* reclusterDEConsensusFast's compute path in one call (Fast:57-400): the DE
+ * of scc_de_run, then scc_distance over its gene union, without returning to
+ * the caller in between (one host round trip fewer per job).  *out receives
+ * the DE result as from scc_de_run (the union: scc_de_result_union); the
+ * distance goes to dist_out as in scc_distance.  An empty union fails with
+ * SCC_ERR_INVALID after *out is set. */
+SCC_API int scc_de_distance(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,
+                    const scc_de_params* params, int32_t metric, int32_t ncomp, void* dist_out, int32_t out_kind,
+                    int32_t out_f32, scc_de_result** out);
 /* The same for the columns [col_lo, col_hi) only: entries
  * [col_lo(2N-col_lo-1)/2, col_hi(2N-col_hi-1)/2) of the packed R `dist`
  * vector, a contiguous slice.  Ranks that split [0, N) into column ranges of

@@ -27,6 +27,7 @@ for s in "$@"; do
     profq) step profq 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 2 ;;
     pmcB) step pmcB 600 bash scripts/pmc_traffic.sh B ;;
     pmcD) step pmcD 900 bash scripts/pmc_traffic.sh D ;;
+    benchsplit) step benchsplit 600 python bench.py --no-cpu-baseline --no-transfers --steps 20 --warmup 5 --split-calls ;;
     benchD) step benchD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchC) step benchC 900 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchE) step benchE 900 python bench.py --config E --no-cpu-baseline --steps 3 --warmup 2 ;;

@@ -40,7 +40,7 @@ EXPORTS = [
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_run_shard_records",
     "scc_de_finish_records", "scc_de_finish_records_pairs", "scc_de_union_first_occ", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
-    "scc_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores", "scc_pca_shard_eigen", "scc_pca_shard_project",
+    "scc_distance", "scc_de_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores", "scc_pca_shard_eigen", "scc_pca_shard_project",
     "scc_distance_scores", "scc_silhouette", "scc_last_pca_scores",
     "scc_hclust_ward_d2", "scc_cutree_hybrid",
 ]
@@ -121,6 +121,7 @@ def load():
         "scc_de_result_nodg": (ctypes.c_int, [vp, vp]),
         "scc_de_result_destroy": (None, [vp]),
         "scc_distance": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, vp, i32, i32]),
+        "scc_de_distance": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), i32, i32, vp, i32, i32, P(vp)]),
         "scc_distance_cols": (ctypes.c_int, [vp, vp, vp, i32, i32, i32, i64, i64, vp, i32, i32]),
         "scc_pca_shard_colsum": (ctypes.c_int, [vp, vp, vp, i32, i64, i64, vp]),
         "scc_pca_shard_gram": (ctypes.c_int, [vp, vp, i32, vp]),
@@ -444,6 +445,30 @@ class Engine:
         self._check(self.lib.scc_distance(self.ctx, ds.handle, _ptr(genes), len(genes), metric, ncomp, _ptr(out),
                                           SCC_PTR_HOST, 1 if f32 else 0))
         return out
+
+    def de_distance(self, ds: Dataset, code, K, mode=SCC_DE_FAST, metric=SCC_DIST_PCA_EUCLID, ncomp=0, out=None,
+                    f32=False, device_out_ptr=None, fetch="union", **de_kw):
+        """scc_de_distance: the DE, then the distance over its union, in one
+        C call.  Returns (DeResult, distance) — the distance None for device
+        output (device_out_ptr; 0 keeps it in the engine)."""
+        code = np.ascontiguousarray(code, np.int32)
+        kw = dict(q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0)
+        kw.update(de_kw)
+        prm = self._de_params(mode, kw["q_val_thrs"], kw["log_fc_thrs"], kw["min_per_cent"], kw["top_n"],
+                              kw["fc_thrs"], kw["mean_scaling_factor"], fetch == "all")
+        r = ctypes.c_void_p()
+        if device_out_ptr is not None:
+            dst, kind, res = ctypes.c_void_p(device_out_ptr or None), SCC_PTR_DEVICE, None
+        else:
+            res = out if out is not None else np.empty(ds.N * (ds.N - 1) // 2, np.float32 if f32 else np.float64)
+            dst, kind = _ptr(res), SCC_PTR_HOST
+        rc = self.lib.scc_de_distance(self.ctx, ds.handle, _ptr(code), K, ctypes.byref(prm), metric, ncomp, dst, kind,
+                                      1 if f32 else 0, ctypes.byref(r))
+        if rc != SCC_OK and r.value:  # the DE succeeded, the distance failed: free the result, raise
+            self.lib.scc_de_result_destroy(r)
+            self._check(rc)
+        de = self._collect(r, rc, ds, mode, K, fetch)
+        return de, res
 
     def distance_cols(self, ds: Dataset, genes, col_lo, col_hi, metric=SCC_DIST_PCA_EUCLID, ncomp=0, out=None,
                       f32=False, device_out_ptr=None):

@@ -499,6 +499,20 @@ extern "C" int scc_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* ge
     return dist_impl(c, ds, genes, nu, metric, ncomp, 0, ds ? ds->N : 0, dist_out, out_kind, out_f32);
 }
 
+extern "C" int scc_de_distance(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K,
+                               const scc_de_params* prm, int32_t metric, int32_t ncomp, void* dist_out,
+                               int32_t out_kind, int32_t out_f32, scc_de_result** out)
+{
+    if (!out) return fail(c, SCC_ERR_INVALID, "scc_de_distance: null result pointer");
+    *out = nullptr;
+    const int rc = scc_de_run(c, ds, code, K, prm, out);
+    if (rc != SCC_OK) return rc;
+    const scc_de_result* r = *out;
+    if (r->union_genes.empty()) return fail(c, SCC_ERR_INVALID, "empty gene union");
+    return dist_impl(c, ds, r->union_genes.data(), (int32_t)r->union_genes.size(), metric, ncomp, 0, ds->N, dist_out,
+                     out_kind, out_f32);
+}
+
 extern "C" int scc_distance_cols(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
                                  int32_t ncomp, int64_t col_lo, int64_t col_hi, void* dist_out, int32_t out_kind,
                                  int32_t out_f32)

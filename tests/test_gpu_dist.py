@@ -402,3 +402,20 @@ def test_gather_wide_union_fallback(eng):
         d = eng.distance(ds, g.astype(np.int32), nat.SCC_DIST_PCA_EUCLID)
         ref = O.dist_euclidean(O.pca_scores(Xd, g))
         assert np.max(np.abs(d - ref)) < 1e-5
+
+
+def test_de_distance_matches_two_calls(eng, cfg_a):
+    """scc_de_distance (DE, then the distance over its union, one C call)
+    returns the same union and the same distance bits as scc_de_run followed
+    by scc_distance."""
+    from scconsensus_amd import _native as nat
+    from scconsensus_amd import api
+    d, X, uni = cfg_a
+    names, code = api.select_clusters(d.labels, 10)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    r1 = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="union")
+    d1 = eng.distance(ds, r1.union, nat.SCC_DIST_PCA_EUCLID)
+    r2, d2 = eng.de_distance(ds, code, len(names), nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID)
+    assert np.array_equal(r1.union, r2.union)
+    assert np.array_equal(np.asarray(r2.union), np.asarray(uni))
+    assert np.array_equal(d1, d2)
