@@ -335,7 +335,7 @@ __device__ __host__ inline int da_rbmin(int cb)
     return r > 0 ? r : 0;
 }
 
-template <bool F32, int DC, int NB, bool NT>
+template <bool F32, int DC, int NB, bool NT, bool V2>
 __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict__ P, int N, int nrb, int cb_lo,
                                                        int ncbl, int c_lo, int c_hi, long long obase,
                                                        void* __restrict__ out)
@@ -405,6 +405,43 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
             if (j >= je) break;
             const long long B = (long long)j * (2LL * N - j - 1) / 2 - j - 1 - obase;  // out index of (i, j) = B + i
             const int delta = (int)((B + r0) & (HALO - 1));
+            if constexpr (V2) {
+                // two consecutive rows per thread, one 16-B (8-B for f32) store:
+                // B + r0 - delta is a multiple of HALO, so an even t2 keeps the
+                // pair aligned (out itself aligned, checked by the launcher)
+                const int t2 = 2 * t;
+                const int i2 = r0 - delta + t2;
+                if (t2 < TR && i2 + 1 > j && i2 < N) {
+                    const double v0 = stage[c][HALO - delta + t2], v1 = stage[c][HALO - delta + t2 + 1];
+                    if (i2 > j && i2 + 1 < N) {
+                        typedef float fv2 __attribute__((ext_vector_type(2)));
+                        typedef double dv2 __attribute__((ext_vector_type(2)));
+                        if (F32) {
+                            const fv2 w = {(float)v0, (float)v1};
+                            if (NT)
+                                __builtin_nontemporal_store(w, (fv2*)((float*)out + B + i2));
+                            else
+                                *(fv2*)((float*)out + B + i2) = w;
+                        } else {
+                            const dv2 w = {v0, v1};
+                            if (NT)
+                                __builtin_nontemporal_store(w, (dv2*)((double*)out + B + i2));
+                            else
+                                *(dv2*)((double*)out + B + i2) = w;
+                        }
+                    } else {  // the column's first row or the matrix's last: one of the two
+                        const int ir = i2 > j ? i2 : i2 + 1;
+                        const double v = i2 > j ? v0 : v1;
+                        if (ir < N) {
+                            if (F32)
+                                ((float*)out)[B + ir] = (float)v;
+                            else
+                                ((double*)out)[B + ir] = v;
+                        }
+                    }
+                }
+                continue;
+            }
             const int i2 = r0 - delta + t;
             if (t < TR && i2 > j && i2 < N) {
                 const double v = stage[c][HALO - delta + t];
@@ -442,12 +479,16 @@ static void launch_dist_aligned(const double* P, int N, int c_lo, int c_hi, void
     }
     const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
     const dim3 grid((unsigned)gx, (unsigned)npair);
-    if (f32)
-        hipLaunchKernelGGL((k_dist_aligned<true, DC, NB, NT>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
-                           obase, out);
-    else
-        hipLaunchKernelGGL((k_dist_aligned<false, DC, NB, NT>), grid, dim3(DA_T), 0, st, P, N, nrb, cb_lo, ncbl, c_lo, c_hi,
-                           obase, out);
+    // paired stores need the output 16-B aligned (8-B for f32); SCC_DIST_V2=0: one entry per thread
+    const char* ve = getenv("SCC_DIST_V2");
+    const bool v2 = !(ve && *ve && atoi(ve) == 0) && ((uintptr_t)out % (f32 ? 8 : 16)) == 0;
+    const void* fn = f32 ? (v2 ? (const void*)k_dist_aligned<true, DC, NB, NT, true>
+                               : (const void*)k_dist_aligned<true, DC, NB, NT, false>)
+                         : (v2 ? (const void*)k_dist_aligned<false, DC, NB, NT, true>
+                               : (const void*)k_dist_aligned<false, DC, NB, NT, false>);
+    void* args[] = {(void*)&P, (void*)&N, (void*)&nrb, (void*)&cb_lo, (void*)&ncbl, (void*)&c_lo, (void*)&c_hi,
+                    (void*)&obase, (void*)&out};
+    (void)hipLaunchKernel(fn, grid, dim3(DA_T), args, 0, st);
 }
 
 // ------------------------------------------------------------------ Pearson
@@ -836,7 +877,9 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     // (SCC_DIST_NT=0: plain; B 0.51 vs 0.54 ms).  Removed after measuring slower
     // at B / D: unaligned row tiles (0.69 / 38.1 ms), barrier-free wave windows
     // (0.59 ms), 256-column tiles (0.78 / 36.2 ms).  Columns per LDS stage (DA_NB):
-    // B 8: 0.57-0.58 ms, 4: 0.566, 16: 0.69.
+    // B 8: 0.57-0.58 ms, 4: 0.566, 16: 0.69.  Two entries per thread in one
+    // 16-B store (SCC_DIST_V2, default; the store phase's address and bound
+    // VALU work halves): 0.552 ms.
     const char* env = getenv("SCC_DIST_COLS");
     const int cols = (env && *env) ? atoi(env) : (N >= 65536 ? 128 : 64);
     const char* nte = getenv("SCC_DIST_NT");
