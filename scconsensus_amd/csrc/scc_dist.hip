@@ -220,7 +220,8 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
     const int kr = lane >> 4, cc = lane & 15;
     // 4 GR_U rows per round: all loads of a round issued before its MFMAs
     // (clamped row, masked value past the chunk), so a round waits on memory
-    // once instead of GR_U times (GR_U 4: B 0.14, C 0.89, D 4.35 ms; 1: 0.18 / 1.43 / 5.22)
+    // once instead of GR_U times (GR_U 4: B 0.14, C 0.89, D 4.35 ms; 1: 0.18 / 1.43 / 5.22;
+    // issuing the next round's loads before this round's MFMAs: B 0.166 ms)
     for (int c = c0; c < c1; c += 4 * GR_U) {
         double a0[GR_U], a1[GR_U], b0[GR_U], b1[GR_U];
 #pragma unroll
