@@ -333,6 +333,20 @@ SCC_API int scc_hclust_ward_d2(const double* dist, int64_t n, int32_t* merge, do
 SCC_API int scc_cutree_hybrid(const int32_t* merge, const double* height, int64_t n, const double* dist,
                               int32_t deep_split, int32_t min_cluster_size, int32_t* labels, double* cut_height);
 
+/* ---- diagnostics (tests): the PCA eigensolver's parts on device pointers --
+ * Not on the R path.  Each synchronises the device and returns 0 on success.
+ *   scc_diag_eigen_topk   top-k eigenpairs of a device n x n symmetric A (lda)
+ *                         through the engine's eigensolver (Z [n][16], W [k]);
+ *                         *path: which solver answered (0 direct, 1 subspace
+ *                         iteration, 2 Chebyshev-filtered subspace iteration)
+ *   scc_diag_small_syev   the one-workgroup solver for n <= 64 (Rayleigh-Ritz)
+ *   scc_diag_cholinv      T = R^-1 of G + shift_rel tr(G) I = R^T R, P = 48 or 64
+ *   scc_diag_eig_last_path  the calling thread's last answer path */
+SCC_API int scc_diag_eigen_topk(const double* A, int n, int lda, int k, double* Z, double* W, int* path);
+SCC_API int scc_diag_small_syev(const double* H, int n, int ldh, int k, double* Y, double* theta, unsigned* flag);
+SCC_API int scc_diag_cholinv(const double* G, int P, double shift_rel, double* T, unsigned* flag);
+SCC_API int scc_diag_eig_last_path(void);
+
 #ifdef __cplusplus
 }
 #endif

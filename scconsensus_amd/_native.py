@@ -43,6 +43,7 @@ EXPORTS = [
     "scc_distance", "scc_de_distance", "scc_distance_cols", "scc_pca_shard_colsum", "scc_pca_shard_gram", "scc_pca_shard_scores", "scc_pca_shard_eigen", "scc_pca_shard_project",
     "scc_distance_scores", "scc_silhouette", "scc_last_pca_scores",
     "scc_hclust_ward_d2", "scc_cutree_hybrid",
+    "scc_diag_eigen_topk", "scc_diag_small_syev", "scc_diag_cholinv", "scc_diag_eig_last_path",
 ]
 
 
@@ -133,6 +134,10 @@ def load():
         "scc_last_pca_scores": (ctypes.c_int, [vp, vp, P(i32)]),
         "scc_hclust_ward_d2": (ctypes.c_int, [vp, i64, vp, vp, vp]),
         "scc_cutree_hybrid": (ctypes.c_int, [vp, vp, i64, vp, i32, i32, vp, P(dbl)]),
+        "scc_diag_eigen_topk": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, P(ctypes.c_int)]),
+        "scc_diag_small_syev": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp]),
+        "scc_diag_cholinv": (ctypes.c_int, [vp, i32, dbl, vp, vp]),
+        "scc_diag_eig_last_path": (ctypes.c_int, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -452,10 +457,15 @@ class Engine:
         C call.  Returns (DeResult, distance) — the distance None for device
         output (device_out_ptr; 0 keeps it in the engine)."""
         code = np.ascontiguousarray(code, np.int32)
-        kw = dict(q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0)
+        kw = dict(q_val_thrs=0.1, log_fc_thrs=0.5, min_per_cent=20.0, top_n=30, fc_thrs=1.5, mean_scaling_factor=5.0,
+                  test_all=None, test="wilcox")
+        unknown = set(de_kw) - set(kw)
+        if unknown:
+            raise TypeError(f"de_distance: unknown DE arguments {sorted(unknown)}")
         kw.update(de_kw)
         prm = self._de_params(mode, kw["q_val_thrs"], kw["log_fc_thrs"], kw["min_per_cent"], kw["top_n"],
-                              kw["fc_thrs"], kw["mean_scaling_factor"], fetch == "all")
+                              kw["fc_thrs"], kw["mean_scaling_factor"],
+                              fetch == "all" if kw["test_all"] is None else kw["test_all"], kw["test"])
         r = ctypes.c_void_p()
         if device_out_ptr is not None:
             dst, kind, res = ctypes.c_void_p(device_out_ptr or None), SCC_PTR_DEVICE, None

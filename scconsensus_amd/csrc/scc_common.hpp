@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 
 typedef unsigned long long u64;
 typedef long long i64;
@@ -187,6 +188,23 @@ __device__ inline double scc_sqrt_nr(double s)
 // wave index inside the workgroup, as a wave-uniform (SGPR) value: loops
 // bounded by it stay scalar instead of being treated as divergent
 __device__ inline int scc_wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
+// CU count of the current device, cached per device ordinal (host threads
+// driving different devices or contexts may call this concurrently)
+inline int scc_device_cus(int fallback)
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fallback;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) {
+        (void)hipGetLastError();
+        return fallback;
+    }
+    cache[dev].store(v, std::memory_order_relaxed);
+    return v;
+}
 
 __host__ __device__ inline int scc_next_pow2(int n)
 {

@@ -774,13 +774,7 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
         hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
     else if (ld <= GATHER_LDS_LD && sizeof(double) * 4 * (size_t)ld + 2 * (size_t)G <= 120 * 1024 &&
              !(getenv("SCC_GATHER_LM") && atoi(getenv("SCC_GATHER_LM")) == 0)) {
-        static int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                cus = 256;
-        }
+        const int cus = scc_device_cus(256);
         const size_t lds = sizeof(double) * 4 * (size_t)ld + ((2 * (size_t)G + 15) & ~(size_t)15);
         hipFuncSetAttribute((const void*)k_gather_csc_lm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         const int grid = std::max(1, std::min((N + 3) / 4, 2 * cus));

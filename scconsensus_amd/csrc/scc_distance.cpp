@@ -772,6 +772,12 @@ extern "C" int scc_silhouette(scc_ctx* c, int64_t n_cells, const int32_t* groups
     std::vector<double> w(N);
     HIPCHK(c, hipMemcpyAsync(w.data(), d_w, sizeof(double) * N, hipMemcpyDeviceToHost, s0));
     HIPCHK(c, hipStreamSynchronize(s0));
+    // widths read from an engine-kept distance whose eigensolve failed are
+    // not an answer: report the flag that distance left (and drop it)
+    if (!dist && (rc = check_pending_eig(c))) {
+        c->d_last_dist = nullptr;
+        return rc;
+    }
     if (widths) std::copy(w.begin(), w.end(), widths);
     if (clus_avg) {  // summary(.)$clus.avg.widths: mean width per cluster (long double sums, R mean)
         std::vector<long double> sum(C, 0.0L);

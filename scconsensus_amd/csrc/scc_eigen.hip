@@ -29,8 +29,10 @@
 // Output Z[u*16 + q] = q-th largest eigenvector (q < k), zero padded to 16;
 // W[q] the q-th largest eigenvalue.
 #include "scc_common.hpp"
+#include "scc.h"
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 #define TRI_T 256
 #define TRI_W (TRI_T / 64)
@@ -1770,13 +1772,7 @@ static int tri_reg_rows(int n) { return tri_nj(n) ? TRI_W * TRI_MR : 0; }
 
 static int eig_nwg(int n)
 {
-    static int cus = -1;
-    if (cus < 0) {
-        int dev = 0;
-        hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 64;
-    }
+    const int cus = scc_device_cus(64);
     const char* env = getenv("SCC_EIG_NWG");
     int nwg = (env && *env) ? atoi(env) : (n + 9) / 10;
     nwg = nwg < 8 ? 8 : nwg;
@@ -1837,8 +1833,17 @@ static void side_stream(hipStream_t* s, hipEvent_t* fork_ev, hipEvent_t* join_ev
 
 extern "C" size_t scc_si_scratch_doubles(int n);
 extern "C" int scc_si_wanted(int n);
+extern "C" int scc_fsi_wanted(int n);
+extern "C" size_t scc_fsi_scratch_doubles(int n);
+extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
+                                    int* ok, hipStream_t st);
 extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
                                    int* ok, hipStream_t st);
+
+// which solver answered the calling thread's last scc_launch_eigen_topk:
+// 0 direct, 1 subspace iteration, 2 filtered subspace iteration (diagnostic)
+static thread_local int g_eig_last_path = 0;
+extern "C" SCC_API int scc_diag_eig_last_path() { return g_eig_last_path; }
 
 // scratch of the direct solver alone
 extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k)
@@ -1852,7 +1857,10 @@ extern "C" size_t scc_eigen_topk_scratch_direct(int n, int lda, int k)
 // direct solver + (for large n) the subspace iteration tried first (scc_subspace.hip)
 extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 {
-    return scc_eigen_topk_scratch_direct(n, lda, k) + (scc_si_wanted(n) ? scc_si_scratch_doubles(n) : 0);
+    size_t extra = 0;
+    if (scc_fsi_wanted(n)) extra = scc_fsi_scratch_doubles(n);
+    if (scc_si_wanted(n)) extra = std::max(extra, scc_si_scratch_doubles(n));
+    return scc_eigen_topk_scratch_direct(n, lda, k) + extra;
 }
 
 // A: n x n symmetric (full), row-major, lda (read only).  scratch: see
@@ -1864,6 +1872,12 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
                                             double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
                                             unsigned long long* stamps, hipStream_t st)
 {
+    // the side stream and its fork / join events are shared by every context
+    // on a device: one host thread at a time enqueues this launch sequence, so
+    // another context cannot re-record fork_ev / join_ev between our record
+    // and the wait on it (launches are asynchronous: the lock is held briefly)
+    static std::mutex launch_mu;
+    std::lock_guard<std::mutex> guard(launch_mu);
     int nwg;
     bool rows_lds, lu_lds;
     eig_plan(n, nwg, rows_lds, lu_lds);
@@ -1873,7 +1887,24 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if (nwg_out) *nwg_out = nwg;
     hipError_t e = hipMemsetAsync(flags, 0, 64, st);  // counter, err, XCD pick [3], follow-up counters [6]
     if (e != hipSuccess) return e;
-    if (scc_si_wanted(n)) {
+    g_eig_last_path = 0;
+    if (scc_fsi_wanted(n)) {
+        // |U| >= 128: Chebyshev-filtered subspace iteration first (scc_subspace.hip),
+        // accepted only when every test passes (else the direct solver below)
+        if (marks && marks[0]) hipEventRecord(marks[0], st);
+        int ok = 0;
+        e = scc_eigen_fsi(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, st);
+        if (e != hipSuccess) return e;
+        if (ok) {
+            g_eig_last_path = 2;
+            if (marks)
+                for (int m = 1; m < 6; ++m)
+                    if (marks[m]) hipEventRecord(marks[m], st);
+            return hipSuccess;
+        }
+        e = hipMemsetAsync(flags, 0, 64, st);
+        if (e != hipSuccess) return e;
+    } else if (scc_si_wanted(n)) {
         // large |U|: block subspace iteration first; accepted only when every
         // Ritz residual passes (else the direct solver below runs)
         if (marks && marks[0]) hipEventRecord(marks[0], st);
@@ -1881,6 +1912,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         e = scc_eigen_si(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, st);
         if (e != hipSuccess) return e;
         if (ok) {
+            g_eig_last_path = 1;
             if (marks)
                 for (int m = 1; m < 6; ++m)
                     if (marks[m]) hipEventRecord(marks[m], st);
@@ -1915,13 +1947,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     if (lds < 82 * 1024) lds = 82 * 1024;
     t.lds_rows_cap = rows_lds ? (int)((lds / sizeof(double) - (5 * (size_t)n + 64 + EIG_MAX_WG)) / n) : 0;
     if (marks && marks[0]) hipEventRecord(marks[0], st);
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 64;
-    }
+    const int cus = scc_device_cus(64);
     {
         // register rows for n <= 896 (6, 8 or 14 column slots per lane; the rest
         // of a workgroup's rows in LDS), else LDS / HBM rows
@@ -2046,4 +2072,23 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     launch_eig_finish(zfin, n, lda, k, W, v.tnorm, Z, st);
     if (marks && marks[5]) hipEventRecord(marks[5], st);
     return hipGetLastError();
+}
+
+// diagnostic (tests): top-k eigenpairs of a device matrix A (n x n, lda) into
+// Z (n x 16) and W (k) through scc_launch_eigen_topk; returns 0 on success,
+// *path = scc_diag_eig_last_path()
+extern "C" SCC_API int scc_diag_eigen_topk(const double* A, int n, int lda, int k,
+                                                                          double* Z, double* W, int* path)
+{
+    double* scr = nullptr;
+    const size_t sz = sizeof(double) * scc_eigen_scratch_doubles(n, lda, k);
+    if (hipMalloc((void**)&scr, sz) != hipSuccess) return 1;
+    unsigned int* err = nullptr;
+    hipError_t e = scc_launch_eigen_topk(A, n, lda, k, scr, Z, W, &err, nullptr, nullptr, nullptr, nullptr);
+    unsigned int h = 0;
+    if (e == hipSuccess && err) e = hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (path) *path = g_eig_last_path;
+    hipFree(scr);
+    return (e == hipSuccess && h == 0) ? 0 : 1;
 }

@@ -695,7 +695,6 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     const int* tab_src = H.data();
     if (c->h_tab_n < H.size()) {
         if (c->h_tab) hipHostFree(c->h_tab);
-    if (c->h_flag) hipHostFree(c->h_flag);
         c->h_tab = nullptr;
         c->h_tab_n = 0;
         if (hipHostMalloc((void**)&c->h_tab, sizeof(int) * H.size(), hipHostMallocDefault) == hipSuccess)

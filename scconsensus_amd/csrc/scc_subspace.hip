@@ -27,6 +27,8 @@
 #include "scc_common.hpp"
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
+#include <mutex>
 #include <vector>
 
 #define SI_B 64
@@ -458,6 +460,396 @@ extern "C" int scc_si_wanted(int n)
 extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
                                             double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
                                             unsigned long long* stamps, hipStream_t st);
+
+// ===========================================================================
+// Filtered subspace iteration (Chebyshev-accelerated; the default for
+// 128 <= |U|): the same 64-column block, but each segment applies the degree-m
+// Chebyshev polynomial of C that is bounded by 1 on the damped interval [0, b]
+// and grows like T_m(2 lambda / b - 1) above it, b tracking the 65th
+// eigenvalue (the smallest Rayleigh quotient of the orthonormal block, the
+// largest seen so far).  At config B (lambda_65 / lambda_15 = 0.877, the 15th
+// eigenvalue inside the noise bulk) plain subspace iteration needs ~200
+// products; the filter needs ~40 (a numpy model of this exact schedule on the
+// config-B Gram: scripts/fsi_model.py).  Per segment:
+//   W = C Q                          k_fsi_mul (plain; column partials of Q.W)
+//   Y1 = (2 / b) W - Q               k_fsi_cheb1 (b from the partials)
+//   Y_{t+1} = (4/b) C Y_t - 2 Y_t - Y_{t-1}   k_fsi_mul (recurrence epilogue)
+//   Q = orth(Y_m)                    shifted CholQR3 (k_fsi_gram, k_fsi_cholinv,
+//                                    k_fsi_apply; the first pass shifted by
+//                                    ~11 (m n + n^2) u tr(G), Fukaya et al.)
+// then Rayleigh-Ritz in one workgroup (k_small_syev on H = Q^T C Q) and the
+// same residual test, sign rule and missed-eigenpair guard as above.  The ~150
+// launches are captured once per (shape, buffers) into a hipGraph and replayed
+// (eager launches are host-bound at ~3.5 us each).  Deterministic: every sum
+// has a fixed order.
+#define FSI_NMIN 128
+#define FSI_LB 24  // k-steps of 4 rows per operand load batch
+#define FSI_TOL 1e-11
+
+// out = coef[0] (C X) + coef[1] X + coef[2] Zp over rows [0, np) (rows >= n of
+// X and Zp are zero, and stay zero); dpart[ti][col] = sum over the tile's rows
+// of X * out.  grid (np / 16, 4): one 16 x 16 tile per workgroup, the 4 waves
+// take contiguous quarters of the k range with their loads batched ahead
+__global__ void __launch_bounds__(256) k_fsi_mul(const double* __restrict__ C, int ldc, int n, int np,
+                                                 const double* __restrict__ X, const double* __restrict__ Zp,
+                                                 const double* __restrict__ coef, double* __restrict__ out,
+                                                 double* __restrict__ dpart)
+{
+    const int ti = blockIdx.x, i0 = ti * 16, j0 = blockIdx.y * 16;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kr = lane >> 4, cc = lane & 15;
+    const int ic = min(i0 + cc, n - 1);
+    const bool icok = i0 + cc < n;
+    const int S = np >> 2, per = (S + 3) >> 2;
+    const int s0 = w * per, s1 = min(S, s0 + per);
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int sb = s0; sb < s1; sb += FSI_LB) {
+        double a[FSI_LB], b[FSI_LB];
+#pragma unroll
+        for (int u = 0; u < FSI_LB; ++u) {
+            const int kk = 4 * min(sb + u, s1 - 1) + kr;
+            a[u] = C[(size_t)min(kk, n - 1) * ldc + ic];  // A[i][k] = C[k][i0 + i] (symmetric)
+            b[u] = X[(size_t)kk * SI_B + j0 + cc];
+        }
+#pragma unroll
+        for (int u = 0; u < FSI_LB; ++u) {
+            const bool in = sb + u < s1;
+            const bool ok = in && icok && 4 * (sb + u) + kr < n;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ok ? a[u] : 0.0, in ? b[u] : 0.0, acc, 0, 0, 0);
+        }
+    }
+    __shared__ d4 red[3][64];
+    if (w > 0) red[w - 1][lane] = acc;
+    __syncthreads();
+    if (w != 0) return;
+    acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
+    const double al = coef[0], be = coef[1], ga = coef[2];
+    double dp = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const size_t e = (size_t)(i0 + kr + 4 * r) * SI_B + j0 + cc;
+        const double x = X[e], z = Zp ? Zp[e] : 0.0;
+        const double v = fma(al, acc[r], fma(be, x, ga * z));
+        out[e] = v;
+        dp = fma(x, v, dp);
+    }
+    if (dpart) {
+        dp += __shfl_xor(dp, 16, 64);
+        dp += __shfl_xor(dp, 32, 64);
+        if (lane < 16) dpart[(size_t)ti * SI_B + j0 + cc] = dp;
+    }
+}
+
+// G = X^T Y (64 x 64) over rows [0, np): grid (4, 4), loads batched as k_fsi_mul
+__global__ void __launch_bounds__(256) k_fsi_gram(const double* __restrict__ X, const double* __restrict__ Y, int np,
+                                                  double* __restrict__ G)
+{
+    const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kr = lane >> 4, cc = lane & 15;
+    const int S = np >> 2, per = (S + 3) >> 2;
+    const int s0 = w * per, s1 = min(S, s0 + per);
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int sb = s0; sb < s1; sb += FSI_LB) {
+        double a[FSI_LB], b[FSI_LB];
+#pragma unroll
+        for (int u = 0; u < FSI_LB; ++u) {
+            const int kk = 4 * min(sb + u, s1 - 1) + kr;
+            a[u] = X[(size_t)kk * SI_B + i0 + cc];
+            b[u] = Y[(size_t)kk * SI_B + j0 + cc];
+        }
+#pragma unroll
+        for (int u = 0; u < FSI_LB; ++u) {
+            const bool in = sb + u < s1;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? a[u] : 0.0, in ? b[u] : 0.0, acc, 0, 0, 0);
+        }
+    }
+    __shared__ d4 red[3][64];
+    if (w > 0) red[w - 1][lane] = acc;
+    __syncthreads();
+    if (w != 0) return;
+    acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) G[(i0 + kr + 4 * r) * SI_B + j0 + cc] = acc[r];
+}
+
+// Y1 = (2 / b) W - Q with b = max(coef_in[3], min over columns of Q.W) (the
+// partials of the plain product; every workgroup forms b in the same order);
+// workgroup 0 writes the segment's recurrence coefficients {4/b, -2, -1, b}.
+// flag bit 64: no positive Rayleigh quotient (C = 0 on the block)
+__global__ void __launch_bounds__(256) k_fsi_cheb1(const double* __restrict__ W, const double* __restrict__ Q,
+                                                   const double* __restrict__ dpart, int nt,
+                                                   const double* __restrict__ coef_in, double* __restrict__ coef_out,
+                                                   double* __restrict__ Y1, u32* __restrict__ flag)
+{
+    __shared__ double s_b;
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        double s = 0.0;
+        for (int t = 0; t < nt; ++t) s += dpart[(size_t)t * SI_B + tid];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s = fmin(s, __shfl_xor(s, o, 64));
+        if (tid == 0) {
+            double b = fmax(coef_in[3], s);
+            const bool bad = !(b > 0.0) || !(b < INFINITY);
+            if (bad) b = 1.0;
+            s_b = b;
+            if (blockIdx.x == 0 && blockIdx.y == 0) {
+                coef_out[0] = 4.0 / b;
+                coef_out[1] = -2.0;
+                coef_out[2] = -1.0;
+                coef_out[3] = b;
+                if (bad) atomicOr(flag, 64u);
+            }
+        }
+    }
+    __syncthreads();
+    const double s2 = 2.0 / s_b;
+    const int row = blockIdx.x * 16 + (tid >> 4), col = blockIdx.y * 16 + (tid & 15);
+    const size_t e = (size_t)row * SI_B + col;
+    Y1[e] = fma(s2, W[e], -Q[e]);
+}
+
+// Q = Y T (T upper 64 x 64): grid (np / 16, 4), one wave per 16 x 16 tile
+__global__ void __launch_bounds__(64) k_fsi_apply(const double* __restrict__ Y, const double* __restrict__ T,
+                                                  double* __restrict__ Q)
+{
+    const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16;
+    const int lane = threadIdx.x & 63, kr = lane >> 4, cc = lane & 15;
+    const int smax = (j0 + 16) / 4;  // T[k][j] = 0 for k > j
+    double a[16], b[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        a[s] = Y[(size_t)(i0 + cc) * SI_B + 4 * s + kr];  // A[i][k] = Y[i0 + i][k]
+        b[s] = T[(4 * s + kr) * SI_B + j0 + cc];          // B[k][j] = T[k][j0 + j]
+    }
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+        if (s < smax) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Q[(size_t)(i0 + kr + 4 * r) * SI_B + j0 + cc] = acc[r];
+}
+
+// the filter's damped interval must lie below the 15th Ritz value (theta_k <=
+// lambda_k, so b < theta_k proves no wanted eigenvalue was damped): flag bit 32
+__global__ void k_fsi_bound_check(const double* __restrict__ coef, const double* __restrict__ theta, int k,
+                                  u32* __restrict__ flag)
+{
+    if (threadIdx.x == 0 && !(coef[3] < theta[k - 1])) atomicOr(flag, 32u);
+}
+
+extern "C" hipError_t scc_launch_small_syev(const double* H, int n, int ldh, int k, double* Y, double* theta,
+                                            u32* flag, hipStream_t st);
+extern "C" hipError_t scc_launch_fsi_cholinv(const double* G, int P, double shift_rel, double* T, u32* flag,
+                                             hipStream_t st);
+extern "C" void scc_small_syev_prepare();
+
+__global__ void k_fsi_coef0(double* __restrict__ coef)
+{
+    if (threadIdx.x < 4) coef[threadIdx.x] = threadIdx.x == 0 ? 1.0 : 0.0;
+}
+
+static int fsi_env(const char* name, int dflt)
+{
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}
+
+// segments and their degree: SCC_EIG_FSI_SEG (default 6), SCC_EIG_FSI_DEG (8)
+static int fsi_segments() { return std::max(1, std::min(64, fsi_env("SCC_EIG_FSI_SEG", 6))); }
+static int fsi_degree() { return std::max(2, std::min(16, fsi_env("SCC_EIG_FSI_DEG", 8))); }
+
+extern "C" int scc_fsi_wanted(int n)
+{
+    const int e = fsi_env("SCC_EIG_FSI", 0);  // (default off until measured on the GPU)
+    if (e == 0) return 0;
+    return n >= FSI_NMIN;
+}
+
+extern "C" size_t scc_fsi_scratch_doubles(int n)
+{
+    const size_t np = si_npad(n), nt = np / 16, nblk = (np + 255) / 256;
+    const int S = fsi_segments();
+    return 4 * np * SI_B + 2 * (size_t)SI_B * SI_B + nt * SI_B + (size_t)(S + 2) * 4 + SI_B * 16 + 16 + 16 +
+           3 * nblk * 16 + 64 + 2 * np + SI_B + 8 + 64;
+}
+
+namespace {
+struct FsiGraphEntry {
+    int dev, n, ldc, k, S, m, live, guard;
+    const void *C, *scr, *Z, *W;
+    hipGraphExec_t exec;
+};
+std::mutex g_fsi_mu;
+std::vector<FsiGraphEntry> g_fsi_graphs;
+
+hipStream_t fsi_capture_stream(int dev)
+{
+    static hipStream_t cs[64] = {};
+    if (dev < 0 || dev >= 64) return nullptr;
+    if (!cs[dev] && hipStreamCreateWithFlags(&cs[dev], hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        cs[dev] = nullptr;
+    }
+    return cs[dev];
+}
+}  // namespace
+
+// Same contract as scc_eigen_si: *ok = 1 when the filtered result passed every
+// test (Z, W written), 0: run the direct solver.  Synchronises st.
+extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
+                                    int* ok, hipStream_t st)
+{
+    *ok = 0;
+    if (n < FSI_NMIN || k > 16 || k < 1) return hipSuccess;
+    const size_t np = si_npad(n), nt = np / 16;
+    const int nblk = (int)((np + 255) / 256);
+    const int S = fsi_segments(), m = fsi_degree();
+    double* Q = scr;
+    double* Ya = Q + np * SI_B;
+    double* Yb = Ya + np * SI_B;
+    double* Yc = Yb + np * SI_B;
+    double* G = Yc + np * SI_B;
+    double* T = G + SI_B * SI_B;
+    double* dpart = T + SI_B * SI_B;
+    double* coef = dpart + nt * SI_B;  // [S + 2][4]
+    double* Yv = coef + (size_t)(S + 2) * 4;
+    double* theta = Yv + SI_B * 16;
+    double* sgn = theta + 16;
+    double* rpart = sgn + 16;
+    double* mpart = rpart + (size_t)nblk * 32;
+    u32* flag = (u32*)(mpart + (size_t)nblk * 16);
+    double* gu = (double*)(flag + 128);
+    double* gy = gu + np;
+    double* gz = gy + np;
+    double* gsc = gz + SI_B;
+    const int live = std::max(SI_B, std::min(n, fsi_env("SCC_EIG_SI_INIT_ROWS", n)));
+    const int guard = n <= SI_GUARD_NMAX;
+    const double shift_rel = 11.0 * ((double)np * SI_B + (double)SI_B * (SI_B + 1)) * 1.1102230246251565e-16;
+    scc_small_syev_prepare();  // kernel attributes, outside any capture
+    const dim3 gt((unsigned)nt, SI_B / 16), gg(SI_B / 16, SI_B / 16);
+    auto enqueue = [&](hipStream_t s) -> hipError_t {
+        hipError_t e;
+        if ((e = hipMemsetAsync(flag, 0, sizeof(u32) * 4, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_fsi_coef0, dim3(1), dim3(64), 0, s, coef);  // slot 0: plain product {1, 0, 0, b = 0}
+        hipLaunchKernelGGL(k_si_init, dim3((unsigned)((np * SI_B + 255) / 256)), dim3(256), 0, s, (int)np,
+                           std::min(live, n), Ya);
+        auto orth = [&](double* src, double* tmp, double* dst, int passes) -> hipError_t {
+            // passes 2: src -> tmp -> dst; 3: src -> dst -> tmp -> dst
+            double* seq[4] = {src, passes == 2 ? tmp : dst, passes == 2 ? dst : tmp, dst};
+            for (int p = 0; p < passes; ++p) {
+                hipLaunchKernelGGL(k_fsi_gram, gg, dim3(256), 0, s, seq[p], seq[p], (int)np, G);
+                hipError_t e2 = scc_launch_fsi_cholinv(G, SI_B, p == 0 ? shift_rel : 0.0, T, flag, s);
+                if (e2 != hipSuccess) return e2;
+                hipLaunchKernelGGL(k_fsi_apply, gt, dim3(64), 0, s, seq[p], T, seq[p + 1]);
+            }
+            return hipGetLastError();
+        };
+        if ((e = orth(Ya, Yb, Q, 2)) != hipSuccess) return e;
+        for (int sg = 0; sg < S; ++sg) {
+            // W = C Q (into Ya) with the column partials of Q.W, then Y1 (into Yb)
+            hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, Q, (const double*)nullptr, coef,
+                               Ya, dpart);
+            hipLaunchKernelGGL(k_fsi_cheb1, gt, dim3(256), 0, s, Ya, Q, dpart, (int)nt, coef + 4 * sg,
+                               coef + 4 * (sg + 1), Yb, flag);
+            double* prev = Q;
+            double* cur = Yb;
+            double* nxt = Ya;
+            for (int t = 2; t <= m; ++t) {
+                hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, cur, prev,
+                                   coef + 4 * (sg + 1), nxt, (double*)nullptr);
+                double* fr = prev == Q ? Yc : prev;  // Q (Y_0) is overwritten only by the orthonormalisation
+                prev = cur;
+                cur = nxt;
+                nxt = fr;
+            }
+            double* tmp = (prev != Q) ? prev : nxt;
+            if ((e = orth(cur, tmp, Q, 3)) != hipSuccess) return e;
+        }
+        // Rayleigh-Ritz on span(Q): W = C Q (Ya), H = Q^T W, its top-k eigenpairs
+        hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, Q, (const double*)nullptr, coef, Ya,
+                           (double*)nullptr);
+        hipLaunchKernelGGL(k_fsi_gram, gg, dim3(256), 0, s, Q, Ya, (int)np, G);
+        if ((e = scc_launch_small_syev(G, SI_B, SI_B, k, Yv, theta, flag, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_si_ritz, dim3(nblk), dim3(256), 0, s, Q, Ya, Yv, theta, n, k, Z, rpart, mpart);
+        hipLaunchKernelGGL(k_si_check, dim3(1), dim3(64), 0, s, rpart, mpart, nblk, theta, k, FSI_TOL, sgn, Wout,
+                           flag);
+        hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, s, Z, sgn, n);
+        hipLaunchKernelGGL(k_fsi_bound_check, dim3(1), dim3(64), 0, s, coef + 4 * S, theta, k, flag);
+        if (guard) {
+            const dim3 gstep((n + 15) / 16);
+            hipLaunchKernelGGL(k_sig_init, dim3((n + 255) / 256), dim3(256), 0, s, n, gu);
+            hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, s, Q, n, gu, nullptr, gsc, gz, theta, k, flag, 0);
+            hipLaunchKernelGGL(k_sig_step, gstep, dim3(256), 0, s, C, ldc, n, gu, gsc, Q, gz, gy, 0);
+            double* u = gy;
+            double* y = gu;
+            for (int it = 0; it < SI_GUARD_IT; ++it) {
+                hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, s, Ya, n, u, it ? y : nullptr, gsc, gz, theta,
+                                   k, flag, 0);
+                hipLaunchKernelGGL(k_sig_step, gstep, dim3(256), 0, s, C, ldc, n, u, gsc, Q, gz, y, 1);
+                std::swap(u, y);
+            }
+            hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, s, Ya, n, u, y, gsc, gz, theta, k, flag, 1);
+        }
+        return hipGetLastError();
+    };
+    hipError_t e = hipSuccess;
+    int dev = 0;
+    hipGetDevice(&dev);
+    bool launched = false;
+    if (fsi_env("SCC_EIG_FSI_GRAPH", 1)) {
+        std::lock_guard<std::mutex> lk(g_fsi_mu);
+        hipGraphExec_t ex = nullptr;
+        for (const auto& g : g_fsi_graphs)
+            if (g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m && g.live == live &&
+                g.guard == guard && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
+                ex = g.exec;
+                break;
+            }
+        if (!ex) {
+            hipStream_t cs = fsi_capture_stream(dev);
+            hipGraph_t gr = nullptr;
+            if (cs && hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+                const hipError_t ce = enqueue(cs);
+                const hipError_t ee = hipStreamEndCapture(cs, &gr);
+                if (ce == hipSuccess && ee == hipSuccess && gr &&
+                    hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0) == hipSuccess) {
+                    if (g_fsi_graphs.size() >= 8) {
+                        hipGraphExecDestroy(g_fsi_graphs.front().exec);
+                        g_fsi_graphs.erase(g_fsi_graphs.begin());
+                    }
+                    g_fsi_graphs.push_back({dev, n, ldc, k, S, m, live, guard, C, scr, Z, Wout, ex});
+                } else {
+                    ex = nullptr;
+                }
+                if (gr) hipGraphDestroy(gr);
+            }
+            (void)hipGetLastError();
+        }
+        if (ex) {
+            if ((e = hipGraphLaunch(ex, st)) != hipSuccess) return e;
+            launched = true;
+        }
+    }
+    if (!launched && (e = enqueue(st)) != hipSuccess) return e;
+    u32 h = 0;
+    if ((e = hipMemcpyAsync(&h, flag, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (getenv("SCC_EIG_SI_LOG")) {
+        double lg[16] = {0}, cf[4] = {0}, th[16] = {0};
+        if (hipMemcpy(lg, flag + 8, sizeof(double) * 16, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(cf, coef + 4 * S, sizeof(double) * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(th, theta, sizeof(double) * 16, hipMemcpyDeviceToHost) == hipSuccess) {
+            double rmax = 0.0;
+            for (int q = 0; q < k; ++q) rmax = std::max(rmax, lg[q]);
+            fprintf(stderr, "[scc fsi] n=%d seg=%d deg=%d flag=%u maxres=%.3g b=%.6g theta_k=%.6g graph=%d\n", n, S, m,
+                    h, rmax, cf[3], th[k - 1], launched ? 1 : 0);
+        }
+    }
+    *ok = (h == 0) ? 1 : 0;
+    return hipSuccess;
+}
 
 // Returns hipSuccess and *ok = 1 when the subspace result was accepted (Z, W
 // written); *ok = 0: nothing usable, run the direct solver.  Synchronises st.
