@@ -22,6 +22,14 @@ disjoint score rows), then each rank's equal-entry column slice of the packed
 distance.  `--mode jobs` (opt-in, "scaling": "weak"): every rank runs its own
 job (seed offset by rank) with no data-path collective.  The step time is the
 max over ranks.
+
+`--route devices` measures the route R's `nCores` takes instead
+(Fast:33,61-65 -> scc_opts.devices): ONE process, one engine context over a
+device list (`--gpus N`: devices 0..N-1; SCC_BENCH_DEVICES="0,0" rehearses a
+two-entry list on one GPU), the DE's gene blocks and the distance's column
+slices spread over the list inside libscc (peer copies, no RCCL).  Under a
+multi-rank launch (the driver's `--gpus N` runs) rank 0 also times this route
+over all N GPUs after the rank route and reports it as "route_devices".
 """
 from __future__ import annotations
 
@@ -59,6 +67,9 @@ def _args(argv=None):
                     help="scc_de_run then scc_distance (two C calls) instead of the fused scc_de_distance")
     ap.add_argument("--mode", choices=["shard", "jobs"], default="shard",
                     help="shard: ONE job over all ranks (strong scaling); jobs: one job per rank (weak scaling)")
+    ap.add_argument("--route", choices=["ranks", "devices"], default="ranks",
+                    help="ranks: one process per GPU (torch.distributed / RCCL); devices: one process over a device "
+                         "list inside libscc (the R drop-in's nCores route)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: the launcher / rank / timing path with a placeholder step (tests)")
     return ap.parse_args(argv)
@@ -219,9 +230,50 @@ def dry_run(a, dist):
     dist.close()
 
 
+def _device_list(a):
+    env = os.environ.get("SCC_BENCH_DEVICES")
+    if env:
+        return [int(x) for x in env.split(",") if x.strip() != ""]
+    return list(range(a.gpus))
+
+
+def devices_route(a, d, code, K, devices, steps, warmup):
+    """One process, one context over `devices` (scc_opts.devices): the fused
+    DE + distance step with the distance kept in HBM, timed like the main
+    line (synchronize on both sides)."""
+    from scconsensus_amd import _native as nat
+    eng = nat.Engine(devices[0], devices=devices if len(devices) > 1 else None)
+    try:
+        if hasattr(d.indptr, "data_ptr"):
+            ds = eng.dataset_csc_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
+        else:
+            ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+
+        def step():
+            return eng.de_distance(ds, code, K, nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)[0]
+
+        for _ in range(max(1, warmup)):
+            r = step()
+        eng.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = step()
+        eng.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        ds.close()
+    finally:
+        eng.close()
+    n_dev = len(set(devices))
+    return {"route": "devices", "devices": devices, "n_gpus": n_dev, "ms_per_step": ms,
+            "value": d.N * (d.N - 1) / 2 / (ms / 1e3), "unit": "cell-pairs/s", "union": len(r.union),
+            "parallelism": f"devices{len(devices)}" + (f" on {n_dev} GPU(s)" if n_dev != len(devices) else "")}
+
+
 def main():
     a = _args()
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if a.route == "devices" and "WORLD_SIZE" not in os.environ:
+        a.mode = "shard"
+    elif a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(a))
     shard = a.mode == "shard"
     if shard and not a.dry_run:
@@ -231,8 +283,10 @@ def main():
     # SCC_DIST_BACKEND=gloo rehearses several ranks on one GPU (tests only).
     dist = parallel.init(os.environ.get("SCC_DIST_BACKEND") or ("gloo" if a.dry_run else None))
     rank, world, local = dist.rank, dist.world, dist.local_rank
-    if world != a.gpus:
+    route_devices = a.route == "devices" and world == 1
+    if world != a.gpus and not route_devices:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+    devices = _device_list(a) if route_devices else [0]
     if a.dry_run:
         return dry_run(a, dist)
     from scconsensus_amd import _native as nat
@@ -252,7 +306,8 @@ def main():
     names, code = api.select_clusters(d.labels, 10)
     K = len(names)
     P = K * (K - 1) // 2
-    eng = nat.Engine(gpu, profile=not a.no_stage_events)
+    eng = nat.Engine(gpu, profile=not a.no_stage_events,
+                     devices=devices if route_devices and len(devices) > 1 else None)
     if a.config == "E":
         ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
         return de_only(a, eng, ds, d, code, K, dist, world)
@@ -440,6 +495,17 @@ def main():
     kernels = {f: roof(f) for f in alg if f in stage_ms and stage_ms[f] > 0}
     jobs = world if not shard else 1
     value = jobs * npairs_cells / (ms / 1e3)
+    side_devices = None
+    if world > 1 and shard and a.config in ("A", "B", "C", "D"):
+        # the R drop-in's route over the same N GPUs: rank 0 alone drives a
+        # device list [0 .. N-1] (the other ranks wait at the barrier)
+        dist.barrier()
+        if rank == 0:
+            try:
+                side_devices = devices_route(a, d, code, K, list(range(world)), max(1, min(a.steps, 10)), a.warmup)
+            except Exception as ex:  # reported, never silently dropped
+                side_devices = {"route": "devices", "error": repr(ex)}
+        dist.barrier()
     out = {
         "metric": f"end-to-end DE+distance cell-pairs/sec at config {a.config}"
                   + (" (26k PBMC shape)" if a.config == "B" else ""),
@@ -459,7 +525,9 @@ def main():
         "config": {"workload": f"config {a.config}: reclusterDEConsensusFast DE (all {P} pairs) + PCA15 "
                                f"Euclidean dist, {d.N} cells x {d.G} genes, K={K}",
                    "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": nnz, "union": nu,
-                   "parallelism": f"shard{world}" if shard else f"jobs{world}"},
+                   "parallelism": (f"devices{len(devices)}" if route_devices and len(devices) > 1
+                                   else (f"shard{world}" if shard else f"jobs{world}"))},
+        "route": "devices" if route_devices else "ranks",
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "stage_ms_source": (f"{dom}: HIP events over the timed region (the only stage timed there); the others: "
                             f"{nprof} warm-up step(s) with every stage timed (each event adds ~12 us of GPU idle, "
@@ -468,6 +536,11 @@ def main():
         "roofline": roof_dom,
         "kernels": kernels,
     }
+    if route_devices:
+        out["devices"] = devices
+        out["n_gpus"] = len(set(devices))
+    if side_devices is not None:
+        out["route_devices"] = side_devices
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         ng = a.cpu_sample_genes if a.config in ("A", "B") else max(16, int(300 * 66 * 26000 / (P * d.N)))
         out["cpu_baseline"] = cpu_baseline(d, code, K, r.union, ng)

@@ -49,14 +49,35 @@
             method = if (metric == 0L) "euclidean" else "pearson", class = "dist")
 }
 
+# hclust(ward.D2) as Fast:406-411; with options(scConsensus.engineTree = TRUE)
+# the engine's C++ restatement (no fastcluster needed; same merge rule)
+.scc_hclust <- function(d) {
+  if (isTRUE(getOption("scConsensus.engineTree", FALSE))) {
+    t <- .Call("C_scc_hclust", d)
+    return(structure(list(merge = t[[1]], height = t[[2]], order = t[[3]], labels = attr(d, "Labels"),
+                          method = "ward.D2", call = match.call(), dist.method = attr(d, "method")),
+                     class = "hclust"))
+  }
+  if (requireNamespace("fastcluster", quietly = TRUE)) fastcluster::hclust(d, method = "ward.D2")
+  else stats::hclust(d, method = "ward.D2")
+}
+
 .scc_tree_and_colors <- function(d, deepSplitValues, minClusterSize, with_si) {
-  tree <- if (requireNamespace("fastcluster", quietly = TRUE)) fastcluster::hclust(d, method = "ward.D2")
-          else stats::hclust(d, method = "ward.D2")
-  dm <- as.matrix(d)
+  tree <- .scc_hclust(d)
+  # cutreeDynamic needs distM = as.matrix(d): N^2 doubles on the host (5.4 GB
+  # at 26k cells, 80 GB at 100k, 320 GB at 200k).  options(scConsensus.engineCut
+  # = TRUE) runs the engine's restatement of the hybrid cut on the packed d
+  # instead (parity against dynamicTreeCut itself unpinned: INTEGRATION.md)
+  engine_cut <- isTRUE(getOption("scConsensus.engineCut", FALSE))
+  dm <- if (engine_cut) NULL else as.matrix(d)
   colors <- list()
   for (dsv in deepSplitValues) {
-    grp <- dynamicTreeCut::cutreeDynamic(dendro = tree, distM = dm, deepSplit = dsv,
-                                         pamStage = FALSE, minClusterSize = minClusterSize)
+    grp <- if (engine_cut) {
+      .Call("C_scc_cutree", tree$merge, as.double(tree$height), d, as.integer(dsv), as.integer(minClusterSize))
+    } else {
+      dynamicTreeCut::cutreeDynamic(dendro = tree, distM = dm, deepSplit = dsv,
+                                    pamStage = FALSE, minClusterSize = minClusterSize)
+    }
     colors[[paste("deepsplit:", dsv)]] <- WGCNA::labels2colors(grp)
     # deepSplitInfo's SI (Fast:433, computed and discarded by the reference):
     # the engine's silhouette on its HBM-resident copy of d (no N x N matrix)

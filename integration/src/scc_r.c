@@ -14,10 +14,17 @@
  *   C_scc_distance  R/reclusterDEConsensusFast.R:398-400 (prcomp_irlba + dist), :403 (1 - cor)
  *   C_scc_release   frees the device copy early (the finalizer does it otherwise)
  *   C_scc_devices   nCores (Fast:33,61-65) -> the context's device list
+ *   C_scc_si        deepSplitInfo's silhouette SI (Fast:433) on the engine-kept dist
+ *   C_scc_cutree    dynamicTreeCut::cutreeDynamic(..., distM = as.matrix(d), pamStage = FALSE)
+ *                   (Fast:421-427) on the packed dist: no N x N host matrix
+ *                   (options(scConsensus.engineCut = TRUE))
+ *   C_scc_hclust    hclust(d, "ward.D2") (Fast:406-411) restated in C++
+ *                   (options(scConsensus.engineTree = TRUE))
  */
 #include <R.h>
 #include <Rinternals.h>
 #include <R_ext/Rdynload.h>
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -257,6 +264,55 @@ SEXP C_scc_si(SEXP groups)
     return Rf_ScalarReal(s / ng);
 }
 
+/* n from the length of a "dist" body, n (n - 1) / 2 */
+static int64_t dist_n(SEXP d)
+{
+    const double nd = (double)XLENGTH(d);
+    int64_t n = (int64_t)((1.0 + sqrt(1.0 + 8.0 * nd)) / 2.0 + 0.5);
+    if (n * (n - 1) / 2 != (int64_t)XLENGTH(d)) Rf_error("scConsensus engine: not a dist body (length %.0f)", nd);
+    return n;
+}
+
+/* cutreeDynamic(dendro, distM = as.matrix(d), deepSplit, pamStage = FALSE,
+ * minClusterSize) with method "hybrid" and the default cut height
+ * (Fast:421-427), on the packed d: merge is the hclust merge matrix ((n-1) x 2
+ * integer, column-major as R stores it), height its heights.  Returns the
+ * integer labels (0 = unassigned, 1.. by decreasing size), as cutreeDynamic. */
+SEXP C_scc_cutree(SEXP merge, SEXP height, SEXP d, SEXP deep, SEXP minsize)
+{
+    const int64_t n = dist_n(d);
+    if (XLENGTH(merge) != 2 * (n - 1) || XLENGTH(height) != n - 1)
+        Rf_error("scConsensus engine: merge / height do not match the dist of %lld cells", (long long)n);
+    SEXP m = PROTECT(Rf_coerceVector(merge, INTSXP));
+    SEXP lab = PROTECT(Rf_allocVector(INTSXP, n));
+    const int rc = scc_cutree_hybrid(INTEGER(m), REAL(height), n, REAL(d), Rf_asInteger(deep), Rf_asInteger(minsize),
+                                     INTEGER(lab), NULL);
+    UNPROTECT(2);
+    if (rc != SCC_OK) Rf_error("scConsensus engine: cutree failed (%d)", rc);
+    return lab;
+}
+
+/* hclust(d, method = "ward.D2") (Fast:406-411): list(merge, height, order) of
+ * an R hclust object (the wrapper adds labels / method / call / dist.method) */
+SEXP C_scc_hclust(SEXP d)
+{
+    const int64_t n = dist_n(d);
+    SEXP merge = PROTECT(Rf_allocMatrix(INTSXP, (int)(n - 1), 2));
+    SEXP height = PROTECT(Rf_allocVector(REALSXP, n - 1));
+    SEXP order = PROTECT(Rf_allocVector(INTSXP, n));
+    const int rc = scc_hclust_ward_d2(REAL(d), n, INTEGER(merge), REAL(height), INTEGER(order));
+    if (rc != SCC_OK) {
+        UNPROTECT(3);
+        Rf_error("scConsensus engine: hclust failed (%d)", rc);
+    }
+    SEXP out = PROTECT(Rf_allocVector(VECSXP, 3));
+    SET_VECTOR_ELT(out, 0, merge);
+    SET_VECTOR_ELT(out, 1, height);
+    SET_VECTOR_ELT(out, 2, order);
+    UNPROTECT(4);
+    return out;
+}
+
 static const R_CallMethodDef call_methods[] = {
     {"C_scc_dataset", (DL_FUNC)&C_scc_dataset, 4},
     {"C_scc_release", (DL_FUNC)&C_scc_release, 1},
@@ -265,6 +321,8 @@ static const R_CallMethodDef call_methods[] = {
     {"C_scc_distance", (DL_FUNC)&C_scc_distance, 4},
     {"C_scc_si", (DL_FUNC)&C_scc_si, 1},
     {"C_scc_devices", (DL_FUNC)&C_scc_devices, 1},
+    {"C_scc_cutree", (DL_FUNC)&C_scc_cutree, 5},
+    {"C_scc_hclust", (DL_FUNC)&C_scc_hclust, 1},
     {NULL, NULL, 0}};
 
 /* the package is scConsensus (NAMESPACE: useDynLib(scConsensus, .registration = TRUE)) */

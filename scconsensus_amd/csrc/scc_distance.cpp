@@ -12,6 +12,7 @@
 #include "scc_internal.hpp"
 
 #include <chrono>
+#include <functional>
 #include <thread>
 
 using namespace scc_rt;
@@ -181,8 +182,13 @@ static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi,
 // output devices[0] keeps only its own slice of the engine-kept copy; the
 // others stay on their devices until scc_silhouette needs them
 // (last_dist_pending).
-static int dist_multi(scc_ctx* c, const double* d_P, int N, int64_t col_lo, int64_t col_hi, void* d_out,
-                      void* dist_out, int32_t out_kind, int32_t out_f32)
+// The payload a device needs to write its slice: the N x 16 scores (PCA +
+// Euclid) or the N x ldz fp32 z-scores (Pearson); `launch(payload, a, b, dst,
+// stream)` emits columns [a, b) at dst.
+using SliceLaunch = std::function<hipError_t(const void*, int64_t, int64_t, void*, hipStream_t)>;
+static int dist_multi(scc_ctx* c, const void* d_pay, size_t pay_bytes, const SliceLaunch& launch, const char* scope,
+                      int N, int64_t col_lo, int64_t col_hi, void* d_out, void* dist_out, int32_t out_kind,
+                      int32_t out_f32)
 {
     const int D = 1 + (int)c->peers.size();
     const size_t es = out_f32 ? 4 : 8;
@@ -205,23 +211,21 @@ static int dist_multi(scc_ctx* c, const double* d_P, int N, int64_t col_lo, int6
             hipSetDevice(x->device);
             const int64_t a = cut[d], b = cut[d + 1];
             const size_t off = colbase(a) - base0, n = colbase(b) - colbase(a);
-            const double* P = d_P;
+            const void* P = d_pay;
             auto run = [&]() -> int {
                 int rc;
-                if (d) {  // the scores on this device
-                    double* xp = nullptr;
-                    if ((rc = ws(x, "d_P", (size_t)N * 16, &xp))) return rc;
+                if (d) {  // the payload on this device
+                    void* xp = nullptr;
+                    if ((rc = ws_get(x, "d_pay", pay_bytes, &xp))) return rc;
                     if (x->device == c->device)
-                        HIPCHK(x, hipMemcpyAsync(xp, d_P, sizeof(double) * N * 16, hipMemcpyDeviceToDevice, x->s0));
+                        HIPCHK(x, hipMemcpyAsync(xp, d_pay, pay_bytes, hipMemcpyDeviceToDevice, x->s0));
                     else
-                        HIPCHK(x, hipMemcpyPeerAsync(xp, x->device, d_P, c->device, sizeof(double) * N * 16, x->s0));
+                        HIPCHK(x, hipMemcpyPeerAsync(xp, x->device, d_pay, c->device, pay_bytes, x->s0));
                     P = xp;
                 }
                 if (a == b) return SCC_OK;
-                auto emit = [&](int64_t ca, int64_t cb, void* dst) {
-                    return scc_launch_dist_euclid(P, N, (int)ca, (int)cb, dst, out_f32, x->s0);
-                };
-                Scope sc(x, "dist", x->s0);
+                auto emit = [&](int64_t ca, int64_t cb, void* dst) { return launch(P, ca, cb, dst, x->s0); };
+                Scope sc(x, scope, x->s0);
                 void* mine = (char*)d_out + off * es;  // devices[0]: straight into the output / kept copy
                 if (d) {
                     if ((rc = ws_get(x, "d_dist", std::max<size_t>(n, 1) * es, &mine))) return rc;
@@ -404,7 +408,12 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
             return scc_launch_dist_euclid(d_P, N, (int)a, (int)b, dst, out_f32, s0);
         };
         if (!c->peers.empty()) {
-            if ((rc = dist_multi(c, d_P, N, col_lo, col_hi, d_out, dist_out, out_kind, out_f32))) return rc;
+            const SliceLaunch launch = [&](const void* pay, int64_t a, int64_t b, void* dst, hipStream_t st) {
+                return scc_launch_dist_euclid((const double*)pay, N, (int)a, (int)b, dst, out_f32, st);
+            };
+            if ((rc = dist_multi(c, d_P, sizeof(double) * (size_t)N * 16, launch, "dist", N, col_lo, col_hi, d_out,
+                                 dist_out, out_kind, out_f32)))
+                return rc;
         } else {
             Scope sc(c, "dist", s0);
             if (out_kind == SCC_PTR_HOST) {
@@ -430,12 +439,23 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         auto emit = [&](int64_t a, int64_t b, void* dst) {
             return scc_launch_pearson(d_X, N, nu, ld, d_Zp, ldz, (int)a, (int)b, dst, out_f32, s0);
         };
+        if (!c->peers.empty()) {
+            // device list: column slices of 1 - r, each device with its own copy
+            // of the z-scores (the same kernel per slice: bit-identical to one device)
+            const SliceLaunch launch = [&](const void* pay, int64_t a, int64_t b, void* dst, hipStream_t st) {
+                return scc_launch_pearson(nullptr, N, nu, ld, (float*)pay, ldz, (int)a, (int)b, dst, out_f32, st);
+            };
+            if ((rc = dist_multi(c, d_Zp, sizeof(float) * ((size_t)N * ldz + 32), launch, "pearson", N, col_lo, col_hi,
+                                 d_out, dist_out, out_kind, out_f32)))
+                return rc;
+        } else {
         Scope sc(c, "pearson", s0);
         if (out_kind == SCC_PTR_HOST) {
             if ((rc = stream_to_host(c, N, col_lo, col_hi, out_f32 ? 4 : 8, (char*)d_out, (char*)dist_out, emit)))
                 return rc;
         } else {
             HIPCHK(c, emit(col_lo, col_hi, d_out));
+        }
         }
     }
     // what scc_silhouette(dist = NULL) reads: only an output the engine owns

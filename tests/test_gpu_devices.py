@@ -102,3 +102,27 @@ def test_distance_slices_bitwise(engines, cfg_a):
         np.testing.assert_array_equal(part, ref[a0: a0 + len(part)])
         f32 = e.distance(ds, uni, f32=True)
         np.testing.assert_array_equal(f32, engines[0].distance(dss[0], uni, f32=True))
+
+
+def test_pearson_slices_bitwise(engines, cfg_a):
+    """1 - r (Fast:403) over the device list: each device writes its column
+    slice from its own copy of the z-scores with the one-device kernel, so the
+    output is bit-identical to one device (host, device and f32 outputs, and a
+    column slice)."""
+    d, names, code = cfg_a
+    dss = _datasets(engines, d)
+    uni = engines[0].de_run(dss[0], code, len(names), nat.SCC_DE_FAST, fetch="union").union
+    N = d.N
+    ref = engines[0].distance(dss[0], uni, nat.SCC_DIST_PEARSON)
+    ref32 = engines[0].distance(dss[0], uni, nat.SCC_DIST_PEARSON, f32=True)
+    for e, ds in zip(engines[1:], dss[1:]):
+        np.testing.assert_array_equal(e.distance(ds, uni, nat.SCC_DIST_PEARSON), ref)
+        np.testing.assert_array_equal(e.distance(ds, uni, nat.SCC_DIST_PEARSON, f32=True), ref32)
+        dev = torch.empty(N * (N - 1) // 2, dtype=torch.float64, device="cuda:0")
+        e.distance(ds, uni, nat.SCC_DIST_PEARSON, device_out_ptr=dev.data_ptr())
+        e.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy(), ref)
+        lo, hi = 300, 1700
+        part = e.distance_cols(ds, uni, lo, hi, metric=nat.SCC_DIST_PEARSON)
+        a0 = lo * (2 * N - lo - 1) // 2
+        np.testing.assert_array_equal(part, ref[a0: a0 + len(part)])
