@@ -346,6 +346,8 @@ SCC_API int scc_diag_eigen_topk(const double* A, int n, int lda, int k, double* 
 SCC_API int scc_diag_small_syev(const double* H, int n, int ldh, int k, double* Y, double* theta, unsigned* flag);
 SCC_API int scc_diag_cholinv(const double* G, int P, double shift_rel, double* T, unsigned* flag);
 SCC_API int scc_diag_eig_last_path(void);
+/* s_memtime stamps of the last scc_diag_small_syev's phases [8] */
+SCC_API int scc_diag_small_syev_stamps(unsigned long long* out);
 
 #ifdef __cplusplus
 }

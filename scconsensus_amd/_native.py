@@ -44,6 +44,7 @@ EXPORTS = [
     "scc_distance_scores", "scc_silhouette", "scc_last_pca_scores",
     "scc_hclust_ward_d2", "scc_cutree_hybrid",
     "scc_diag_eigen_topk", "scc_diag_small_syev", "scc_diag_cholinv", "scc_diag_eig_last_path",
+    "scc_diag_small_syev_stamps",
 ]
 
 
@@ -138,6 +139,7 @@ def load():
         "scc_diag_small_syev": (ctypes.c_int, [vp, i32, i32, i32, vp, vp, vp]),
         "scc_diag_cholinv": (ctypes.c_int, [vp, i32, dbl, vp, vp]),
         "scc_diag_eig_last_path": (ctypes.c_int, []),
+        "scc_diag_small_syev_stamps": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

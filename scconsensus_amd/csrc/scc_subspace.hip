@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(256) k_fsi_mul(const double* __restrict__ C, i
     if (w != 0) return;
     acc = ((acc + red[0][lane]) + red[1][lane]) + red[2][lane];
     const double al = coef[0], be = coef[1], ga = coef[2];
-    double dp = 0.0;
+    double dp = 0.0, dq = 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const size_t e = (size_t)(i0 + kr + 4 * r) * SI_B + j0 + cc;
@@ -532,11 +532,17 @@ __global__ void __launch_bounds__(256) k_fsi_mul(const double* __restrict__ C, i
         const double v = fma(al, acc[r], fma(be, x, ga * z));
         out[e] = v;
         dp = fma(x, v, dp);
+        dq = fma(x, x, dq);
     }
-    if (dpart) {
+    if (dpart) {  // [ti][col]: Q.W, [ti][64 + col]: Q.Q over the tile's rows
         dp += __shfl_xor(dp, 16, 64);
         dp += __shfl_xor(dp, 32, 64);
-        if (lane < 16) dpart[(size_t)ti * SI_B + j0 + cc] = dp;
+        dq += __shfl_xor(dq, 16, 64);
+        dq += __shfl_xor(dq, 32, 64);
+        if (lane < 16) {
+            dpart[(size_t)ti * 2 * SI_B + j0 + cc] = dp;
+            dpart[(size_t)ti * 2 * SI_B + SI_B + j0 + cc] = dq;
+        }
     }
 }
 
@@ -573,7 +579,7 @@ __global__ void __launch_bounds__(256) k_fsi_gram(const double* __restrict__ X, 
     for (int r = 0; r < 4; ++r) G[(i0 + kr + 4 * r) * SI_B + j0 + cc] = acc[r];
 }
 
-// Y1 = (2 / b) W - Q with b = max(coef_in[3], min over columns of Q.W) (the
+// Y1 = (2 / b) W - Q with b = max(coef_in[3], min over columns of q.Cq / q.q) (the
 // partials of the plain product; every workgroup forms b in the same order);
 // workgroup 0 writes the segment's recurrence coefficients {4/b, -2, -1, b}.
 // flag bit 64: no positive Rayleigh quotient (C = 0 on the block)
@@ -585,8 +591,14 @@ __global__ void __launch_bounds__(256) k_fsi_cheb1(const double* __restrict__ W,
     __shared__ double s_b;
     const int tid = threadIdx.x;
     if (tid < 64) {
-        double s = 0.0;
-        for (int t = 0; t < nt; ++t) s += dpart[(size_t)t * SI_B + tid];
+        // the column's Rayleigh quotient q.Cq / q.q (the basis is orthonormal only
+        // to the one shifted CholQR pass between segments)
+        double s = 0.0, sq = 0.0;
+        for (int t = 0; t < nt; ++t) {
+            s += dpart[(size_t)t * 2 * SI_B + tid];
+            sq += dpart[(size_t)t * 2 * SI_B + SI_B + tid];
+        }
+        s = sq > 0.0 ? s / sq : 0.0;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) s = fmin(s, __shfl_xor(s, o, 64));
         if (tid == 0) {
@@ -657,7 +669,12 @@ static int fsi_env(const char* name, int dflt)
 }
 
 // segments and their degree: SCC_EIG_FSI_SEG (default 6), SCC_EIG_FSI_DEG (8)
-static int fsi_segments() { return std::max(1, std::min(64, fsi_env("SCC_EIG_FSI_SEG", 6))); }
+static int fsi_segments() { return std::max(1, std::min(64, fsi_env("SCC_EIG_FSI_SEG", 5))); }
+// shifted CholQR passes between segments (SCC_EIG_FSI_PASSES, default 2: the
+// filter only needs a well-conditioned basis of the span; the Rayleigh quotients
+// that set b divide by q.q) and before Rayleigh-Ritz (3: orthonormal to
+// working precision, which Rayleigh-Ritz assumes)
+static int fsi_passes() { return std::max(1, std::min(3, fsi_env("SCC_EIG_FSI_PASSES", 2))); }
 static int fsi_degree() { return std::max(2, std::min(16, fsi_env("SCC_EIG_FSI_DEG", 8))); }
 
 extern "C" int scc_fsi_wanted(int n)
@@ -671,13 +688,13 @@ extern "C" size_t scc_fsi_scratch_doubles(int n)
 {
     const size_t np = si_npad(n), nt = np / 16, nblk = (np + 255) / 256;
     const int S = fsi_segments();
-    return 4 * np * SI_B + 2 * (size_t)SI_B * SI_B + nt * SI_B + (size_t)(S + 2) * 4 + SI_B * 16 + 16 + 16 +
+    return 4 * np * SI_B + 2 * (size_t)SI_B * SI_B + 2 * nt * SI_B + (size_t)(S + 2) * 4 + SI_B * 16 + 16 + 16 +
            3 * nblk * 16 + 64 + 2 * np + SI_B + 8 + 64;
 }
 
 namespace {
 struct FsiGraphEntry {
-    int dev, n, ldc, k, S, m, live, guard;
+    int dev, n, ldc, k, S, m, passes, live, guard;
     const void *C, *scr, *Z, *W;
     hipGraphExec_t exec;
 };
@@ -705,7 +722,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     if (n < FSI_NMIN || k > 16 || k < 1) return hipSuccess;
     const size_t np = si_npad(n), nt = np / 16;
     const int nblk = (int)((np + 255) / 256);
-    const int S = fsi_segments(), m = fsi_degree();
+    const int S = fsi_segments(), m = fsi_degree(), passes = fsi_passes();
     double* Q = scr;
     double* Ya = Q + np * SI_B;
     double* Yb = Ya + np * SI_B;
@@ -713,7 +730,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     double* G = Yc + np * SI_B;
     double* T = G + SI_B * SI_B;
     double* dpart = T + SI_B * SI_B;
-    double* coef = dpart + nt * SI_B;  // [S + 2][4]
+    double* coef = dpart + 2 * nt * SI_B;  // [S + 2][4]
     double* Yv = coef + (size_t)(S + 2) * 4;
     double* theta = Yv + SI_B * 16;
     double* sgn = theta + 16;
@@ -736,7 +753,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         hipLaunchKernelGGL(k_si_init, dim3((unsigned)((np * SI_B + 255) / 256)), dim3(256), 0, s, (int)np,
                            std::min(live, n), Ya);
         auto orth = [&](double* src, double* tmp, double* dst, int passes) -> hipError_t {
-            // passes 2: src -> tmp -> dst; 3: src -> dst -> tmp -> dst
+            // passes 1: src -> dst; 2: src -> tmp -> dst; 3: src -> dst -> tmp -> dst
             double* seq[4] = {src, passes == 2 ? tmp : dst, passes == 2 ? dst : tmp, dst};
             for (int p = 0; p < passes; ++p) {
                 hipLaunchKernelGGL(k_fsi_gram, gg, dim3(256), 0, s, seq[p], seq[p], (int)np, G);
@@ -746,7 +763,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             }
             return hipGetLastError();
         };
-        if ((e = orth(Ya, Yb, Q, 2)) != hipSuccess) return e;
+        if ((e = orth(Ya, Yb, Q, 1)) != hipSuccess) return e;
         for (int sg = 0; sg < S; ++sg) {
             // W = C Q (into Ya) with the column partials of Q.W, then Y1 (into Yb)
             hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, Q, (const double*)nullptr, coef,
@@ -765,7 +782,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
                 nxt = fr;
             }
             double* tmp = (prev != Q) ? prev : nxt;
-            if ((e = orth(cur, tmp, Q, 3)) != hipSuccess) return e;
+            if ((e = orth(cur, tmp, Q, sg + 1 < S ? passes : 3)) != hipSuccess) return e;
         }
         // Rayleigh-Ritz on span(Q): W = C Q (Ya), H = Q^T W, its top-k eigenpairs
         hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, Q, (const double*)nullptr, coef, Ya,
@@ -802,7 +819,8 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         std::lock_guard<std::mutex> lk(g_fsi_mu);
         hipGraphExec_t ex = nullptr;
         for (const auto& g : g_fsi_graphs)
-            if (g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m && g.live == live &&
+            if (g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m && g.passes == passes &&
+                g.live == live &&
                 g.guard == guard && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
                 ex = g.exec;
                 break;
@@ -819,7 +837,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
                         hipGraphExecDestroy(g_fsi_graphs.front().exec);
                         g_fsi_graphs.erase(g_fsi_graphs.begin());
                     }
-                    g_fsi_graphs.push_back({dev, n, ldc, k, S, m, live, guard, C, scr, Z, Wout, ex});
+                    g_fsi_graphs.push_back({dev, n, ldc, k, S, m, passes, live, guard, C, scr, Z, Wout, ex});
                 } else {
                     ex = nullptr;
                 }
