@@ -257,6 +257,71 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
             }
 }
 
+// The same Gram with 128 x 128 output tiles (each wave 64 x 64: 4 x 4 MFMA
+// tiles): every row segment of Xc is fetched by half as many workgroups (the
+// re-fetch factor is the number of column tiles: 14 at config D's |U| = 845
+// with 64-wide tiles, 17x the operand in FETCH_SIZE).  The slab layout is
+// k_gram_reduce's (64-wide blocks ti <= tj): the lower 64-block of a diagonal
+// 128 tile is not computed (its mirror is), and a tile whose second 64-block
+// falls past ld (ld % 128 == 64) leaves those waves idle.
+__global__ void __launch_bounds__(256) k_gram_f64_128(const double* __restrict__ Xc, int Npad, int ld, int ntile,
+                                                      int rows_per_chunk, double* __restrict__ slabs)
+{
+    int t = blockIdx.x, ti = 0;
+    while (t >= ntile - ti) {
+        t -= ntile - ti;
+        ++ti;
+    }
+    const int tj = ti + t;
+    const int chunk = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = scc_wave_id();
+    const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
+    const int i0 = ti * 128 + wi, j0 = tj * 128 + wj;
+    const int c0 = chunk * rows_per_chunk, c1 = min(Npad, c0 + rows_per_chunk);
+    if (ti == tj && wi > wj) return;   // the mirror of (wj, wi)
+    if (i0 >= ld || j0 >= ld) return;  // past the last 64-column block
+    d4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    const int kr = lane >> 4, cc = lane & 15;
+    constexpr int U = 2;
+    for (int c = c0; c < c1; c += 4 * U) {
+        double av[U][4], bv[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int rr = c + 4 * u + kr;
+            const double* row = Xc + (size_t)min(rr, c1 - 1) * ld;
+            const bool ok = rr < c1;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const double x = row[i0 + 16 * m + cc], y = row[j0 + 16 * m + cc];
+                av[u][m] = ok ? x : 0.0;
+                bv[u][m] = ok ? y : 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u][a], bv[u][b], acc[a][b], 0, 0, 0);
+    }
+    double* S = slabs + (size_t)chunk * ld * ld;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = i0 + a * 16 + kr + 4 * r;
+                const int col = j0 + b * 16 + cc;
+                S[(size_t)row * ld + col] = acc[a][b][r];
+            }
+}
+
 // C[i][j] = sum_k slabs[k][i][j] in chunk order for tiles ti <= tj, mirrored
 __global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ slabs, int nchunk, int ld,
                                                      double* __restrict__ C)
@@ -847,10 +912,20 @@ extern "C" hipError_t scc_launch_center_parts(double* Xc, int n, int nu, int ld,
 extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C,
                                       hipStream_t st)
 {
-    const int ntile = ld / 64;
     const int rpc = ((Npad + nchunk - 1) / nchunk + 3) & ~3;
-    hipLaunchKernelGGL(k_gram_f64, dim3(ntile * (ntile + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, ntile, rpc,
-                       slabs);
+    // 128-wide output tiles from |U| > 384 (half the operand re-fetch;
+    // SCC_GRAM_T=64 / 128 forces either)
+    const char* gt = getenv("SCC_GRAM_T");
+    const int tw = (gt && *gt) ? (atoi(gt) == 128 ? 128 : 64) : (ld > 384 ? 128 : 64);
+    if (tw == 128) {
+        const int nt = (ld + 127) / 128;
+        hipLaunchKernelGGL(k_gram_f64_128, dim3(nt * (nt + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, nt, rpc,
+                           slabs);
+    } else {
+        const int ntile = ld / 64;
+        hipLaunchKernelGGL(k_gram_f64, dim3(ntile * (ntile + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, ntile,
+                           rpc, slabs);
+    }
     hipLaunchKernelGGL(k_gram_reduce, dim3(2048), dim3(256), 0, st, slabs, nchunk, ld, C);
     return hipGetLastError();
 }

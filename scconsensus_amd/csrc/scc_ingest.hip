@@ -81,9 +81,15 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
                                                     int* __restrict__ nodg, dd* __restrict__ wave_expm1,
-                                                    int want_expm1, int glo, int ghi, int rng, int hw,
+                                                    int want_expm1, int glo, int ghi, int rng_in, int hw,
                                                     int* __restrict__ err)
 {
+    // rng_in 1: a gene-shard range of a validated dataset (below); 2: the whole
+    // range of a validated dataset with no explicit zeros (FAST): the counts
+    // need only the row indices (4 of the 12 bytes per stored value), nodg
+    // comes from the dataset's cache and the value checks were done by the
+    // validating read -- the CSC is then read once in full (by the scatter)
+    const bool rng = rng_in == 1, ro = rng_in == 2;
     // genes outside [glo, ghi) (a shard of the gene rows) are not counted; nodg
     // and the expm1 sum still see every entry -- unless rng (a validated CSC
     // dataset, FAST mode): then each cell's entries of the tiles covering
@@ -135,7 +141,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                 for (int u = 0; u < 4; ++u) {
                     const i64 k = k0 + u * 64 + lane;
                     const i64 kc = k < ke ? k : ke - 1;  // k0 < ke, so ke - 1 >= b
-                    const double x = vals[kc];
+                    const double x = ro ? 1.0 : vals[kc];
                     xs[u] = k < ke ? x : 0.0;
                     if (DENSE) {
                         gs[u] = k < ke ? (int)(k - b) : -1;
@@ -160,9 +166,11 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                     }
                     if (win > 0) continue;
                     const bool gok = (g >= 0) & (g < G);
-                    bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2);
-                    pos += (x > 0.0);
-                    if (want_expm1) se = dd_add_d(se, expm1(x));
+                    if (!ro) {
+                        bad |= (!(x - x == 0.0) ? 1 : 0) | (gok ? 0 : 2) | ((x == 0.0 && gok) ? 0x1000 : 0);
+                        pos += (x > 0.0);
+                        if (want_expm1) se = dd_add_d(se, expm1(x));
+                    }
                     if (!DENSE && a >= 0) {
                         // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
                         const int gp = gps[u];
@@ -183,7 +191,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                 for (int t = tl + 1 + lane; t <= tend; t += 64) bp[t] = ke;
             }
             pos = u32_wave_sum(pos);
-            if (lane == 0 && !rng) nodg[c] = (int)pos;
+            if (lane == 0 && !rng && !ro) nodg[c] = (int)pos;
         }
         if (a < 0) break;  // unkept chunk: side work only (one pass)
         __syncthreads();

@@ -119,6 +119,7 @@ struct scc_dataset {
     // only its tiles (k_ing_hist rng) and takes nodg (clustering-independent)
     // from this device cache.  The data must not change while the dataset lives.
     mutable bool validated = false;
+    mutable bool no_zeros = false;  // the validating read saw no explicit (stored) zero
     mutable int* d_nodg = nullptr;  // [N], always owned
     // device list: the replica on each peer engine of the context (same order
     // as scc_ctx::peers), and the stored values per gene that balance the

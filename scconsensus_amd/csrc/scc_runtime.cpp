@@ -673,8 +673,9 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     bool hist_rng = false, hist_full = false;
     // after an error-free run whose ingest read every entry: the dataset is
     // validated and its nodg cached (for later gene-shard runs)
-    auto note_validated = [&]() -> int {
+    auto note_validated = [&](int err_bits) -> int {
         if (!hist_full || ds->validated || ds->dense) return SCC_OK;
+        ds->no_zeros = !(err_bits & 0x1000);  // the full read saw no explicit zero
         if (!ds->d_nodg && hipMalloc((void**)&ds->d_nodg, sizeof(int) * N) != hipSuccess) {
             hipGetLastError();
             ds->d_nodg = nullptr;
@@ -709,15 +710,20 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     HIPCHK(c, hipMemcpyAsync(d_tab, tab_src, sizeof(int) * H.size(), hipMemcpyHostToDevice, s0));
     const char* ife = getenv("SCC_INGEST_FULL");
     hist_rng = !ds->dense && ds->validated && ds->d_nodg && fast && (glo > 0 || ghi < G) && !(ife && atoi(ife));
-    hist_full = !hist_rng;
+    // a validated dataset without explicit zeros, FAST, all genes: the counting
+    // pass reads the row indices only (the scatter reads the CSC in full)
+    const bool hist_ro = !hist_rng && !ds->dense && ds->validated && ds->no_zeros && ds->d_nodg && fast &&
+                         !(ife && atoi(ife));
+    hist_full = !hist_rng && !hist_ro;
     {
         Scope sc(c, "ingest", s0);
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
         HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 16, s0));
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
-                                         hist_rng ? 1 : 0, d_err, s0));
-        if (hist_rng) HIPCHK(c, hipMemcpyAsync(d_nodg, ds->d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
+                                         hist_rng ? 1 : (hist_ro ? 2 : 0), d_err, s0));
+        if (hist_rng || hist_ro)
+            HIPCHK(c, hipMemcpyAsync(d_nodg, ds->d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
         uint32_t* d_cscr;
         WS("colscan", scc_ingest_colscan_scratch(nc, G), d_cscr);
         HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, d_cscr, s0));
@@ -979,7 +985,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         if (e & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
         if (e & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
         if (e & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
-        return note_validated();
+        return note_validated(e);
     }
     if (stage == DE_FINISH) {
         const char* src = (const char*)shard;
@@ -1099,7 +1105,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
     if (hdr[1] & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
     if (hdr[1] & 16) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: record out of range");
-    if ((rc = note_validated())) return rc;
+    if ((rc = note_validated(hdr[1]))) return rc;
     scc_de_result* r = new scc_de_result();
     r->ctx = c;
     r->generation = c->generation;

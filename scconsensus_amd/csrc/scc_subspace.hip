@@ -651,6 +651,121 @@ __global__ void k_fsi_bound_check(const double* __restrict__ coef, const double*
     if (threadIdx.x == 0 && !(coef[3] < theta[k - 1])) atomicOr(flag, 32u);
 }
 
+// The missed-eigenpair guard of the filtered path in ONE launch per product
+// (k_sig_norm + k_sig_step took two, one of them a single workgroup reading
+// the whole n x 64 W): workgroup t owns rows [16 t, 16 t + 16) and leaves
+// per-tile partials of W^T x, |x|^2 and x.u_prev for the next launch, which
+// reduces the nt partials itself (fixed order: every workgroup forms the same
+// sums).  mode 0: x = g (the pseudo-random start) and the partials of V^T g;
+// mode 1: x = g - V (V^T g); mode 2: x = C u / |u| - V (W^T u) / |u| (the
+// deflated operator P C P on u in range(P), W = C V); mode 3 (one workgroup):
+// rho = (u/|u|)^T P C P (u/|u|) from the partials, flag bit 8 when rho reaches
+// theta_k (an eigenvalue above the 15th Ritz value outside the basis).
+#define SGF_W 66  // partials per tile: [0, 64) M^T x, 64: |x|^2, 65: x . u_prev / |u_prev|
+__device__ inline unsigned sig_hash(int i)
+{
+    unsigned h = (unsigned)i * 0x85ebca6bu ^ 0xc2b2ae35u;
+    h ^= h >> 16;
+    h *= 0x27d4eb2du;
+    h ^= h >> 15;
+    return h;
+}
+__global__ void __launch_bounds__(256) k_sig_fused(const double* __restrict__ C, int ldc, int n,
+                                                   const double* __restrict__ V, const double* __restrict__ W,
+                                                   const double* __restrict__ u, const double* __restrict__ part_in,
+                                                   int nt, double* __restrict__ x, double* __restrict__ part_out,
+                                                   const double* __restrict__ theta, int k, u32* __restrict__ flag,
+                                                   int mode)
+{
+    __shared__ double z[SI_B];
+    __shared__ double sc[2];
+    __shared__ double xr[16], ur[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
+    if (mode == 3) {
+        if (tid < 64) {
+            double rho = 0.0, s = 0.0;
+            for (int t = 0; t < nt; ++t) {
+                rho += part_in[(size_t)t * SGF_W + 65];
+                s += part_in[(size_t)t * SGF_W + 64];
+            }
+            // rho is the Rayleigh quotient of the normalised previous vector;
+            // an empty complement (s == 0) misses nothing
+            if (tid == 0 && s > 0.0 && !(rho < theta[k - 1])) atomicOr(flag, 8u);
+        }
+        return;
+    }
+    // reductions of the previous launch's partials (fixed order)
+    if (tid < SI_B + 1 && mode >= 1) {
+        const int c = tid < SI_B ? tid : 64;
+        double acc = 0.0;
+        for (int t = 0; t < nt; ++t) acc += part_in[(size_t)t * SGF_W + c];
+        if (tid < SI_B)
+            z[tid] = acc;
+        else
+            sc[0] = acc;
+    }
+    __syncthreads();
+    const double inv = (mode == 2) ? (sc[0] > 0.0 ? 1.0 / sqrt(sc[0]) : 0.0) : 1.0;
+    const int r0 = blockIdx.x * 16;
+    // rows r0 + 4 wv + j (j < 4): x_row, the input row u_row (mode 2: u / |u|)
+    double xv[4], uv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = r0 + 4 * wv + j;
+        const int rc = min(row, n - 1);
+        double acc = 0.0;
+        if (mode == 2) {
+            for (int cb0 = 0; cb0 < n; cb0 += 512) {  // 8 loads per lane in flight
+                double cv[8], uu[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const int cb = min(cb0 + lane + 64 * m, n - 1);
+                    cv[m] = C[(size_t)rc * ldc + cb];
+                    uu[m] = u[cb];
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) acc = fma(cb0 + lane + 64 * m < n ? cv[m] : 0.0, uu[m], acc);
+            }
+            acc = sig_wave_sum(acc) * inv;
+        }
+        const double g = (double)(sig_hash(rc) & 0xffffff) / 16777216.0 - 0.5;
+        double base = (mode == 2) ? acc : g;
+        if (mode >= 1) base = fma(-V[(size_t)rc * SI_B + lane], (mode == 2 ? z[lane] * inv : z[lane]), 0.0);
+        // (the deflation term, summed over the 64 basis columns)
+        const double dfl = (mode >= 1) ? sig_wave_sum(base) : 0.0;
+        const double val = ((mode == 2) ? acc : g) + dfl;
+        xv[j] = row < n ? val : 0.0;
+        uv[j] = (row < n && mode == 2) ? u[rc] * inv : 0.0;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xr[4 * wv + j] = xv[j];
+            ur[4 * wv + j] = uv[j];
+        }
+    }
+    __syncthreads();
+    if (tid < 16 && r0 + tid < n) x[r0 + tid] = xr[tid];
+    // partials over the tile's rows: M^T x (M = V in mode 0, W after), |x|^2, x . u
+    const double* M = (mode == 0) ? V : W;
+    if (tid < SI_B) {
+        double acc = 0.0;
+        for (int j = 0; j < 16; ++j) {
+            const int row = min(r0 + j, n - 1);
+            acc = fma(M[(size_t)row * SI_B + tid], xr[j], acc);
+        }
+        part_out[(size_t)blockIdx.x * SGF_W + tid] = acc;
+    } else if (tid == 64) {
+        double s2 = 0.0, xu = 0.0;
+        for (int j = 0; j < 16; ++j) {
+            s2 = fma(xr[j], xr[j], s2);
+            xu = fma(xr[j], ur[j], xu);
+        }
+        part_out[(size_t)blockIdx.x * SGF_W + 64] = s2;
+        part_out[(size_t)blockIdx.x * SGF_W + 65] = xu;
+    }
+}
+
 extern "C" hipError_t scc_launch_small_syev(const double* H, int n, int ldh, int k, double* Y, double* theta,
                                             u32* flag, hipStream_t st);
 extern "C" hipError_t scc_launch_fsi_cholinv(const double* G, int P, double shift_rel, double* T, u32* flag,
@@ -689,7 +804,7 @@ extern "C" size_t scc_fsi_scratch_doubles(int n)
     const size_t np = si_npad(n), nt = np / 16, nblk = (np + 255) / 256;
     const int S = fsi_segments();
     return 4 * np * SI_B + 2 * (size_t)SI_B * SI_B + 2 * nt * SI_B + (size_t)(S + 2) * 4 + SI_B * 16 + 16 + 16 +
-           3 * nblk * 16 + 64 + 2 * np + SI_B + 8 + 64;
+           3 * nblk * 16 + 64 + 2 * np + 2 * nt * SGF_W + 64;
 }
 
 namespace {
@@ -739,8 +854,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     u32* flag = (u32*)(mpart + (size_t)nblk * 16);
     double* gu = (double*)(flag + 128);
     double* gy = gu + np;
-    double* gz = gy + np;
-    double* gsc = gz + SI_B;
+    double* gpart = gy + np;  // [2][nt][SGF_W] guard partials
     const int live = std::max(SI_B, std::min(n, fsi_env("SCC_EIG_SI_INIT_ROWS", n)));
     const int guard = n <= SI_GUARD_NMAX;
     const double shift_rel = 11.0 * ((double)np * SI_B + (double)SI_B * (SI_B + 1)) * 1.1102230246251565e-16;
@@ -795,19 +909,24 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, s, Z, sgn, n);
         hipLaunchKernelGGL(k_fsi_bound_check, dim3(1), dim3(64), 0, s, coef + 4 * S, theta, k, flag);
         if (guard) {
-            const dim3 gstep((n + 15) / 16);
-            hipLaunchKernelGGL(k_sig_init, dim3((n + 255) / 256), dim3(256), 0, s, n, gu);
-            hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, s, Q, n, gu, nullptr, gsc, gz, theta, k, flag, 0);
-            hipLaunchKernelGGL(k_sig_step, gstep, dim3(256), 0, s, C, ldc, n, gu, gsc, Q, gz, gy, 0);
-            double* u = gy;
-            double* y = gu;
+            // x0 = g (partials V^T g), x1 = P g, then SI_GUARD_IT products of P C P
+            const int gt2 = (n + 15) / 16;
+            double* pa = gpart;
+            double* pb = gpart + (size_t)gt2 * SGF_W;
+            double* xa = gu;
+            double* xb = gy;
+            hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)nullptr,
+                               (const double*)nullptr, gt2, xa, pa, theta, k, flag, 0);
+            hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)xa, pa, gt2,
+                               xb, pb, theta, k, flag, 1);
             for (int it = 0; it < SI_GUARD_IT; ++it) {
-                hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, s, Ya, n, u, it ? y : nullptr, gsc, gz, theta,
-                                   k, flag, 0);
-                hipLaunchKernelGGL(k_sig_step, gstep, dim3(256), 0, s, C, ldc, n, u, gsc, Q, gz, y, 1);
-                std::swap(u, y);
+                std::swap(xa, xb);
+                std::swap(pa, pb);
+                hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)xa, pa,
+                                   gt2, xb, pb, theta, k, flag, 2);
             }
-            hipLaunchKernelGGL(k_sig_norm, dim3(1), dim3(SIG_T), 0, s, Ya, n, u, y, gsc, gz, theta, k, flag, 1);
+            hipLaunchKernelGGL(k_sig_fused, dim3(1), dim3(64), 0, s, C, ldc, n, Q, Ya, (const double*)xb, pb, gt2,
+                               xa, pa, theta, k, flag, 3);
         }
         return hipGetLastError();
     };
