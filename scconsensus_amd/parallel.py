@@ -70,6 +70,17 @@ class Dist:
                 self.dist.all_reduce(tensor, op=self.dist.ReduceOp.MIN)
         return tensor
 
+    def broadcast_(self, tensor, src: int = 0):
+        """In-place copy of rank ``src``'s tensor to every rank."""
+        if self.active:
+            if self._host_staged(tensor):
+                h = tensor.cpu()
+                self.dist.broadcast(h, src=src)
+                tensor.copy_(h)
+            else:
+                self.dist.broadcast(tensor, src=src)
+        return tensor
+
     def all_gather_cat(self, tensor):
         """The ranks' equal-sized 1-D tensors concatenated in rank order."""
         if not self.active:

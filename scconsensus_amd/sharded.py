@@ -91,6 +91,18 @@ def _raise_if(codes, msg=""):
         raise ShardError(bad, msg or f"rank {codes.index(bad)} reported scc error {bad}")
 
 
+def _stage_to_host(t):
+    """An asynchronous copy of device tensor ``t`` into pinned host memory,
+    ordered on the current stream (valid once that stream has been
+    synchronised); CPU tensors are returned as they are."""
+    import torch
+    if getattr(t, "is_cuda", False):
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        return h
+    return t
+
+
 def de_sharded(eng, ds, code, K, dist: parallel.Dist, device, fetch="rows", weights=None, exchange="records",
                pair_split=True, **params):
     """The DE of one job over all ranks of ``dist``; every rank returns the same
@@ -122,6 +134,8 @@ def _de_sharded(eng, ds, code, K, dist, device, fetch, weights, exchange, pair_s
     buf = torch.empty(cap * REC_WORDS, dtype=torch.int64, device=device)
     n, st, msg = _call(eng.de_run_shard_records, ds, code, K, lo, hi, buf.data_ptr(), cap, **shard_kw)
     n = n or 0
+    # the one host read of the records exchange: RCCL sizes a gather on the
+    # host, and the gather's stride is the ranks' largest record count
     info = dist.all_gather_cat(torch.tensor([st, n], dtype=torch.int64, device=device)).view(-1, 2).cpu().numpy()
     _raise_if(info[:, 0], msg)
     counts = info[:, 1].astype(np.int64)
@@ -143,9 +157,12 @@ def _de_sharded(eng, ds, code, K, dist, device, fetch, weights, exchange, pair_s
         keys[keys == -1] = _I64_MAX  # unselected (all ones) sorts last under a signed MIN
         first[-1] = -st  # the status rides along: MIN = minus the largest error code
         dist.all_reduce_min_(first)
-        _raise_if([-int(first[-1].item())], msg)
         keys[keys == _I64_MAX] = -1
+        # the status word is copied behind the union's own read-back (same
+        # stream), so checking it costs no extra host round trip
+        st_host = _stage_to_host(first[-1:])
         union = eng.de_union_first_occ(keys.data_ptr(), ds.G)
+        _raise_if([-int(st_host[0])], msg)
         return nat.DeResult(nat.SCC_DE_FAST, K, P, union, np.zeros(0, np.int32))
     return eng.de_finish_records(ds, code, K, recs.data_ptr(), counts, stride, fetch=fetch, **shard_kw)
 
@@ -157,10 +174,13 @@ def pca_sharded(eng, ds, genes, dist: parallel.Dist, device, ncomp=0):
     Every stage's status word rides in its collective; they are read back
     once, at the end (one host round trip)."""
     with _on_stream(eng, device):
-        return _pca_sharded(eng, ds, genes, dist, device, ncomp)
+        full, status, msgs = _pca_sharded(eng, ds, genes, dist, device, ncomp)
+        _raise_if(status.cpu().numpy(), msgs[0] if msgs else "another rank's PCA stage failed")
+    return full
 
 
 def _pca_sharded(eng, ds, genes, dist, device, ncomp):
+    """(scores, status words on the device, messages): no host read."""
     import torch
 
     genes = np.ascontiguousarray(genes, np.int32)
@@ -182,12 +202,12 @@ def _pca_sharded(eng, ds, genes, dist, device, ncomp):
     gram = torch.zeros(nu * nu + 1, **f64)
     gram[-1] = call(eng.pca_shard_gram, pcs.data_ptr(), dist.world, gram.data_ptr())
     dist.all_reduce_sum_(gram)
-    # the eigenvectors of rank 0, broadcast (a sum with zeros elsewhere): ONE
-    # eigensolve, so every rank's score block comes from the same vectors
+    # the eigenvectors of rank 0, broadcast: ONE eigensolve, so every rank's
+    # score block comes from the same vectors
     vecs = torch.zeros(nu * 16 + 1, **f64)
     if dist.rank == 0:
         vecs[-1] = call(eng.pca_shard_eigen, gram.data_ptr(), vecs.data_ptr(), ncomp)
-    dist.all_reduce_sum_(vecs)
+    dist.broadcast_(vecs, src=0)
     # this rank's rows, then an all-gather of equal-size blocks (a block holds
     # at most `rows` cells: N / world rounded up) and the status word
     rows = -(-N // dist.world)
@@ -197,12 +217,11 @@ def _pca_sharded(eng, ds, genes, dist, device, ncomp):
     blk[: (hi - lo) * 16] = full[lo * 16: hi * 16]
     blk[-1] = st
     allb = dist.all_gather_cat(blk).view(dist.world, rows * 16 + 1)
-    status = torch.stack([parts[:, -1].max(), gram[-1], vecs[-1], allb[:, -1].max()]).cpu().numpy()
-    _raise_if(status, msgs[0] if msgs else "another rank's PCA stage failed")
+    status = torch.stack([parts[:, -1].max(), gram[-1], vecs[-1], allb[:, -1].max()])
     for r in range(dist.world):
         a, b = cell_shard(N, r, dist.world)
         full[a * 16: b * 16] = allb[r, : (b - a) * 16]
-    return full
+    return full, status, msgs
 
 
 def column_shard(N: int, rank: int, world: int) -> tuple[int, int]:
@@ -236,9 +255,17 @@ def distance_sharded(eng, ds, genes, dist: parallel.Dist, device=None, f32=False
 
     if device is None:
         device = torch.device(f"cuda:{torch.cuda.current_device()}")
-    if scores is None:
-        scores = pca_sharded(eng, ds, genes, dist, device, ncomp)
     lo, hi = column_shard(ds.N, dist.rank, dist.world)
     with _on_stream(eng, device):
+        status, msgs = None, []
+        if scores is None:
+            # the PCA's status words are checked after the distance is queued
+            # behind them: the job's one host read
+            scores, status, msgs = _pca_sharded(eng, ds, genes, dist, device, ncomp)
+            st_host = _stage_to_host(status)
         out = eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, f32=f32, device_out_ptr=device_out_ptr)
+        if status is not None:
+            if getattr(status, "is_cuda", False):
+                torch.cuda.current_stream(device).synchronize()
+            _raise_if(st_host.numpy(), msgs[0] if msgs else "another rank's PCA stage failed")
     return lo, hi, out
