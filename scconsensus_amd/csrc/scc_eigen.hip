@@ -1896,7 +1896,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         e = scc_eigen_fsi(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, st);
         if (e != hipSuccess) return e;
         if (ok) {
-            g_eig_last_path = 2;
+            g_eig_last_path = ok == 2 ? 3 : 2;  // 3: the persistent engine ran the filter loop
             if (marks)
                 for (int m = 1; m < 6; ++m)
                     if (marks[m]) hipEventRecord(marks[m], st);

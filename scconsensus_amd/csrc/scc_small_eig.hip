@@ -16,6 +16,7 @@
 //                  through LDS, no cross-lane register traffic but one readlane
 //                  per step.
 #include "scc_common.hpp"
+#include "scc_fsi_dev.hpp"
 #include "scc.h"
 #include <mutex>
 
@@ -25,15 +26,6 @@
 
 static constexpr double kSeEps = 2.220446049250313e-16;
 
-__device__ inline double se_wave_sum(double v)
-{
-    v += scc_xor_lane_f64<32>(v);
-    v += scc_xor_lane_f64<16>(v);
-    v += scc_xor_lane_f64<8>(v);
-    v += scc_xor_lane_f64<4>(v);
-    v += scc_xor_lane_f64<2>(v);
-    return v + scc_xor_lane_f64<1>(v);
-}
 __device__ inline double se_wave_min(double v)
 {
     v = fmin(v, scc_xor_lane_f64<32>(v));
@@ -52,15 +44,6 @@ __device__ inline double se_wave_max(double v)
     v = fmax(v, scc_xor_lane_f64<2>(v));
     return fmax(v, scc_xor_lane_f64<1>(v));
 }
-// uniform value of lane l (compile-time or wave-uniform) of a lane-varying double
-__device__ __forceinline__ double se_readlane(double x, int l)
-{
-    const u64 b = (u64)__double_as_longlong(x);
-    const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)b, l);
-    const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(b >> 32), l);
-    return __longlong_as_double((long long)(((u64)hi << 32) | lo));
-}
-
 // number of eigenvalues of the 64 x 64 tridiagonal T (d, e^2) below x: signs
 // of the leading principal minors p_i = (d_i - x) p_{i-1} - e_{i-1}^2 p_{i-2}
 // (one FMA on the dependent chain, no division), a zero pivot counted negative
@@ -625,11 +608,55 @@ __global__ void __launch_bounds__(64) k_fsi_cholinv64(const double* __restrict__
     for (int i = 0; i < 64; ++i) T[j * 64 + i] = w[i];
 }
 
+// T = R^{-1} = (L^{-1})^T for G + shift I = L L^T, one 256-thread workgroup
+__global__ void __launch_bounds__(256) k_fsi_cholinv_blk(const double* __restrict__ G, double shift_rel,
+                                                        double* __restrict__ T, u32* __restrict__ flag)
+{
+    __shared__ double A[64 * CB_S];
+    __shared__ double X[64 * CB_S];
+    __shared__ double Ri[64];
+    __shared__ double s_tr;
+    __shared__ int s_bad;
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        const double tr = se_wave_sum(G[tid * 64 + tid]);
+        if (tid == 0) {
+            s_tr = tr;
+            s_bad = !(tr >= 0.0) || !(tr < INFINITY);
+        }
+    }
+    __syncthreads();
+    const double shift = shift_rel * s_tr;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int e = tid + 256 * u, i = e >> 6, j = e & 63;
+        A[i * CB_S + j] = G[e] + (i == j ? shift : 0.0);
+    }
+    __syncthreads();
+    fsi_cholinv_blk(A, X, Ri, &s_bad);
+    // T[i][j] = X[j][i]
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int e = tid + 256 * u, i = e >> 6, j = e & 63;
+        T[e] = X[j * CB_S + i];
+    }
+    if (tid == 0 && s_bad && flag) atomicOr(flag, 1u);
+}
+
+static int cholinv_variant()
+{
+    const char* e = getenv("SCC_FSI_CHOL");  // 0: the one-wave kernel
+    return (e && *e) ? atoi(e) : 1;
+}
+
 extern "C" hipError_t scc_launch_fsi_cholinv(const double* G, int P, double shift_rel, double* T, u32* flag,
                                              hipStream_t st)
 {
     if (P != 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_fsi_cholinv64, dim3(1), dim3(64), 0, st, G, shift_rel, T, flag);
+    if (cholinv_variant())
+        hipLaunchKernelGGL(k_fsi_cholinv_blk, dim3(1), dim3(256), 0, st, G, shift_rel, T, flag);
+    else
+        hipLaunchKernelGGL(k_fsi_cholinv64, dim3(1), dim3(64), 0, st, G, shift_rel, T, flag);
     return hipGetLastError();
 }
 

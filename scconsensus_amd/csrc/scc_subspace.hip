@@ -25,6 +25,7 @@
 // sharded job).  Output layout as scc_launch_eigen_topk: Z[u*16 + q], W[q],
 // largest-magnitude component of each vector positive.
 #include "scc_common.hpp"
+#include "scc_fsi_dev.hpp"
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
@@ -34,7 +35,6 @@
 #define SI_B 64
 #define SI_TOL 1e-11
 
-typedef double d4 __attribute__((ext_vector_type(4)));
 
 // X^T Y tile (16 x 16) over rows [0, n) of two n x 64 row-major blocks, the 4
 // waves of the workgroup taking interleaved 4-row steps with four steps' loads
@@ -777,6 +777,416 @@ __global__ void k_fsi_coef0(double* __restrict__ coef)
     if (threadIdx.x < 4) coef[threadIdx.x] = threadIdx.x == 0 ? 1.0 : 0.0;
 }
 
+// ===========================================================================
+// The filter loop as ONE persistent launch (k_fsi_engine): the ~80 launches of
+// the initial orthonormalisation, the S segments of m products and their
+// CholQR passes (each a kernel boundary of ~1.3 us plus a ramp) become hand-offs
+// between co-resident workgroups.  Workgroup g owns the 16 x 16 tile (row tile
+// rt = g / 4, column group cq = g % 4) of every n x 64 block:
+//   product     its 16 rows of C (LDS, loaded once) times the column group's 16
+//               columns of the previous block (handed off), the 4 waves taking
+//               quarters of k exactly as k_fsi_mul, the recurrence epilogue on the
+//               tile it keeps in registers; the column groups run independently
+//               between orthonormalisations;
+//   b           the first product of a segment leaves per-tile partials of q.w and
+//               q.q; every workgroup sums them in the same order (k_fsi_cheb1)
+//               and forms Y1 = (2/b) W - Q on the fly as the next product's operand;
+//   CholQR      workgroups 0..9 each form one 16 x 16 block of G = Y^T Y (the
+//               upper 10; G is exactly symmetric), every workgroup factors G
+//               redundantly (fsi_cholinv_blk: no hand-off for T) and forms its
+//               tile of Y T (k_fsi_apply's order).
+// Every sum has the launch path's order, so the basis is bit-identical to it.
+// Hand-off (MI355X_MICROARCH.md, valid form row 1): every handed-off double is
+// stored and loaded `sc1` (8-byte agent-scope relaxed atomics), each storing wave
+// waits vmcnt(0), a workgroup barrier, then one lane stores the workgroup's
+// phase number in its flag (`sc1`); consumers poll the producers' flags with
+// `sc1` loads from wave 0 and the other waves load after a barrier.  The grid
+// (4 n/16 workgroups, ~150 KB LDS each: one per CU, <= 168) is co-resident on an
+// otherwise idle device; every poll is bounded: on a time-out (or another
+// workgroup's) err is set and the host reruns the solve on the launch path.
+#define FX_FS 32        // flag stride (u32): one 128-B line per workgroup
+#define FX_NPMAX 672    // C tile (16 x np doubles) + the Cholesky's 2 x 64 x CB_S in LDS
+#define FX_SPIN (1u << 22)
+#define FX_LB 12  // k-steps per operand load batch (the MFMA order is k_fsi_mul's whatever the batch)
+
+struct FxArgs {
+    const double* C;
+    int ldc, n, np, nt, nwg;
+    int S, m, passes, live;
+    double shift_rel;
+    double* Yb;     // [3][np][64] rotating blocks (handed off)
+    double* Gb;     // [16][256] Gram blocks (handed off)
+    double* part;   // [nwg][32] per-tile q.w (0..15), q.q (16..31) (handed off)
+    u32* flags;     // [nwg][FX_FS] phase published (zeroed per launch)
+    double* Qout;   // [np][64] the final basis
+    double* coef;   // [(S + 2) * 4] recurrence coefficients, as the launch path
+    u32* flag;      // numeric flags (1: pivot, 64: no positive Rayleigh quotient)
+    u32* err;       // 1: a hand-off timed out (zeroed per launch)
+};
+
+__device__ __forceinline__ double fx_ld(const double* p)
+{
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((const u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void fx_st(double* p, double v)
+{
+    __hip_atomic_store((u64*)p, (u64)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// this workgroup's stores are visible: every wave's vmcnt(0), a barrier, the flag
+__device__ __forceinline__ void fx_publish(u32* flags, u32 ph)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&flags[(size_t)blockIdx.x * FX_FS], ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wait until the flags of workgroups base + stride i (i < count) reach ph; false:
+// abort (time-out here or elsewhere), uniformly over the workgroup
+__device__ __forceinline__ bool fx_wait(const u32* flags, u32* err, int base, int stride, int count, u32 ph,
+                                        int* s_abort)
+{
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        u32 spins = 0;
+        bool bad = false;
+        for (;;) {
+            bool mine = true;
+            for (int i = lane; i < count; i += 64)
+                mine &= __hip_atomic_load(&flags[(size_t)(base + stride * i) * FX_FS], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) >= ph;
+            if (__all(mine)) break;
+            ++spins;
+            if (spins > FX_SPIN ||
+                ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                bad = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (bad && lane == 0) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *s_abort = 1;
+        }
+    }
+    __syncthreads();
+    return *s_abort == 0;
+}
+
+// 16 x 16 tile (row tile of Cs, columns 16 cq..) of Cs * B over k in [0, np):
+// B[k][c] = Y[k][c] (mode 0) or s2 W[k][c] - Y[k][c] (mode 1, W = Wm); the 4 waves
+// take contiguous quarters of k (k_fsi_mul's split and batching); wave 0
+// returns the sum, in k_fsi_mul's order
+__device__ __forceinline__ d4 fx_product(const double* Cs, int np, const double* Y, const double* Wm, double s2,
+                                         int cq, double* red)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kr = lane >> 4, cc = lane & 15;
+    const int S = np >> 2, per = (S + 3) >> 2;
+    const int s0 = w * per, s1 = min(S, s0 + per);
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int sb = s0; sb < s1; sb += FX_LB) {
+        double av[FX_LB], bv[FX_LB];
+#pragma unroll
+        for (int u = 0; u < FX_LB; ++u) {
+            const int kk = 4 * min(sb + u, s1 - 1) + kr;
+            av[u] = Cs[kk * 16 + cc];
+            const size_t e = (size_t)kk * SI_B + 16 * cq + cc;
+            bv[u] = Wm ? fma(s2, fx_ld(Wm + e), -fx_ld(Y + e)) : fx_ld(Y + e);
+        }
+#pragma unroll
+        for (int u = 0; u < FX_LB; ++u) {
+            const bool in = sb + u < s1;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? av[u] : 0.0, in ? bv[u] : 0.0, acc, 0, 0, 0);
+        }
+    }
+    d4* rd = (d4*)red;
+    if (w > 0) rd[(w - 1) * 64 + lane] = acc;
+    __syncthreads();
+    if (w == 0) acc = ((acc + rd[lane]) + rd[64 + lane]) + rd[128 + lane];
+    __syncthreads();
+    return acc;
+}
+
+// block (ci, cj) of Y^T Y over rows [0, np) (k_fsi_gram's split and order)
+__device__ __forceinline__ d4 fx_gram(const double* Y, int np, int ci, int cj, double* red)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kr = lane >> 4, cc = lane & 15;
+    const int S = np >> 2, per = (S + 3) >> 2;
+    const int s0 = w * per, s1 = min(S, s0 + per);
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int sb = s0; sb < s1; sb += FX_LB) {
+        double av[FX_LB], bv[FX_LB];
+#pragma unroll
+        for (int u = 0; u < FX_LB; ++u) {
+            const int kk = 4 * min(sb + u, s1 - 1) + kr;
+            av[u] = fx_ld(Y + (size_t)kk * SI_B + 16 * ci + cc);
+            bv[u] = fx_ld(Y + (size_t)kk * SI_B + 16 * cj + cc);
+        }
+#pragma unroll
+        for (int u = 0; u < FX_LB; ++u) {
+            const bool in = sb + u < s1;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? av[u] : 0.0, in ? bv[u] : 0.0, acc, 0, 0, 0);
+        }
+    }
+    d4* rd = (d4*)red;
+    if (w > 0) rd[(w - 1) * 64 + lane] = acc;
+    __syncthreads();
+    if (w == 0) acc = ((acc + rd[lane]) + rd[64 + lane]) + rd[128 + lane];
+    __syncthreads();
+    return acc;
+}
+
+__device__ __forceinline__ size_t fx_elem(int rt, int cq, int r)
+{
+    const int lane = threadIdx.x & 63;
+    return (size_t)(16 * rt + (lane >> 4) + 4 * r) * SI_B + 16 * cq + (lane & 15);
+}
+
+__global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ int s_abort, s_bad;
+    __shared__ double s_b;
+    const int np = a.np, nt = a.nt, nwg = a.nwg;
+    u32* const flags = a.flags;
+    u32* const err = a.err;
+    const int g = blockIdx.x, rt = g >> 2, cq = g & 3;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double* Cs = sm;                        // [np][16]: Cs[k * 16 + i] = C[16 rt + i][k]
+    double* A = Cs + (size_t)16 * np;       // [64][CB_S] Cholesky
+    double* X = A + 64 * CB_S;              // [64][CB_S] L^{-1}; product reduction scratch
+    double* Ri = X + 64 * CB_S;             // [64]
+    const size_t blk = (size_t)np * SI_B;
+    if (tid == 0) {
+        s_abort = 0;
+        s_bad = 0;
+    }
+    for (int e = tid; e < 16 * np; e += 256) {
+        const int k = e >> 4, r = 16 * rt + (e & 15);
+        Cs[e] = (k < a.n && r < a.n) ? a.C[(size_t)k * a.ldc + r] : 0.0;
+    }
+    if (g == 0 && tid < 4) a.coef[tid] = tid == 0 ? 1.0 : 0.0;  // slot 0: the plain product
+    u32 ph = 0;
+    // the start block (k_si_init): this workgroup's tile into slot 0
+    if (wv == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const size_t e = fx_elem(rt, cq, r);
+            const int row = (int)(e / SI_B);
+            unsigned h = (unsigned)e * 2654435761u ^ 0x9e3779b9u;
+            h ^= h >> 13;
+            h *= 0x5bd1e995u;
+            h ^= h >> 15;
+            const double v = (row < min(a.live, a.n)) ? (double)(h & 0xffffff) / 16777216.0 - 0.5 : 0.0;
+            fx_st(a.Yb + e, v);
+        }
+    }
+    fx_publish(flags, ++ph);
+    u32 ph_src = ph;  // the phase that published the current block
+    int slot_src = 0;
+    d4 own = {0.0, 0.0, 0.0, 0.0};  // wave 0: this tile of the current block
+
+    // CholQR passes on the block in slot_src: Gram (workgroups 0..9), redundant
+    // Cholesky + inverse, this tile of Y T into the other slots in turn
+    auto orth = [&](int passes, const int* dst_slots) -> bool {
+        for (int p = 0; p < passes; ++p) {
+            const double* Y = a.Yb + slot_src * blk;
+            ++ph;
+            if (g < 10) {
+                if (!fx_wait(flags, err, 0, 1, nwg, ph_src, &s_abort)) return false;
+                // g -> (ci, cj), ci <= cj: 0..3 (0, j), 4..6 (1, j), 7..8 (2, j), 9 (3, 3)
+                const int ci = g < 4 ? 0 : (g < 7 ? 1 : (g < 9 ? 2 : 3));
+                const int cj = g < 4 ? g : (g < 7 ? g - 3 : (g < 9 ? g - 5 : 3));
+                const d4 acc = fx_gram(Y, np, ci, cj, X);
+                if (wv == 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        fx_st(a.Gb + (size_t)(ci * 4 + cj) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15), acc[r]);
+                }
+                fx_publish(flags, ph);
+            }
+            const u32 ph_g = ph;
+            ++ph;  // the apply's phase (a Gram workgroup's flag already reads ph_g)
+            // every workgroup: G (mirrored), shifted on the first pass, factored
+            if (!fx_wait(flags, err, 0, 1, 10, ph_g, &s_abort)) return false;
+            if (g >= 10 && !fx_wait(flags, err, 4 * rt, 1, 4, ph_src, &s_abort)) return false;  // this row's tiles of Y
+            for (int e = tid; e < 64 * 64; e += 256) {
+                const int i = e >> 6, j = e & 63, bi = i >> 4, bj = j >> 4;
+                const double v = (bi <= bj) ? fx_ld(a.Gb + (size_t)(bi * 4 + bj) * 256 + (i & 15) * 16 + (j & 15))
+                                            : fx_ld(a.Gb + (size_t)(bj * 4 + bi) * 256 + (j & 15) * 16 + (i & 15));
+                A[i * CB_S + j] = v + 0.0;  // (k_fsi_cholinv_blk adds the shift or 0.0 everywhere)
+            }
+            __syncthreads();
+            if (p == 0) {
+                if (wv == 0) {
+                    const double tr = se_wave_sum(A[lane * CB_S + lane]);
+                    if (lane == 0) {
+                        s_b = tr;  // (s_b is free here)
+                        if (!(tr >= 0.0) || !(tr < INFINITY)) s_bad = 1;
+                    }
+                }
+                __syncthreads();
+                const double shift = a.shift_rel * s_b;
+                if (tid < 64) A[tid * CB_S + tid] += shift;
+                __syncthreads();
+            }
+            fsi_cholinv_blk(A, X, Ri, &s_bad);
+            // this tile of Q = Y T (k_fsi_apply): one wave, T[k][j] = X[j][k]
+            const int dst = dst_slots[p];
+            if (wv == 0) {
+                const int kr = lane >> 4, cc = lane & 15, j0 = 16 * cq;
+                const int smax = (j0 + 16) / 4;
+                double av[16], bv[16];
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    av[s] = s < smax ? fx_ld(Y + (size_t)(16 * rt + cc) * SI_B + 4 * s + kr) : 0.0;
+                    bv[s] = X[(j0 + cc) * CB_S + 4 * s + kr];
+                }
+                d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                    if (s < smax) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+                own = acc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) fx_st(a.Yb + dst * blk + fx_elem(rt, cq, r), acc[r]);
+            }
+            if (g == 0 && tid == 0 && s_bad) atomicOr(a.flag, 1u);
+            fx_publish(flags, ph);
+            ph_src = ph;
+            slot_src = dst;
+        }
+        return true;
+    };
+    auto other = [](int x, int y) { return 3 - x - y; };  // the slot that is neither x nor y
+    {
+        const int d1[1] = {1};
+        if (!orth(1, d1)) return;
+    }
+    double b_prev = 0.0;
+    for (int sg = 0; sg < a.S; ++sg) {
+        const int sQ = slot_src;
+        const int sW = (sQ + 1) % 3, s2 = other(sQ, sW);
+        const u32 phQ = ph_src;
+        const d4 q_own = own;
+        // W = C Q (plain) and the tile's q.w, q.q partials
+        ++ph;
+        if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return;
+        // (W overwrites the slot the last CholQR pass but one wrote: the row's other
+        // workgroups must be past their applies, which read it)
+        if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return;
+        d4 w_own = fx_product(Cs, np, a.Yb + sQ * blk, nullptr, 0.0, cq, X);
+        if (wv == 0) {
+            double dp = 0.0, dq = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double v = fma(1.0, w_own[r], fma(0.0, q_own[r], 0.0 * 0.0));
+                w_own[r] = v;
+                fx_st(a.Yb + sW * blk + fx_elem(rt, cq, r), v);
+                dp = fma(q_own[r], v, dp);
+                dq = fma(q_own[r], q_own[r], dq);
+            }
+            dp += __shfl_xor(dp, 16, 64);
+            dp += __shfl_xor(dp, 32, 64);
+            dq += __shfl_xor(dq, 16, 64);
+            dq += __shfl_xor(dq, 32, 64);
+            if (lane < 16) {
+                fx_st(a.part + (size_t)g * 32 + lane, dp);
+                fx_st(a.part + (size_t)g * 32 + 16 + lane, dq);
+            }
+        }
+        fx_publish(flags, ph);
+        const u32 phW = ph;
+        // b (k_fsi_cheb1's sums, in every workgroup), then Y2 = (4/b) C Y1 - 2 Y1 - Q
+        // with Y1 = (2/b) W - Q formed on the fly
+        ++ph;
+        if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return;
+        if (tid < 64) {
+            const int c = tid, gq = c >> 4, cl = c & 15;
+            double s = 0.0, sq = 0.0;
+            for (int t = 0; t < nt; ++t) {
+                s += fx_ld(a.part + (size_t)(4 * t + gq) * 32 + cl);
+                sq += fx_ld(a.part + (size_t)(4 * t + gq) * 32 + 16 + cl);
+            }
+            s = sq > 0.0 ? s / sq : 0.0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) s = fmin(s, __shfl_xor(s, o, 64));
+            if (tid == 0) {
+                double b = fmax(b_prev, s);
+                const bool bad = !(b > 0.0) || !(b < INFINITY);
+                if (bad) b = 1.0;
+                s_b = b;
+                if (g == 0) {
+                    a.coef[4 * (sg + 1) + 0] = 4.0 / b;
+                    a.coef[4 * (sg + 1) + 1] = -2.0;
+                    a.coef[4 * (sg + 1) + 2] = -1.0;
+                    a.coef[4 * (sg + 1) + 3] = b;
+                    if (bad) atomicOr(a.flag, 64u);
+                }
+            }
+        }
+        __syncthreads();
+        const double b = s_b;
+        b_prev = b;
+        const double al = 4.0 / b, s2b = 2.0 / b;
+        d4 y1_own, prev_own, cur_own;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y1_own[r] = fma(s2b, w_own[r], -q_own[r]);
+        // Y2: operand (2/b) W - Q from slots sW, sQ; epilogue on Y1 (x) and Q (z)
+        {
+            const d4 acc = fx_product(Cs, np, a.Yb + sQ * blk, a.Yb + sW * blk, s2b, cq, X);
+            if (wv == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double v = fma(al, acc[r], fma(-2.0, y1_own[r], -1.0 * q_own[r]));
+                    cur_own[r] = v;
+                    fx_st(a.Yb + s2 * blk + fx_elem(rt, cq, r), v);
+                }
+            }
+            prev_own = y1_own;
+            fx_publish(flags, ph);
+        }
+        int s_cur = s2, s_free = sW;  // W and Q are dead once every tile of Y2 is out
+        for (int t = 3; t <= a.m; ++t) {
+            const u32 ph_in = ph;
+            ++ph;
+            if (!fx_wait(flags, err, cq, 4, nt, ph_in, &s_abort)) return;
+            const d4 acc = fx_product(Cs, np, a.Yb + s_cur * blk, nullptr, 0.0, cq, X);
+            d4 nxt;
+            if (wv == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    nxt[r] = fma(al, acc[r], fma(-2.0, cur_own[r], -1.0 * prev_own[r]));
+                    fx_st(a.Yb + s_free * blk + fx_elem(rt, cq, r), nxt[r]);
+                }
+            }
+            prev_own = cur_own;
+            cur_own = nxt;
+            const int sx = s_cur;
+            s_cur = s_free;
+            s_free = (sx == sQ) ? other(s_cur, sQ) : sx;
+            fx_publish(flags, ph);
+        }
+        own = cur_own;
+        ph_src = ph;
+        slot_src = s_cur;
+        // orthonormalise into the two other slots in turn
+        const int pz = (sg + 1 < a.S) ? a.passes : 3;
+        const int o1 = (s_cur + 1) % 3, o2 = (s_cur + 2) % 3;
+        const int ds[3] = {o1, s_cur, o1};
+        (void)o2;
+        if (!orth(pz, ds)) return;
+    }
+    // the final basis for the Rayleigh-Ritz launches
+    if (wv == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.Qout[fx_elem(rt, cq, r)] = own[r];
+    }
+}
+
 static int fsi_env(const char* name, int dflt)
 {
     const char* e = getenv(name);
@@ -804,12 +1214,27 @@ extern "C" size_t scc_fsi_scratch_doubles(int n)
     const size_t np = si_npad(n), nt = np / 16, nblk = (np + 255) / 256;
     const int S = fsi_segments();
     return 4 * np * SI_B + 2 * (size_t)SI_B * SI_B + 2 * nt * SI_B + (size_t)(S + 2) * 4 + SI_B * 16 + 16 + 16 +
-           3 * nblk * 16 + 64 + 2 * np + 2 * nt * SGF_W + 64;
+           3 * nblk * 16 + 64 + 2 * np + 2 * nt * SGF_W + 64 + 64 * nt + 64;
+}
+
+// the persistent engine for n <= FX_NPMAX (SCC_EIG_FSI_ENGINE=0: the launch per step)
+static bool fx_usable(int n)
+{
+    return fsi_env("SCC_EIG_FSI_ENGINE", 1) != 0 && (int)si_npad(n) <= FX_NPMAX;
+}
+static size_t fx_lds_bytes(int np) { return sizeof(double) * ((size_t)16 * np + 2 * 64 * CB_S + 64); }
+static void fx_prepare()
+{
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void*)k_fsi_engine, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)fx_lds_bytes(FX_NPMAX));
+    });
 }
 
 namespace {
 struct FsiGraphEntry {
-    int dev, n, ldc, k, S, m, passes, live, guard;
+    int dev, n, ldc, k, S, m, passes, live, guard, engine;
     const void *C, *scr, *Z, *W;
     hipGraphExec_t exec;
 };
@@ -828,8 +1253,9 @@ hipStream_t fsi_capture_stream(int dev)
 }
 }  // namespace
 
-// Same contract as scc_eigen_si: *ok = 1 when the filtered result passed every
-// test (Z, W written), 0: run the direct solver.  Synchronises st.
+// Same contract as scc_eigen_si: *ok != 0 when the filtered result passed every
+// test (Z, W written; 2: the persistent engine ran the filter loop, 1: a launch
+// per step), 0: run the direct solver.  Synchronises st.
 extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
                                     int* ok, hipStream_t st)
 {
@@ -855,14 +1281,79 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     double* gu = (double*)(flag + 128);
     double* gy = gu + np;
     double* gpart = gy + np;  // [2][nt][SGF_W] guard partials
+    u32* fxflags = (u32*)(gpart + 2 * nt * SGF_W);  // [4 nt][FX_FS] the engine's phase flags
+    u32* fxerr = flag + 64;
     const int live = std::max(SI_B, std::min(n, fsi_env("SCC_EIG_SI_INIT_ROWS", n)));
     const int guard = n <= SI_GUARD_NMAX;
     const double shift_rel = 11.0 * ((double)np * SI_B + (double)SI_B * (SI_B + 1)) * 1.1102230246251565e-16;
     scc_small_syev_prepare();  // kernel attributes, outside any capture
+    fx_prepare();
     const dim3 gt((unsigned)nt, SI_B / 16), gg(SI_B / 16, SI_B / 16);
+    int use_engine = fx_usable(n) ? 1 : 0;
+    auto rayleigh_ritz = [&](hipStream_t s) -> hipError_t {
+        hipError_t e;
+        // Rayleigh-Ritz on span(Q): W = C Q (Ya), H = Q^T W, its top-k eigenpairs
+        hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, Q, (const double*)nullptr, coef, Ya,
+                           (double*)nullptr);
+        hipLaunchKernelGGL(k_fsi_gram, gg, dim3(256), 0, s, Q, Ya, (int)np, G);
+        if ((e = scc_launch_small_syev(G, SI_B, SI_B, k, Yv, theta, flag, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_si_ritz, dim3(nblk), dim3(256), 0, s, Q, Ya, Yv, theta, n, k, Z, rpart, mpart);
+        hipLaunchKernelGGL(k_si_check, dim3(1), dim3(64), 0, s, rpart, mpart, nblk, theta, k, FSI_TOL, sgn, Wout,
+                           flag);
+        hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, s, Z, sgn, n);
+        hipLaunchKernelGGL(k_fsi_bound_check, dim3(1), dim3(64), 0, s, coef + 4 * S, theta, k, flag);
+        if (guard) {
+            // x0 = g (partials V^T g), x1 = P g, then SI_GUARD_IT products of P C P
+            const int gt2 = (n + 15) / 16;
+            double* pa = gpart;
+            double* pb = gpart + (size_t)gt2 * SGF_W;
+            double* xa = gu;
+            double* xb = gy;
+            hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)nullptr,
+                               (const double*)nullptr, gt2, xa, pa, theta, k, flag, 0);
+            hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)xa, pa, gt2,
+                               xb, pb, theta, k, flag, 1);
+            for (int it = 0; it < SI_GUARD_IT; ++it) {
+                std::swap(xa, xb);
+                std::swap(pa, pb);
+                hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)xa, pa,
+                                   gt2, xb, pb, theta, k, flag, 2);
+            }
+            hipLaunchKernelGGL(k_sig_fused, dim3(1), dim3(64), 0, s, C, ldc, n, Q, Ya, (const double*)xb, pb, gt2,
+                               xa, pa, theta, k, flag, 3);
+        }
+        return hipGetLastError();
+    };
     auto enqueue = [&](hipStream_t s) -> hipError_t {
         hipError_t e;
         if ((e = hipMemsetAsync(flag, 0, sizeof(u32) * 4, s)) != hipSuccess) return e;
+        if (use_engine) {
+            // the filter loop in one persistent launch, then the Rayleigh-Ritz launches
+            if ((e = hipMemsetAsync(fxflags, 0, sizeof(u32) * FX_FS * 4 * nt, s)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(fxerr, 0, sizeof(u32), s)) != hipSuccess) return e;
+            FxArgs fa;
+            fa.C = C;
+            fa.ldc = ldc;
+            fa.n = n;
+            fa.np = (int)np;
+            fa.nt = (int)nt;
+            fa.nwg = 4 * (int)nt;
+            fa.S = S;
+            fa.m = m;
+            fa.passes = passes;
+            fa.live = live;
+            fa.shift_rel = shift_rel;
+            fa.Yb = Ya;
+            fa.Gb = G;
+            fa.part = dpart;
+            fa.flags = fxflags;
+            fa.Qout = Q;
+            fa.coef = coef;
+            fa.flag = flag;
+            fa.err = fxerr;
+            hipLaunchKernelGGL(k_fsi_engine, dim3(4 * (unsigned)nt), dim3(256), fx_lds_bytes((int)np), s, fa);
+            return rayleigh_ritz(s);
+        }
         hipLaunchKernelGGL(k_fsi_coef0, dim3(1), dim3(64), 0, s, coef);  // slot 0: plain product {1, 0, 0, b = 0}
         hipLaunchKernelGGL(k_si_init, dim3((unsigned)((np * SI_B + 255) / 256)), dim3(256), 0, s, (int)np,
                            std::min(live, n), Ya);
@@ -898,37 +1389,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             double* tmp = (prev != Q) ? prev : nxt;
             if ((e = orth(cur, tmp, Q, sg + 1 < S ? passes : 3)) != hipSuccess) return e;
         }
-        // Rayleigh-Ritz on span(Q): W = C Q (Ya), H = Q^T W, its top-k eigenpairs
-        hipLaunchKernelGGL(k_fsi_mul, gt, dim3(256), 0, s, C, ldc, n, (int)np, Q, (const double*)nullptr, coef, Ya,
-                           (double*)nullptr);
-        hipLaunchKernelGGL(k_fsi_gram, gg, dim3(256), 0, s, Q, Ya, (int)np, G);
-        if ((e = scc_launch_small_syev(G, SI_B, SI_B, k, Yv, theta, flag, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_si_ritz, dim3(nblk), dim3(256), 0, s, Q, Ya, Yv, theta, n, k, Z, rpart, mpart);
-        hipLaunchKernelGGL(k_si_check, dim3(1), dim3(64), 0, s, rpart, mpart, nblk, theta, k, FSI_TOL, sgn, Wout,
-                           flag);
-        hipLaunchKernelGGL(k_si_sign, dim3((n * 16 + 255) / 256), dim3(256), 0, s, Z, sgn, n);
-        hipLaunchKernelGGL(k_fsi_bound_check, dim3(1), dim3(64), 0, s, coef + 4 * S, theta, k, flag);
-        if (guard) {
-            // x0 = g (partials V^T g), x1 = P g, then SI_GUARD_IT products of P C P
-            const int gt2 = (n + 15) / 16;
-            double* pa = gpart;
-            double* pb = gpart + (size_t)gt2 * SGF_W;
-            double* xa = gu;
-            double* xb = gy;
-            hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)nullptr,
-                               (const double*)nullptr, gt2, xa, pa, theta, k, flag, 0);
-            hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)xa, pa, gt2,
-                               xb, pb, theta, k, flag, 1);
-            for (int it = 0; it < SI_GUARD_IT; ++it) {
-                std::swap(xa, xb);
-                std::swap(pa, pb);
-                hipLaunchKernelGGL(k_sig_fused, dim3(gt2), dim3(256), 0, s, C, ldc, n, Q, Ya, (const double*)xa, pa,
-                                   gt2, xb, pb, theta, k, flag, 2);
-            }
-            hipLaunchKernelGGL(k_sig_fused, dim3(1), dim3(64), 0, s, C, ldc, n, Q, Ya, (const double*)xb, pb, gt2,
-                               xa, pa, theta, k, flag, 3);
-        }
-        return hipGetLastError();
+        return rayleigh_ritz(s);
     };
     hipError_t e = hipSuccess;
     int dev = 0;
@@ -939,8 +1400,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         hipGraphExec_t ex = nullptr;
         for (const auto& g : g_fsi_graphs)
             if (g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m && g.passes == passes &&
-                g.live == live &&
-                g.guard == guard && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
+                g.live == live && g.guard == guard && g.engine == use_engine && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
                 ex = g.exec;
                 break;
             }
@@ -956,7 +1416,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
                         hipGraphExecDestroy(g_fsi_graphs.front().exec);
                         g_fsi_graphs.erase(g_fsi_graphs.begin());
                     }
-                    g_fsi_graphs.push_back({dev, n, ldc, k, S, m, passes, live, guard, C, scr, Z, Wout, ex});
+                    g_fsi_graphs.push_back({dev, n, ldc, k, S, m, passes, live, guard, use_engine, C, scr, Z, Wout, ex});
                 } else {
                     ex = nullptr;
                 }
@@ -970,9 +1430,21 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         }
     }
     if (!launched && (e = enqueue(st)) != hipSuccess) return e;
-    u32 h = 0;
+    u32 h = 0, herr = 0;
     if ((e = hipMemcpyAsync(&h, flag, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if (use_engine && (e = hipMemcpyAsync(&herr, fxerr, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (herr) {
+        // a hand-off of the persistent engine timed out (the device was shared and
+        // its workgroups were not co-resident): the same solve, a launch per step
+        if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc fsi] engine hand-off timed out: launch path\n");
+        use_engine = 0;
+        launched = false;
+        if ((e = enqueue(st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(&h, flag, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    }
     if (getenv("SCC_EIG_SI_LOG")) {
         double lg[16] = {0}, cf[4] = {0}, th[16] = {0};
         if (hipMemcpy(lg, flag + 8, sizeof(double) * 16, hipMemcpyDeviceToHost) == hipSuccess &&
@@ -980,11 +1452,11 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             hipMemcpy(th, theta, sizeof(double) * 16, hipMemcpyDeviceToHost) == hipSuccess) {
             double rmax = 0.0;
             for (int q = 0; q < k; ++q) rmax = std::max(rmax, lg[q]);
-            fprintf(stderr, "[scc fsi] n=%d seg=%d deg=%d flag=%u maxres=%.3g b=%.6g theta_k=%.6g graph=%d\n", n, S, m,
-                    h, rmax, cf[3], th[k - 1], launched ? 1 : 0);
+            fprintf(stderr, "[scc fsi] n=%d seg=%d deg=%d flag=%u maxres=%.3g b=%.6g theta_k=%.6g graph=%d engine=%d\n",
+                    n, S, m, h, rmax, cf[3], th[k - 1], launched ? 1 : 0, use_engine);
         }
     }
-    *ok = (h == 0) ? 1 : 0;
+    *ok = (h == 0) ? (use_engine ? 2 : 1) : 0;  // 2: accepted, the engine ran the filter loop
     return hipSuccess;
 }
 

@@ -41,10 +41,15 @@ def cholqr(Y, passes, shift_rel):
 
 def main():
     arg = sys.argv[1] if len(sys.argv) > 1 else "B"
-    Xu = np.load(arg) if arg.endswith(".npy") else union_matrix(arg)
+    if arg.endswith(".npy"):
+        Xu = np.load(arg)
+    else:
+        Xu = union_matrix(arg)
+        if os.environ.get("SAVE"):
+            np.save(os.environ["SAVE"], Xu)
     Xc = Xu - Xu.mean(0)
     C = Xc.T @ Xc
-    n, p, k = C.shape[0], 64, 15
+    n, p, k = C.shape[0], int(os.environ.get("P", 64)), 15
     S = int(os.environ.get("SEG", 5))
     m = int(os.environ.get("DEG", 8))
     passes = int(os.environ.get("PASSES", 2))
