@@ -6,8 +6,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
 mkdir -p gpurun_out
 step() {  # step <name> <timeout_s> <cmd...>
   local name=$1 t=$2; shift 2
-  echo "=== $name" ; timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  echo "=== $name"
+  # a heartbeat line a minute, so a long single test is not taken for a hang
+  ( while sleep 60; do echo "[$name] $(date +%T) running"; done ) & local hb=$!
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
   echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
   return 0

@@ -20,424 +20,18 @@
 #include "scc.h"
 #include <mutex>
 
-#define SE_N 64
-#define SE_T 256
-#define SE_MAXK 16
-
-static constexpr double kSeEps = 2.220446049250313e-16;
-
-__device__ inline double se_wave_min(double v)
-{
-    v = fmin(v, scc_xor_lane_f64<32>(v));
-    v = fmin(v, scc_xor_lane_f64<16>(v));
-    v = fmin(v, scc_xor_lane_f64<8>(v));
-    v = fmin(v, scc_xor_lane_f64<4>(v));
-    v = fmin(v, scc_xor_lane_f64<2>(v));
-    return fmin(v, scc_xor_lane_f64<1>(v));
-}
-__device__ inline double se_wave_max(double v)
-{
-    v = fmax(v, scc_xor_lane_f64<32>(v));
-    v = fmax(v, scc_xor_lane_f64<16>(v));
-    v = fmax(v, scc_xor_lane_f64<8>(v));
-    v = fmax(v, scc_xor_lane_f64<4>(v));
-    v = fmax(v, scc_xor_lane_f64<2>(v));
-    return fmax(v, scc_xor_lane_f64<1>(v));
-}
-// number of eigenvalues of the 64 x 64 tridiagonal T (d, e^2) below x: signs
-// of the leading principal minors p_i = (d_i - x) p_{i-1} - e_{i-1}^2 p_{i-2}
-// (one FMA on the dependent chain, no division), a zero pivot counted negative
-// (LAPACK dstebz's -pivmin), the pair rescaled by a power of two every 8
-// steps.  Fixed length: the loop unrolls completely and its LDS loads are
-// issued ahead of the chain (a bound check per step made every step wait on
-// its load, ~190 cycles a step).
-__device__ __forceinline__ int se_count64(const double* dg, const double* e2, double x, double pivmin)
-{
-    double pp = 1.0, pc = dg[0] - x;
-    if (pc == 0.0) pc = -pivmin;
-    int neg = pc < 0.0;
-#pragma unroll
-    for (int i0 = 1; i0 < SE_N; i0 += 9) {
-        double dv[9], ev[9];
-#pragma unroll
-        for (int u = 0; u < 9; ++u) {
-            dv[u] = dg[min(i0 + u, SE_N - 1)];
-            ev[u] = e2[min(i0 + u, SE_N - 1) - 1];
-        }
-#pragma unroll
-        for (int u = 0; u < 9; ++u) {
-            if (i0 + u >= SE_N) break;  // compile-time
-            double pn = fma(dv[u] - x, pc, -ev[u] * pp);
-            pn = (pn == 0.0) ? -pivmin * pc : pn;
-            neg += (pn < 0.0) != (pc < 0.0);
-            pp = pc;
-            pc = pn;
-        }
-        const int ex = ilogb(pc);
-        if (ex > 256 || ex < -256) {
-            pc = ldexp(pc, -ex);
-            pp = ldexp(pp, -ex);
-        }
-    }
-    return neg;
-}
-
 // phase stamps of the last k_small_syev (s_memtime at the start of each phase;
 // diagnostic, read by scc_diag_small_syev_stamps)
 __device__ u64 g_se_stamps[8];
 
-// dynamic LDS of k_small_syev (doubles)
-#define SE_LUS (5 * SE_N + 2)                   // per-eigenpair LU stride (padded: lanes on distinct banks)
-#define SE_YS (SE_N + 2)                        // tridiagonal eigenvector stride (padded likewise)
-#define SE_LDS_V 0                              // [64][64] reflector i in row i
-#define SE_LDS_LU (SE_LDS_V + SE_N * SE_N)      // [16][SE_LUS] LU factors per eigenpair
-#define SE_LDS_Y (SE_LDS_LU + SE_MAXK * SE_LUS) // [16][SE_YS] tridiagonal eigenvectors
-#define SE_LDS_TOTAL (SE_LDS_Y + SE_MAXK * SE_YS)
-
 extern "C" size_t scc_small_syev_lds_bytes() { return sizeof(double) * SE_LDS_TOTAL; }
 
-// H: n x n (ldh, n <= 64), symmetrised on load; k <= min(16, n) wanted.
-// Y[r * 16 + q]: the q-th largest eigenvector (q < k; columns k..15 zero),
-// theta[q] its Rayleigh quotient.  The matrix is always reduced as 64 x 64:
-// rows and columns >= n become a decoupled diagonal block at a value below
-// every eigenvalue (-(max row sum) - 1), so the top k are those of H and every
-// loop has a compile-time length.  The matrix lives in registers, thread (r,
-// q) holding row r, columns q + 4u.  flag |= 16 when a value is not finite or
-// a cluster's vectors are dependent.
 __global__ void __launch_bounds__(SE_T) k_small_syev(const double* __restrict__ H, int n, int ldh, int k,
                                                     double* __restrict__ Y, double* __restrict__ theta,
                                                     u32* __restrict__ flag)
 {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double(*Vr)[SE_N] = (double(*)[SE_N])(sm + SE_LDS_V);
-    double* LU = sm + SE_LDS_LU;
-    double(*Yt)[SE_YS] = (double(*)[SE_YS])(sm + SE_LDS_Y);
-    __shared__ double dg[SE_N], eo[SE_N], e2[SE_N], ta[SE_N], pv[SE_N], vc[SE_N], colv[SE_N], rsum[SE_N];
-    __shared__ double th[SE_MAXK], blo[SE_MAXK], bhi[SE_MAXK], gsc[4];
-    __shared__ int cnt[SE_T];
-    __shared__ int s_bad;
-    const int tid = threadIdx.x, lane = tid & 63, wv = scc_wave_id();
-    const int r = tid >> 2, q = tid & 3;  // this thread: row r, columns q + 4u
-    if (tid == 0) s_bad = 0;
-    double a[16];
-    {
-        const int rc = min(r, n - 1);
-        double h1[16], h2[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int cc = min(q + 4 * u, n - 1);
-            h1[u] = H[(size_t)rc * ldh + cc];
-            h2[u] = H[(size_t)cc * ldh + rc];
-        }
-        double as = 0.0;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const bool in = r < n && q + 4 * u < n;
-            a[u] = in ? 0.5 * (h1[u] + h2[u]) : 0.0;
-            as += fabs(a[u]);
-        }
-        as += scc_xor_lane_f64<1>(as);
-        as += scc_xor_lane_f64<2>(as);
-        if (q == 0) rsum[r] = as;
-    }
-    __syncthreads();
-    {
-        const double pad = -se_wave_max(rsum[lane]) - 1.0;  // below every eigenvalue of H
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-            if (r >= n && r == q + 4 * u) a[u] = pad;
-    }
-    if (tid == 0) g_se_stamps[0] = __builtin_amdgcn_s_memtime();
-    // ---- tridiagonalisation (LAPACK dsytd2 order), column i: its owners write
-    // it to LDS, wave 0 forms the reflector, p = tau A22 v (4 threads per row),
-    // w = p - (tau/2)(p.v) v, A22 -= v w^T + w v^T in registers
-#pragma unroll
-    for (int i = 0; i < SE_N - 2; ++i) {
-        constexpr int dummy = 0;
-        (void)dummy;
-        const int ui = i >> 2, qi = i & 3;
-        if (q == qi) {
-            if (r > i) colv[r] = a[ui];
-            if (r == i) dg[i] = a[ui];
-        }
-        __syncthreads();
-        if (wv == 0) {
-            const int rr = i + 1 + lane;
-            const double x = colv[min(rr, SE_N - 1)];
-            const double alpha = colv[i + 1];
-            const double sq = se_wave_sum((rr >= i + 2 && rr < SE_N) ? x * x : 0.0);
-            double beta = alpha, t = 0.0, scal = 0.0;
-            if (sq > 0.0) {
-                beta = -copysign(sqrt(alpha * alpha + sq), alpha);
-                t = (beta - alpha) / beta;
-                scal = 1.0 / (alpha - beta);
-            }
-            if (rr < SE_N) {
-                const double v = (rr == i + 1) ? 1.0 : x * scal;
-                vc[rr] = v;
-                Vr[i][rr] = v;
-            }
-            if (lane == 0) {
-                eo[i] = beta;
-                ta[i] = t;
-            }
-        }
-        __syncthreads();
-        const double t = ta[i];
-        double vv[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const double v = vc[q + 4 * u];
-            vv[u] = (q + 4 * u > i) ? v : 0.0;
-        }
-        double part = 0.0;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) part = fma(a[u], vv[u], part);
-        part += scc_xor_lane_f64<1>(part);
-        part += scc_xor_lane_f64<2>(part);
-        if (q == 0 && r > i) pv[r] = t * part;
-        __syncthreads();
-        const int rr = i + 1 + lane;
-        const double K = -0.5 * t * se_wave_sum(rr < SE_N ? pv[min(rr, SE_N - 1)] * vc[min(rr, SE_N - 1)] : 0.0);
-        const double vr = (r > i) ? vc[r] : 0.0;
-        const double wr = (r > i) ? fma(K, vr, pv[r]) : 0.0;
-        double pw[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) pw[u] = pv[q + 4 * u];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const double wc = (q + 4 * u > i) ? fma(K, vv[u], pw[u]) : 0.0;
-            a[u] = fma(-vr, wc, fma(-wr, vv[u], a[u]));
-        }
-    }
-    if (q == 2 && r == SE_N - 2) dg[SE_N - 2] = a[15];
-    if (q == 2 && r == SE_N - 1) eo[SE_N - 2] = a[15];
-    if (q == 3 && r == SE_N - 1) dg[SE_N - 1] = a[15];
-    if (tid == 0) {
-        eo[SE_N - 1] = 0.0;
-        ta[SE_N - 2] = 0.0;
-        ta[SE_N - 1] = 0.0;
-    }
-    __syncthreads();
-    if (tid == 0) g_se_stamps[1] = __builtin_amdgcn_s_memtime();
-    // ---- Gershgorin bounds, pivmin (LAPACK dstebz)
-    if (wv == 0) {
-        const int i = lane;
-        const double ei = eo[i], dgi = dg[i];
-        e2[i] = ei * ei;
-        const double rad = (i > 0 ? fabs(eo[max(i - 1, 0)]) : 0.0) + fabs(ei);
-        const double gl = se_wave_min(dgi - rad);
-        const double gu = se_wave_max(dgi + rad);
-        const double em = se_wave_max(ei * ei);
-        if (lane == 0) {
-            gsc[0] = gl;
-            gsc[1] = gu;
-            gsc[2] = em;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) g_se_stamps[2] = __builtin_amdgcn_s_memtime();
-    const double tnorm = fmax(fabs(gsc[0]), fabs(gsc[1]));
-    const double pivmin = fmax(2.2250738585072014e-308 * fmax(1.0, gsc[2]), 1e-300);
-    const double glo = gsc[0] - 2.0 * tnorm * kSeEps * SE_N - 1e-300;
-    const double ghi = gsc[1] + 2.0 * tnorm * kSeEps * SE_N + 1e-300;
-    // ---- eigenvalues: one shared round of 256 points, then 16 points per
-    // wanted eigenvalue per round until the bracket is below
-    // max(1e-12 |lambda|, 2 eps ||T||) (inverse iteration's need; the value
-    // returned is the Rayleigh quotient)
-    {
-        const double x = glo + (ghi - glo) * (double)(tid + 1) / (double)(SE_T + 1);
-        cnt[tid] = se_count64(dg, e2, x, pivmin);
-    }
-    __syncthreads();
-    const int qg = tid >> 4, jg = tid & 15;
-    const int idx = SE_N - 1 - qg;  // ascending index of the qg-th largest (the pad block is lowest)
-    const bool want = qg < k;
-    if (want && jg == 0) {
-        int lo = 0, hi = SE_T;  // first point with cnt > idx (cnt is nondecreasing in the point)
-        while (lo < hi) {
-            const int m = (lo + hi) >> 1;
-            if (cnt[m] > idx)
-                hi = m;
-            else
-                lo = m + 1;
-        }
-        blo[qg] = (lo == 0) ? glo : glo + (ghi - glo) * (double)lo / (double)(SE_T + 1);
-        bhi[qg] = (lo == SE_T) ? ghi : glo + (ghi - glo) * (double)(lo + 1) / (double)(SE_T + 1);
-    }
-    __syncthreads();
-    bool done = !want;
-    for (int it = 0; it < 24; ++it) {
-        if (!__syncthreads_or(!done)) break;
-        const double lo = want ? blo[qg] : 0.0, hi = want ? bhi[qg] : 0.0;
-        if (!done) {
-            const double x = lo + (hi - lo) * (double)(jg + 1) / 17.0;
-            const int c = se_count64(dg, e2, x, pivmin);
-            const u64 m = __ballot(c > idx);
-            const u32 bits = (u32)(m >> (16 * ((tid >> 4) & 3))) & 0xffffu;
-            const int js = bits ? __builtin_ctz(bits) : 16;
-            const double nlo = (js == 0) ? lo : lo + (hi - lo) * (double)js / 17.0;
-            const double nhi = (js == 16) ? hi : lo + (hi - lo) * (double)(js + 1) / 17.0;
-            if (jg == 0) {
-                blo[qg] = nlo;
-                bhi[qg] = nhi;
-            }
-            if (nhi - nlo <= fmax(1e-12 * fmax(fabs(nlo), fabs(nhi)), 2.0 * kSeEps * tnorm) + pivmin ||
-                (nlo == lo && nhi == hi))
-                done = true;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) g_se_stamps[3] = __builtin_amdgcn_s_memtime();
-    // ---- inverse iteration: eigenpair q on lane q of wave 0 (LU with partial
-    // pivoting of T - lambda I, two solves from a pseudo-random start)
-    if (wv == 0 && lane < k) {
-        const int qq = lane;
-        const double lam = 0.5 * (blo[qq] + bhi[qq]);
-        double* fdr = LU + (size_t)qq * SE_LUS;  // 1 / U diagonal
-        double* fu = fdr + SE_N;
-        double* fu2 = fu + SE_N;
-        double* fl = fu2 + SE_N;
-        double* fp = fl + SE_N;
-        double* y = Yt[qq];
-        const double tiny = kSeEps * tnorm + 1e-300;
-        double dcur = dg[0] - lam, ucur = eo[0];
-#pragma unroll
-        for (int i = 0; i < SE_N - 1; ++i) {
-            const double li = eo[i], dn = dg[i + 1] - lam, un = (i < SE_N - 2) ? eo[i + 1] : 0.0;
-            const bool piv = fabs(dcur) < fabs(li);
-            const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
-            const double den = piv ? li : dc;
-            // (piv ? dc : li) / den through a refined hardware reciprocal (a few ulp)
-            const double r0 = __builtin_amdgcn_rcp(den);
-            const double rd = fma(fma(-den, r0, 1.0), r0, r0);
-            const double f = (piv ? dc : li) * rd;
-            fl[i] = f;
-            fdr[i] = rd;
-            const double ua = piv ? dn : ucur, ub = piv ? ucur : dn;
-            fu[i] = ua;
-            fu2[i] = piv ? un : 0.0;
-            fp[i] = piv ? 1.0 : 0.0;
-            dcur = fma(-f, ua, ub);
-            ucur = piv ? -f * un : un;
-        }
-        if (dcur == 0.0) dcur = tiny;
-        fdr[SE_N - 1] = 1.0 / dcur;
-        fu[SE_N - 1] = 0.0;
-        fu2[SE_N - 1] = 0.0;
-        // the iterate in LDS (this lane's row of Yt); fixed-length unrolled loops
-        // let the compiler issue the loads ahead of each dependent chain
-#pragma unroll
-        for (int i = 0; i < SE_N; ++i) {
-            unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)qq * 40503u + 12345u);
-            h ^= h >> 13;
-            h *= 0x5bd1e995u;
-            h ^= h >> 15;
-            y[i] = 0.5 + (double)(h & 0xffff) / 65536.0;
-        }
-        for (int iter = 0; iter < 2; ++iter) {
-            double bi = y[0];  // y <- L^-1 P y
-#pragma unroll
-            for (int i = 0; i < SE_N - 1; ++i) {
-                const bool piv = fp[i] != 0.0;
-                const double bn = y[i + 1];
-                const double xa = piv ? bn : bi, xb = piv ? bi : bn;
-                y[i] = xa;
-                bi = fma(-fl[i], xa, xb);
-            }
-            y[SE_N - 1] = bi;
-            double z1 = 0.0, z2 = 0.0;  // y <- U^-1 y from the bottom
-#pragma unroll
-            for (int i = SE_N - 1; i >= 0; --i) {
-                const double z0 = fma(-fu[i], z2, fma(-fu2[i], z1, y[i])) * fdr[i];
-                y[i] = z0;
-                z1 = z2;
-                z2 = z0;
-            }
-            double mx = 0.0, sacc = 0.0;
-#pragma unroll
-            for (int i = 0; i < SE_N; ++i) mx = fmax(mx, fabs(y[i]));
-            const double sc = (mx > 0.0 && mx < INFINITY) ? 1.0 / mx : 1.0;
-#pragma unroll
-            for (int i = 0; i < SE_N; ++i) sacc = fma(y[i] * sc, y[i] * sc, sacc);
-            const double inv = sc / sqrt(sacc);
-#pragma unroll
-            for (int i = 0; i < SE_N; ++i) y[i] *= inv;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) g_se_stamps[4] = __builtin_amdgcn_s_memtime();
-    // ---- Gram-Schmidt inside clusters (|lambda_p - lambda_q| <= 1e-3 ||T||,
-    // LAPACK dstein), in order, then the Rayleigh quotients y^T T y (wave 0,
-    // lane = entry)
-    if (wv == 0) {
-        const int i = lane;
-        const double di = dg[i], ei = eo[i], em = eo[max(i - 1, 0)];
-        for (int qq = 0; qq < k; ++qq) {
-            double yq = Yt[qq][i];
-            const double lq = 0.5 * (blo[qq] + bhi[qq]);
-            bool touched = false;
-            for (int p = 0; p < qq; ++p) {
-                const double lp = 0.5 * (blo[p] + bhi[p]);
-                if (fabs(lp - lq) > 1e-3 * tnorm) continue;
-                const double yp = Yt[p][i];
-                const double d = se_wave_sum(yp * yq);
-                yq = fma(-d, yp, yq);
-                touched = true;
-            }
-            if (touched) {
-                const double s2 = se_wave_sum(yq * yq);
-                if (!(s2 > 1e-6)) s_bad = 1;  // the cluster's vectors were (nearly) dependent
-                yq *= 1.0 / sqrt(s2);
-                Yt[qq][i] = yq;
-            }
-            const double yu = Yt[qq][min(i + 1, SE_N - 1)], yd = Yt[qq][max(i - 1, 0)];
-            const double tv = yq * di + (i + 1 < SE_N ? ei * yu : 0.0) + (i > 0 ? em * yd : 0.0);
-            const double rq = se_wave_sum(yq * tv);
-            if (lane == 0) th[qq] = rq;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) g_se_stamps[5] = __builtin_amdgcn_s_memtime();
-    // ---- back-transformation y <- H_0 ... H_{61} y: group qg (16 lanes) holds
-    // eigenvector qg, entries r = jg + 16 u in registers
-    double yv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) yv[u] = want ? Yt[qg][jg + 16 * u] : 0.0;
-#pragma unroll
-    for (int i = SE_N - 3; i >= 0; --i) {
-        double vv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int rr = jg + 16 * u;
-            const double v = Vr[i][rr];
-            vv[u] = (rr > i) ? v : 0.0;
-        }
-        const double ti = ta[i];
-        double d = 0.0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) d = fma(vv[u], yv[u], d);
-        d += scc_xor_lane_f64<1>(d);
-        d += scc_xor_lane_f64<2>(d);
-        d += scc_xor_lane_f64<4>(d);
-        d += scc_xor_lane_f64<8>(d);
-        const double td = ti * d;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) yv[u] = fma(-td, vv[u], yv[u]);
-    }
-    bool bad = false;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int rr = jg + 16 * u;
-        if (rr < n) Y[(size_t)rr * 16 + qg] = want ? yv[u] : 0.0;
-        bad |= !(fabs(yv[u]) < INFINITY);
-    }
-    if (want && jg == 0) {
-        theta[qg] = th[qg];
-        bad |= !(fabs(th[qg]) < INFINITY);
-    }
-    if ((bad || (tid == 0 && s_bad)) && flag) atomicOr(flag, 16u);
-    if (tid == 0) g_se_stamps[6] = __builtin_amdgcn_s_memtime();
+    se_syev<false>([=](int i, int j) { return H[(size_t)i * ldh + j]; }, n, k, Y, theta, flag, sm, g_se_stamps);
 }
 
 // the dynamic-LDS attribute, set once per process before any launch or capture

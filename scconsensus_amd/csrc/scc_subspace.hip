@@ -820,19 +820,21 @@ struct FxArgs {
     u32* flags;     // [nwg][FX_FS] phase published (zeroed per launch)
     double* Qout;   // [np][64] the final basis
     double* coef;   // [(S + 2) * 4] recurrence coefficients, as the launch path
-    u32* flag;      // numeric flags (1: pivot, 64: no positive Rayleigh quotient)
+    u32* flag;      // numeric flags (1: pivot, 64: no positive Rayleigh quotient; the
+                    // Rayleigh-Ritz bits 2, 4, 8, 16, 32 as the launch path)
     u32* err;       // 1: a hand-off timed out (zeroed per launch)
+    // Rayleigh-Ritz, the Ritz test and the guard (rr = 1; 0: the launches do them)
+    int rr, k, guard;
+    double tol;
+    double* Yv;     // [64][16] Ritz coefficients (handed off)
+    double* theta;  // [16] (handed off)
+    double* rp;     // [nt][48] Ritz partials (handed off)
+    double* gx;     // [2][np] guard vectors (handed off)
+    double* gp;     // [2][nt][SGF_W] guard partials (handed off)
+    double* Z;      // [n][16] out
+    double* Wout;   // [16] out
 };
 
-__device__ __forceinline__ double fx_ld(const double* p)
-{
-    return __longlong_as_double(
-        (long long)__hip_atomic_load((const u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void fx_st(double* p, double v)
-{
-    __hip_atomic_store((u64*)p, (u64)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // this workgroup's stores are visible: every wave's vmcnt(0), a barrier, the flag
 __device__ __forceinline__ void fx_publish(u32* flags, u32 ph)
@@ -911,7 +913,7 @@ __device__ __forceinline__ d4 fx_product(const double* Cs, int np, const double*
 }
 
 // block (ci, cj) of Y^T Y over rows [0, np) (k_fsi_gram's split and order)
-__device__ __forceinline__ d4 fx_gram(const double* Y, int np, int ci, int cj, double* red)
+__device__ __forceinline__ d4 fx_gram(const double* Y, const double* Y2, int np, int ci, int cj, double* red)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int kr = lane >> 4, cc = lane & 15;
@@ -924,7 +926,7 @@ __device__ __forceinline__ d4 fx_gram(const double* Y, int np, int ci, int cj, d
         for (int u = 0; u < FX_LB; ++u) {
             const int kk = 4 * min(sb + u, s1 - 1) + kr;
             av[u] = fx_ld(Y + (size_t)kk * SI_B + 16 * ci + cc);
-            bv[u] = fx_ld(Y + (size_t)kk * SI_B + 16 * cj + cc);
+            bv[u] = fx_ld(Y2 + (size_t)kk * SI_B + 16 * cj + cc);
         }
 #pragma unroll
         for (int u = 0; u < FX_LB; ++u) {
@@ -938,6 +940,98 @@ __device__ __forceinline__ d4 fx_gram(const double* Y, int np, int ci, int cj, d
     if (w == 0) acc = ((acc + rd[lane]) + rd[64 + lane]) + rd[128 + lane];
     __syncthreads();
     return acc;
+}
+
+// one step of the missed-eigenpair guard for the 16 rows of tile t (k_sig_fused's
+// arithmetic; V, W, u and the partials are handed off): mode 0 x = g, 1 x = P g,
+// 2 x = P C P u / |u|, 3 the test (one workgroup)
+__device__ void fx_sig_step(const double* __restrict__ C, int ldc, int n, const double* V, const double* W,
+                            const double* u, const double* part_in, int nt, double* x, double* part_out,
+                            const double* theta, int k, u32* flag, int mode, int t, double* lds)
+{
+    double* z = lds;        // [64]
+    double* sc = z + SI_B;  // [2]
+    double* xr = sc + 2;    // [16]
+    double* ur = xr + 16;   // [16]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (mode == 3) {
+        if (tid < 64) {
+            double rho = 0.0, s = 0.0;
+            for (int q = 0; q < nt; ++q) {
+                rho += fx_ld(part_in + (size_t)q * SGF_W + 65);
+                s += fx_ld(part_in + (size_t)q * SGF_W + 64);
+            }
+            if (tid == 0 && s > 0.0 && !(rho < fx_ld(theta + k - 1))) atomicOr(flag, 8u);
+        }
+        __syncthreads();
+        return;
+    }
+    if (tid < SI_B + 1 && mode >= 1) {
+        const int c = tid < SI_B ? tid : 64;
+        double acc = 0.0;
+        for (int q = 0; q < nt; ++q) acc += fx_ld(part_in + (size_t)q * SGF_W + c);
+        if (tid < SI_B)
+            z[tid] = acc;
+        else
+            sc[0] = acc;
+    }
+    __syncthreads();
+    const double inv = (mode == 2) ? (sc[0] > 0.0 ? 1.0 / sqrt(sc[0]) : 0.0) : 1.0;
+    const int r0 = 16 * t;
+    double xv[4], uv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = r0 + 4 * wv + j;
+        const int rc = min(row, n - 1);
+        double acc = 0.0;
+        if (mode == 2) {
+            for (int cb0 = 0; cb0 < n; cb0 += 512) {
+                double cv[8], uu[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const int cb = min(cb0 + lane + 64 * m, n - 1);
+                    cv[m] = C[(size_t)rc * ldc + cb];
+                    uu[m] = fx_ld(u + cb);
+                }
+#pragma unroll
+                for (int m = 0; m < 8; ++m) acc = fma(cb0 + lane + 64 * m < n ? cv[m] : 0.0, uu[m], acc);
+            }
+            acc = sig_wave_sum(acc) * inv;
+        }
+        const double g = (double)(sig_hash(rc) & 0xffffff) / 16777216.0 - 0.5;
+        double base = (mode == 2) ? acc : g;
+        if (mode >= 1) base = fma(-fx_ld(V + (size_t)rc * SI_B + lane), (mode == 2 ? z[lane] * inv : z[lane]), 0.0);
+        const double dfl = (mode >= 1) ? sig_wave_sum(base) : 0.0;
+        const double val = ((mode == 2) ? acc : g) + dfl;
+        xv[j] = row < n ? val : 0.0;
+        uv[j] = (row < n && mode == 2) ? fx_ld(u + rc) * inv : 0.0;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xr[4 * wv + j] = xv[j];
+            ur[4 * wv + j] = uv[j];
+        }
+    }
+    __syncthreads();
+    if (tid < 16 && r0 + tid < n) fx_st(x + r0 + tid, xr[tid]);
+    const double* M = (mode == 0) ? V : W;
+    if (tid < SI_B) {
+        double acc = 0.0;
+        for (int j = 0; j < 16; ++j) {
+            const int row = min(r0 + j, n - 1);
+            acc = fma(fx_ld(M + (size_t)row * SI_B + tid), xr[j], acc);
+        }
+        fx_st(part_out + (size_t)t * SGF_W + tid, acc);
+    } else if (tid == 64) {
+        double s2 = 0.0, xu = 0.0;
+        for (int j = 0; j < 16; ++j) {
+            s2 = fma(xr[j], xr[j], s2);
+            xu = fma(xr[j], ur[j], xu);
+        }
+        fx_st(part_out + (size_t)t * SGF_W + 64, s2);
+        fx_st(part_out + (size_t)t * SGF_W + 65, xu);
+    }
 }
 
 __device__ __forceinline__ size_t fx_elem(int rt, int cq, int r)
@@ -1001,7 +1095,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                 // g -> (ci, cj), ci <= cj: 0..3 (0, j), 4..6 (1, j), 7..8 (2, j), 9 (3, 3)
                 const int ci = g < 4 ? 0 : (g < 7 ? 1 : (g < 9 ? 2 : 3));
                 const int cj = g < 4 ? g : (g < 7 ? g - 3 : (g < 9 ? g - 5 : 3));
-                const d4 acc = fx_gram(Y, np, ci, cj, X);
+                const d4 acc = fx_gram(Y, Y, np, ci, cj, X);
                 if (wv == 0) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
@@ -1180,10 +1274,135 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         (void)o2;
         if (!orth(pz, ds)) return;
     }
-    // the final basis for the Rayleigh-Ritz launches
-    if (wv == 0) {
+    if (!a.rr) {
+        // the final basis for the Rayleigh-Ritz launches
+        if (wv == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a.Qout[fx_elem(rt, cq, r)] = own[r];
+            for (int r = 0; r < 4; ++r) a.Qout[fx_elem(rt, cq, r)] = own[r];
+        }
+        return;
+    }
+    // ---- Rayleigh-Ritz: W = C Q (k_fsi_mul, plain), H = Q^T W (16 blocks)
+    const int sQ = slot_src, sW = (sQ + 1) % 3;
+    const double* Qb = a.Yb + sQ * blk;
+    const double* Wb = a.Yb + sW * blk;
+    {
+        const u32 phQ = ph_src;
+        const d4 q_own = own;
+        ++ph;
+        if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return;
+        if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return;
+        const d4 acc = fx_product(Cs, np, Qb, nullptr, 0.0, cq, X);
+        if (wv == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                fx_st(a.Yb + sW * blk + fx_elem(rt, cq, r), fma(1.0, acc[r], fma(0.0, q_own[r], 0.0 * 0.0)));
+        }
+        fx_publish(flags, ph);
+    }
+    const u32 phW = ph;
+    ++ph;
+    const u32 phH = ph;
+    if (g < 16) {
+        if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return;
+        const int ci = g >> 2, cj = g & 3;
+        const d4 acc = fx_gram(Qb, Wb, np, ci, cj, X);
+        if (wv == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                fx_st(a.Gb + (size_t)(ci * 4 + cj) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15), acc[r]);
+        }
+        fx_publish(flags, ph);
+    }
+    if (cq != 0) return;  // the rest runs on one workgroup per row tile
+    ++ph;
+    const u32 phS = ph;
+    if (g == 0) {
+        // the 64 x 64 eigenproblem on workgroup 0 (its LDS is free now)
+        if (!fx_wait(flags, err, 0, 1, 16, phH, &s_abort)) return;
+        const double* Gb = a.Gb;
+        se_syev<true>(
+            [=](int i, int j) { return fx_ld(Gb + (size_t)((i >> 4) * 4 + (j >> 4)) * 256 + (i & 15) * 16 + (j & 15)); },
+            SI_B, a.k, a.Yv, a.theta, a.flag, sm, (u64*)nullptr);
+        fx_publish(flags, ph);
+    }
+    // Ritz vectors of this row tile and their residual partials (k_si_ritz's per-row order)
+    ++ph;
+    const u32 phR = ph;
+    if (!fx_wait(flags, err, 0, 1, 1, phS, &s_abort)) return;
+    if (!fx_wait(flags, err, 4 * rt, 1, 4, phW, &s_abort)) return;
+    double* rs = X;  // [16 rows][16]: r^2, then u^2, then u (LDS)
+    const int row = 16 * rt + (tid >> 4), q = tid & 15;
+    double u = 0.0, cu = 0.0;
+    {
+        const int rc = min(row, a.n - 1);
+        for (int j = 0; j < SI_B; ++j) {
+            const double yq = q < a.k ? fx_ld(a.Yv + j * 16 + q) : 0.0;
+            u = fma(fx_ld(Qb + (size_t)rc * SI_B + j), yq, u);
+            cu = fma(fx_ld(Wb + (size_t)rc * SI_B + j), yq, cu);
+        }
+        if (row >= a.n) u = cu = 0.0;
+        const double th = q < a.k ? fx_ld(a.theta + q) : 0.0;
+        const double r = (q < a.k) ? fma(-th, u, cu) : 0.0;
+        rs[(tid >> 4) * 16 + q] = r * r;
+        rs[256 + (tid >> 4) * 16 + q] = u * u;
+        rs[512 + (tid >> 4) * 16 + q] = u;
+    }
+    __syncthreads();
+    if (tid < 16) {
+        double s = 0.0, nn = 0.0, mm = 0.0;
+        for (int i = 0; i < 16; ++i) {
+            s += rs[i * 16 + tid];
+            nn += rs[256 + i * 16 + tid];
+            const double v = rs[512 + i * 16 + tid];
+            mm = (fabs(v) > fabs(mm)) ? v : mm;
+        }
+        fx_st(a.rp + (size_t)rt * 48 + tid, s);
+        fx_st(a.rp + (size_t)rt * 48 + 16 + tid, nn);
+        fx_st(a.rp + (size_t)rt * 48 + 32 + tid, mm);
+    }
+    fx_publish(flags, ph);
+    // every row tile forms the totals (fixed order), signs its rows; workgroup 0
+    // writes the eigenvalues and the test bits (k_si_check, k_fsi_bound_check)
+    ++ph;
+    if (!fx_wait(flags, err, 0, 4, nt, phR, &s_abort)) return;
+    double* tot = X + 768;  // [16] sign
+    if (tid < 16) {
+        double s = 0.0, nn = 0.0, mm = 0.0;
+        for (int t = 0; t < nt; ++t) {
+            s += fx_ld(a.rp + (size_t)t * 48 + tid);
+            nn += fx_ld(a.rp + (size_t)t * 48 + 16 + tid);
+            const double v = fx_ld(a.rp + (size_t)t * 48 + 32 + tid);
+            mm = (fabs(v) > fabs(mm)) ? v : mm;
+        }
+        tot[tid] = (mm < 0.0) ? -1.0 : 1.0;
+        if (g == 0 && tid < a.k) {
+            const double th0 = fabs(fx_ld(a.theta));
+            a.Wout[tid] = fx_ld(a.theta + tid);
+            ((double*)(a.flag + 8))[tid] = sqrt(s) / th0;
+            if (!(sqrt(s) <= a.tol * th0)) atomicOr(a.flag, 2u);
+            if (!(fabs(nn - 1.0) <= 1e-9)) atomicOr(a.flag, 4u);
+            if (tid == 0 && !(b_prev < fx_ld(a.theta + a.k - 1))) atomicOr(a.flag, 32u);  // the last b
+        }
+    }
+    __syncthreads();
+    if (row < a.n) a.Z[(size_t)row * 16 + q] = u * tot[q];
+    if (!a.guard) return;
+    // ---- the missed-eigenpair guard: x0 = g, x1 = P g, SI_GUARD_IT products of P C P
+    const double* xin = nullptr;
+    const double* pin = nullptr;
+    for (int step = 0; step < SI_GUARD_IT + 3; ++step) {
+        const int mode = step == 0 ? 0 : (step == 1 ? 1 : (step == SI_GUARD_IT + 2 ? 3 : 2));
+        if (mode == 3 && g != 0) break;
+        double* xo = a.gx + (size_t)(step & 1) * np;
+        double* po = a.gp + (size_t)(step & 1) * nt * SGF_W;
+        const u32 ph_prev = ph;
+        ++ph;
+        if (step > 0 && !fx_wait(flags, err, 0, 4, nt, ph_prev, &s_abort)) return;
+        fx_sig_step(a.C, a.ldc, a.n, Qb, Wb, xin, pin, nt, xo, po, a.theta, a.k, a.flag, mode, rt, X + 1024);
+        if (mode != 3) fx_publish(flags, ph);
+        xin = xo;
+        pin = po;
     }
 }
 
@@ -1222,7 +1441,10 @@ static bool fx_usable(int n)
 {
     return fsi_env("SCC_EIG_FSI_ENGINE", 1) != 0 && (int)si_npad(n) <= FX_NPMAX;
 }
-static size_t fx_lds_bytes(int np) { return sizeof(double) * ((size_t)16 * np + 2 * 64 * CB_S + 64); }
+static size_t fx_lds_bytes(int np)
+{
+    return sizeof(double) * std::max((size_t)16 * np + 2 * 64 * CB_S + 64, (size_t)SE_LDS_TOTAL);
+}
 static void fx_prepare()
 {
     static std::once_flag once;
@@ -1351,7 +1573,19 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             fa.coef = coef;
             fa.flag = flag;
             fa.err = fxerr;
+            fa.rr = fsi_env("SCC_EIG_FSI_ENGINE_RR", 1) != 0;
+            fa.k = k;
+            fa.guard = guard;
+            fa.tol = FSI_TOL;
+            fa.Yv = Yv;
+            fa.theta = theta;
+            fa.rp = dpart;  // (the b partials are dead by then)
+            fa.gx = gu;
+            fa.gp = gpart;
+            fa.Z = Z;
+            fa.Wout = Wout;
             hipLaunchKernelGGL(k_fsi_engine, dim3(4 * (unsigned)nt), dim3(256), fx_lds_bytes((int)np), s, fa);
+            if (fa.rr) return hipGetLastError();
             return rayleigh_ritz(s);
         }
         hipLaunchKernelGGL(k_fsi_coef0, dim3(1), dim3(64), 0, s, coef);  // slot 0: plain product {1, 0, 0, b = 0}
