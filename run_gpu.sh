@@ -38,6 +38,7 @@ for s in "$@"; do
     dbgx) AMD_LOG_LEVEL=1 step dbgx 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_exchange.py -x -v --timeout 120 --timeout-method thread ;;
     sticky) AMD_LOG_LEVEL=2 step sticky 300 python -u scripts/dbg_sticky.py ;;
     fsi) step fsi 600 python -u -m pytest tests/test_gpu_fsi.py tests/test_gpu_regress.py tests/test_gpu_devices.py -v --timeout 120 --timeout-method thread ;;
+    fsiguard) step fsiguard 600 python -u -m pytest tests/test_gpu_dist.py -k "guard" -v --timeout 120 --timeout-method thread ;;
     benchfsi) SCC_EIG_FSI=1 SCC_EIG_SI_LOG=1 step benchfsi 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
     proffsi) SCC_EIG_FSI=1 step proffsi 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proffsi -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 2 ;;
     smalleig) step smalleig 300 rocprofv3 --kernel-trace --stats -d gpurun_out/smalleig -o run --output-format csv -- python3 scripts/small_eig_bench.py ;;

@@ -1875,9 +1875,11 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     // the side stream and its fork / join events are shared by every context
     // on a device: one host thread at a time enqueues this launch sequence, so
     // another context cannot re-record fork_ev / join_ev between our record
-    // and the wait on it (launches are asynchronous: the lock is held briefly)
-    static std::mutex launch_mu;
-    std::lock_guard<std::mutex> guard(launch_mu);
+    // and the wait on it (launches are asynchronous: the lock is held briefly).
+    // Recursive: the subspace iteration's Rayleigh-Ritz step solves its 64 x 64
+    // matrix through this same entry point on the same thread.
+    static std::recursive_mutex launch_mu;
+    std::lock_guard<std::recursive_mutex> guard(launch_mu);
     int nwg;
     bool rows_lds, lu_lds;
     eig_plan(n, nwg, rows_lds, lu_lds);

@@ -19,6 +19,22 @@ __device__ __forceinline__ void fx_st(double* p, double v)
     __hip_atomic_store((u64*)p, (u64)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// sum over t < count of p[t * stride] in t order; the loads (sc1: a round trip
+// to memory each) are issued 8 at a time, with no branch between them
+__device__ __forceinline__ double fx_sum(const double* p, size_t stride, int count)
+{
+    double s = 0.0;
+    for (int t0 = 0; t0 < count; t0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = fx_ld(p + (size_t)min(t0 + u, count - 1) * stride);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = (t0 + u < count) ? s + v[u] : s;
+    }
+    return s;
+}
+
+
 __device__ inline double se_wave_sum(double v)
 {
     v += scc_xor_lane_f64<32>(v);

@@ -833,16 +833,28 @@ struct FxArgs {
     double* gp;     // [2][nt][SGF_W] guard partials (handed off)
     double* Z;      // [n][16] out
     double* Wout;   // [16] out
+    u64* stamps;    // g_fx_stamps or nullptr
 };
 
 
 // this workgroup's stores are visible: every wave's vmcnt(0), a barrier, the flag
-__device__ __forceinline__ void fx_publish(u32* flags, u32 ph)
+// diagnostic phase stamps of workgroup 0 (SCC_EIG_FSI_STAMPS=1): [2 ph] its
+// waits of phase ph done, [2 ph + 1] phase ph published (s_memrealtime, 100 MHz)
+#define FX_NSTAMP 1024
+__device__ u64 g_fx_stamps[FX_NSTAMP];
+
+__device__ __forceinline__ void fx_stamp(u64* st, u32 idx)
+{
+    if (st && blockIdx.x == 0 && threadIdx.x == 0 && idx < FX_NSTAMP) st[idx] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ void fx_publish(u32* flags, u32 ph, u64* st = nullptr)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(&flags[(size_t)blockIdx.x * FX_FS], ph, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fx_stamp(st, 2 * ph + 1);
 }
 
 // wait until the flags of workgroups base + stride i (i < count) reach ph; false:
@@ -881,6 +893,7 @@ __device__ __forceinline__ bool fx_wait(const u32* flags, u32* err, int base, in
 // B[k][c] = Y[k][c] (mode 0) or s2 W[k][c] - Y[k][c] (mode 1, W = Wm); the 4 waves
 // take contiguous quarters of k (k_fsi_mul's split and batching); wave 0
 // returns the sum, in k_fsi_mul's order
+template <bool Y1>
 __device__ __forceinline__ d4 fx_product(const double* Cs, int np, const double* Y, const double* Wm, double s2,
                                          int cq, double* red)
 {
@@ -896,7 +909,12 @@ __device__ __forceinline__ d4 fx_product(const double* Cs, int np, const double*
             const int kk = 4 * min(sb + u, s1 - 1) + kr;
             av[u] = Cs[kk * 16 + cc];
             const size_t e = (size_t)kk * SI_B + 16 * cq + cc;
-            bv[u] = Wm ? fma(s2, fx_ld(Wm + e), -fx_ld(Y + e)) : fx_ld(Y + e);
+            if (Y1) {
+                const double w = fx_ld(Wm + e), y = fx_ld(Y + e);
+                bv[u] = fma(s2, w, -y);
+            } else {
+                bv[u] = fx_ld(Y + e);
+            }
         }
 #pragma unroll
         for (int u = 0; u < FX_LB; ++u) {
@@ -956,11 +974,7 @@ __device__ void fx_sig_step(const double* __restrict__ C, int ldc, int n, const 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (mode == 3) {
         if (tid < 64) {
-            double rho = 0.0, s = 0.0;
-            for (int q = 0; q < nt; ++q) {
-                rho += fx_ld(part_in + (size_t)q * SGF_W + 65);
-                s += fx_ld(part_in + (size_t)q * SGF_W + 64);
-            }
+            const double rho = fx_sum(part_in + 65, SGF_W, nt), s = fx_sum(part_in + 64, SGF_W, nt);
             if (tid == 0 && s > 0.0 && !(rho < fx_ld(theta + k - 1))) atomicOr(flag, 8u);
         }
         __syncthreads();
@@ -968,8 +982,7 @@ __device__ void fx_sig_step(const double* __restrict__ C, int ldc, int n, const 
     }
     if (tid < SI_B + 1 && mode >= 1) {
         const int c = tid < SI_B ? tid : 64;
-        double acc = 0.0;
-        for (int q = 0; q < nt; ++q) acc += fx_ld(part_in + (size_t)q * SGF_W + c);
+        const double acc = fx_sum(part_in + c, SGF_W, nt);
         if (tid < SI_B)
             z[tid] = acc;
         else
@@ -1017,11 +1030,12 @@ __device__ void fx_sig_step(const double* __restrict__ C, int ldc, int n, const 
     if (tid < 16 && r0 + tid < n) fx_st(x + r0 + tid, xr[tid]);
     const double* M = (mode == 0) ? V : W;
     if (tid < SI_B) {
+        double mv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) mv[j] = fx_ld(M + (size_t)min(r0 + j, n - 1) * SI_B + tid);
         double acc = 0.0;
-        for (int j = 0; j < 16; ++j) {
-            const int row = min(r0 + j, n - 1);
-            acc = fma(fx_ld(M + (size_t)row * SI_B + tid), xr[j], acc);
-        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc = fma(mv[j], xr[j], acc);
         fx_st(part_out + (size_t)t * SGF_W + tid, acc);
     } else if (tid == 64) {
         double s2 = 0.0, xu = 0.0;
@@ -1079,7 +1093,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
             fx_st(a.Yb + e, v);
         }
     }
-    fx_publish(flags, ++ph);
+    fx_publish(flags, ++ph, a.stamps);
     u32 ph_src = ph;  // the phase that published the current block
     int slot_src = 0;
     d4 own = {0.0, 0.0, 0.0, 0.0};  // wave 0: this tile of the current block
@@ -1091,7 +1105,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
             const double* Y = a.Yb + slot_src * blk;
             ++ph;
             if (g < 10) {
-                if (!fx_wait(flags, err, 0, 1, nwg, ph_src, &s_abort)) return false;
+                if (!fx_wait(flags, err, 0, 1, nwg, ph_src, &s_abort)) return false; fx_stamp(a.stamps, 2 * ph);
                 // g -> (ci, cj), ci <= cj: 0..3 (0, j), 4..6 (1, j), 7..8 (2, j), 9 (3, 3)
                 const int ci = g < 4 ? 0 : (g < 7 ? 1 : (g < 9 ? 2 : 3));
                 const int cj = g < 4 ? g : (g < 7 ? g - 3 : (g < 9 ? g - 5 : 3));
@@ -1101,18 +1115,27 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                     for (int r = 0; r < 4; ++r)
                         fx_st(a.Gb + (size_t)(ci * 4 + cj) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15), acc[r]);
                 }
-                fx_publish(flags, ph);
+                fx_publish(flags, ph, a.stamps);
             }
             const u32 ph_g = ph;
             ++ph;  // the apply's phase (a Gram workgroup's flag already reads ph_g)
             // every workgroup: G (mirrored), shifted on the first pass, factored
-            if (!fx_wait(flags, err, 0, 1, 10, ph_g, &s_abort)) return false;
-            if (g >= 10 && !fx_wait(flags, err, 4 * rt, 1, 4, ph_src, &s_abort)) return false;  // this row's tiles of Y
-            for (int e = tid; e < 64 * 64; e += 256) {
-                const int i = e >> 6, j = e & 63, bi = i >> 4, bj = j >> 4;
-                const double v = (bi <= bj) ? fx_ld(a.Gb + (size_t)(bi * 4 + bj) * 256 + (i & 15) * 16 + (j & 15))
-                                            : fx_ld(a.Gb + (size_t)(bj * 4 + bi) * 256 + (j & 15) * 16 + (i & 15));
-                A[i * CB_S + j] = v + 0.0;  // (k_fsi_cholinv_blk adds the shift or 0.0 everywhere)
+            if (!fx_wait(flags, err, 0, 1, 10, ph_g, &s_abort)) return false; fx_stamp(a.stamps, 2 * ph);
+            if (g >= 10 && !fx_wait(flags, err, 4 * rt, 1, 4, ph_src, &s_abort)) return false; fx_stamp(a.stamps, 2 * ph);  // this row's tiles of Y
+            {
+                double gv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int e = tid + 256 * u, i = e >> 6, j = e & 63, bi = i >> 4, bj = j >> 4;
+                    const size_t off = (bi <= bj) ? (size_t)(bi * 4 + bj) * 256 + (i & 15) * 16 + (j & 15)
+                                                  : (size_t)(bj * 4 + bi) * 256 + (j & 15) * 16 + (i & 15);
+                    gv[u] = fx_ld(a.Gb + off);
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int e = tid + 256 * u;
+                    A[(e >> 6) * CB_S + (e & 63)] = gv[u] + 0.0;  // (k_fsi_cholinv_blk adds the shift or 0.0 everywhere)
+                }
             }
             __syncthreads();
             if (p == 0) {
@@ -1137,7 +1160,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                 double av[16], bv[16];
 #pragma unroll
                 for (int s = 0; s < 16; ++s) {
-                    av[s] = s < smax ? fx_ld(Y + (size_t)(16 * rt + cc) * SI_B + 4 * s + kr) : 0.0;
+                    av[s] = fx_ld(Y + (size_t)(16 * rt + cc) * SI_B + 4 * s + kr);  // (s >= smax: unused)
                     bv[s] = X[(j0 + cc) * CB_S + 4 * s + kr];
                 }
                 d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -1149,7 +1172,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                 for (int r = 0; r < 4; ++r) fx_st(a.Yb + dst * blk + fx_elem(rt, cq, r), acc[r]);
             }
             if (g == 0 && tid == 0 && s_bad) atomicOr(a.flag, 1u);
-            fx_publish(flags, ph);
+            fx_publish(flags, ph, a.stamps);
             ph_src = ph;
             slot_src = dst;
         }
@@ -1168,11 +1191,11 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         const d4 q_own = own;
         // W = C Q (plain) and the tile's q.w, q.q partials
         ++ph;
-        if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return;
+        if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
         // (W overwrites the slot the last CholQR pass but one wrote: the row's other
         // workgroups must be past their applies, which read it)
-        if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return;
-        d4 w_own = fx_product(Cs, np, a.Yb + sQ * blk, nullptr, 0.0, cq, X);
+        if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
+        d4 w_own = fx_product<false>(Cs, np, a.Yb + sQ * blk, nullptr, 0.0, cq, X);
         if (wv == 0) {
             double dp = 0.0, dq = 0.0;
 #pragma unroll
@@ -1192,19 +1215,16 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                 fx_st(a.part + (size_t)g * 32 + 16 + lane, dq);
             }
         }
-        fx_publish(flags, ph);
+        fx_publish(flags, ph, a.stamps);
         const u32 phW = ph;
         // b (k_fsi_cheb1's sums, in every workgroup), then Y2 = (4/b) C Y1 - 2 Y1 - Q
         // with Y1 = (2/b) W - Q formed on the fly
         ++ph;
-        if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return;
+        if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
         if (tid < 64) {
             const int c = tid, gq = c >> 4, cl = c & 15;
-            double s = 0.0, sq = 0.0;
-            for (int t = 0; t < nt; ++t) {
-                s += fx_ld(a.part + (size_t)(4 * t + gq) * 32 + cl);
-                sq += fx_ld(a.part + (size_t)(4 * t + gq) * 32 + 16 + cl);
-            }
+            double s = fx_sum(a.part + (size_t)gq * 32 + cl, 128, nt);
+            const double sq = fx_sum(a.part + (size_t)gq * 32 + 16 + cl, 128, nt);
             s = sq > 0.0 ? s / sq : 0.0;
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) s = fmin(s, __shfl_xor(s, o, 64));
@@ -1231,7 +1251,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         for (int r = 0; r < 4; ++r) y1_own[r] = fma(s2b, w_own[r], -q_own[r]);
         // Y2: operand (2/b) W - Q from slots sW, sQ; epilogue on Y1 (x) and Q (z)
         {
-            const d4 acc = fx_product(Cs, np, a.Yb + sQ * blk, a.Yb + sW * blk, s2b, cq, X);
+            const d4 acc = fx_product<true>(Cs, np, a.Yb + sQ * blk, a.Yb + sW * blk, s2b, cq, X);
             if (wv == 0) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -1241,14 +1261,14 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                 }
             }
             prev_own = y1_own;
-            fx_publish(flags, ph);
+            fx_publish(flags, ph, a.stamps);
         }
         int s_cur = s2, s_free = sW;  // W and Q are dead once every tile of Y2 is out
         for (int t = 3; t <= a.m; ++t) {
             const u32 ph_in = ph;
             ++ph;
-            if (!fx_wait(flags, err, cq, 4, nt, ph_in, &s_abort)) return;
-            const d4 acc = fx_product(Cs, np, a.Yb + s_cur * blk, nullptr, 0.0, cq, X);
+            if (!fx_wait(flags, err, cq, 4, nt, ph_in, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
+            const d4 acc = fx_product<false>(Cs, np, a.Yb + s_cur * blk, nullptr, 0.0, cq, X);
             d4 nxt;
             if (wv == 0) {
 #pragma unroll
@@ -1262,7 +1282,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
             const int sx = s_cur;
             s_cur = s_free;
             s_free = (sx == sQ) ? other(s_cur, sQ) : sx;
-            fx_publish(flags, ph);
+            fx_publish(flags, ph, a.stamps);
         }
         own = cur_own;
         ph_src = ph;
@@ -1290,21 +1310,21 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         const u32 phQ = ph_src;
         const d4 q_own = own;
         ++ph;
-        if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return;
-        if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return;
-        const d4 acc = fx_product(Cs, np, Qb, nullptr, 0.0, cq, X);
+        if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
+        if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
+        const d4 acc = fx_product<false>(Cs, np, Qb, nullptr, 0.0, cq, X);
         if (wv == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 fx_st(a.Yb + sW * blk + fx_elem(rt, cq, r), fma(1.0, acc[r], fma(0.0, q_own[r], 0.0 * 0.0)));
         }
-        fx_publish(flags, ph);
+        fx_publish(flags, ph, a.stamps);
     }
     const u32 phW = ph;
     ++ph;
     const u32 phH = ph;
     if (g < 16) {
-        if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return;
+        if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
         const int ci = g >> 2, cj = g & 3;
         const d4 acc = fx_gram(Qb, Wb, np, ci, cj, X);
         if (wv == 0) {
@@ -1312,37 +1332,48 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
             for (int r = 0; r < 4; ++r)
                 fx_st(a.Gb + (size_t)(ci * 4 + cj) * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15), acc[r]);
         }
-        fx_publish(flags, ph);
+        fx_publish(flags, ph, a.stamps);
     }
     if (cq != 0) return;  // the rest runs on one workgroup per row tile
     ++ph;
     const u32 phS = ph;
     if (g == 0) {
         // the 64 x 64 eigenproblem on workgroup 0 (its LDS is free now)
-        if (!fx_wait(flags, err, 0, 1, 16, phH, &s_abort)) return;
+        if (!fx_wait(flags, err, 0, 1, 16, phH, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
         const double* Gb = a.Gb;
         se_syev<true>(
             [=](int i, int j) { return fx_ld(Gb + (size_t)((i >> 4) * 4 + (j >> 4)) * 256 + (i & 15) * 16 + (j & 15)); },
             SI_B, a.k, a.Yv, a.theta, a.flag, sm, (u64*)nullptr);
-        fx_publish(flags, ph);
+        fx_publish(flags, ph, a.stamps);
     }
     // Ritz vectors of this row tile and their residual partials (k_si_ritz's per-row order)
     ++ph;
     const u32 phR = ph;
-    if (!fx_wait(flags, err, 0, 1, 1, phS, &s_abort)) return;
-    if (!fx_wait(flags, err, 4 * rt, 1, 4, phW, &s_abort)) return;
+    if (!fx_wait(flags, err, 0, 1, 1, phS, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
+    if (!fx_wait(flags, err, 4 * rt, 1, 4, phW, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
     double* rs = X;  // [16 rows][16]: r^2, then u^2, then u (LDS)
     const int row = 16 * rt + (tid >> 4), q = tid & 15;
     double u = 0.0, cu = 0.0;
     {
         const int rc = min(row, a.n - 1);
-        for (int j = 0; j < SI_B; ++j) {
-            const double yq = q < a.k ? fx_ld(a.Yv + j * 16 + q) : 0.0;
-            u = fma(fx_ld(Qb + (size_t)rc * SI_B + j), yq, u);
-            cu = fma(fx_ld(Wb + (size_t)rc * SI_B + j), yq, cu);
+        for (int j0 = 0; j0 < SI_B; j0 += 8) {
+            double yv[8], qv[8], wv8[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                yv[j] = fx_ld(a.Yv + (j0 + j) * 16 + q);
+                qv[j] = fx_ld(Qb + (size_t)rc * SI_B + j0 + j);
+                wv8[j] = fx_ld(Wb + (size_t)rc * SI_B + j0 + j);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const double yq = q < a.k ? yv[j] : 0.0;
+                u = fma(qv[j], yq, u);
+                cu = fma(wv8[j], yq, cu);
+            }
         }
         if (row >= a.n) u = cu = 0.0;
-        const double th = q < a.k ? fx_ld(a.theta + q) : 0.0;
+        const double thl = fx_ld(a.theta + q);
+        const double th = q < a.k ? thl : 0.0;
         const double r = (q < a.k) ? fma(-th, u, cu) : 0.0;
         rs[(tid >> 4) * 16 + q] = r * r;
         rs[256 + (tid >> 4) * 16 + q] = u * u;
@@ -1361,19 +1392,21 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         fx_st(a.rp + (size_t)rt * 48 + 16 + tid, nn);
         fx_st(a.rp + (size_t)rt * 48 + 32 + tid, mm);
     }
-    fx_publish(flags, ph);
+    fx_publish(flags, ph, a.stamps);
     // every row tile forms the totals (fixed order), signs its rows; workgroup 0
     // writes the eigenvalues and the test bits (k_si_check, k_fsi_bound_check)
     ++ph;
-    if (!fx_wait(flags, err, 0, 4, nt, phR, &s_abort)) return;
+    if (!fx_wait(flags, err, 0, 4, nt, phR, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
     double* tot = X + 768;  // [16] sign
     if (tid < 16) {
-        double s = 0.0, nn = 0.0, mm = 0.0;
-        for (int t = 0; t < nt; ++t) {
-            s += fx_ld(a.rp + (size_t)t * 48 + tid);
-            nn += fx_ld(a.rp + (size_t)t * 48 + 16 + tid);
-            const double v = fx_ld(a.rp + (size_t)t * 48 + 32 + tid);
-            mm = (fabs(v) > fabs(mm)) ? v : mm;
+        const double s = fx_sum(a.rp + tid, 48, nt), nn = fx_sum(a.rp + 16 + tid, 48, nt);
+        double mm = 0.0;
+        for (int t0 = 0; t0 < nt; t0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = fx_ld(a.rp + (size_t)min(t0 + u, nt - 1) * 48 + 32 + tid);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) mm = (t0 + u < nt && fabs(v[u]) > fabs(mm)) ? v[u] : mm;
         }
         tot[tid] = (mm < 0.0) ? -1.0 : 1.0;
         if (g == 0 && tid < a.k) {
@@ -1400,7 +1433,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         ++ph;
         if (step > 0 && !fx_wait(flags, err, 0, 4, nt, ph_prev, &s_abort)) return;
         fx_sig_step(a.C, a.ldc, a.n, Qb, Wb, xin, pin, nt, xo, po, a.theta, a.k, a.flag, mode, rt, X + 1024);
-        if (mode != 3) fx_publish(flags, ph);
+        if (mode != 3) fx_publish(flags, ph, a.stamps);
         xin = xo;
         pin = po;
     }
@@ -1584,6 +1617,14 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             fa.gp = gpart;
             fa.Z = Z;
             fa.Wout = Wout;
+            fa.stamps = nullptr;
+            if (fsi_env("SCC_EIG_FSI_STAMPS", 0)) {
+                void* sp = nullptr;
+                if (hipGetSymbolAddress(&sp, HIP_SYMBOL(g_fx_stamps)) == hipSuccess) {
+                    fa.stamps = (u64*)sp;
+                    (void)hipMemsetAsync(sp, 0, sizeof(u64) * FX_NSTAMP, s);
+                }
+            }
             hipLaunchKernelGGL(k_fsi_engine, dim3(4 * (unsigned)nt), dim3(256), fx_lds_bytes((int)np), s, fa);
             if (fa.rr) return hipGetLastError();
             return rayleigh_ritz(s);
@@ -1688,6 +1729,20 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             for (int q = 0; q < k; ++q) rmax = std::max(rmax, lg[q]);
             fprintf(stderr, "[scc fsi] n=%d seg=%d deg=%d flag=%u maxres=%.3g b=%.6g theta_k=%.6g graph=%d engine=%d\n",
                     n, S, m, h, rmax, cf[3], th[k - 1], launched ? 1 : 0, use_engine);
+        }
+    }
+    if (use_engine && fsi_env("SCC_EIG_FSI_STAMPS", 0)) {
+        static u64 hs[FX_NSTAMP];
+        if (hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_fx_stamps), sizeof(hs)) == hipSuccess) {
+            u64 t0 = hs[3], prev = hs[3];  // phase 1 published
+            fprintf(stderr, "[scc fsi stamps] phase: wait_us compute_us (from the previous publish), 10 ns ticks\n");
+            for (int ph = 2; ph < FX_NSTAMP / 2; ++ph) {
+                const u64 w = hs[2 * ph], p = hs[2 * ph + 1];
+                if (!p) continue;
+                const double wu = w ? (double)(w - prev) / 100.0 : 0.0, cu = (double)(p - (w ? w : prev)) / 100.0;
+                fprintf(stderr, "[scc fsi stamps] %3d %8.2f %8.2f  t=%8.2f\n", ph, wu, cu, (double)(p - t0) / 100.0);
+                prev = p;
+            }
         }
     }
     *ok = (h == 0) ? (use_engine ? 2 : 1) : 0;  // 2: accepted, the engine ran the filter loop
