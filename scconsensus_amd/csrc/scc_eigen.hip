@@ -1835,6 +1835,7 @@ extern "C" size_t scc_si_scratch_doubles(int n);
 extern "C" int scc_si_wanted(int n);
 extern "C" int scc_fsi_wanted(int n);
 extern "C" size_t scc_fsi_scratch_doubles(int n);
+extern "C" void scc_fsi_forget(const void* p, size_t bytes);
 extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
                                     int* ok, hipStream_t st);
 extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
@@ -2091,6 +2092,7 @@ extern "C" SCC_API int scc_diag_eigen_topk(const double* A, int n, int lda, int 
     if (e == hipSuccess && err) e = hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (path) *path = g_eig_last_path;
+    scc_fsi_forget(scr, sz);
     hipFree(scr);
     return (e == hipSuccess && h == 0) ? 0 : 1;
 }

@@ -165,6 +165,8 @@ inline int fail(scc_ctx* c, int code, const std::string& msg)
             return fail((ctx), SCC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
     } while (0)
 
+extern "C" void scc_fsi_forget(const void* p, size_t bytes);  // scc_subspace.hip: cached graphs over p
+
 // grow-only named workspace buffer
 inline int ws_get(scc_ctx* c, const char* name, size_t bytes, void** out)
 {
@@ -177,6 +179,7 @@ inline int ws_get(scc_ctx* c, const char* name, size_t bytes, void** out)
     if (it != c->ws.end()) {
         hipStreamSynchronize(c->s0);
         hipStreamSynchronize(c->s1);
+        scc_fsi_forget(it->second.first, it->second.second);
         hipFree(it->second.first);
         c->ws.erase(it);
     }
@@ -213,6 +216,7 @@ inline int ws_keep(scc_ctx* c, const char* name, size_t bytes, size_t used, void
         }
         hipStreamSynchronize(c->s0);
         hipStreamSynchronize(c->s1);
+        scc_fsi_forget(it->second.first, it->second.second);
         hipFree(it->second.first);
         c->ws.erase(it);
     }

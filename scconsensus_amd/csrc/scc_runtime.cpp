@@ -97,7 +97,10 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     scc_distance_release(c);
     hipStreamSynchronize(c->s0);
     hipStreamSynchronize(c->s1);
-    for (auto& kv : c->ws) hipFree(kv.second.first);
+    for (auto& kv : c->ws) {
+        scc_fsi_forget(kv.second.first, kv.second.second);
+        hipFree(kv.second.first);
+    }
     for (auto& pe : c->pending) {
         hipEventDestroy(pe.a);
         hipEventDestroy(pe.b);

@@ -1334,16 +1334,51 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         }
         fx_publish(flags, ph, a.stamps);
     }
+    // ---- the missed-eigenpair guard (x0 = g, x1 = P g, SI_GUARD_IT products of
+    // P C P) runs on the cq == 1 workgroups (one per row tile) while workgroup 0
+    // solves the 64 x 64 eigenproblem; workgroup 0 makes the final test (it
+    // needs theta_k) once both are done
+    const u32 ph_g0 = ph;  // the guard's phases are ph_g0 + 1 .. ph_g0 + SI_GUARD_IT + 2
+    if (cq == 1) {
+        if (!a.guard) return;
+        if (!fx_wait(flags, err, 4 * rt, 1, 4, phW, &s_abort)) return;  // this row's tiles of Q and W
+        const double* xin = nullptr;
+        const double* pin = nullptr;
+        for (int step = 0; step < SI_GUARD_IT + 2; ++step) {
+            const int mode = step == 0 ? 0 : (step == 1 ? 1 : 2);
+            double* xo = a.gx + (size_t)(step & 1) * np;
+            double* po = a.gp + (size_t)(step & 1) * nt * SGF_W;
+            const u32 ph_prev = ph;
+            ++ph;
+            if (step > 0 && !fx_wait(flags, err, 1, 4, nt, ph_prev, &s_abort)) return;
+            fx_sig_step(a.C, a.ldc, a.n, Qb, Wb, xin, pin, nt, xo, po, a.theta, a.k, a.flag, mode, rt, X + 1024);
+            fx_publish(flags, ph, g == 1 ? a.stamps : nullptr);
+            xin = xo;
+            pin = po;
+        }
+        return;
+    }
     if (cq != 0) return;  // the rest runs on one workgroup per row tile
     ++ph;
     const u32 phS = ph;
     if (g == 0) {
-        // the 64 x 64 eigenproblem on workgroup 0 (its LDS is free now)
+        // the 64 x 64 eigenproblem on workgroup 0 (its LDS is free now); H staged
+        // in the solver's LU region (first written after H is in registers)
         if (!fx_wait(flags, err, 0, 1, 16, phH, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
-        const double* Gb = a.Gb;
-        se_syev<true>(
-            [=](int i, int j) { return fx_ld(Gb + (size_t)((i >> 4) * 4 + (j >> 4)) * 256 + (i & 15) * 16 + (j & 15)); },
-            SI_B, a.k, a.Yv, a.theta, a.flag, sm, (u64*)nullptr);
+        double* Hs = sm + SE_LDS_LU;
+        {
+            double hv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = tid + 256 * u, i = e >> 6, j = e & 63;
+                hv[u] = fx_ld(a.Gb + (size_t)((i >> 4) * 4 + (j >> 4)) * 256 + (i & 15) * 16 + (j & 15));
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) Hs[tid + 256 * u] = hv[u];
+        }
+        __syncthreads();
+        se_syev<true>([=](int i, int j) { return Hs[i * 64 + j]; }, SI_B, a.k, a.Yv, a.theta, a.flag, sm,
+                      (u64*)nullptr);
         fx_publish(flags, ph, a.stamps);
     }
     // Ritz vectors of this row tile and their residual partials (k_si_ritz's per-row order)
@@ -1420,23 +1455,11 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
     }
     __syncthreads();
     if (row < a.n) a.Z[(size_t)row * 16 + q] = u * tot[q];
-    if (!a.guard) return;
-    // ---- the missed-eigenpair guard: x0 = g, x1 = P g, SI_GUARD_IT products of P C P
-    const double* xin = nullptr;
-    const double* pin = nullptr;
-    for (int step = 0; step < SI_GUARD_IT + 3; ++step) {
-        const int mode = step == 0 ? 0 : (step == 1 ? 1 : (step == SI_GUARD_IT + 2 ? 3 : 2));
-        if (mode == 3 && g != 0) break;
-        double* xo = a.gx + (size_t)(step & 1) * np;
-        double* po = a.gp + (size_t)(step & 1) * nt * SGF_W;
-        const u32 ph_prev = ph;
-        ++ph;
-        if (step > 0 && !fx_wait(flags, err, 0, 4, nt, ph_prev, &s_abort)) return;
-        fx_sig_step(a.C, a.ldc, a.n, Qb, Wb, xin, pin, nt, xo, po, a.theta, a.k, a.flag, mode, rt, X + 1024);
-        if (mode != 3) fx_publish(flags, ph, a.stamps);
-        xin = xo;
-        pin = po;
-    }
+    if (!a.guard || g != 0) return;
+    // the guard's test (k_sig_fused mode 3) on its last partials
+    if (!fx_wait(flags, err, 1, 4, nt, ph_g0 + SI_GUARD_IT + 2, &s_abort)) return;
+    fx_sig_step(a.C, a.ldc, a.n, Qb, Wb, nullptr, a.gp + (size_t)((SI_GUARD_IT + 1) & 1) * nt * SGF_W, nt, nullptr,
+                nullptr, a.theta, a.k, a.flag, 3, 0, X + 1024);
 }
 
 static int fsi_env(const char* name, int dflt)
@@ -1496,6 +1519,28 @@ struct FsiGraphEntry {
 std::mutex g_fsi_mu;
 std::vector<FsiGraphEntry> g_fsi_graphs;
 
+}  // namespace
+
+// Drop the cached graphs whose scratch lies in [p, p + bytes): called before
+// that memory is freed.  A graph replayed after its scratch was freed and
+// handed out again (even at the same address) was seen writing pointer-sized
+// garbage into the flag words (diag scratch hipMalloc'd per call).
+extern "C" void scc_fsi_forget(const void* p, size_t bytes)
+{
+    std::lock_guard<std::mutex> lk(g_fsi_mu);
+    const char* lo = (const char*)p;
+    for (size_t i = 0; i < g_fsi_graphs.size();) {
+        const char* s = (const char*)g_fsi_graphs[i].scr;
+        if (s >= lo && s < lo + bytes) {
+            (void)hipGraphExecDestroy(g_fsi_graphs[i].exec);
+            g_fsi_graphs.erase(g_fsi_graphs.begin() + i);
+        } else {
+            ++i;
+        }
+    }
+}
+
+namespace {
 hipStream_t fsi_capture_stream(int dev)
 {
     static hipStream_t cs[64] = {};
@@ -1677,6 +1722,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             if (g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m && g.passes == passes &&
                 g.live == live && g.guard == guard && g.engine == use_engine && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
                 ex = g.exec;
+                if (fsi_env("SCC_EIG_FSI_DEBUG", 0)) fprintf(stderr, "[scc fsi dbg] graph hit scr=%p flag=%p\n", scr, (void*)flag);
                 break;
             }
         if (!ex) {
@@ -1710,6 +1756,12 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     if (use_engine && (e = hipMemcpyAsync(&herr, fxerr, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess)
         return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (fsi_env("SCC_EIG_FSI_DEBUG", 0)) {
+        u32 h2[4] = {0, 0, 0, 0};
+        (void)hipMemcpy(h2, flag, sizeof(h2), hipMemcpyDeviceToHost);
+        fprintf(stderr, "[scc fsi dbg] scr=%p flag=%p h=%u reread=%u %u %u %u launched=%d ngraphs=%zu\n", scr,
+                (void*)flag, h, h2[0], h2[1], h2[2], h2[3], launched ? 1 : 0, g_fsi_graphs.size());
+    }
     if (herr) {
         // a hand-off of the persistent engine timed out (the device was shared and
         // its workgroups were not co-resident): the same solve, a launch per step

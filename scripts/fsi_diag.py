@@ -115,9 +115,37 @@ def stamps():
     print("path", path.value, flush=True)
 
 
+def repeat():
+    """the bitwise-test sequence many times: path and flag per call"""
+    import torch
+    from scconsensus_amd import _native as nat
+    L = nat.load()
+    os.environ["SCC_EIG_FSI"] = "1"
+    os.environ["SCC_EIG_SI_LOG"] = "1"
+    mats = []
+    for n, seed, vs in ((323, 5, 9), (323, 323, 11)):
+        lam = b_like(n, np.random.default_rng(seed))
+        V, _ = np.linalg.qr(np.random.default_rng(vs).standard_normal((n, n)))
+        mats.append((V * lam) @ V.T)
+    for it in range(12):
+        for mi, C in enumerate(mats):
+            for e in ("1", "0"):
+                os.environ["SCC_EIG_FSI_ENGINE"] = e
+                n = C.shape[0]
+                Cd = torch.tensor(C, dtype=torch.float64, device="cuda:0")
+                Z = torch.zeros(n * 16, dtype=torch.float64, device="cuda:0")
+                W = torch.zeros(16, dtype=torch.float64, device="cuda:0")
+                path = ctypes.c_int(-1)
+                L.scc_diag_eigen_topk(ctypes.c_void_p(Cd.data_ptr()), n, n, 15, ctypes.c_void_p(Z.data_ptr()),
+                                      ctypes.c_void_p(W.data_ptr()), ctypes.byref(path))
+                print(f"it={it} mat={mi} engine={e} path={path.value}", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1]
-    if what == "stamps":
+    if what == "repeat":
+        repeat()
+    elif what == "stamps":
         stamps()
     elif what == "eig":
         eig()
