@@ -287,7 +287,7 @@ __device__ __forceinline__ int se_count64(const double* dg, const double* e2, do
 // LDS; SC1: Y and theta are handed off to other workgroups (sc1 stores);
 // stamps: phase s_memtime stamps (nullptr: none).
 template <bool SC1, class HL>
-__device__ void se_syev(HL hload, int n, int k, double* __restrict__ Y, double* __restrict__ theta,
+__device__ __attribute__((always_inline)) void se_syev(HL hload, int n, int k, double* __restrict__ Y, double* __restrict__ theta,
                         u32* __restrict__ flag, double* sm, u64* stamps)
 {
     double(*Vr)[SE_N] = (double(*)[SE_N])(sm + SE_LDS_V);

@@ -1477,11 +1477,17 @@ static int fsi_segments() { return std::max(1, std::min(64, fsi_env("SCC_EIG_FSI
 static int fsi_passes() { return std::max(1, std::min(3, fsi_env("SCC_EIG_FSI_PASSES", 2))); }
 static int fsi_degree() { return std::max(2, std::min(16, fsi_env("SCC_EIG_FSI_DEG", 8))); }
 
+// Default: the filtered iteration for FSI_NMIN <= n <= FX_NPMAX, where the
+// persistent engine runs it (config B: 0.88 ms against the direct solver's
+// 1.35); larger n keep the block subspace iteration / direct solver.
+// SCC_EIG_FSI=0: never; =1: for every n >= FSI_NMIN (a launch per step above
+// FX_NPMAX).
 extern "C" int scc_fsi_wanted(int n)
 {
-    const int e = fsi_env("SCC_EIG_FSI", 0);  // (default off until measured on the GPU)
+    const int e = fsi_env("SCC_EIG_FSI", -1);
     if (e == 0) return 0;
-    return n >= FSI_NMIN;
+    if (e > 0) return n >= FSI_NMIN;
+    return n >= FSI_NMIN && (int)si_npad(n) <= FX_NPMAX && fsi_env("SCC_EIG_FSI_ENGINE", 1) != 0;
 }
 
 extern "C" size_t scc_fsi_scratch_doubles(int n)

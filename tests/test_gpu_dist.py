@@ -99,6 +99,7 @@ def test_eigensolver_sizes(eng, n, monkeypatch):
     SVD."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")  # the direct solvers (subspace iteration: its own tests)
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     rng = np.random.default_rng(100 + n)
     X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
     ds = eng.dataset_dense(X)
@@ -131,6 +132,7 @@ def test_eigensolver_rows_beyond_lds(eng, monkeypatch):
     """|U| = 2100: each workgroup's rows no longer fit its LDS (global row store)."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     rng = np.random.default_rng(11)
     n, N = 2100, 1200
     X = rng.standard_normal((n, N)) * np.linspace(3.0, 0.5, n)[:, None]
@@ -147,6 +149,7 @@ def test_rank_deficient_and_repeated(eng, monkeypatch):
     repeated eigenvalues inside the top 15, n = 90 and 300."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     for n in (90, 300):
         rng = np.random.default_rng(8 + n)
         N = 700
@@ -172,6 +175,7 @@ def test_eigensolver_workgroup_counts(eng, n, nwg, xcd, monkeypatch):
     hand-off (cross-XCD write-through or one-XCD L2), rows in LDS or in HBM."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     monkeypatch.setenv("SCC_EIG_NWG", str(nwg))
     monkeypatch.setenv("SCC_EIG_XCD", xcd)
     rng = np.random.default_rng(11)
@@ -192,6 +196,7 @@ def test_back_transformations_agree(eng, n, monkeypatch):
     k_tri_back (1) and the per-eigenpair one (0); all against the exact SVD."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     rng = np.random.default_rng(600 + n)
     X = rng.standard_normal((n, 800)) * np.linspace(3.0, 0.5, n)[:, None]
     X[: min(n, 12)] += rng.standard_normal((min(n, 12), 1)) * rng.standard_normal((1, 800)) * 3.0
@@ -216,6 +221,7 @@ def test_twisted_vectors_agree(eng, n, monkeypatch):
     ~3e-3 among eigenvalues 11..16) included."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     rng = np.random.default_rng(700 + n)
     X = rng.standard_normal((n, 900)) * np.linspace(1.0, 0.97, n)[:, None]  # a near-flat bulk
     X[: min(n, 10)] += rng.standard_normal((min(n, 10), 1)) * rng.standard_normal((1, 900)) * 3.0
@@ -235,6 +241,7 @@ def test_workgroup_count_bitwise(eng, monkeypatch):
     workgroups in the hand-off give the same distance bits."""
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     rng = np.random.default_rng(21)
     n = 323
     X = rng.standard_normal((n, 900)) * np.linspace(3.0, 0.5, n)[:, None]
@@ -298,6 +305,7 @@ def test_subspace_iteration(eng, n, monkeypatch, capfd):
     """Block subspace iteration (scc_subspace.hip, tried first for |U| >= 400)
     on a many-cluster spectrum: accepted (its residual test passes), equal to
     the exact SVD and to the direct solver, bit-identical from run to run."""
+    monkeypatch.setenv("SCC_EIG_FSI", "0")  # the block subspace iteration itself
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI_LOG", "1")
     X = _spiky(n, 3000, 40, 900 + n)
@@ -312,6 +320,7 @@ def test_subspace_iteration(eng, n, monkeypatch, capfd):
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(d1 - ref)) < 1e-5
     monkeypatch.setenv("SCC_EIG_SI", "0")
+    monkeypatch.setenv("SCC_EIG_FSI", "0")
     d0 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
     S0 = eng.last_pca_scores(X.shape[1])
     assert np.max(np.abs(d1 - d0)) < 1e-6
@@ -324,6 +333,7 @@ def test_subspace_iteration_falls_back(eng, case, monkeypatch, capfd):
     result fails its residual test and the direct solver's answer is returned.
     A Gram of rank < 64 (40 cells): whichever path answers, the distance is the
     exact SVD's."""
+    monkeypatch.setenv("SCC_EIG_FSI", "0")  # the block subspace iteration itself
     from scconsensus_amd import _native as nat
     monkeypatch.setenv("SCC_EIG_SI_LOG", "1")
     rng = np.random.default_rng(77)
@@ -349,6 +359,7 @@ def test_subspace_guard_catches_missed_eigenpair(eng, monkeypatch, capfd):
     block's rows >= 400 zeroed (test hook): the iteration never sees that
     block, every residual passes, and the deflated power check (flag bit 8)
     must reject the result so the direct solver answers."""
+    monkeypatch.setenv("SCC_EIG_FSI", "0")  # the block subspace iteration itself
     from scconsensus_amd import _native as nat
     rng = np.random.default_rng(12)
     n, N = 500, 3000
@@ -460,3 +471,18 @@ def test_filtered_guard_catches_missed_eigenpair(eng, monkeypatch, capfd, engine
     monkeypatch.delenv("SCC_EIG_SI_INIT_ROWS")
     d2 = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
     assert np.max(np.abs(d2 - ref)) < 1e-5
+
+
+@pytest.mark.parametrize("n", [130, 257, 323, 500, 672])
+def test_eigensolver_sizes_default_path(eng, n):
+    """The default route (the filtered subspace iteration in the persistent
+    engine for 128 <= |U| <= 672, the direct solver when it rejects) against
+    numpy's exact SVD, the same matrices as test_eigensolver_sizes."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(100 + n)
+    X = rng.standard_normal((n, 300)) * np.linspace(2.0, 0.5, n)[:, None]
+    ds = eng.dataset_dense(X)
+    g = np.arange(n)
+    dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(dist - ref)) < 1e-5
