@@ -772,6 +772,17 @@ extern "C" hipError_t scc_launch_fsi_cholinv(const double* G, int P, double shif
                                              hipStream_t st);
 extern "C" void scc_small_syev_prepare();
 
+// zero the engine's control words (numeric flags, error word, phase flags) in
+// one kernel: captured hipMemsetAsync nodes ahead of the engine were seen
+// leaving pointer-sized garbage in exactly those words on graph replays
+__global__ void k_fx_reset(u32* __restrict__ flag, u32* __restrict__ err, u32* __restrict__ fxflags, int nflags)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 4) flag[i] = 0u;
+    if (i == 0) *err = 0u;
+    for (int e = i; e < nflags; e += gridDim.x * blockDim.x) fxflags[e] = 0u;
+}
+
 __global__ void k_fsi_coef0(double* __restrict__ coef)
 {
     if (threadIdx.x < 4) coef[threadIdx.x] = threadIdx.x == 0 ? 1.0 : 0.0;
@@ -1632,11 +1643,9 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     };
     auto enqueue = [&](hipStream_t s) -> hipError_t {
         hipError_t e;
-        if ((e = hipMemsetAsync(flag, 0, sizeof(u32) * 4, s)) != hipSuccess) return e;
         if (use_engine) {
             // the filter loop in one persistent launch, then the Rayleigh-Ritz launches
-            if ((e = hipMemsetAsync(fxflags, 0, sizeof(u32) * FX_FS * 4 * nt, s)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(fxerr, 0, sizeof(u32), s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_fx_reset, dim3(8), dim3(256), 0, s, flag, fxerr, fxflags, (int)(FX_FS * 4 * nt));
             FxArgs fa;
             fa.C = C;
             fa.ldc = ldc;
@@ -1680,6 +1689,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             if (fa.rr) return hipGetLastError();
             return rayleigh_ritz(s);
         }
+        hipLaunchKernelGGL(k_fx_reset, dim3(1), dim3(64), 0, s, flag, fxerr, fxflags, 0);
         hipLaunchKernelGGL(k_fsi_coef0, dim3(1), dim3(64), 0, s, coef);  // slot 0: plain product {1, 0, 0, b = 0}
         hipLaunchKernelGGL(k_si_init, dim3((unsigned)((np * SI_B + 255) / 256)), dim3(256), 0, s, (int)np,
                            std::min(live, n), Ya);
@@ -1767,6 +1777,15 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         (void)hipMemcpy(h2, flag, sizeof(h2), hipMemcpyDeviceToHost);
         fprintf(stderr, "[scc fsi dbg] scr=%p flag=%p h=%u reread=%u %u %u %u launched=%d ngraphs=%zu\n", scr,
                 (void*)flag, h, h2[0], h2[1], h2[2], h2[3], launched ? 1 : 0, g_fsi_graphs.size());
+    }
+    if (herr && fsi_env("SCC_EIG_FSI_DEBUG", 0)) {
+        std::vector<u32> fl((size_t)4 * nt * FX_FS);
+        u32 f4[4] = {0, 0, 0, 0};
+        (void)hipMemcpy(fl.data(), fxflags, sizeof(u32) * fl.size(), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(f4, flag, sizeof(f4), hipMemcpyDeviceToHost);
+        fprintf(stderr, "[scc fsi dbg] hand-off abort: err=%u flag=%u %u %u %u; phases:", herr, f4[0], f4[1], f4[2], f4[3]);
+        for (size_t g = 0; g < (size_t)4 * nt; ++g) fprintf(stderr, " %u", fl[g * FX_FS]);
+        fprintf(stderr, "\n");
     }
     if (herr) {
         // a hand-off of the persistent engine timed out (the device was shared and
