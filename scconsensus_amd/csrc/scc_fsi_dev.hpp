@@ -109,70 +109,153 @@ __device__ __forceinline__ d4 cb_load(const double* Pa, int bi, int bj)
 // A: [64][CB_S] SPD on entry (lower part read; its upper blocks (0, 1..3) are the
 // level scratch); X: [64][CB_S] out; Ri: [64] scratch.  Every thread of the
 // 256-thread workgroup calls it.
-__device__ inline void fsi_cholinv_blk(double* A, double* X, double* Ri, int* s_bad)
+// every lane gets the value of lane 16 r + C (r: its own 16-lane row): DPP
+// row_newbcast, one VALU move per 32 bits, no SGPR round trip
+template <int C>
+__device__ __forceinline__ double cb_bcast_c(double x)
+{
+    return __builtin_amdgcn_mov_dpp(x, 0x150 | C, 0xf, 0xf, true);  // one v_mov_b64_dpp
+}
+__device__ __forceinline__ double cb_bcast(double x, int c)  // c: a constant after unrolling
+{
+    switch (c) {
+    case 0: return cb_bcast_c<0>(x);
+    case 1: return cb_bcast_c<1>(x);
+    case 2: return cb_bcast_c<2>(x);
+    case 3: return cb_bcast_c<3>(x);
+    case 4: return cb_bcast_c<4>(x);
+    case 5: return cb_bcast_c<5>(x);
+    case 6: return cb_bcast_c<6>(x);
+    case 7: return cb_bcast_c<7>(x);
+    case 8: return cb_bcast_c<8>(x);
+    case 9: return cb_bcast_c<9>(x);
+    case 10: return cb_bcast_c<10>(x);
+    case 11: return cb_bcast_c<11>(x);
+    case 12: return cb_bcast_c<12>(x);
+    case 13: return cb_bcast_c<13>(x);
+    case 14: return cb_bcast_c<14>(x);
+    default: return cb_bcast_c<15>(x);
+    }
+}
+
+// X_KK = L_KK^{-1} of diagonal block K (in A) into X, by one wave: lane l
+// holds row i = l & 15 of L_KK; lane j = l & 15 forms column j of the inverse,
+// w_r = (delta_rj - sum_{m<r} L_rm w_m) / L_rr, L_rm broadcast within 16 lanes
+__device__ __forceinline__ void cb_diag_inverse(const double* A, double* X, const double* Ri, int K)
+{
+    const int lane = threadIdx.x & 63, i = lane & 15, j = i;
+    double a[16], gk[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        a[c] = A[(16 * K + i) * CB_S + 16 * K + c];
+        gk[c] = Ri[16 * K + c];
+    }
+    double w[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        double sacc = (r == j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < r; ++m) sacc = fma(-cb_bcast(a[m], r), w[m], sacc);
+        w[r] = (r >= j) ? sacc * gk[r] : 0.0;
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[(16 * K + r) * CB_S + 16 * K + j] = w[r];
+    }
+}
+
+__device__ inline void fsi_cholinv_blk(double* A, double* X, double* Ri, int* s_bad, u64* st = nullptr)
 {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int ns = 0;
+    auto stamp = [&]() {
+        if (st && tid == 0) st[ns] = __builtin_amdgcn_s_memtime();
+        ++ns;
+    };
+    stamp();
 #pragma unroll
     for (int K = 0; K < 4; ++K) {
+        // (a) wave 0: block column K in one 16-step chain.  Lane l: c = l & 15,
+        // r = l >> 4; every 16-lane row keeps a copy of diagonal row 16K + c (so
+        // the multipliers L[16K + c][k] are a row_newbcast away in every row),
+        // and rows r >= 1 also carry panel row 16(K + r) + c below the block
         if (wv == 0) {
-            const int row = 16 * K + lane, rc = min(row, 63);
-            double a[16];
+            const int c = lane & 15, r = lane >> 4;
+            const int brow = 16 * (K + r) + c;
+            const bool below = r >= 1 && K + r < 4;
+            double d[16], bl[16], gk[16];
 #pragma unroll
-            for (int c = 0; c < 16; ++c) a[c] = A[rc * CB_S + 16 * K + c];
+            for (int q = 0; q < 16; ++q) {
+                d[q] = A[(16 * K + c) * CB_S + 16 * K + q];
+                bl[q] = A[min(brow, 63) * CB_S + 16 * K + q];
+            }
             bool bad = false;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                const double d = se_readlane(a[k], k);
-                bad |= !(d > 0.0);
-                const double dd = d > 0.0 ? d : 1.0;
+                const double pv = cb_bcast(d[k], k);
+                bad |= !(pv > 0.0);
+                const double dd = pv > 0.0 ? pv : 1.0;
                 double g = __builtin_amdgcn_rsq(dd);
                 g = g * fma(-0.5 * dd * g, g, 1.5);
-                const double l = (lane > k) ? a[k] * g : (lane == k ? dd * g : 0.0);
-                a[k] = l;
-                if (lane == 0) Ri[16 * K + k] = g;
+                gk[k] = g;
+                const double ld = (c > k) ? d[k] * g : (c == k ? dd * g : 0.0);
+                const double lb = bl[k] * g;
+                d[k] = ld;
+                bl[k] = lb;
 #pragma unroll
-                for (int c = k + 1; c < 16; ++c) a[c] = fma(-l, se_readlane(l, c), a[c]);
+                for (int q = k + 1; q < 16; ++q) {
+                    const double m = cb_bcast(ld, q);  // L[16K + q][k]
+                    d[q] = fma(-ld, m, d[q]);
+                    bl[q] = fma(-lb, m, bl[q]);
+                }
             }
-            if (row < 64) {
+            if (lane < 16) {
 #pragma unroll
-                for (int c = 0; c < 16; ++c) A[row * CB_S + 16 * K + c] = (lane >= c) ? a[c] : 0.0;
+                for (int q = 0; q < 16; ++q) A[(16 * K + c) * CB_S + 16 * K + q] = (c >= q) ? d[q] : 0.0;
+            }
+            if (below) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) A[brow * CB_S + 16 * K + q] = bl[q];
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) Ri[16 * K + k] = gk[k];
             }
             if (bad && lane == 0) *s_bad = 1;
         }
         __syncthreads();
-        // trailing blocks (I, J), K < J <= I <= 3, dealt over the waves
+        stamp();
+        // (b) wave 1: the inverse of the diagonal block (needed by the levels only);
+        // wave 0: the next block column's trailing update (look-ahead: it goes
+        // straight on to factor it); waves 2, 3: the other trailing blocks
+        if (wv == 1) cb_diag_inverse(A, X, Ri, K);
         int b = 0;
 #pragma unroll
         for (int J = K + 1; J < 4; ++J)
 #pragma unroll
-            for (int I = J; I < 4; ++I, ++b) {
-                if ((b & 3) != wv) continue;
+            for (int I = J; I < 4; ++I) {
+                bool mine;
+                if (J == K + 1) {
+                    mine = wv == 0;
+                } else {
+                    mine = (b & 1) + 2 == wv;
+                    ++b;
+                }
+                if (!mine) continue;
                 d4 acc = cb_load(A, I, J);
                 acc = cb_block_mm<true>(A, I, K, A, J, K, -1.0, acc);
                 cb_store(A, I, J, acc);
             }
-        __syncthreads();
     }
-    // diagonal blocks of X = L^{-1}: wave I, lane j = column j of block I
-    {
-        const int I = wv, j = lane & 15;
-        double w[16];
+    __syncthreads();
+    stamp();
+    // the zero blocks above the diagonal of X
+    if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            double s = (i == j) ? 1.0 : 0.0;
+        for (int J = 0; J < 4; ++J)
+            if (J > wv) {
 #pragma unroll
-            for (int m = 0; m < i; ++m) s = fma(-A[(16 * I + i) * CB_S + 16 * I + m], w[m], s);
-            w[i] = (i >= j) ? s * Ri[16 * I + i] : 0.0;
-        }
-        if (lane < 16) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) X[(16 * I + i) * CB_S + 16 * I + j] = w[i];
-        }
-#pragma unroll
-        for (int J = 0; J < 4; ++J)  // the zero blocks above the diagonal
-            if (J > I && lane < 16) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) X[(16 * I + i) * CB_S + 16 * J + j] = 0.0;
+                for (int r = 0; r < 16; ++r) X[(16 * wv + r) * CB_S + 16 * J + lane] = 0.0;
             }
     }
     __syncthreads();
@@ -339,75 +422,66 @@ __device__ __attribute__((always_inline)) void se_syev(HL hload, int n, int k, d
             if (r >= n && r == q + 4 * u) a[u] = pad;
     }
     if (tid == 0 && stamps) stamps[0] = __builtin_amdgcn_s_memtime();
-    // ---- tridiagonalisation (LAPACK dsytd2 order), column i: its owners write
-    // it to LDS, wave 0 forms the reflector, p = tau A22 v (4 threads per row),
-    // w = p - (tau/2)(p.v) v, A22 -= v w^T + w v^T in registers
+    // ---- tridiagonalisation (LAPACK dsytd2 order) by ONE wave, lane r holding
+    // row r of the matrix in registers: no workgroup barrier per column (the
+    // 4-thread-per-row version spent ~1.1 us a column on three of them).
+    // Column i: reflector from the lanes below the diagonal (one wave sum),
+    // v to LDS and back as broadcasts, p = tau A v (4 partial sums), w, and the
+    // rank-2 update of the trailing columns.  The matrix is staged through the
+    // LU region (row stride 65: a lane per row without bank conflicts).
+    {
+        double* Ms = LU;  // [64][65], dead until the inverse iteration
 #pragma unroll
-    for (int i = 0; i < SE_N - 2; ++i) {
-        constexpr int dummy = 0;
-        (void)dummy;
-        const int ui = i >> 2, qi = i & 3;
-        if (q == qi) {
-            if (r > i) colv[r] = a[ui];
-            if (r == i) dg[i] = a[ui];
-        }
-        __syncthreads();
-        if (wv == 0) {
-            const int rr = i + 1 + lane;
-            const double x = colv[min(rr, SE_N - 1)];
-            const double alpha = colv[i + 1];
-            const double sq = se_wave_sum((rr >= i + 2 && rr < SE_N) ? x * x : 0.0);
+        for (int u = 0; u < 16; ++u) Ms[r * 65 + q + 4 * u] = a[u];
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const double* Ms = LU;
+        double am[SE_N];
+#pragma unroll
+        for (int j = 0; j < SE_N; ++j) am[j] = Ms[lane * 65 + j];
+        double* wbuf = pv;  // w of the current column
+#pragma unroll
+        for (int i = 0; i < SE_N - 2; ++i) {
+            const double dii = se_readlane(am[i], i);  // (not "lane == i ? am[i]": that becomes am[lane])
+            if (lane == 0) dg[i] = dii;
+            const double x = (lane > i) ? am[i] : 0.0;
+            const double alpha = se_readlane(am[i], i + 1);
+            const double sq = se_wave_sum((lane > i + 1) ? x * x : 0.0);
             double beta = alpha, t = 0.0, scal = 0.0;
             if (sq > 0.0) {
                 beta = -copysign(sqrt(alpha * alpha + sq), alpha);
                 t = (beta - alpha) / beta;
                 scal = 1.0 / (alpha - beta);
             }
-            if (rr < SE_N) {
-                const double v = (rr == i + 1) ? 1.0 : x * scal;
-                vc[rr] = v;
-                Vr[i][rr] = v;
-            }
+            const double v = (lane == i + 1) ? 1.0 : ((lane > i + 1) ? x * scal : 0.0);
+            Vr[i][lane] = v;
             if (lane == 0) {
                 eo[i] = beta;
                 ta[i] = t;
             }
+            // p = tau A v over the trailing columns (v_j broadcast from LDS)
+            double p4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = i + 1; j < SE_N; ++j) p4[(j - i - 1) & 3] = fma(am[j], Vr[i][j], p4[(j - i - 1) & 3]);
+            const double p = t * ((p4[0] + p4[1]) + (p4[2] + p4[3]));
+            const double K = -0.5 * t * se_wave_sum((lane > i) ? p * v : 0.0);
+            const double w = (lane > i) ? fma(K, v, p) : 0.0;
+            wbuf[lane] = w;
+            // A22 -= v w^T + w v^T (rows <= i have v = w = 0: unchanged)
+#pragma unroll
+            for (int j = i + 1; j < SE_N; ++j) am[j] = fma(-v, wbuf[j], fma(-w, Vr[i][j], am[j]));
         }
-        __syncthreads();
-        const double t = ta[i];
-        double vv[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const double v = vc[q + 4 * u];
-            vv[u] = (q + 4 * u > i) ? v : 0.0;
+        const double d62 = se_readlane(am[SE_N - 2], SE_N - 2), e62 = se_readlane(am[SE_N - 2], SE_N - 1);
+        const double d63 = se_readlane(am[SE_N - 1], SE_N - 1);
+        if (lane == 0) {
+            dg[SE_N - 2] = d62;
+            eo[SE_N - 2] = e62;
+            dg[SE_N - 1] = d63;
+            eo[SE_N - 1] = 0.0;
+            ta[SE_N - 2] = 0.0;
+            ta[SE_N - 1] = 0.0;
         }
-        double part = 0.0;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) part = fma(a[u], vv[u], part);
-        part += scc_xor_lane_f64<1>(part);
-        part += scc_xor_lane_f64<2>(part);
-        if (q == 0 && r > i) pv[r] = t * part;
-        __syncthreads();
-        const int rr = i + 1 + lane;
-        const double K = -0.5 * t * se_wave_sum(rr < SE_N ? pv[min(rr, SE_N - 1)] * vc[min(rr, SE_N - 1)] : 0.0);
-        const double vr = (r > i) ? vc[r] : 0.0;
-        const double wr = (r > i) ? fma(K, vr, pv[r]) : 0.0;
-        double pw[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) pw[u] = pv[q + 4 * u];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const double wc = (q + 4 * u > i) ? fma(K, vv[u], pw[u]) : 0.0;
-            a[u] = fma(-vr, wc, fma(-wr, vv[u], a[u]));
-        }
-    }
-    if (q == 2 && r == SE_N - 2) dg[SE_N - 2] = a[15];
-    if (q == 2 && r == SE_N - 1) eo[SE_N - 2] = a[15];
-    if (q == 3 && r == SE_N - 1) dg[SE_N - 1] = a[15];
-    if (tid == 0) {
-        eo[SE_N - 1] = 0.0;
-        ta[SE_N - 2] = 0.0;
-        ta[SE_N - 1] = 0.0;
     }
     __syncthreads();
     if (tid == 0 && stamps) stamps[1] = __builtin_amdgcn_s_memtime();
@@ -489,35 +563,46 @@ __device__ __attribute__((always_inline)) void se_syev(HL hload, int n, int k, d
         double* fu = fdr + SE_N;
         double* fu2 = fu + SE_N;
         double* fl = fu2 + SE_N;
-        double* fp = fl + SE_N;
         double* y = Yt[qq];
         const double tiny = kSeEps * tnorm + 1e-300;
+        // (LDS operands staged in registers 8 steps at a time: a load behind a
+        // store of the same array would otherwise wait at every step)
         double dcur = dg[0] - lam, ucur = eo[0];
+        u64 pmask = 0;
 #pragma unroll
-        for (int i = 0; i < SE_N - 1; ++i) {
-            const double li = eo[i], dn = dg[i + 1] - lam, un = (i < SE_N - 2) ? eo[i + 1] : 0.0;
-            const bool piv = fabs(dcur) < fabs(li);
-            const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
-            const double den = piv ? li : dc;
-            // (piv ? dc : li) / den through a refined hardware reciprocal (a few ulp)
-            const double r0 = __builtin_amdgcn_rcp(den);
-            const double rd = fma(fma(-den, r0, 1.0), r0, r0);
-            const double f = (piv ? dc : li) * rd;
-            fl[i] = f;
-            fdr[i] = rd;
-            const double ua = piv ? dn : ucur, ub = piv ? ucur : dn;
-            fu[i] = ua;
-            fu2[i] = piv ? un : 0.0;
-            fp[i] = piv ? 1.0 : 0.0;
-            dcur = fma(-f, ua, ub);
-            ucur = piv ? -f * un : un;
+        for (int i0 = 0; i0 < SE_N - 1; i0 += 8) {
+            double ev[9], dv[8];
+#pragma unroll
+            for (int u = 0; u < 9; ++u) ev[u] = eo[min(i0 + u, SE_N - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) dv[u] = dg[min(i0 + u + 1, SE_N - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u;
+                if (i >= SE_N - 1) break;  // compile-time
+                const double li = ev[u], dn = dv[u] - lam, un = (i < SE_N - 2) ? ev[u + 1] : 0.0;
+                const bool piv = fabs(dcur) < fabs(li);
+                const double dc = (!piv && dcur == 0.0) ? tiny : dcur;
+                const double den = piv ? li : dc;
+                // (piv ? dc : li) / den through a refined hardware reciprocal (a few ulp)
+                const double r0 = __builtin_amdgcn_rcp(den);
+                const double rd = fma(fma(-den, r0, 1.0), r0, r0);
+                const double f = (piv ? dc : li) * rd;
+                fl[i] = f;
+                fdr[i] = rd;
+                const double ua = piv ? dn : ucur, ub = piv ? ucur : dn;
+                fu[i] = ua;
+                fu2[i] = piv ? un : 0.0;
+                pmask |= (u64)(piv ? 1 : 0) << i;
+                dcur = fma(-f, ua, ub);
+                ucur = piv ? -f * un : un;
+            }
         }
         if (dcur == 0.0) dcur = tiny;
         fdr[SE_N - 1] = 1.0 / dcur;
         fu[SE_N - 1] = 0.0;
         fu2[SE_N - 1] = 0.0;
-        // the iterate in LDS (this lane's row of Yt); fixed-length unrolled loops
-        // let the compiler issue the loads ahead of each dependent chain
+        // the iterate in LDS (this lane's row of Yt)
 #pragma unroll
         for (int i = 0; i < SE_N; ++i) {
             unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)qq * 40503u + 12345u);
@@ -529,21 +614,49 @@ __device__ __attribute__((always_inline)) void se_syev(HL hload, int n, int k, d
         for (int iter = 0; iter < 2; ++iter) {
             double bi = y[0];  // y <- L^-1 P y
 #pragma unroll
-            for (int i = 0; i < SE_N - 1; ++i) {
-                const bool piv = fp[i] != 0.0;
-                const double bn = y[i + 1];
-                const double xa = piv ? bn : bi, xb = piv ? bi : bn;
-                y[i] = xa;
-                bi = fma(-fl[i], xa, xb);
+            for (int i0 = 0; i0 < SE_N - 1; i0 += 8) {
+                double yv[8], lv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    yv[u] = y[min(i0 + u + 1, SE_N - 1)];
+                    lv[u] = fl[min(i0 + u, SE_N - 2)];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u;
+                    if (i >= SE_N - 1) break;
+                    const bool piv = (pmask >> i) & 1;
+                    const double bn = yv[u];
+                    const double xa = piv ? bn : bi, xb = piv ? bi : bn;
+                    yv[u] = xa;  // (the new y[i])
+                    bi = fma(-lv[u], xa, xb);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (i0 + u < SE_N - 1) y[i0 + u] = yv[u];
             }
             y[SE_N - 1] = bi;
             double z1 = 0.0, z2 = 0.0;  // y <- U^-1 y from the bottom
 #pragma unroll
-            for (int i = SE_N - 1; i >= 0; --i) {
-                const double z0 = fma(-fu[i], z2, fma(-fu2[i], z1, y[i])) * fdr[i];
-                y[i] = z0;
-                z1 = z2;
-                z2 = z0;
+            for (int i1 = SE_N - 1; i1 >= 0; i1 -= 8) {
+                double yv[8], a1[8], a2[8], dr[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i1 - u;
+                    yv[u] = y[i];
+                    a1[u] = fu[i];
+                    a2[u] = fu2[i];
+                    dr[u] = fdr[i];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const double z0 = fma(-a1[u], z2, fma(-a2[u], z1, yv[u])) * dr[u];
+                    yv[u] = z0;
+                    z1 = z2;
+                    z2 = z0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) y[i1 - u] = yv[u];
             }
             double mx = 0.0, sacc = 0.0;
 #pragma unroll
@@ -553,7 +666,13 @@ __device__ __attribute__((always_inline)) void se_syev(HL hload, int n, int k, d
             for (int i = 0; i < SE_N; ++i) sacc = fma(y[i] * sc, y[i] * sc, sacc);
             const double inv = sc / sqrt(sacc);
 #pragma unroll
-            for (int i = 0; i < SE_N; ++i) y[i] *= inv;
+            for (int i0 = 0; i0 < SE_N; i0 += 16) {
+                double yv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) yv[u] = y[i0 + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) y[i0 + u] = yv[u] * inv;
+            }
         }
     }
     __syncthreads();

@@ -18,6 +18,7 @@
 #include "scc_common.hpp"
 #include "scc_fsi_dev.hpp"
 #include "scc.h"
+#include <cstdio>
 #include <mutex>
 
 // phase stamps of the last k_small_syev (s_memtime at the start of each phase;
@@ -203,8 +204,10 @@ __global__ void __launch_bounds__(64) k_fsi_cholinv64(const double* __restrict__
 }
 
 // T = R^{-1} = (L^{-1})^T for G + shift I = L L^T, one 256-thread workgroup
+__device__ u64 g_cb_stamps[32];  // diagnostic: k_fsi_cholinv_blk phase stamps (SCC_FSI_CHOL_STAMPS=1)
 __global__ void __launch_bounds__(256) k_fsi_cholinv_blk(const double* __restrict__ G, double shift_rel,
-                                                        double* __restrict__ T, u32* __restrict__ flag)
+                                                        double* __restrict__ T, u32* __restrict__ flag,
+                                                        u64* __restrict__ st)
 {
     __shared__ double A[64 * CB_S];
     __shared__ double X[64 * CB_S];
@@ -227,7 +230,8 @@ __global__ void __launch_bounds__(256) k_fsi_cholinv_blk(const double* __restric
         A[i * CB_S + j] = G[e] + (i == j ? shift : 0.0);
     }
     __syncthreads();
-    fsi_cholinv_blk(A, X, Ri, &s_bad);
+    fsi_cholinv_blk(A, X, Ri, &s_bad, st);
+    if (st && threadIdx.x == 0) st[31] = __builtin_amdgcn_s_memtime();
     // T[i][j] = X[j][i]
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -247,8 +251,15 @@ extern "C" hipError_t scc_launch_fsi_cholinv(const double* G, int P, double shif
                                              hipStream_t st)
 {
     if (P != 64) return hipErrorInvalidValue;
-    if (cholinv_variant())
-        hipLaunchKernelGGL(k_fsi_cholinv_blk, dim3(1), dim3(256), 0, st, G, shift_rel, T, flag);
+    if (cholinv_variant()) {
+        u64* stp = nullptr;
+        const char* e = getenv("SCC_FSI_CHOL_STAMPS");
+        if (e && *e == '1') {
+            void* sp = nullptr;
+            if (hipGetSymbolAddress(&sp, HIP_SYMBOL(g_cb_stamps)) == hipSuccess) stp = (u64*)sp;
+        }
+        hipLaunchKernelGGL(k_fsi_cholinv_blk, dim3(1), dim3(256), 0, st, G, shift_rel, T, flag, stp);
+    }
     else
         hipLaunchKernelGGL(k_fsi_cholinv64, dim3(1), dim3(64), 0, st, G, shift_rel, T, flag);
     return hipGetLastError();
@@ -266,7 +277,17 @@ extern "C" SCC_API int scc_diag_cholinv(const double* G, int P, double shift_rel
                                                                        double* T, unsigned* flag)
 {
     if (scc_launch_fsi_cholinv(G, P, shift_rel, T, flag, nullptr) != hipSuccess) return 1;
-    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    const char* e = getenv("SCC_FSI_CHOL_STAMPS");
+    if (e && *e == '1') {
+        u64 h[32];
+        if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cb_stamps), sizeof(h)) == hipSuccess) {
+            fprintf(stderr, "[scc chol stamps] cycles from start:");
+            for (int i = 1; i < 14; ++i) fprintf(stderr, " %llu", (unsigned long long)(h[i] - h[0]));
+            fprintf(stderr, " end %llu\n", (unsigned long long)(h[31] - h[0]));
+        }
+    }
+    return 0;
 }
 
 extern "C" SCC_API int scc_diag_small_syev_stamps(unsigned long long* out)
