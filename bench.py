@@ -67,6 +67,8 @@ def _args(argv=None):
                     help="scc_de_run then scc_distance (two C calls) instead of the fused scc_de_distance")
     ap.add_argument("--mode", choices=["shard", "jobs"], default="shard",
                     help="shard: ONE job over all ranks (strong scaling); jobs: one job per rank (weak scaling)")
+    ap.add_argument("--de", choices=["fast", "slow"], default="fast",
+                    help="reclusterDEConsensusFast (default) or reclusterDEConsensus (SLOW: every gene for every pair)")
     ap.add_argument("--route", choices=["ranks", "devices"], default="ranks",
                     help="ranks: one process per GPU (torch.distributed / RCCL); devices: one process over a device "
                          "list inside libscc (the R drop-in's nCores route)")
@@ -249,8 +251,10 @@ def devices_route(a, d, code, K, devices, steps, warmup):
         else:
             ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
 
+        mode = nat.SCC_DE_SLOW if getattr(a, "de", "fast") == "slow" else nat.SCC_DE_FAST
+
         def step():
-            return eng.de_distance(ds, code, K, nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)[0]
+            return eng.de_distance(ds, code, K, mode, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)[0]
 
         for _ in range(max(1, warmup)):
             r = step()
@@ -330,10 +334,12 @@ def main():
         else:
             gene_w = np.bincount(d.indices, minlength=d.G)
 
+    de_mode = nat.SCC_DE_SLOW if a.de == "slow" else nat.SCC_DE_FAST
+
     def step(dist_out=0):
         """dist_out 0: the distance stays in HBM; a host array: streamed into it."""
         if multi:  # one job: gene row-blocks + record all-gather, PCA over cell blocks, this rank's columns
-            r = sharded.de_sharded(eng, ds, code, K, dist, tdev, fetch="union", weights=gene_w)
+            r = sharded.de_sharded(eng, ds, code, K, dist, tdev, fetch="union", weights=gene_w, mode=de_mode)
             if dist_out is None or isinstance(dist_out, int):
                 sharded.distance_sharded(eng, ds, r.union, dist, tdev, device_out_ptr=0)
             else:
@@ -343,7 +349,7 @@ def main():
                                                                                  - lo * (2 * ds.N - lo - 1) // 2])
             return r
         if a.split_calls:  # scc_de_run, then scc_distance on the returned union
-            r = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")
+            r = eng.de_run(ds, code, K, de_mode, fetch="union")
             if isinstance(dist_out, int):
                 eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
             else:
@@ -351,9 +357,9 @@ def main():
             return r
         # scc_de_distance: the same two stages in one C call
         if isinstance(dist_out, int):
-            r, _ = eng.de_distance(ds, code, K, nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
+            r, _ = eng.de_distance(ds, code, K, de_mode, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)
         else:
-            r, _ = eng.de_distance(ds, code, K, nat.SCC_DE_FAST, nat.SCC_DIST_PCA_EUCLID, out=dist_out)
+            r, _ = eng.de_distance(ds, code, K, de_mode, nat.SCC_DIST_PCA_EUCLID, out=dist_out)
         return r
 
     def timed(nsteps, **kw):
@@ -508,7 +514,7 @@ def main():
         dist.barrier()
     out = {
         "metric": f"end-to-end DE+distance cell-pairs/sec at config {a.config}"
-                  + (" (26k PBMC shape)" if a.config == "B" else ""),
+                  + (" (26k PBMC shape)" if a.config == "B" else "") + (" [SLOW DE]" if a.de == "slow" else ""),
         "value": value,
         "unit": "cell-pairs/s",
         "n_gpus": world,
@@ -522,7 +528,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY §8d NB log1p generator" + (", seed per rank)" if not shard else ")"),
-        "config": {"workload": f"config {a.config}: reclusterDEConsensusFast DE (all {P} pairs) + PCA15 "
+        "config": {"workload": f"config {a.config}: reclusterDEConsensus{'' if a.de == 'slow' else 'Fast'} DE "
+                               f"(all {P} pairs) + PCA15 "
                                f"Euclidean dist, {d.N} cells x {d.G} genes, K={K}",
                    "cells": d.N, "genes": d.G, "clusters": K, "pairs": P, "nnz": nnz, "union": nu,
                    "parallelism": (f"devices{len(devices)}" if route_devices and len(devices) > 1

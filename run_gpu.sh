@@ -35,6 +35,9 @@ for s in "$@"; do
     benchD) step benchD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchC) step benchC 900 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchE) step benchE 900 python bench.py --config E --no-cpu-baseline --steps 3 --warmup 2 ;;
+    benchBslow) step benchBslow 600 python bench.py --de slow --no-cpu-baseline --no-transfers --no-pearson --steps 10 --warmup 3 ;;
+    benchDslow) step benchDslow 900 python bench.py --config D --de slow --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
+    benchdev) SCC_BENCH_DEVICES=0,0 step benchdev 600 python bench.py --route devices --no-cpu-baseline --no-transfers --no-pearson --steps 10 --warmup 3 ;;
     dbgx) AMD_LOG_LEVEL=1 step dbgx 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_exchange.py -x -v --timeout 120 --timeout-method thread ;;
     sticky) AMD_LOG_LEVEL=2 step sticky 300 python -u scripts/dbg_sticky.py ;;
     fsi) step fsi 600 python -u -m pytest tests/test_gpu_fsi.py tests/test_gpu_regress.py tests/test_gpu_devices.py -v --timeout 120 --timeout-method thread ;;
