@@ -409,7 +409,15 @@ def main():
         "eig_tridiag": ("mfma", 4.0 / 3.0 * nu ** 3, "k_tridiag"),
         "gram": ("mfma", 2.0 * d.N * nu * nu / 2 / world, "k_gram_f64"),
     }
-    if nu >= 400 and stage_ms.get("eig_vec", 0.0) < 0.02:
+    if 128 <= nu <= 1024 and stage_ms.get("eig_vec", 0.0) < 0.02:
+        # the filtered subspace iteration in one persistent launch answered
+        # (scc_subspace.hip k_fsi_engine): 5 segments of 8 products + the
+        # Rayleigh-Ritz product of C (n x n) by the 64-column block, 13 Grams
+        # of the block; no k_tridiag at size n
+        alg["eig_tridiag"] = ("mfma", 41 * 2.0 * nu * nu * 64 + 13 * 2.0 * nu * 64 * 64,
+                              "eigen stage: filtered subspace iteration in one persistent launch (k_fsi_engine: "
+                              "41 block products, 12 CholQR passes, Rayleigh-Ritz and the guard)")
+    elif nu >= 400 and stage_ms.get("eig_vec", 0.0) < 0.02:
         # (eig_vec is the gap between two events recorded back to back when the
         # subspace iteration answered: a few microseconds, never the 0.3+ ms of
         # the direct solver's vectors)

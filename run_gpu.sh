@@ -30,6 +30,8 @@ for s in "$@"; do
     benchq2) step benchq2 600 python bench.py --no-cpu-baseline --no-transfers --steps 20 --warmup 5 ;;
     profq) step profq 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profq -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 2 ;;
     pmcB) step pmcB 600 bash scripts/pmc_traffic.sh B ;;
+    profD) step profD 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profD -o run --output-format csv -- python3 bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
+    profE) step profE 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profE -o run --output-format csv -- python3 bench.py --config E --no-cpu-baseline --steps 2 --warmup 1 ;;
     pmcD) step pmcD 900 bash scripts/pmc_traffic.sh D ;;
     benchsplit) step benchsplit 600 python bench.py --no-cpu-baseline --no-transfers --steps 20 --warmup 5 --split-calls ;;
     benchD) step benchD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;

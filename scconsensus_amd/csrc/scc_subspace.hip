@@ -816,7 +816,8 @@ __global__ void k_fsi_coef0(double* __restrict__ coef)
 // otherwise idle device; every poll is bounded: on a time-out (or another
 // workgroup's) err is set and the host reruns the solve on the launch path.
 #define FX_FS 32        // flag stride (u32): one 128-B line per workgroup
-#define FX_NPMAX 672    // C tile (16 x np doubles) + the Cholesky's 2 x 64 x CB_S in LDS
+#define FX_NPRES 672    // C tile (16 x np doubles) and the Cholesky's 2 x 64 x CB_S side by side in LDS
+#define FX_NPMAX 1024   // above FX_NPRES the Cholesky borrows the C tile's LDS (reloaded after each CholQR)
 #define FX_SPIN (1u << 22)
 #define FX_LB 12  // k-steps per operand load batch (the MFMA order is k_fsi_mul's whatever the batch)
 
@@ -1075,19 +1076,27 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
     u32* const err = a.err;
     const int g = blockIdx.x, rt = g >> 2, cq = g & 3;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // LDS: np <= FX_NPRES  [C tile][A: Cholesky][X: L^-1 / reduction scratch][Ri]
+    //      np >  FX_NPRES  [C tile][reduction scratch][Ri], A and X over the C tile
+    //                      during a CholQR pass (the tile is reloaded after it)
+    const bool cs_alias = np > FX_NPRES;
     double* Cs = sm;                        // [np][16]: Cs[k * 16 + i] = C[16 rt + i][k]
-    double* A = Cs + (size_t)16 * np;       // [64][CB_S] Cholesky
-    double* X = A + 64 * CB_S;              // [64][CB_S] L^{-1}; product reduction scratch
-    double* Ri = X + 64 * CB_S;             // [64]
+    double* A = cs_alias ? sm : Cs + (size_t)16 * np;  // [64][CB_S] Cholesky
+    double* X = A + 64 * CB_S;              // [64][CB_S] L^{-1}
+    double* red = cs_alias ? Cs + (size_t)16 * np : X;  // product / Gram reduction scratch (768 doubles)
+    double* Ri = cs_alias ? red + 768 : X + 64 * CB_S;  // [64]
     const size_t blk = (size_t)np * SI_B;
     if (tid == 0) {
         s_abort = 0;
         s_bad = 0;
     }
-    for (int e = tid; e < 16 * np; e += 256) {
-        const int k = e >> 4, r = 16 * rt + (e & 15);
-        Cs[e] = (k < a.n && r < a.n) ? a.C[(size_t)k * a.ldc + r] : 0.0;
-    }
+    auto load_cs = [&]() {
+        for (int e = tid; e < 16 * np; e += 256) {
+            const int k = e >> 4, r = 16 * rt + (e & 15);
+            Cs[e] = (k < a.n && r < a.n) ? a.C[(size_t)k * a.ldc + r] : 0.0;
+        }
+    };
+    load_cs();
     if (g == 0 && tid < 4) a.coef[tid] = tid == 0 ? 1.0 : 0.0;  // slot 0: the plain product
     u32 ph = 0;
     // the start block (k_si_init): this workgroup's tile into slot 0
@@ -1120,7 +1129,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
                 // g -> (ci, cj), ci <= cj: 0..3 (0, j), 4..6 (1, j), 7..8 (2, j), 9 (3, 3)
                 const int ci = g < 4 ? 0 : (g < 7 ? 1 : (g < 9 ? 2 : 3));
                 const int cj = g < 4 ? g : (g < 7 ? g - 3 : (g < 9 ? g - 5 : 3));
-                const d4 acc = fx_gram(Y, Y, np, ci, cj, X);
+                const d4 acc = fx_gram(Y, Y, np, ci, cj, red);
                 if (wv == 0) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
@@ -1187,6 +1196,10 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
             ph_src = ph;
             slot_src = dst;
         }
+        if (cs_alias) {  // the Cholesky used the C tile's LDS
+            load_cs();
+            __syncthreads();
+        }
         return true;
     };
     auto other = [](int x, int y) { return 3 - x - y; };  // the slot that is neither x nor y
@@ -1206,7 +1219,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         // (W overwrites the slot the last CholQR pass but one wrote: the row's other
         // workgroups must be past their applies, which read it)
         if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
-        d4 w_own = fx_product<false>(Cs, np, a.Yb + sQ * blk, nullptr, 0.0, cq, X);
+        d4 w_own = fx_product<false>(Cs, np, a.Yb + sQ * blk, nullptr, 0.0, cq, red);
         if (wv == 0) {
             double dp = 0.0, dq = 0.0;
 #pragma unroll
@@ -1262,7 +1275,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         for (int r = 0; r < 4; ++r) y1_own[r] = fma(s2b, w_own[r], -q_own[r]);
         // Y2: operand (2/b) W - Q from slots sW, sQ; epilogue on Y1 (x) and Q (z)
         {
-            const d4 acc = fx_product<true>(Cs, np, a.Yb + sQ * blk, a.Yb + sW * blk, s2b, cq, X);
+            const d4 acc = fx_product<true>(Cs, np, a.Yb + sQ * blk, a.Yb + sW * blk, s2b, cq, red);
             if (wv == 0) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -1279,7 +1292,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
             const u32 ph_in = ph;
             ++ph;
             if (!fx_wait(flags, err, cq, 4, nt, ph_in, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
-            const d4 acc = fx_product<false>(Cs, np, a.Yb + s_cur * blk, nullptr, 0.0, cq, X);
+            const d4 acc = fx_product<false>(Cs, np, a.Yb + s_cur * blk, nullptr, 0.0, cq, red);
             d4 nxt;
             if (wv == 0) {
 #pragma unroll
@@ -1323,7 +1336,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
         ++ph;
         if (!fx_wait(flags, err, cq, 4, nt, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
         if (!fx_wait(flags, err, 4 * rt, 1, 4, phQ, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
-        const d4 acc = fx_product<false>(Cs, np, Qb, nullptr, 0.0, cq, X);
+        const d4 acc = fx_product<false>(Cs, np, Qb, nullptr, 0.0, cq, red);
         if (wv == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -1337,7 +1350,7 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
     if (g < 16) {
         if (!fx_wait(flags, err, 0, 1, nwg, phW, &s_abort)) return; fx_stamp(a.stamps, 2 * ph);
         const int ci = g >> 2, cj = g & 3;
-        const d4 acc = fx_gram(Qb, Wb, np, ci, cj, X);
+        const d4 acc = fx_gram(Qb, Wb, np, ci, cj, red);
         if (wv == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -1488,9 +1501,9 @@ static int fsi_segments() { return std::max(1, std::min(64, fsi_env("SCC_EIG_FSI
 static int fsi_passes() { return std::max(1, std::min(3, fsi_env("SCC_EIG_FSI_PASSES", 2))); }
 static int fsi_degree() { return std::max(2, std::min(16, fsi_env("SCC_EIG_FSI_DEG", 8))); }
 
-// Default: the filtered iteration for FSI_NMIN <= n <= FX_NPMAX, where the
-// persistent engine runs it (config B: 0.88 ms against the direct solver's
-// 1.35); larger n keep the block subspace iteration / direct solver.
+// Default: the filtered iteration for FSI_NMIN <= n <= FX_NPMAX (1024), where
+// the persistent engine runs it (config B: 0.77 ms against the direct solver's
+// 1.35, C 0.90); larger n keep the block subspace iteration / direct solver.
 // SCC_EIG_FSI=0: never; =1: for every n >= FSI_NMIN (a launch per step above
 // FX_NPMAX).
 extern "C" int scc_fsi_wanted(int n)
@@ -1516,14 +1529,15 @@ static bool fx_usable(int n)
 }
 static size_t fx_lds_bytes(int np)
 {
-    return sizeof(double) * std::max((size_t)16 * np + 2 * 64 * CB_S + 64, (size_t)SE_LDS_TOTAL);
+    const size_t own = np > FX_NPRES ? (size_t)16 * np + 768 + 64 : (size_t)16 * np + 2 * 64 * CB_S + 64;
+    return sizeof(double) * std::max(own, (size_t)SE_LDS_TOTAL);
 }
 static void fx_prepare()
 {
     static std::once_flag once;
     std::call_once(once, [] {
         (void)hipFuncSetAttribute((const void*)k_fsi_engine, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)fx_lds_bytes(FX_NPMAX));
+                                  (int)std::max(fx_lds_bytes(FX_NPRES), fx_lds_bytes(FX_NPMAX)));
     });
 }
 

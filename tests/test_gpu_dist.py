@@ -473,7 +473,7 @@ def test_filtered_guard_catches_missed_eigenpair(eng, monkeypatch, capfd, engine
     assert np.max(np.abs(d2 - ref)) < 1e-5
 
 
-@pytest.mark.parametrize("n", [130, 257, 323, 500, 672])
+@pytest.mark.parametrize("n", [130, 257, 323, 500, 672, 700, 1000])
 def test_eigensolver_sizes_default_path(eng, n):
     """The default route (the filtered subspace iteration in the persistent
     engine for 128 <= |U| <= 672, the direct solver when it rejects) against

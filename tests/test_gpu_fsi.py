@@ -124,7 +124,7 @@ def test_filtered_subspace_on_b_like_spectrum(lib):
     np.testing.assert_allclose(Z.T @ Z, np.eye(k), atol=1e-10)
 
 
-@pytest.mark.parametrize("n", [323, 130, 500])
+@pytest.mark.parametrize("n", [323, 130, 500, 845])
 def test_engine_bitwise_equals_launch_path(lib, monkeypatch, n):
     """The persistent engine (one launch for the whole filter loop) keeps every
     sum of the launch-per-step path in the same order: Z and W bit-identical,
@@ -146,8 +146,8 @@ def test_engine_bitwise_equals_launch_path(lib, monkeypatch, n):
     if n == 323:
         assert out["1"][0] == 3, "the persistent engine did not answer"
         assert out["0"][0] == 2
-    else:
-        assert out["1"][0] == out["0"][0] == 0
+    else:  # the same verdict (accepted by both, or rejected by both)
+        assert {out["1"][0], out["0"][0]} in ({3, 2}, {0})
     assert np.array_equal(out["1"][1], out["0"][1])
     assert np.array_equal(out["1"][2], out["0"][2])
 
