@@ -42,6 +42,13 @@ for s in "$@"; do
     benchdev) SCC_BENCH_DEVICES=0,0 step benchdev 600 python bench.py --route devices --no-cpu-baseline --no-transfers --no-pearson --steps 10 --warmup 3 ;;
     dbgx) AMD_LOG_LEVEL=1 step dbgx 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_exchange.py -x -v --timeout 120 --timeout-method thread ;;
     sticky) AMD_LOG_LEVEL=2 step sticky 300 python -u scripts/dbg_sticky.py ;;
+    rank) step rank 600 python -u -m pytest tests/test_gpu_rank_mfma.py tests/test_gpu_de.py -x -v --timeout 200 --timeout-method thread ;;
+    rkstB) SCC_RW_DEBUG=7 step rkstB 300 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
+    rkstD) SCC_RW_DEBUG=7 step rkstD 600 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 1 --warmup 1 ;;
+    rkDslow) SCC_RW_DEBUG=7 step rkDslow 900 python bench.py --config D --de slow --no-cpu-baseline --no-transfers --no-pearson --steps 1 --warmup 1 ;;
+    rkD256) SCC_RANK_MFMA_MIN=256 step rkD256 600 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
+    rkD128) SCC_RANK_MFMA_MIN=128 step rkD128 600 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
+    rkC256) SCC_RANK_MFMA_MIN=256 step rkC256 600 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
     fsi) step fsi 600 python -u -m pytest tests/test_gpu_fsi.py tests/test_gpu_regress.py tests/test_gpu_devices.py -v --timeout 120 --timeout-method thread ;;
     fsiguard) step fsiguard 600 python -u -m pytest tests/test_gpu_dist.py -k "guard" -v --timeout 120 --timeout-method thread ;;
     benchfsi) SCC_EIG_FSI=1 SCC_EIG_SI_LOG=1 step benchfsi 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;

@@ -67,6 +67,7 @@ struct ScRankLaunch {
     int wv_lo, wv_hi;      // wave kernel launch: genes with wv_lo < tested pairs <= wv_hi
     int wv_base;           // ... and their tested pairs [wv_base, wv_base + 64 * slots)
     int wv_filter;         // 0: one launch holds every gene (no per-bucket class test)
+    int rw_mfma;           // K <= 64: the wave buckets' pair counts on the int8 matrix cores (k_rank_mfma)
     ScRankItem* fatbk;     // [fat_cap] buckets of > 64 distinct values (re-split into sub-buckets)
     int4* fatg;            // [G] {gene, first fatbk entry, parents}: the re-split work units
     int4* rsseg;           // [fat_cap] {gene, first sub-bucket id, sub-buckets}: in-parent cross terms
@@ -185,6 +186,7 @@ size_t scc_rank_tables_stride(int ntp_max, int K);
 hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st);
 hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st);
+void scc_rank_mfma_stamps(hipStream_t st, int print);
 hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid_genes, hipStream_t st);
 hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid, hipStream_t st);

@@ -828,6 +828,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.wave_target = wave_target;
         L.rw_slots = P <= 128 ? 2 : P <= 256 ? 4 : P <= 512 ? 8 : 16;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
+        L.rw_mfma = env_int("SCC_RANK_MFMA", 1);
         L.cross_wave = env_int("SCC_CROSS_WAVE", 0);
         L.bucket_cap = bucket_cap;
         L.sbuckets = d_sbk;
@@ -903,7 +904,9 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             HIPCHK(c, hipEventRecord(c->ev_fork, s0));
             HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
         }
+        if (L.dbg == 7) scc_rank_mfma_stamps(s0, 0);
         HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0));
+        if (L.dbg == 7) scc_rank_mfma_stamps(s0, 1);
         HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, si));
         HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, si));
         HIPCHK(c, scc_launch_rank_items(&L, 2, ncu, si));
