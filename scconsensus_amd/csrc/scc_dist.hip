@@ -19,6 +19,8 @@
 //                   1 - r epilogue fused into coalesced packed-column stores.
 #include "scc_common.hpp"
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
@@ -404,25 +406,39 @@ __device__ __host__ inline int da_rbmin(int cb)
 template <bool F32, int DC, int NB, bool NT, bool V2>
 __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict__ P, int N, int nrb, int cb_lo,
                                                        int ncbl, int c_lo, int c_hi, long long obase,
-                                                       void* __restrict__ out)
+                                                       void* __restrict__ out, const int2* __restrict__ tiles,
+                                                       int ntiles)
 {
     constexpr int HALO = F32 ? 32 : 16;  // outputs per 128-B line
     constexpr int TR = DA_T - HALO;      // rows owned per tile
     __shared__ double stage[NB][DA_T];
     __shared__ double cn[DC];
-    // folded triangle: grid row y holds column block y then its mirror
-    const int y = blockIdx.y;
-    int x = blockIdx.x;
-    int cb = cb_lo + y;
-    const int cntA = nrb - da_rbmin<TR, DC>(cb);
-    if (x >= cntA) {
-        x -= cntA;
-        const int cb2 = cb_lo + ncbl - 1 - y;
-        if (cb2 <= cb) return;
-        cb = cb2;
-        if (x >= nrb - da_rbmin<TR, DC>(cb)) return;
+    int cb, r0;
+    if (tiles) {
+        // tile list in panel order (dist_tile_list), dealt to the XCDs as
+        // contiguous runs: the hardware gives consecutive workgroup ids to
+        // consecutive XCDs, so id -> (id % 8) * per + id / 8
+        const int per = (ntiles + 7) >> 3;
+        const int L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+        if (L >= ntiles) return;
+        const int2 e = tiles[L];
+        cb = e.x;
+        r0 = e.y * TR;
+    } else {
+        // folded triangle: grid row y holds column block y then its mirror
+        const int y = blockIdx.y;
+        int x = blockIdx.x;
+        cb = cb_lo + y;
+        const int cntA = nrb - da_rbmin<TR, DC>(cb);
+        if (x >= cntA) {
+            x -= cntA;
+            const int cb2 = cb_lo + ncbl - 1 - y;
+            if (cb2 <= cb) return;
+            cb = cb2;
+            if (x >= nrb - da_rbmin<TR, DC>(cb)) return;
+        }
+        r0 = (da_rbmin<TR, DC>(cb) + x) * TR;
     }
-    const int r0 = (da_rbmin<TR, DC>(cb) + x) * TR;
     const int jb = max(cb * DC, c_lo);
     const int je = min(min(cb * DC + DC, c_hi), min(N - 1, r0 + TR - 1));  // columns with a row in the window
     if (jb >= je) return;
@@ -528,23 +544,85 @@ __global__ void __launch_bounds__(DA_T) k_dist_aligned(const double* __restrict_
     }
 }
 
+// Tile order for large N (the N x 16 scores past an XCD's 4 MB L2): panels of
+// R row blocks (R * TR score rows, ~2 MB), each panel's column blocks in turn
+// and the panel's row blocks inside a column block, the list cut into 8
+// contiguous runs, one per XCD.  A panel's row scores stay in the XCD's L2
+// while its column blocks pass, a column block's scores are fetched once per
+// panel.  The folded grid fetched a tile's row scores from HBM for every
+// column block: 20 GB of FETCH_SIZE under 160 GB of writes at config D.
+// Lists are built once per (device, N, column range, shape) and cached.
+struct DistTileList {
+    int dev, N, c_lo, c_hi, DC, TR;
+    int2* d;
+    int n;
+};
+static std::mutex g_dtl_mu;
+static std::vector<DistTileList> g_dtl;
+
+template <int DC>
+static const int2* dist_tile_list(int N, int c_lo, int c_hi, int TR, int nrb, int* count)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_dtl_mu);
+    for (const DistTileList& t : g_dtl)
+        if (t.dev == dev && t.N == N && t.c_lo == c_lo && t.c_hi == c_hi && t.DC == DC && t.TR == TR) {
+            *count = t.n;
+            return t.d;
+        }
+    const int cb_lo = c_lo / DC, cb_hi = (c_hi + DC - 1) / DC;
+    const int R = std::max(8, (2 << 20) / (TR * 128));
+    std::vector<int2> v;
+    for (int p0 = 0; p0 < nrb; p0 += R)
+        for (int cb = cb_lo; cb < cb_hi; ++cb) {
+            const int rmin = (cb * DC + 1) / TR - 1;
+            const int lo = std::max(std::max(rmin, 0), p0), hi = std::min(nrb, p0 + R);
+            for (int rb = lo; rb < hi; ++rb) v.push_back(int2{cb, rb});
+        }
+    int2* d = nullptr;
+    if (v.empty() || hipMalloc(&d, v.size() * sizeof(int2)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, v.data(), v.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    if (g_dtl.size() >= 16) {  // (streamed column ranges: keep the newest lists)
+        (void)hipFree(g_dtl.front().d);
+        g_dtl.erase(g_dtl.begin());
+    }
+    g_dtl.push_back(DistTileList{dev, N, c_lo, c_hi, DC, TR, d, (int)v.size()});
+    *count = (int)v.size();
+    return d;
+}
+
 template <int DC, int NB, bool NT>
 static void launch_dist_aligned(const double* P, int N, int c_lo, int c_hi, void* out, int f32, hipStream_t st)
 {
     const int HALO = f32 ? 32 : 16, TR = DA_T - HALO;
     const int nrb = (N + HALO - 1) / TR + 1;
     const int cb_lo = c_lo / DC, cb_hi = (c_hi + DC - 1) / DC, ncbl = cb_hi - cb_lo;
-    const int npair = (ncbl + 1) / 2;
-    int gx = 1;
-    for (int y = 0; y < npair; ++y) {
-        const int a = cb_lo + y, b = cb_lo + ncbl - 1 - y;
-        const int ra = f32 ? da_rbmin<DA_T - 32, DC>(a) : da_rbmin<DA_T - 16, DC>(a);
-        const int rbb = f32 ? da_rbmin<DA_T - 32, DC>(b) : da_rbmin<DA_T - 16, DC>(b);
-        const int cnt = (nrb - ra) + (b > a ? nrb - rbb : 0);
-        gx = std::max(gx, cnt);
-    }
     const long long obase = (long long)c_lo * (2LL * N - c_lo - 1) / 2;
-    const dim3 grid((unsigned)gx, (unsigned)npair);
+    // the panel-ordered tile list from 64k cells (SCC_DIST_ORDER=0: the folded grid; bit-identical)
+    const char* oe = getenv("SCC_DIST_ORDER");
+    const int order = (oe && *oe) ? atoi(oe) : (N >= 65536 ? 1 : 0);
+    const int2* tiles = nullptr;
+    int ntiles = 0;
+    if (order) tiles = dist_tile_list<DC>(N, c_lo, c_hi, TR, nrb, &ntiles);
+    dim3 grid;
+    if (tiles) {
+        grid = dim3((unsigned)(8 * ((ntiles + 7) / 8)));
+    } else {
+        const int npair = (ncbl + 1) / 2;
+        int gx = 1;
+        for (int y = 0; y < npair; ++y) {
+            const int a = cb_lo + y, b = cb_lo + ncbl - 1 - y;
+            const int ra = f32 ? da_rbmin<DA_T - 32, DC>(a) : da_rbmin<DA_T - 16, DC>(a);
+            const int rbb = f32 ? da_rbmin<DA_T - 32, DC>(b) : da_rbmin<DA_T - 16, DC>(b);
+            const int cnt = (nrb - ra) + (b > a ? nrb - rbb : 0);
+            gx = std::max(gx, cnt);
+        }
+        grid = dim3((unsigned)gx, (unsigned)npair);
+    }
     // paired stores need the output 16-B aligned (8-B for f32); SCC_DIST_V2=0: one entry per thread
     const char* ve = getenv("SCC_DIST_V2");
     const bool v2 = !(ve && *ve && atoi(ve) == 0) && ((uintptr_t)out % (f32 ? 8 : 16)) == 0;
@@ -552,8 +630,8 @@ static void launch_dist_aligned(const double* P, int N, int c_lo, int c_hi, void
                                : (const void*)k_dist_aligned<true, DC, NB, NT, false>)
                          : (v2 ? (const void*)k_dist_aligned<false, DC, NB, NT, true>
                                : (const void*)k_dist_aligned<false, DC, NB, NT, false>);
-    void* args[] = {(void*)&P, (void*)&N, (void*)&nrb, (void*)&cb_lo, (void*)&ncbl, (void*)&c_lo, (void*)&c_hi,
-                    (void*)&obase, (void*)&out};
+    void* args[] = {(void*)&P,     (void*)&N,    (void*)&nrb, (void*)&cb_lo,   (void*)&ncbl, (void*)&c_lo,
+                    (void*)&c_hi,  (void*)&obase, (void*)&out, (void*)&tiles, (void*)&ntiles};
     (void)hipLaunchKernel(fn, grid, dim3(DA_T), args, 0, st);
 }
 

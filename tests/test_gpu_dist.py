@@ -257,8 +257,8 @@ def test_workgroup_count_bitwise(eng, monkeypatch):
 @pytest.mark.parametrize("f32", [False, True])
 def test_distance_kernels_agree(eng, f32, monkeypatch):
     """The distance store kernel's tile widths (64 / 128 columns), store
-    kinds (plain / nontemporal) and store widths (two entries per thread or
-    one) give bit-identical packed output (same
+    kinds (plain / nontemporal), store widths (two entries per thread or
+    one) and tile orders (folded grid / panel list) give bit-identical packed output (same
     arithmetic, only the store pattern differs), over the full vector and over
     column slices whose starts are not line-aligned."""
     from scconsensus_amd import _native as nat
@@ -269,14 +269,17 @@ def test_distance_kernels_agree(eng, f32, monkeypatch):
     ds = eng.dataset_dense(X)
     g = np.arange(0, G, 2)
     outs = []
-    for cols, nt, v2 in [("64", "1", "1"), ("64", "0", "1"), ("128", "1", "1"), ("128", "0", "1"), ("64", "1", "0"),
-                         ("128", "0", "0")]:
+    for cols, nt, v2, order in [("64", "1", "1", "0"), ("64", "0", "1", "0"), ("128", "1", "1", "0"),
+                                ("128", "0", "1", "0"), ("64", "1", "0", "0"), ("128", "0", "0", "0"),
+                                ("64", "1", "1", "1"), ("128", "1", "1", "1")]:
         monkeypatch.setenv("SCC_DIST_COLS", cols)
         monkeypatch.setenv("SCC_DIST_NT", nt)
         monkeypatch.setenv("SCC_DIST_V2", v2)  # paired stores (default) or one entry per thread
+        monkeypatch.setenv("SCC_DIST_ORDER", order)  # panel-ordered tile list (default from 64k cells)
         outs.append(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID, f32=f32))
     monkeypatch.setenv("SCC_DIST_NT", "1")
     monkeypatch.setenv("SCC_DIST_V2", "1")
+    monkeypatch.setenv("SCC_DIST_ORDER", "1")
     assert all(np.array_equal(outs[0], o) for o in outs[1:])
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(outs[0] - ref)) < (1e-4 if f32 else 1e-5)
