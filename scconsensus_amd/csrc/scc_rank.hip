@@ -2525,6 +2525,304 @@ __global__ void __launch_bounds__(256) k_rank_mfma(ScRankLaunch A)
         for (int q = 0; q < 8; ++q) atomicAdd(&g_rk_stamps[q], (unsigned long long)tph[q]);
 }
 
+// The same products on 16 x 16 x 64 tiles (K <= 16 * NC): one MFMA covers a
+// bucket's 64 elements, a cluster tile is 4 accumulator registers, so the
+// kernel stays small enough for several waves per SIMD (the 32 x 32 form's
+// per-bucket chain was latency-exposed at one or two).  Slots: lane l holds
+// row / column l & 15 and, in byte t of its 16-byte fragment (lane group
+// g = l >> 4), element e(g, t) = 16 (t >> 2) + 4 g + (t & 3): the row the
+// accumulator layout puts in register t & 3 of lane group g of row tile
+// t >> 2, so four packed accumulator tiles are the next product's operand.
+__device__ inline rk_v4i rk_mfma16(rk_v4i a, rk_v4i b, rk_v4i c)
+{
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+template <int NC>
+__device__ constexpr int rk_tile16(int ma, int nb)  // upper tiles (ma <= nb) in row order
+{
+    return ma * NC - ma * (ma - 1) / 2 + (nb - ma);
+}
+
+template <int NC>
+__global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
+{
+    constexpr int NTL = NC * (NC + 1) / 2;
+    constexpr int TL = NC == 1 ? 2 : 8;  // tested-pair list entries per lane (P <= 120 / 496)
+    __shared__ __attribute__((aligned(16))) RkWaveLds Ls[4];
+    __shared__ u32 Lbuf[4][NTL * 256];   // one accumulator matrix of a flush, [tile][a & 15][b & 15]
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    RkWaveLds& Lw = Ls[wv];
+    u32* buf = Lbuf[wv];
+    const int NW = gridDim.x * 4, W = blockIdx.x * 4 + wv;
+    const int cnt = min(A.counts[4], A.bucket_cap);
+    const int K = A.K, G = A.G, P = A.P;
+    const int CH = max(16, min(512, cnt / (4 * NW)));
+    const int g4 = lane >> 4, r16 = lane & 15;
+    const rk_v4i zero = {0, 0, 0, 0};
+    // L rows 16 mt + r16: bytes [e(g4, t) < i] (constant per lane)
+    rk_v4i Lm[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) Lm[mt][d] = (int)rk_lt_bytes(16 * mt + r16, 16 * d + 4 * g4);
+    rk_v4i R[NTL], X[NTL];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) R[t] = X[t] = zero;
+    Lw.F[lane] = 0;
+    int cur = -1, ntp = 0, nrun = 0;
+    bool rtie = false;
+    u64 gk = ~0ull;
+    auto flush = [&]() {
+        const u32* tl = A.gene_tp + (size_t)cur * P;
+        u32 tv[TL];
+#pragma unroll
+        for (int q = 0; q < TL; ++q) tv[q] = tl[min(q * 64 + lane, max(ntp - 1, 0))];
+        auto out = [&](rk_v4i* Mx, unsigned long long* acc) {
+#pragma unroll
+            for (int ma = 0; ma < NC; ++ma)
+#pragma unroll
+                for (int nb = ma; nb < NC; ++nb) {
+                    const int t = rk_tile16<NC>(ma, nb);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) buf[t * 256 + (4 * g4 + r) * 16 + r16] = (u32)Mx[t][r];
+                    Mx[t] = zero;
+                }
+            wsync();
+#pragma unroll
+            for (int q = 0; q < TL; ++q) {
+                if (q * 64 >= ntp) break;
+                const u32 v = tv[q];
+                const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+                const u32 x = buf[rk_tile16<NC>(a >> 4, b >> 4) * 256 + (a & 15) * 16 + (b & 15)];
+                if (q * 64 + lane < ntp && x) atomicAdd(&acc[(size_t)(v & 0xffffu) * G + cur], (unsigned long long)x);
+            }
+            wsync();
+        };
+        out(R, (unsigned long long*)A.accE);
+        if (rtie) {
+            out(X, (unsigned long long*)A.accX);
+            const u64 f = Lw.F[lane];
+            if (lane < K && f) atomicAdd((unsigned long long*)&A.accF[(size_t)lane * G + cur], (unsigned long long)f);
+            Lw.F[lane] = 0;
+            wsync();
+        }
+        nrun = 0;
+        rtie = false;
+    };
+    for (int c0 = W * CH; c0 < cnt; c0 += NW * CH) {
+        const int c1 = min(cnt, c0 + CH);
+        for (int s0 = c0; s0 < c1; s0 += 64) {
+            const int s1 = min(c1, s0 + 64);
+            ScRankItem D{0, 0, 0, 0, 0};
+            if (lane < s1 - s0) D = A.sbuckets[s0 + lane];
+            u64 rem;
+            if (A.wv_filter) {
+                const int ntg = (lane < s1 - s0 && D.n > 0) ? A.gene_nt[D.gene] : -1;
+                rem = __ballot(ntg > A.wv_lo && ntg <= A.wv_hi);
+            } else {
+                rem = __ballot(lane < s1 - s0 && D.n > 0);
+            }
+            if (!rem) continue;
+            const u32 dlo = (u32)(u64)D.base, dhi = (u32)((u64)D.base >> 32);
+            auto dbase = [&](int li) {
+                return (i64)(((u64)(u32)__builtin_amdgcn_readlane((int)dhi, li) << 32) |
+                             (u32)__builtin_amdgcn_readlane((int)dlo, li));
+            };
+            u64 nkey;
+            u32 ncode;
+            {
+                const int l0 = __builtin_ctzll(rem);
+                const i64 b0 = dbase(l0);
+                const int n0 = __builtin_amdgcn_readlane(D.n, l0);
+                nkey = lane < n0 ? A.keys2[b0 + lane] : ~0ull;
+                ncode = lane < n0 ? (u32)A.codes2[b0 + lane] : 255u;
+            }
+            while (rem) {
+                const int li = __builtin_ctzll(rem);
+                rem &= rem - 1;
+                const int g = __builtin_amdgcn_readlane(D.gene, li);
+                const int n = __builtin_amdgcn_readlane(D.n, li);
+                const int bucket = __builtin_amdgcn_readlane(D.bucket, li);
+                const int src = __builtin_amdgcn_readlane(D.src, li);
+                const i64 bbase = dbase(li);
+                u64 key = nkey;
+                u32 code = ncode;
+                if (rem) {
+                    const int l1 = __builtin_ctzll(rem);
+                    const i64 b1 = dbase(l1);
+                    const int n1 = __builtin_amdgcn_readlane(D.n, l1);
+                    nkey = lane < n1 ? A.keys2[b1 + lane] : ~0ull;
+                    ncode = lane < n1 ? (u32)A.codes2[b1 + lane] : 255u;
+                }
+                if (g != cur || nrun >= 16384) {
+                    if (cur >= 0) flush();
+                    if (g != cur) {
+                        cur = g;
+                        gk = A.gkmin[g];
+                        ntp = A.gene_nt[g];
+                    }
+                }
+                ++nrun;
+                if (src == 2) {  // one repeated key (as k_rank_mfma)
+                    u32 myc = 0;
+                    for (int i00 = 0; i00 < n; i00 += 256) {
+                        u32 cd[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int i = i00 + u * 64 + lane;
+                            cd[u] = i < n ? (u32)A.codes2[bbase + i] : 255u;
+                        }
+                        for (int c = 0; c < K; ++c) {
+                            u32 t = 0;
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) t += (u32)__popcll(__ballot(cd[u] == (u32)c));
+                            if (lane == c) myc += t;
+                        }
+                    }
+                    if (lane < K) {
+                        A.hbg[(size_t)bucket * K + lane] = myc;
+                        if (myc >= 2) Lw.F[lane] += f_tie(myc);
+                    }
+                    rtie = true;
+                    Lw.cnt[lane] = myc;
+                    wsync();
+                    const u32* tl = A.gene_tp + (size_t)g * P;
+                    for (int j = lane; j < ntp; j += 64) {
+                        const u32 v = tl[j];
+                        const u64 ca = Lw.cnt[(v >> 16) & 0xffu], cb = Lw.cnt[v >> 24];
+                        if (ca && cb) {
+                            const size_t o = (size_t)(v & 0xffffu) * G + g;
+                            atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)(ca * cb));
+                            atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)(ca * cb * (ca + cb)));
+                        }
+                    }
+                    wsync();
+                    continue;
+                }
+                const bool vl = lane < n;
+                if (gk != ~0ull) {
+                    u64 ck = vl ? (((key - gk) << SCC_CODE_BITS) | code) : ~0ull;
+                    if (n > 1) bitonic_merge_ck<1, 2>(ck);
+                    if (n > 2) bitonic_merge_ck<2, 4>(ck);
+                    if (n > 4) bitonic_merge_ck<4, 8>(ck);
+                    if (n > 8) bitonic_merge_ck<8, 16>(ck);
+                    if (n > 16) bitonic_merge_ck<16, 32>(ck);
+                    if (n > 32) bitonic_merge_ck<32, 0>(ck);
+                    key = ck >> SCC_CODE_BITS;
+                    code = vl ? (u32)(ck & SCC_CODE_MASK) : 255u;
+                } else {
+                    if (n > 1) bitonic_merge<1>(key, code, (lane & 2) == 0, lane);
+                    if (n > 2) bitonic_merge<2>(key, code, (lane & 4) == 0, lane);
+                    if (n > 4) bitonic_merge<4>(key, code, (lane & 8) == 0, lane);
+                    if (n > 8) bitonic_merge<8>(key, code, (lane & 16) == 0, lane);
+                    if (n > 16) bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
+                    if (n > 32) bitonic_merge<32>(key, code, true, lane);
+                }
+                // ---- one-hot operand: sorted codes at their slots, element i at
+                // byte 16 ((i >> 2) & 3) + 4 (i >> 4) + (i & 3)
+                const int sg = (((lane >> 2) & 3) << 4) | ((lane >> 4) << 2) | (lane & 3);
+                Lw.code[sg] = (u8)code;
+                wsync();
+                const rk_v4i cw = *(const rk_v4i*)(Lw.code + 16 * g4);
+                rk_v4i ob[NC];
+#pragma unroll
+                for (int t = 0; t < NC; ++t)
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) ob[t][d] = (int)rk_eq_bytes((u32)cw[d], (u32)(r16 + 16 * t));
+#pragma unroll
+                for (int t = 0; t < NC; ++t) {  // the bucket's cluster histogram row
+                    u32 sm = (u32)ob[t][0] + (u32)ob[t][1] + (u32)ob[t][2] + (u32)ob[t][3];
+                    u32 c = (sm * 0x01010101u) >> 24;
+                    c += (u32)__shfl_xor((int)c, 16, 64);
+                    c += (u32)__shfl_xor((int)c, 32, 64);
+                    if (g4 == 0 && r16 + 16 * t < K) A.hbg[(size_t)bucket * K + r16 + 16 * t] = c;
+                }
+                // ---- M = L O (row tiles of 16 elements), R += O^T (2 M)
+                const int nmt = (n + 15) >> 4;
+                rk_v4i mb[NC];
+#pragma unroll
+                for (int t = 0; t < NC; ++t) mb[t] = zero;
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) {
+                    if (mt >= nmt) break;
+#pragma unroll
+                    for (int t = 0; t < NC; ++t) {
+                        const rk_v4i m = rk_mfma16(Lm[mt], ob[t], zero);
+                        mb[t][mt] = (int)((u32)(2 * m[0]) | ((u32)(2 * m[1]) << 8) | ((u32)(2 * m[2]) << 16) |
+                                          ((u32)(2 * m[3]) << 24));
+                    }
+                }
+#pragma unroll
+                for (int ma = 0; ma < NC; ++ma)
+#pragma unroll
+                    for (int nb = ma; nb < NC; ++nb) {
+                        const int t = rk_tile16<NC>(ma, nb);
+                        R[t] = rk_mfma16(ob[ma], mb[nb], R[t]);
+                    }
+                // ---- tie groups and runs
+                const u64 kp = ((u64)(u32)__shfl_up((int)(u32)(key >> 32), 1, 64) << 32) |
+                               (u64)(u32)__shfl_up((int)(u32)key, 1, 64);
+                const u32 cpv = (u32)__shfl_up((int)code, 1, 64);
+                const u64 vmask = (n >= 64) ? ~0ull : ((1ull << n) - 1);
+                const bool gs_me = (lane == 0) || (kp != key);
+                const u64 gst = __ballot(gs_me && vl);
+                const bool anytie = ((~gst) & vmask & ~1ull) != 0;
+                if (anytie) {
+                    rtie = true;
+                    const u64 le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+                    const bool rs_me = (lane == 0) || (kp != key) || (cpv != code);
+                    const u64 rst = __ballot(rs_me && vl);
+                    const u64 raft = rst & ~le;
+                    const int re = raft ? __builtin_ctzll(raft) : n;
+                    const int rs = 63 - __clzll((long long)((rst & le) | 1ull));
+                    if (rs_me && vl && re - lane >= 2)
+                        atomicAdd((unsigned long long*)&Lw.F[code], (unsigned long long)f_tie((u64)(re - lane)));
+                    const int gs = 63 - __clzll((long long)((gst & le) | 1ull));
+                    const u64 gaft = gst & ~le;
+                    const int ge = gaft ? __builtin_ctzll(gaft) : n;
+                    Lw.dcnt[sg] = (u8)(vl ? re - rs : 0);
+                    wsync();
+                    const rk_v4i dw = *(const rk_v4i*)(Lw.dcnt + 16 * g4);
+                    rk_v4i odb[NC], qb[NC];
+#pragma unroll
+                    for (int t = 0; t < NC; ++t) {
+                        qb[t] = zero;
+#pragma unroll
+                        for (int d = 0; d < 4; ++d) odb[t][d] = (int)(((u32)ob[t][d] * 0xffu) & (u32)dw[d]);
+                    }
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt) {
+                        if (mt >= nmt) break;
+                        const int gsr = __shfl(gs, 16 * mt + r16, 64), ger = __shfl(ge, 16 * mt + r16, 64);
+                        rk_v4i eq;
+#pragma unroll
+                        for (int d = 0; d < 4; ++d)
+                            eq[d] = (int)(rk_lt_bytes(ger, 16 * d + 4 * g4) - rk_lt_bytes(gsr, 16 * d + 4 * g4));
+#pragma unroll
+                        for (int t = 0; t < NC; ++t) {
+                            const rk_v4i q = rk_mfma16(eq, ob[t], zero);
+                            qb[t][mt] = (int)((u32)q[0] | ((u32)q[1] << 8) | ((u32)q[2] << 16) | ((u32)q[3] << 24));
+                        }
+                    }
+#pragma unroll
+                    for (int ma = 0; ma < NC; ++ma)
+#pragma unroll
+                        for (int nb = ma; nb < NC; ++nb) {
+                            const int t = rk_tile16<NC>(ma, nb);
+                            R[t] = rk_mfma16(ob[ma], qb[nb], R[t]);
+                            X[t] = rk_mfma16(odb[ma], qb[nb], X[t]);
+                            X[t] = rk_mfma16(qb[ma], odb[nb], X[t]);
+                        }
+                    wsync();
+                }
+                wsync();
+            }
+        }
+    }
+    if (cur >= 0) flush();
+}
+
 // ===================================================================== cross
 // Cross-bucket rank sums: for tested pair (a, b) of gene g,
 //   S_ab += sum over buckets beta of h_beta[a] * #(b-elements in buckets < beta)
@@ -2746,6 +3044,20 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
         if (e != hipSuccess || L->rw_mfma == 2) return e;
     }
     ScRankLaunch A = *L;
+    // the 16-wide matrix-core kernel for the genes the slot kernels would take:
+    // by default at K <= 16 (four waves per SIMD; config B rank 0.785 -> 0.744
+    // ms), SCC_RANK_MFMA16=1 also at K <= 32 (two waves: config C 8.6 -> 10.2 ms)
+    if (L->rw_mfma16 > 0 ? L->K <= 32 : (L->rw_mfma16 < 0 && L->K <= 16)) {
+        ScRankLaunch M = *L;
+        M.wv_filter = mfma ? 1 : 0;
+        M.wv_lo = -1;
+        M.wv_hi = mfma ? mfma_min : (1 << 30);
+        if (L->K <= 16)
+            hipLaunchKernelGGL(k_rank_mfma16<1>, dim3(grid), dim3(256), 0, st, M);
+        else
+            hipLaunchKernelGGL(k_rank_mfma16<2>, dim3(grid), dim3(256), 0, st, M);
+        return hipGetLastError();
+    }
     for (int c = 0; c < 4; ++c) {
         if (c > 0 && 64 * L->rw_slots < hi[c]) break;
         if (mfma && hi[c] > mfma_min) return hipSuccess;  // the genes past mfma_min: done on the matrix cores

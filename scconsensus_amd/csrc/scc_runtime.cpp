@@ -829,6 +829,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.rw_slots = P <= 128 ? 2 : P <= 256 ? 4 : P <= 512 ? 8 : 16;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
         L.rw_mfma = env_int("SCC_RANK_MFMA", 1);
+        L.rw_mfma16 = env_int("SCC_RANK_MFMA16", -1);
         L.cross_wave = env_int("SCC_CROSS_WAVE", 0);
         L.bucket_cap = bucket_cap;
         L.sbuckets = d_sbk;

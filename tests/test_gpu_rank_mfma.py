@@ -38,12 +38,22 @@ def test_mfma_matches_slot_kernel(eng, K, decimals, monkeypatch):
     Kc = len(names)
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     res = {}
-    for flag in ("2", "1", "0"):  # every gene on the matrix cores / the genes past 512 pairs / none
-        monkeypatch.setenv("SCC_RANK_MFMA", flag)
+    # every gene on the 32-wide matrix-core kernel / the genes past 512 pairs /
+    # none; "16": the 16-wide kernel (K <= 32) for the genes the slot kernels take
+    for flag in ("2", "1", "0", "16"):
+        monkeypatch.setenv("SCC_RANK_MFMA", "1" if flag == "16" else flag)
+        monkeypatch.setenv("SCC_RANK_MFMA16", "1" if flag == "16" else "0")  # (default: on at K <= 16)
         f = eng.de_run(ds, code, Kc, nat.SCC_DE_FAST, fetch="all", test_all=True, min_per_cent=1.0,
                        log_fc_thrs=0.0)
         s = eng.de_run(ds, code, Kc, nat.SCC_DE_SLOW, fetch="all")
         res[flag] = (f, s)
+    monkeypatch.delenv("SCC_RANK_MFMA16")
+    f16, s16 = res["16"]
+    f0, s0 = res["0"]
+    np.testing.assert_array_equal(f16.u2, f0.u2)
+    np.testing.assert_array_equal(f16.p, f0.p)
+    np.testing.assert_array_equal(s16.u2, s0.u2)
+    np.testing.assert_array_equal(s16.p, s0.p)
     f1, s1 = res["2"]
     f0, s0 = res["0"]
     np.testing.assert_array_equal(f1.u2, f0.u2)
