@@ -486,10 +486,15 @@ def main():
     # same union, measured beside the step (not part of the reference's path)
     if not a.no_pearson and not multi:
         os.environ["SCC_PROFILE_STAGES"] = "zscore,pearson"
-        eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)  # warm-up (first launch, buffers)
+        # warm-up: the first launch allocates; the GPU sat idle through the
+        # PCIe-bound transfer measurements before this, so a few more launches
+        # bring the clocks back before the timed ones (1 warm-up launch gave
+        # 0.57-0.63 of peak run to run on the same binary)
+        for _ in range(6):
+            eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)
         eng.synchronize()
         eng.reset_timers()
-        for _ in range(5):
+        for _ in range(10):
             eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)
         eng.synchronize()
         for f in ("zscore", "pearson"):
