@@ -852,6 +852,7 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 #define RSW_CAP 256
 #define RSW_HCAP 512
 #define RSW_PACC 1280     // genes with <= this many tested pairs keep them (and their sums) in registers
+#define RSW_TS_SMALL 8    // the wave re-split's launch for genes with <= 512 tested pairs
 
 // ===================================================================== split
 #define SP_T 1024
@@ -1468,18 +1469,19 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
 // same binning, packing, in-place scatter and in-parent cross term as
 // resplit_one, with wave-level ordering only (no workgroup barriers) and four
 // parents per workgroup in flight.
-struct ResplitWLds {
+struct ResplitWLds {  // (offsets and running counts <= RSW_CAP: 16 bits; 12.3 KB a wave, three workgroups per CU)
     u32 hist[RSW_BINS];
     u32 excl[RSW_BINS];
     u32 bid[RSW_BINS];
     u64 rep[RSW_BINS];
     u32 bcur[2 * RSW_BINS + 1];
-    u32 boff[2 * RSW_BINS + 2];
+    uint16_t boff[2 * RSW_BINS + 2];
     u8 bdiff[2 * RSW_BINS + 4];
     u32 m[SCC_MAX_K];
     u32 hs[RSW_HCAP];
-    u32 bs[RSW_HCAP];
+    uint16_t bs[RSW_HCAP];
 };
+static_assert(4 * sizeof(ResplitWLds) <= 160 * 1024 / 3, "wave re-split: three workgroups per CU");
 
 __device__ inline void wsync()
 {
@@ -1487,6 +1489,11 @@ __device__ inline void wsync()
     __builtin_amdgcn_wave_barrier();
 }
 
+// TS: tested-pair slots held in registers (64 pairs each).  Two launches
+// split the genes: TS = RSW_TS_SMALL takes those with <= 64 * RSW_TS_SMALL
+// tested pairs (config D FAST: all of them; 3 waves per SIMD instead of 2),
+// RSW_PACC / 64 the others (SLOW at K = 50: 1225 pairs).
+template <int TS>
 __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
 {
     __shared__ ResplitWLds Ls[4];
@@ -1513,7 +1520,8 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     // atomic per (run of one gene, pair) instead of one per (parent, pair).
     // The consecutive sub-buckets also keep the wave kernel's register
     // accumulation on one gene.
-    constexpr int TS = RSW_PACC / 64;
+    constexpr int PACC = 64 * TS;  // genes past it: per-(parent, pair) atomics (as past RSW_PACC before)
+    constexpr bool SMALL = TS < RSW_PACC / 64;
     const int nw = gridDim.x * 4, w = blockIdx.x * 4 + wv;
     const int f0 = (int)((long long)cnt * w / nw), f1 = (int)((long long)cnt * (w + 1) / nw);
     u32 tpr[TS], par[TS];
@@ -1521,7 +1529,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     for (int s = 0; s < TS; ++s) tpr[s] = par[s] = 0;
     int pg = -1, pnt = 0, pn = 0;
     auto flush_par = [&]() {
-        if (pg >= 0 && pn > 0 && pnt <= RSW_PACC) {
+        if (pg >= 0 && pn > 0 && pnt <= PACC) {
 #pragma unroll
             for (int s = 0; s < TS; ++s) {
                 if (s * 64 >= pnt) break;
@@ -1535,13 +1543,17 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     for (int f = f0; f < f1; ++f) {
         const ScRankItem it = list[f];
         const int n = it.n, g = it.gene;
+        {  // this launch's genes (a gene's parents are together in the list)
+            const int nt_g = A.gene_nt[g];
+            if (SMALL ? nt_g > PACC : nt_g <= 64 * RSW_TS_SMALL) continue;
+        }
         // a parent adds at most 128 * 128 to one pair: flush before u32 could wrap
         if (g != pg || pn >= 65536) {
             flush_par();
             if (g != pg) {
                 pg = g;
                 pnt = A.gene_nt[g];
-                if (pnt > 0 && pnt <= RSW_PACC) {
+                if (pnt > 0 && pnt <= PACC) {
                     const u32* tl = A.gene_tp + (size_t)g * A.P;
 #pragma unroll
                     for (int s = 0; s < TS; ++s) tpr[s] = tl[min(s * 64 + lane, pnt - 1)];
@@ -1744,7 +1756,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
         }
         wsync();
         const int ntp = pnt;
-        if (ntp <= RSW_PACC) {
+        if (ntp <= PACC) {
             // m[a] = 0 or m[b] = 0 makes every product zero: no test needed
             ++pn;
 #pragma unroll
@@ -3124,13 +3136,16 @@ extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, h
     const long long waves = 2LL * grid * 4;
     W.rsw_chunk = (int)std::max(8LL, std::min(128LL, (long long)L->bucket_cap / (16 * waves)));
     W.rs_level = 0;
-    hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
+    hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
+    if (L->P > 64 * RSW_TS_SMALL) hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, st, W);
     const size_t acc_lds = sizeof(u64) * (size_t)std::max(L->P, 1);
     hipFuncSetAttribute((const void*)k_rank_resplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_lds);
     hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), acc_lds, st, *L);
     if (L->fat2) {  // sub-buckets the first level left with > 64 distinct values
         W.rs_level = 1;
-        hipLaunchKernelGGL(k_rank_resplit_w, dim3(2 * grid), dim3(256), 0, st, W);
+        hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
+        if (L->P > 64 * RSW_TS_SMALL)
+            hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, st, W);
     }
     return hipGetLastError();
 }
