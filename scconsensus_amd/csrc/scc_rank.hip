@@ -2078,7 +2078,6 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 wsync();
                 cm = cms[wv][lane];
                 if (K > 64) cm1 = cms[wv][lane + 64];
-                wsync();
             }
             if (lane < K) A.hbg[(size_t)bucket * K + lane] = (u32)__popcll(cm);
             if (lane + 64 < K) A.hbg[(size_t)bucket * K + lane + 64] = (u32)__popcll(cm1);
@@ -2107,11 +2106,13 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 #pragma unroll
             for (int q = 0; q < RW_SLOTS; ++q) {
                 if (q * 64 >= ntp || A.dbg == 1) break;
-                u64 ma = shfl_u64(cm, (int)(pa[q] & 63u)), mb = shfl_u64(cm, (int)(pb[q] & 63u));
-                if (K > 64) {
-                    const u64 ma1 = shfl_u64(cm1, (int)(pa[q] & 63u)), mb1 = shfl_u64(cm1, (int)(pb[q] & 63u));
-                    ma = pa[q] >= 64 ? ma1 : ma;
-                    mb = pb[q] >= 64 ? mb1 : mb;
+                u64 ma, mb;
+                if (K > 16) {  // the pair's masks straight from the leaders' LDS posts (two reads, no lane moves)
+                    ma = cms[wv][pa[q]];
+                    mb = cms[wv][pb[q]];
+                } else {
+                    ma = shfl_u64(cm, (int)(pa[q] & 63u));
+                    mb = shfl_u64(cm, (int)(pb[q] & 63u));
                 }
                 if (q * 64 + lane < ntp && ma && mb) {
                     u32 S, E, X;
@@ -2121,6 +2122,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                     aX[q] += X;
                 }
             }
+            if (K > 16) wsync();  // the masks are reposted by the next bucket
         }
     }
     if (cur >= 0) {
