@@ -374,6 +374,49 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
     }
 }
 
+// The same product on fp64 MFMA (16 x 16 x 4): a wave owns 16 cells, Z
+// passes through LDS 64 rows at a time, and lane (i, g) loads 16 consecutive
+// entries of cell i's row (two 64-byte loads; 16 cells x 4 lane groups read
+// 256 contiguous bytes of every row) that feed 16 MFMA steps, step s pairing
+// the row's entry 16 g + s with Z's row 16 g + s (the same k order on both
+// operands).  The per-thread loop above read one double per row per
+// iteration, 64 rows ld apart per load instruction.
+__global__ void __launch_bounds__(256) k_scores_mfma(const double* __restrict__ Xc, int N, int nu, int ld,
+                                                     const double* __restrict__ Z16, int k, double* __restrict__ P)
+{
+    __shared__ double zs[64][16];
+    const int lane = threadIdx.x & 63, w = scc_wave_id();
+    const int c0 = (blockIdx.x * 4 + w) * 16;
+    const int i = lane & 15, g = lane >> 4;
+    const double* row = Xc + (size_t)min(c0 + i, N - 1) * ld;  // rows past N: computed, not stored
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int u0 = 0; u0 < nu; u0 += 64) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+            const int uu = e >> 4, q = e & 15, u = u0 + uu;
+            zs[uu][q] = (u < nu && q < k) ? Z16[(size_t)u * 16 + q] : 0.0;
+        }
+        typedef double dv2 __attribute__((ext_vector_type(2)));
+        double xa[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) {  // (u0 + 16 g + 16 <= ld: ld is a multiple of 64)
+            const dv2 v = *(const dv2*)(row + u0 + 16 * g + 2 * s2);
+            xa[2 * s2] = v.x;
+            xa[2 * s2 + 1] = v.y;
+        }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) xa[s] = (u0 + 16 * g + s < nu) ? xa[s] : 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[s], zs[16 * g + s][i], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // accumulator r: cell c0 + g + 4 r, component i
+        const int cell = c0 + g + 4 * r;
+        if (cell < N) P[(size_t)cell * 16 + i] = acc[r];
+    }
+}
+
 // ------------------------------------------------------------------ Euclidean dist
 // Per element |p_i|^2 + |p_j|^2 - 2 p_i.p_j over the k <= 15 components (the
 // difference form where that cancels) and a Newton-refined sqrt (scc_sqrt_nr;
@@ -1011,7 +1054,13 @@ extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nc
 extern "C" hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
                                         hipStream_t st)
 {
-    hipLaunchKernelGGL(k_scores, dim3((N + 255) / 256), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P);
+    // fp64 MFMA form (SCC_SCORES_MFMA=0: one thread per cell)
+    const char* mfe = getenv("SCC_SCORES_MFMA");
+    const bool mf = !(mfe && *mfe && atoi(mfe) == 0);
+    if (mf && ld % 64 == 0)
+        hipLaunchKernelGGL(k_scores_mfma, dim3((N + 63) / 64), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P);
+    else
+        hipLaunchKernelGGL(k_scores, dim3((N + 255) / 256), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P);
     return hipGetLastError();
 }
 

@@ -489,3 +489,23 @@ def test_eigensolver_sizes_default_path(eng, n):
     dist = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
     ref = O.dist_euclidean(O.pca_scores(X, g))
     assert np.max(np.abs(dist - ref)) < 1e-5
+
+
+@pytest.mark.parametrize("nu", [37, 200, 450])
+def test_scores_kernels_agree(eng, nu, monkeypatch):
+    """Scores on fp64 MFMA (default) against the one-thread-per-cell loop: the
+    same products in another summation order (1e-12 relative on the
+    distance), and both against the exact SVD at the 1e-5 bar."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(nu + 1)
+    G, N = 600, 2011
+    X = np.abs(rng.standard_normal((G, N))) * (rng.random((G, N)) < 0.3)
+    ds = eng.dataset_dense(X)
+    g = np.sort(rng.choice(G, nu, replace=False))
+    outs = []
+    for mf in ("1", "0"):
+        monkeypatch.setenv("SCC_SCORES_MFMA", mf)
+        outs.append(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID))
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-12, atol=1e-12)
+    ref = O.dist_euclidean(O.pca_scores(X, g))
+    assert np.max(np.abs(outs[0] - ref)) < 1e-5
