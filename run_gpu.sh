@@ -50,6 +50,7 @@ for s in "$@"; do
     rkD128) SCC_RANK_MFMA_MIN=128 step rkD128 600 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
     rkC256) SCC_RANK_MFMA_MIN=256 step rkC256 600 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
     distt) step distt 600 python -u -m pytest tests/test_gpu_dist.py -k "kernels_agree or sizes" -x -v --timeout 200 --timeout-method thread ;;
+    pca) step pca 900 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_exchange.py tests/test_gpu_devices.py tests/test_gpu_shard.py -x -v --timeout 200 --timeout-method thread ;;
     scores) step scores 600 python -u -m pytest tests/test_gpu_dist.py -k "scores or kernels_agree" -x -v --timeout 200 --timeout-method thread ;;
     gram) step gram 600 python -u -m pytest tests/test_gpu_dist.py -k "gram" -x -v --timeout 200 --timeout-method thread ;;
     rk16B) SCC_RANK_MFMA16=1 step rk16B 300 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 10 --warmup 3 ;;

@@ -199,8 +199,13 @@ __global__ void __launch_bounds__(256) k_center(double* __restrict__ Xc, int N, 
 // WG = 4 waves -> 64x64 tile of C (upper tiles only); wave -> 32x32 = 2x2 MFMA
 // 16x16x4 tiles.  Lane l holds A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15];
 // accumulator reg r is C[row = (l>>4) + 4r][col = l&15] (f64 layout).
+// mean (nullptr: Xc is centred already): the column means subtracted on the
+// fly from rows < nval (the same x - mean[u] k_center stores, so the same
+// bits), rows past nval zero.  (The 128-wide kernel below keeps an explicit
+// centring pass: eight more registers took it from two waves per SIMD to one.)
 __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc, int Npad, int ld, int ntile,
-                                                  int rows_per_chunk, double* __restrict__ slabs)
+                                                  int rows_per_chunk, double* __restrict__ slabs,
+                                                  const double* __restrict__ mean, int nval)
 {
     // upper-triangular tile index -> (ti, tj), ti <= tj
     int t = blockIdx.x, ti = 0;
@@ -220,6 +225,9 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
     const int kr = lane >> 4, cc = lane & 15;
+    const double mx0 = mean ? mean[i0 + cc] : 0.0, mx1 = mean ? mean[i0 + 16 + cc] : 0.0;
+    const double my0 = mean ? mean[j0 + cc] : 0.0, my1 = mean ? mean[j0 + 16 + cc] : 0.0;
+    const int cv = min(c1, nval);
     // 4 GR_U rows per round: all loads of a round issued before its MFMAs
     // (clamped row, masked value past the chunk), so a round waits on memory
     // once instead of GR_U times (GR_U 4: B 0.14, C 0.89, D 4.35 ms; 1: 0.18 / 1.43 / 5.22;
@@ -232,11 +240,11 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
             const double* row = Xc + (size_t)min(rr, c1 - 1) * ld;
             const double x0 = row[i0 + cc], x1 = row[i0 + 16 + cc];
             const double y0 = row[j0 + cc], y1 = row[j0 + 16 + cc];
-            const bool ok = rr < c1;
-            a0[u] = ok ? x0 : 0.0;
-            a1[u] = ok ? x1 : 0.0;
-            b0[u] = ok ? y0 : 0.0;
-            b1[u] = ok ? y1 : 0.0;
+            const bool ok = rr < cv;
+            a0[u] = ok ? x0 - mx0 : 0.0;
+            a1[u] = ok ? x1 - mx1 : 0.0;
+            b0[u] = ok ? y0 - my0 : 0.0;
+            b1[u] = ok ? y1 - my1 : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < GR_U; ++u) {
@@ -343,7 +351,8 @@ __global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ 
 // P[c][q] = sum_u Xc[c][u] * Z[u][q]; Z row-major [u][16] (PC1 first, columns
 // q >= k are zero).
 __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, int N, int nu, int ld,
-                                                const double* __restrict__ Z16, int k, double* __restrict__ P)
+                                                const double* __restrict__ Z16, int k, double* __restrict__ P,
+                                                const double* __restrict__ mean)
 {
     __shared__ double sv[64][16];
     const int c = blockIdx.x * 256 + threadIdx.x;
@@ -362,7 +371,7 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
             const int ue = min(64, nu - u0);
             const double* row = Xc + (size_t)c * ld + u0;
             for (int uu = 0; uu < ue; ++uu) {
-                const double x = row[uu];
+                const double x = mean ? row[uu] - mean[u0 + uu] : row[uu];
 #pragma unroll
                 for (int q = 0; q < 16; ++q) acc[q] = fma(x, sv[uu][q], acc[q]);
             }
@@ -382,7 +391,8 @@ __global__ void __launch_bounds__(256) k_scores(const double* __restrict__ Xc, i
 // operands).  The per-thread loop above read one double per row per
 // iteration, 64 rows ld apart per load instruction.
 __global__ void __launch_bounds__(256) k_scores_mfma(const double* __restrict__ Xc, int N, int nu, int ld,
-                                                     const double* __restrict__ Z16, int k, double* __restrict__ P)
+                                                     const double* __restrict__ Z16, int k, double* __restrict__ P,
+                                                     const double* __restrict__ mean)
 {
     __shared__ double zs[64][16];
     const int lane = threadIdx.x & 63, w = scc_wave_id();
@@ -405,7 +415,11 @@ __global__ void __launch_bounds__(256) k_scores_mfma(const double* __restrict__ 
             xa[2 * s2 + 1] = v.y;
         }
 #pragma unroll
-        for (int s = 0; s < 16; ++s) xa[s] = (u0 + 16 * g + s < nu) ? xa[s] : 0.0;
+        for (int s = 0; s < 16; ++s) {
+            const int u = u0 + 16 * g + s;
+            const double m = mean ? mean[min(u, nu - 1)] : 0.0;
+            xa[s] = (u < nu) ? (mean ? xa[s] - m : xa[s]) : 0.0;
+        }
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[s], zs[16 * g + s][i], acc, 0, 0, 0);
@@ -974,13 +988,15 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
     return hipGetLastError();
 }
 
+// apply 0: the column means only (the Gram and the scores subtract them on
+// the fly: the same bits, one pass over X[U, ] fewer)
 extern "C" hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nchunk, double* mean,
-                                        hipStream_t st)
+                                        int apply, hipStream_t st)
 {
     const int rpc = (N + nchunk - 1) / nchunk;
     hipLaunchKernelGGL(k_colsum, dim3((ld + 255) / 256, nchunk), dim3(256), 0, st, Xc, N, ld, rpc, part);
     hipLaunchKernelGGL(k_colmean, dim3((ld + 3) / 4), dim3(256), 0, st, part, nchunk, ld, N, mean);
-    hipLaunchKernelGGL(k_center, dim3(4096), dim3(256), 0, st, Xc, N, nu, ld, mean);
+    if (apply) hipLaunchKernelGGL(k_center, dim3(4096), dim3(256), 0, st, Xc, N, nu, ld, mean);
     return hipGetLastError();
 }
 
@@ -1030,14 +1046,21 @@ extern "C" hipError_t scc_launch_center_parts(double* Xc, int n, int nu, int ld,
     return hipGetLastError();
 }
 
+// output tile width of the Gram: 128 from |U| > 384 (half the operand
+// re-fetch; SCC_GRAM_T=64 / 128 forces either)
+extern "C" int scc_gram_tile_width(int ld)
+{
+    const char* gt = getenv("SCC_GRAM_T");
+    return (gt && *gt) ? (atoi(gt) == 128 ? 128 : 64) : (ld > 384 ? 128 : 64);
+}
+
+// mean: centre on the fly (64-wide tiles only; the caller centred Xc otherwise)
 extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C,
-                                      hipStream_t st)
+                                      const double* mean, int nval, hipStream_t st)
 {
     const int rpc = ((Npad + nchunk - 1) / nchunk + 3) & ~3;
-    // 128-wide output tiles from |U| > 384 (half the operand re-fetch;
-    // SCC_GRAM_T=64 / 128 forces either)
-    const char* gt = getenv("SCC_GRAM_T");
-    const int tw = (gt && *gt) ? (atoi(gt) == 128 ? 128 : 64) : (ld > 384 ? 128 : 64);
+    const int tw = scc_gram_tile_width(ld);
+    if (mean && tw != 64) return hipErrorInvalidValue;
     if (tw == 128) {
         const int nt = (ld + 127) / 128;
         hipLaunchKernelGGL(k_gram_f64_128, dim3(nt * (nt + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, nt, rpc,
@@ -1045,22 +1068,22 @@ extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nc
     } else {
         const int ntile = ld / 64;
         hipLaunchKernelGGL(k_gram_f64, dim3(ntile * (ntile + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, ntile,
-                           rpc, slabs);
+                           rpc, slabs, mean, nval);
     }
     hipLaunchKernelGGL(k_gram_reduce, dim3(2048), dim3(256), 0, st, slabs, nchunk, ld, C);
     return hipGetLastError();
 }
 
 extern "C" hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
-                                        hipStream_t st)
+                                        const double* mean, hipStream_t st)
 {
     // fp64 MFMA form (SCC_SCORES_MFMA=0: one thread per cell)
     const char* mfe = getenv("SCC_SCORES_MFMA");
     const bool mf = !(mfe && *mfe && atoi(mfe) == 0);
     if (mf && ld % 64 == 0)
-        hipLaunchKernelGGL(k_scores_mfma, dim3((N + 63) / 64), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P);
+        hipLaunchKernelGGL(k_scores_mfma, dim3((N + 63) / 64), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P, mean);
     else
-        hipLaunchKernelGGL(k_scores, dim3((N + 255) / 256), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P);
+        hipLaunchKernelGGL(k_scores, dim3((N + 255) / 256), dim3(256), 0, st, Xc, N, nu, ld, Z16, k, P, mean);
     return hipGetLastError();
 }
 

@@ -23,9 +23,13 @@ int scc_gather_writes_rows(int ld);
 hipError_t scc_launch_gather(const long long* indptr, const int* rows, const double* vals, const double* dense,
                              int G, int N, const int* umap, const int* genes, int nu, int ld, double* Xc,
                              hipStream_t st);
-hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nchunk, double* mean, hipStream_t st);
-hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C, hipStream_t st);
+hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nchunk, double* mean, int apply,
+                             hipStream_t st);
+hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C, const double* mean,
+                           int nval, hipStream_t st);
+int scc_gram_tile_width(int ld);
 hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
+                             const double* mean,
                              hipStream_t st);
 size_t scc_sil_scratch_doubles(int N, int C);
 hipError_t scc_launch_silhouette(const void* D, int f32, int N, const int* lab, const int* cnt, int C, double* part,
@@ -337,6 +341,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     unsigned int* d_eig_err = nullptr;  // the hand-off's time-out flag, read back after the last launch
     if (metric == SCC_DIST_PCA_EUCLID) {
         double *d_slabs, *d_C, *d_W, *d_Z, *d_P, *d_escr;
+        const bool fused = env_int("SCC_CENTER_FUSED", 1) != 0 && scc_gram_tile_width(ld) == 64;
         const int nchunk = std::max(1, std::min(32, Npad / 512));
         WS("d_slabs", (size_t)nchunk * ld * ld, d_slabs);
         WS("d_C", (size_t)ld * ld, d_C);
@@ -346,11 +351,13 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         WS("d_escr", scc_eigen_scratch_doubles(nu, ld, k), d_escr);
         {
             Scope sc(c, "center", s0);
-            HIPCHK(c, scc_launch_center(d_X, N, nu, ld, (dd*)d_part, nchunk_mean, d_mean, s0));
+            // the means only: the Gram and the scores centre on the fly (SCC_CENTER_FUSED=0: a centring pass)
+            HIPCHK(c, scc_launch_center(d_X, N, nu, ld, (dd*)d_part, nchunk_mean, d_mean, fused ? 0 : 1, s0));
         }
         {
             Scope sc(c, "gram", s0);
-            HIPCHK(c, scc_launch_gram(d_X, Npad, ld, nchunk, d_slabs, d_C, s0));
+            HIPCHK(c, scc_launch_gram(d_X, Npad, ld, nchunk, d_slabs, d_C, fused ? d_mean : nullptr, fused ? N : Npad,
+                                      s0));
         }
         {
             Scope sc(c, "eigen", s0);
@@ -402,7 +409,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         }
         {
             Scope sc(c, "scores", s0);
-            HIPCHK(c, scc_launch_scores(d_X, N, nu, ld, d_Z, k, d_P, s0));
+            HIPCHK(c, scc_launch_scores(d_X, N, nu, ld, d_Z, k, d_P, fused ? d_mean : nullptr, s0));
         }
         auto emit = [&](int64_t a, int64_t b, void* dst) {
             return scc_launch_dist_euclid(d_P, N, (int)a, (int)b, dst, out_f32, s0);
@@ -619,7 +626,7 @@ extern "C" int scc_pca_shard_gram(scc_ctx* c, const void* parts, int32_t world, 
     }
     {
         Scope sc(c, "gram", s0);
-        HIPCHK(c, scc_launch_gram(d_X, npad, ld, nchunk, d_slabs, d_C, s0));
+        HIPCHK(c, scc_launch_gram(d_X, npad, ld, nchunk, d_slabs, d_C, nullptr, npad, s0));
     }
     HIPCHK(c, hipMemcpy2DAsync(gram, sizeof(double) * nu, d_C, sizeof(double) * ld, sizeof(double) * nu, nu,
                                hipMemcpyDeviceToDevice, s0));
@@ -682,7 +689,8 @@ extern "C" int scc_pca_shard_project(scc_ctx* c, const void* vecs, int32_t ncomp
     if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
     if (n > 0) {
         Scope sc(c, "scores", s0);
-        HIPCHK(c, scc_launch_scores(d_X, n, nu, ld, (const double*)vecs, k, (double*)scores + (size_t)c->pca_clo * 16, s0));
+        HIPCHK(c, scc_launch_scores(d_X, n, nu, ld, (const double*)vecs, k, (double*)scores + (size_t)c->pca_clo * 16,
+                                    nullptr, s0));
     }
     HIPCHK(c, hipStreamSynchronize(s0));
     c->last_ncomp = k;

@@ -68,17 +68,39 @@ __device__ inline void bitonic_stage(const A& a, int n, int m, int size, int str
 }
 
 // Full sort of n elements living in one address space (LDS normally).
+// A stage whose compare span (mirrored: size; half-cleaner: 2 stride) is at
+// most 128 keeps every pair of wave w (pairs q in [64 w + T k, +64)) inside
+// elements [128 (w + T/64 k), +128): between two such stages the wave's own
+// order suffices (a wave barrier), and only the stages that span more than 128
+// elements take a workgroup barrier (1024 elements: 10 of 55).
+__device__ inline void bitonic_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <class A>
 __device__ void block_bitonic(const A& a, int n, int tid, int T)
 {
     if (n < 2) return;
     const int m = scc_next_pow2(n);
+    auto sync = [&](int span, int next_span) {
+        if (span <= 128 && next_span <= 128 && (T & 63) == 0)
+            bitonic_wave_sync();
+        else
+            __syncthreads();
+    };
     for (int size = 2; size <= m; size <<= 1) {
         bitonic_stage(a, n, m, size, 0, true, tid, T);
-        __syncthreads();
+        // the next stage's span: the first half-cleaner's (2 * size / 4), else
+        // the next merge's mirrored stage, else none (the end: a full barrier)
+        const int nxt = (size >= 4) ? (size >> 1) : ((size << 1) <= m ? (size << 1) : (1 << 30));
+        sync(size, nxt);
         for (int stride = size >> 2; stride > 0; stride >>= 1) {
             bitonic_stage(a, n, m, size, stride, false, tid, T);
-            __syncthreads();
+            const int next = (stride > 1) ? stride : ((size << 1) <= m ? (size << 1) : (1 << 30));
+            sync(2 * stride, next);
         }
     }
 }
