@@ -2587,7 +2587,17 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
     int cur = -1, ntp = 0, nrun = 0;
     bool rtie = false;
     u64 gk = ~0ull;
+    const bool stm = A.dbg == 7;  // SCC_RW_DEBUG=7: phase clocks into g_rk_stamps
+    u64 tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = stm ? __builtin_amdgcn_s_memtime() : 0;
+    auto stamp = [&](int ph) {
+        if (stm) {
+            const u64 t = __builtin_amdgcn_s_memtime();
+            tph[ph] += t - tprev;
+            tprev = t;
+        }
+    };
     auto flush = [&]() {
+        ++tph[7];
         const u32* tl = A.gene_tp + (size_t)cur * P;
         u32 tv[TL];
 #pragma unroll
@@ -2678,6 +2688,8 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                     }
                 }
                 ++nrun;
+                ++tph[6];
+                stamp(4);
                 if (src == 2) {  // one repeated key (as k_rank_mfma)
                     u32 myc = 0;
                     for (int i00 = 0; i00 < n; i00 += 256) {
@@ -2712,6 +2724,7 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                         }
                     }
                     wsync();
+                    stamp(5);
                     continue;
                 }
                 const bool vl = lane < n;
@@ -2733,6 +2746,7 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                     if (n > 16) bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
                     if (n > 32) bitonic_merge<32>(key, code, true, lane);
                 }
+                stamp(0);
                 // ---- one-hot operand: sorted codes at their slots, element i at
                 // byte 16 ((i >> 2) & 3) + 4 (i >> 4) + (i & 3)
                 const int sg = (((lane >> 2) & 3) << 4) | ((lane >> 4) << 2) | (lane & 3);
@@ -2752,6 +2766,7 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                     c += (u32)__shfl_xor((int)c, 32, 64);
                     if (g4 == 0 && r16 + 16 * t < K) A.hbg[(size_t)bucket * K + r16 + 16 * t] = c;
                 }
+                stamp(1);
                 // ---- M = L O (row tiles of 16 elements), R += O^T (2 M)
                 const int nmt = (n + 15) >> 4;
                 rk_v4i mb[NC];
@@ -2774,6 +2789,7 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                         const int t = rk_tile16<NC>(ma, nb);
                         R[t] = rk_mfma16(ob[ma], mb[nb], R[t]);
                     }
+                stamp(2);
                 // ---- tie groups and runs
                 const u64 kp = ((u64)(u32)__shfl_up((int)(u32)(key >> 32), 1, 64) << 32) |
                                (u64)(u32)__shfl_up((int)(u32)key, 1, 64);
@@ -2831,10 +2847,14 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                     wsync();
                 }
                 wsync();
+                stamp(3);
             }
         }
     }
     if (cur >= 0) flush();
+    stamp(4);
+    if (stm && lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&g_rk_stamps[q], (unsigned long long)tph[q]);
 }
 
 // ===================================================================== cross
