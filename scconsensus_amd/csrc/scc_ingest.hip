@@ -26,6 +26,7 @@
 //                  consecutive keys each at PBMC density) instead of 8-byte
 //                  scattered stores.
 #include "scc_common.hpp"
+#include <algorithm>
 #include "scc_kernels.hpp"
 
 #define ING_T 256
@@ -531,6 +532,35 @@ __global__ void k_reduce_dd(const dd* __restrict__ parts, int n, dd* __restrict_
     for (int i = threadIdx.x; i < n; i += 64) s = dd_add(s, parts[i]);
     s = dd_wave_sum(s);
     if (threadIdx.x == 0) *out = s;
+}
+
+// ------------------------------------------------------------ per-run clears
+// One launch for the DE run's small clears (error words, work counters), the
+// rank accumulators and the first-occurrence keys (~0): four fill launches
+// before, each ~5 us on the stream at config B.
+__global__ void __launch_bounds__(256) k_de_clear(int* __restrict__ err, int* __restrict__ counts,
+                                                  unsigned long long* __restrict__ acc, long long acc_n,
+                                                  unsigned long long* __restrict__ first, int G)
+{
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
+    if (t < 4) err[t] = 0;
+    if (t < 16) counts[t] = 0;
+    if (acc) {
+        typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
+        for (long long e = t; e < acc_n / 2; e += stride) ((u2v*)acc)[e] = u2v{0ull, 0ull};
+        if ((acc_n & 1) && t == 0) acc[acc_n - 1] = 0ull;
+    }
+    if (first)
+        for (long long e = t; e < G; e += stride) first[e] = ~0ull;
+}
+
+extern "C" hipError_t scc_launch_de_clear(int* err, int* counts, unsigned long long* acc, long long acc_n,
+                                          unsigned long long* first, int G, hipStream_t st)
+{
+    const long long work = std::max(acc ? acc_n / 2 : 0ll, (long long)G);
+    const int grid = (int)std::max(1ll, std::min(4096ll, (work + 255) / 256));
+    hipLaunchKernelGGL(k_de_clear, dim3(grid), dim3(256), 0, st, err, counts, acc, acc_n, first, G);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------ host launchers

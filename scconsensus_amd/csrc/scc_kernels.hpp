@@ -156,6 +156,8 @@ struct ScSelectLaunch {
 
 extern "C" {
 int scc_ingest_gene_tile(void);
+hipError_t scc_launch_de_clear(int* err, int* counts, unsigned long long* acc, long long acc_n,
+                               unsigned long long* first, int G, hipStream_t st);
 int scc_ingest_hist_window(int G);
 hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
                                   int G, const int* perm, const int* cc_p0, const int* cc_code, int nc, int ntile,

@@ -674,6 +674,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     const int64_t sig[6] = {G, N, K, prm->mode, ds->nnz, (int64_t)(intptr_t)ds};
     double log_thr = 0.0;
     bool hist_rng = false, hist_full = false;
+    bool de_cleared = false;  // the per-run clears ran (scc_launch_de_clear at the ingest)
     // after an error-free run whose ingest read every entry: the dataset is
     // validated and its nodg cached (for later gene-shard runs)
     auto note_validated = [&](int err_bits) -> int {
@@ -720,8 +721,9 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     hist_full = !hist_rng && !hist_ro;
     {
         Scope sc(c, "ingest", s0);
-        HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
-        HIPCHK(c, hipMemsetAsync(d_counts, 0, sizeof(int) * 16, s0));
+        // error words, counters, rank accumulators and first-occurrence keys in one launch
+        HIPCHK(c, scc_launch_de_clear(d_err, d_counts, ttest ? nullptr : d_acc, (long long)acc_n, d_first, (int)G, s0));
+        de_cleared = true;
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
                                          hist_rng ? 1 : (hist_ro ? 2 : 0), d_err, s0));
@@ -810,7 +812,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     }
     if (!ttest) {
         Scope sc(c, "gene_rank", s0);
-        HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
+        if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
         ScRankLaunch L{};
         L.gstart = d_gstart;
         L.keys = d_keys;
@@ -1034,7 +1036,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if ((rc = ws_get(c, "key_scratch", std::max<size_t>(PG, G) * scc_select_key_bytes(), &d_key))) return rc;
     {
         Scope sc(c, "pair_select", s0);
-        HIPCHK(c, hipMemsetAsync(d_first, 0xFF, sizeof(unsigned long long) * G, s0));
+        if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_first, 0xFF, sizeof(unsigned long long) * G, s0));
         if (fast) HIPCHK(c, scc_launch_count_tested(d_flags, G, P, d_tested, d_rowoff, s0));
         ScSelectLaunch S{};
         S.K = K;
