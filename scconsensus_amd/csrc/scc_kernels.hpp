@@ -77,6 +77,7 @@ struct ScRankLaunch {
     ScRankItem* fat2;      // [fat2_cap] second re-split level (counts[12])
     int fat2_cap;
     int rs_level;          // wave re-split launch: 0 reads fatbk, 1 reads fat2
+    int rsw_all;           // wave re-split: one launch takes every gene (no split by tested pairs)
     int cross_wave;        // 1: gene-level cross terms by the per-(gene, pair) wave kernel
     int* split_genes;      // [G]
     unsigned long long* keys2;  // [nnz] bucket-ordered keys of split genes

@@ -1543,7 +1543,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     for (int f = f0; f < f1; ++f) {
         const ScRankItem it = list[f];
         const int n = it.n, g = it.gene;
-        {  // this launch's genes (a gene's parents are together in the list)
+        if (!A.rsw_all) {  // this launch's genes (a gene's parents are together in the list)
             const int nt_g = A.gene_nt[g];
             if (SMALL ? nt_g > PACC : nt_g <= 64 * RSW_TS_SMALL) continue;
         }
@@ -2107,12 +2107,17 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             for (int q = 0; q < RW_SLOTS; ++q) {
                 if (q * 64 >= ntp || A.dbg == 1) break;
                 u64 ma, mb;
-                if (K > 16) {  // the pair's masks straight from the leaders' LDS posts (two reads, no lane moves)
+                if (K > 16 && K <= 64) {  // the pair's masks straight from the leaders' LDS posts (two reads, no lane moves)
                     ma = cms[wv][pa[q]];
                     mb = cms[wv][pb[q]];
                 } else {
                     ma = shfl_u64(cm, (int)(pa[q] & 63u));
                     mb = shfl_u64(cm, (int)(pb[q] & 63u));
+                    if (K > 64) {
+                        const u64 ma1 = shfl_u64(cm1, (int)(pa[q] & 63u)), mb1 = shfl_u64(cm1, (int)(pb[q] & 63u));
+                        ma = pa[q] >= 64 ? ma1 : ma;
+                        mb = pb[q] >= 64 ? mb1 : mb;
+                    }
                 }
                 if (q * 64 + lane < ntp && ma && mb) {
                     u32 S, E, X;
@@ -3158,14 +3163,17 @@ extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, h
     const long long waves = 2LL * grid * 4;
     W.rsw_chunk = (int)std::max(8LL, std::min(128LL, (long long)L->bucket_cap / (16 * waves)));
     W.rs_level = 0;
-    hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
+    // K > 64 (config E): most genes hold more than 512 tested pairs, one launch
+    // of the wide variant takes every parent (a second pass over the list cost more)
+    W.rsw_all = L->K > 64 ? 1 : 0;
+    if (!W.rsw_all) hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
     if (L->P > 64 * RSW_TS_SMALL) hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, st, W);
     const size_t acc_lds = sizeof(u64) * (size_t)std::max(L->P, 1);
     hipFuncSetAttribute((const void*)k_rank_resplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_lds);
     hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), acc_lds, st, *L);
     if (L->fat2) {  // sub-buckets the first level left with > 64 distinct values
         W.rs_level = 1;
-        hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
+        if (!W.rsw_all) hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
         if (L->P > 64 * RSW_TS_SMALL)
             hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, st, W);
     }
