@@ -287,6 +287,9 @@ static int genes_h2d(scc_ctx* c, int* d_genes, const int32_t* genes, int nu, hip
     return SCC_OK;
 }
 
+// set by scc_de_distance around its distance call: the DE's device union
+static thread_local const int* t_dev_union = nullptr;
+
 static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,
                      int32_t ncomp, int64_t col_lo, int64_t col_hi, void* dist_out, int32_t out_kind, int32_t out_f32)
 {
@@ -328,12 +331,17 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     if (out_kind == SCC_PTR_HOST || !dist_out) {  // NULL device output: keep it in the workspace
         if ((rc = ws_get(c, "d_dist", npairs * (out_f32 ? 4 : 8), &d_out))) return rc;
     }
-    if ((rc = genes_h2d(c, d_genes, genes, nu, s0))) return rc;
+    // scc_de_distance: the DE's union is still in the workspace, on this device
+    // and in this order: used in place of an upload of the host copy
+    if (t_dev_union && c->peers.empty())
+        d_genes = const_cast<int*>(t_dev_union);
+    else if ((rc = genes_h2d(c, d_genes, genes, nu, s0)))
+        return rc;
     {
         Scope sc(c, "gather", s0);
         // the CSC gather writes whole rows (zeros included): only the padding rows need clearing
         const size_t r0 = (ds->dense || !scc_gather_writes_rows(ld)) ? 0 : (size_t)N;
-        HIPCHK(c, hipMemsetAsync(d_X + r0 * ld, 0, sizeof(double) * ((size_t)Npad - r0) * ld, s0));
+        if ((size_t)Npad > r0) HIPCHK(c, hipMemsetAsync(d_X + r0 * ld, 0, sizeof(double) * ((size_t)Npad - r0) * ld, s0));
         HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
         HIPCHK(c, scc_launch_gather(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, N, d_umap, d_genes, nu, ld,
                                     d_X, s0));
@@ -536,8 +544,13 @@ extern "C" int scc_de_distance(scc_ctx* c, const scc_dataset* ds, const int32_t*
     if (rc != SCC_OK) return rc;
     const scc_de_result* r = *out;
     if (r->union_genes.empty()) return fail(c, SCC_ERR_INVALID, "empty gene union");
-    return dist_impl(c, ds, r->union_genes.data(), (int32_t)r->union_genes.size(), metric, ncomp, 0, ds->N, dist_out,
-                     out_kind, out_f32);
+    // the DE's device union (a workspace view, valid while nothing else ran)
+    t_dev_union = (c->peers.empty() && r->generation == c->generation && env_int("SCC_DEVICE_UNION", 1)) ? r->d_union
+                                                                                                     : nullptr;
+    const int drc = dist_impl(c, ds, r->union_genes.data(), (int32_t)r->union_genes.size(), metric, ncomp, 0, ds->N,
+                              dist_out, out_kind, out_f32);
+    t_dev_union = nullptr;
+    return drc;
 }
 
 extern "C" int scc_distance_cols(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, int32_t nu, int32_t metric,

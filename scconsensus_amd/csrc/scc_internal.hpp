@@ -139,6 +139,7 @@ struct scc_de_result {
     double log_thr = 0.0;
     // device views into the context workspace (valid while generation matches)
     const int* d_nodg = nullptr;
+    const int* d_union = nullptr;  // the union in device memory (the single-device engine run; else nullptr)
     const int* d_row_gene = nullptr;
     const double *d_row_p = nullptr, *d_row_q = nullptr, *d_row_lfc = nullptr, *d_row_pct1 = nullptr,
                  *d_row_pct2 = nullptr;

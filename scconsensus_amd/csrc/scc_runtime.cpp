@@ -1123,6 +1123,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     r->P = P;
     r->G = G;
     r->N = N;
+    r->d_union = d_union;
     r->log_thr = log_thr;
     if (hdr[0] < 0 || hdr[0] > G) return fail(c, SCC_ERR_HIP, "union size out of range");
     r->union_genes.assign(hs + 4 + P, hs + 4 + P + hdr[0]);
