@@ -16,7 +16,7 @@
 #include "scc_sort.hpp"
 
 #define WT_DIM 50  // exact test when both clusters < 50 cells
-#define SEL_T 256
+#define SEL_T 1024
 
 // -------------------------------------------------------- cwilcox table
 __device__ inline double cw_lookup(int k, int m, int n, const double* W, const int* woff)
