@@ -85,12 +85,13 @@ __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indp
 // index costs one LDS lookup instead of a dependent global load of umap[row]
 // (three dependent global round trips per batch of 512 entries become two).
 // Used when the map and four LDS rows fit (G * 2 + 4 * ld * 8 bytes).
-__global__ void __launch_bounds__(256) k_gather_csc_lm(const i64* __restrict__ indptr, const int* __restrict__ rows,
+__global__ void __launch_bounds__(1024) k_gather_csc_lm(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                        const double* __restrict__ vals, int N, int G,
                                                        const int* __restrict__ umap, int ld, double* __restrict__ Xc)
 {
-    extern __shared__ __attribute__((aligned(16))) double grow[];  // [4 waves][ld], then the map
-    unsigned short* lmap = (unsigned short*)(grow + 4 * (size_t)ld);
+    extern __shared__ __attribute__((aligned(16))) double grow[];  // [waves][ld], then the map
+    const int nw = blockDim.x >> 6;
+    unsigned short* lmap = (unsigned short*)(grow + nw * (size_t)ld);
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
         const int u = umap[g];
@@ -98,7 +99,7 @@ __global__ void __launch_bounds__(256) k_gather_csc_lm(const i64* __restrict__ i
     }
     __syncthreads();
     double* row = grow + (size_t)wv * ld;
-    for (int c = blockIdx.x * 4 + wv; c < N; c += gridDim.x * 4) {
+    for (int c = blockIdx.x * nw + wv; c < N; c += gridDim.x * nw) {
         for (int u = lane; u < ld; u += 64) row[u] = 0.0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -974,11 +975,24 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
         hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
     else if (ld <= GATHER_LDS_LD && sizeof(double) * 4 * (size_t)ld + 2 * (size_t)G <= 120 * 1024 &&
              !(getenv("SCC_GATHER_LM") && atoi(getenv("SCC_GATHER_LM")) == 0)) {
+        // waves per workgroup (4, 8 or 16 rows in LDS beside one copy of the
+        // map): the most resident waves per CU (a wave per cell is latency
+        // bound: indptr, then rows, then the hits' values), the fewer waves on a tie
         const int cus = scc_device_cus(256);
-        const size_t lds = sizeof(double) * 4 * (size_t)ld + ((2 * (size_t)G + 15) & ~(size_t)15);
+        const size_t mapb = (2 * (size_t)G + 15) & ~(size_t)15, cu_lds = 160 * 1024;
+        int W = 4, best = 0;
+        const char* ew = getenv("SCC_GATHER_W");
+        for (int w = 4; w <= 16; w *= 2) {
+            const size_t l = sizeof(double) * w * (size_t)ld + mapb;
+            if (l > cu_lds) break;
+            const int wgs = std::min((int)(cu_lds / l), 32 / w), res = wgs * w;
+            if ((ew && atoi(ew) == w) || (!ew && res > best)) { W = w; best = res; }
+        }
+        const size_t lds = sizeof(double) * W * (size_t)ld + mapb;
+        const int wgs = std::max(1, std::min((int)(cu_lds / lds), 32 / W));
         hipFuncSetAttribute((const void*)k_gather_csc_lm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        const int grid = std::max(1, std::min((N + 3) / 4, 2 * cus));
-        hipLaunchKernelGGL(k_gather_csc_lm, dim3(grid), dim3(256), lds, st, indptr, rows, vals, N, G, umap, ld, Xc);
+        const int grid = std::max(1, std::min((N + W - 1) / W, wgs * cus));
+        hipLaunchKernelGGL(k_gather_csc_lm, dim3(grid), dim3(64 * W), lds, st, indptr, rows, vals, N, G, umap, ld, Xc);
     } else if (ld <= GATHER_LDS_LD)
         hipLaunchKernelGGL(k_gather_csc<true>, dim3((N + 3) / 4), dim3(256), sizeof(double) * 4 * (size_t)ld, st,
                            indptr, rows, vals, N, G, umap, ld, Xc);

@@ -422,6 +422,30 @@ def test_gather_wide_union_fallback(eng):
         assert np.max(np.abs(d - ref)) < 1e-5
 
 
+@pytest.mark.parametrize("ld_genes", [150, 700])
+def test_gather_workgroup_sizes_bitwise(eng, monkeypatch, ld_genes):
+    """The LDS-map gather with 4, 8 and 16 waves per workgroup (its default
+    picks the most resident waves per CU) and the per-cell gather without the
+    map: the same distance bits (the gather only copies values)."""
+    import scipy.sparse as sp
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(9)
+    G, N = 3000, 1700
+    X = sp.random(G, N, density=0.08, random_state=10, format="csc") * 4.0
+    X.data = np.log1p(X.data)
+    ds = eng.dataset_csc(X.indptr.astype(np.int64), X.indices.astype(np.int32), X.data, G, N)
+    g = np.sort(rng.choice(G, ld_genes, replace=False)).astype(np.int32)
+    monkeypatch.setenv("SCC_GATHER_LM", "0")
+    base = eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID)
+    monkeypatch.delenv("SCC_GATHER_LM")
+    for w in ("4", "8", "16", None):
+        if w is None:
+            monkeypatch.delenv("SCC_GATHER_W", raising=False)
+        else:
+            monkeypatch.setenv("SCC_GATHER_W", w)
+        assert np.array_equal(eng.distance(ds, g, nat.SCC_DIST_PCA_EUCLID), base), w
+
+
 def test_de_distance_matches_two_calls(eng, cfg_a):
     """scc_de_distance (DE, then the distance over its union, one C call)
     returns the same union and the same distance bits as scc_de_run followed
