@@ -34,6 +34,14 @@ for s in "$@"; do
     profE) step profE 900 rocprofv3 --kernel-trace --stats -d gpurun_out/profE -o run --output-format csv -- python3 bench.py --config E --no-cpu-baseline --steps 2 --warmup 1 ;;
     pmcD) step pmcD 900 bash scripts/pmc_traffic.sh D ;;
     benchsplit) step benchsplit 600 python bench.py --no-cpu-baseline --no-transfers --steps 20 --warmup 5 --split-calls ;;
+    cap2kB) SCC_SC_CAP=2048 step cap2kB 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
+    cap3kB) SCC_SC_CAP=3072 step cap3kB 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
+    cap6kB) SCC_SC_CAP=6144 step cap6kB 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
+    cap2kD) SCC_SC_CAP=2048 step cap2kD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
+    cap8kB) SCC_SC_CAP=8192 step cap8kB 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
+    cap12kB) SCC_SC_CAP=12288 step cap12kB 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
+    cap6kD) SCC_SC_CAP=6144 step cap6kD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
+    cap8kD) SCC_SC_CAP=8192 step cap8kD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchD) step benchD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchC) step benchC 900 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchE) step benchE 900 python bench.py --config E --no-cpu-baseline --steps 3 --warmup 2 ;;
