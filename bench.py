@@ -489,12 +489,18 @@ def main():
         # warm-up: the first launch allocates; the GPU sat idle through the
         # PCIe-bound transfer measurements before this, so a few more launches
         # bring the clocks back before the timed ones (1 warm-up launch gave
-        # 0.57-0.63 of peak run to run on the same binary)
-        for _ in range(6):
+        # 0.57-0.63 of peak run to run on the same binary; 6 gave 0.61-0.66):
+        # launches for at least a quarter of a second, then 20 timed
+        t_w = time.perf_counter()
+        for i in range(1000):
             eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)
+            if i >= 5 and i % 4 == 3:
+                eng.synchronize()
+                if time.perf_counter() - t_w > 0.25:
+                    break
         eng.synchronize()
         eng.reset_timers()
-        for _ in range(10):
+        for _ in range(20):
             eng.distance(ds, r.union, nat.SCC_DIST_PEARSON, device_out_ptr=0)
         eng.synchronize()
         for f in ("zscore", "pearson"):
