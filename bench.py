@@ -168,6 +168,43 @@ def cpu_baseline(d, code, K, union, sample_genes, seed=0):
     return out
 
 
+def cold_call(d, code, K, gpu, de_mode):
+    """The R drop-in's one-shot call, timed as one number, in the glue's order
+    (integration/R/scConsensusAMD.R reclusterDEConsensusFast -> scc_r.c;
+    Fast:22-33,398-400): the dataset created from host CSC arrays (H2D), the
+    first -- validating -- scc_de_run returning the union and nodg to the
+    host, then scc_distance into a fresh pageable host vector (R's
+    allocVector).  "first": a new engine context (its workspace allocations,
+    streams and tables; HIP itself is already initialised in this process);
+    "repeat": the next call on that context with a fresh dataset (the second
+    reclusterDEConsensusFast of an R session)."""
+    from scconsensus_amd import _native as nat
+    out = {}
+    t0 = time.perf_counter()
+    eng = nat.Engine(gpu)
+    out["context_create"] = (time.perf_counter() - t0) * 1e3
+    try:
+        for tag in ("first", "repeat"):
+            t0 = time.perf_counter()
+            ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+            t1 = time.perf_counter()
+            r = eng.de_run(ds, code, K, de_mode, fetch="nodg")
+            t2 = time.perf_counter()
+            host = np.empty(d.N * (d.N - 1) // 2, np.float64)
+            eng.distance(ds, r.union, nat.SCC_DIST_PCA_EUCLID, out=host)
+            t3 = time.perf_counter()
+            ds.close()
+            out[tag] = {"total": (t3 - t0) * 1e3, "dataset_h2d": (t1 - t0) * 1e3, "de_to_host": (t2 - t1) * 1e3,
+                        "distance_to_pageable_host": (t3 - t2) * 1e3}
+            del host
+    finally:
+        eng.close()
+    out["first_including_context"] = out["context_create"] + out["first"]["total"]
+    out["note"] = ("ms; each leg ends with its result on the host (the glue's .Call boundaries); "
+                   "value stays the warmed HBM-resident step")
+    return out
+
+
 def de_only(a, eng, ds, d, code, K, dist, world):
     """Config E (BASELINE: "1M-cell sparse CSR input, 100 clusters (4950
     pairs), DE-only"): the FAST DE over all pairs, rows fetched to the host."""
@@ -192,8 +229,43 @@ def de_only(a, eng, ds, d, code, K, dist, world):
     stage_ms = {}
     for f in fams:
         t, n = eng.kernel_time(f)
-        stage_ms[f] = round(t / max(a.steps, 1), 3)  # per step
+        stage_ms[f] = round(t / max(a.steps, 1), 3)  # per step (one engine run, one launch of each stage)
     P = K * (K - 1) // 2
+    nnz, G, N = d.nnz, d.G, d.N
+    ncc = (N + 31) // 32
+    # SURVEY §8(d)'s algorithmic bytes per launch (the same accounting as the
+    # DE + distance line): B_DE = X read once (CSC: 12 B per stored value +
+    # 8 B per cell) + 4 N (codes) + 24 K G (cnt, S_expm1, S_x) + 16 P G (2U + p)
+    alg = {
+        "ingest": (12.0 * nnz + 8.0 * (N + 1) + 8.0 * nnz + 3 * 4.0 * ncc * G,
+                   "ingest stage (k_ing_hist, k_ing_colsum/segscan/colapply, scans, k_ing_scatter)"),
+        "gene_stats": (8.0 * nnz + 32.0 * K * G, "k_gene_stats"),
+        "gene_rank": (8.0 * nnz + 24.0 * P * G,
+                      "rank stage (k_rank_classify/split/resplit/waves/cross; k_rank_item on a second stream)"),
+    }
+    kernels = {}
+    for f, (work, kname) in alg.items():
+        if stage_ms.get(f, 0.0) > 0.0:
+            ach = work / (stage_ms[f] / 1e3) / 1e9
+            kernels[f] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                          "frac": ach / PEAK_HBM_GBS, "kernel": kname, "bytes_per_launch": work,
+                          "avg_launch_ms": stage_ms[f]}
+    b_de = 12.0 * nnz + 8.0 * (N + 1) + 4.0 * N + 24.0 * K * G + 16.0 * P * G
+    ach = b_de / s_step / 1e9
+    kernels["de_total"] = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                           "frac": ach / PEAK_HBM_GBS, "kernel": "the whole DE step (B_DE over the step time)",
+                           "bytes_per_launch": b_de, "avg_launch_ms": s_step * 1e3}
+    dom = max(alg, key=lambda f: stage_ms.get(f, 0.0))
+    roof = dict(kernels.get(dom, {"bound": "hbm", "achieved": None, "kernel": alg[dom][1]}))
+    roof["traffic"] = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_E.json")
+    if os.path.exists(tpath):
+        tk = json.load(open(tpath))["kernels"]
+        pref = {"gene_rank": "k_rank", "ingest": "k_ing", "gene_stats": "k_gene_stats"}[dom]
+        hits = [v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith(pref)]
+        roof["traffic"] = sum(hits) if hits else None
+        roof["traffic_source"] = "profiles/pmc_traffic_E.json (scripts/pmc_traffic.sh E)"
+    roof["note"] = "avg_launch_ms is the whole stage (its kernels back to back), not one kernel"
     out = {"metric": "DE-only seconds per reclusterDEConsensusFast DE at config E", "value": s_step, "unit": "s",
            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": s_step * 1e3,
            "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -204,7 +276,7 @@ def de_only(a, eng, ds, d, code, K, dist, world):
                       "union": len(r.union), "rows": int(len(r.rows.gene)),
                       "engine_runs_per_step": 1 if K <= 128 else (-(-K // 64)) * (-(-K // 64) - 1) // 2,
                       "parallelism": f"jobs{world}" if world > 1 else "single"},
-           "stage_ms_per_step": stage_ms}
+           "stage_ms_per_step": stage_ms, "roofline": roof, "kernels": kernels}
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     dist.close()
@@ -393,21 +465,25 @@ def main():
     nu = len(r.union)
     nnz = d.nnz
     ncc = (d.N + 31) // 32
-    frac_entries = 1.0 / world if multi else 1.0  # a rank's share of the packed output (equal-entry slices)
+    # a rank's (or, on the device-list route, a device's) share of the packed
+    # output: equal-entry column slices, one launch per slice
+    ndev_route = len(devices) if route_devices else 1
+    frac_entries = 1.0 / world if multi else 1.0 / ndev_route
+    nshare = world if multi else ndev_route  # gene blocks / Gram shards per launch
     alg = {
         # packed fp64 R `dist` output + the N x 16 scores read
         "dist": ("hbm", 8.0 * npairs_cells * frac_entries + 16 * 8.0 * d.N, "k_dist_aligned"),
         # the minimum: CSC read once (12 B/nnz + 8 B/cell), keys written once (8 B/nnz), chunk counts (4 B,
         # 3 passes); the kernels read the CSC twice (count, then scatter), which this does not credit
-        "ingest": ("hbm", (12.0 * nnz + 8.0 * (d.N + 1)) + 8.0 * nnz / world + 3 * 4.0 * ncc * d.G / world,
+        "ingest": ("hbm", (12.0 * nnz + 8.0 * (d.N + 1)) + 8.0 * nnz / nshare + 3 * 4.0 * ncc * d.G / nshare,
                    "ingest stage (k_ing_hist, k_ing_colsum/segscan/colapply, scans, k_ing_scatter)"),
-        "gene_stats": ("hbm", (8.0 * nnz + 32.0 * K * d.G) / world, "k_gene_stats"),
+        "gene_stats": ("hbm", (8.0 * nnz + 32.0 * K * d.G) / nshare, "k_gene_stats"),
         # keys read once; per (pair, gene) accumulators written (S, E, X)
-        "gene_rank": ("hbm", (8.0 * nnz + 24.0 * P * d.G) / world,
+        "gene_rank": ("hbm", (8.0 * nnz + 24.0 * P * d.G) / nshare,
                       "rank stage (k_rank_classify/split/resplit/waves/cross; k_rank_item on a second stream)"),
         # Householder tridiagonalisation 4/3 n^3 fp64 flops (one hand-off per column: latency-bound)
         "eig_tridiag": ("mfma", 4.0 / 3.0 * nu ** 3, "k_tridiag"),
-        "gram": ("mfma", 2.0 * d.N * nu * nu / 2 / world, "k_gram_f64"),
+        "gram": ("mfma", 2.0 * d.N * nu * nu / 2 / (world if multi else 1), "k_gram_f64"),  # one device on the list route
     }
     if 128 <= nu <= 1024 and stage_ms.get("eig_vec", 0.0) < 0.02:
         # the filtered subspace iteration in one persistent launch answered
@@ -439,7 +515,9 @@ def main():
     tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
     if os.path.exists(tpath) and not multi:
         tk = json.load(open(tpath))["kernels"]
-        hits = [v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith(alg[dom][2])]
+        kpre = {"dist": "k_dist", "ingest": "k_ing", "gene_stats": "k_gene_stats", "gene_rank": "k_rank",
+                "gram": "k_gram", "eig_tridiag": "k_fsi_engine" if "k_fsi_engine" in alg[dom][2] else "k_tridiag"}
+        hits = [v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith(kpre.get(dom, alg[dom][2]))]
         traffic = sum(hits) if hits else None
 
     def roof(f):
@@ -508,6 +586,10 @@ def main():
             stage_ms[f] = t[0] / max(t[1], 1)
         alg["pearson"] = ("mfma32", float(d.N) * (d.N - 1) * nu, "k_pearson_mfma")
 
+    cold = None
+    if not a.no_transfers and world == 1 and not route_devices and a.config not in DEVICE_GEN:
+        cold = cold_call(d, code, K, gpu, de_mode)
+
     roof_dom = roof(dom)
     roof_dom["traffic"] = traffic
     roof_dom["traffic_source"] = (f"profiles/pmc_traffic_{a.config}.json (scripts/pmc_traffic.sh)"
@@ -567,6 +649,8 @@ def main():
         out["n_gpus"] = len(set(devices))
     if side_devices is not None:
         out["route_devices"] = side_devices
+    if cold is not None:
+        out["cold_call_ms"] = cold
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         ng = a.cpu_sample_genes if a.config in ("A", "B") else max(16, int(300 * 66 * 26000 / (P * d.N)))
         out["cpu_baseline"] = cpu_baseline(d, code, K, r.union, ng)

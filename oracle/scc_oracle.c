@@ -326,35 +326,6 @@ double orc_r_var(const double *x, long n, double mean)
     return (double)(s / (long double)(n - 1));
 }
 
-/* Regularised incomplete beta I_x(a, b) by Lentz's continued fraction on the
- * side where it converges fast (x < (a+1)/(a+b+2)), else 1 - I_{1-x}(b, a).
- * DEVIATION: R's pbeta is TOMS 708 (bratio); Student t tails agree with scipy to ~1e-11
- * relative here (checked against scipy in tests/test_oracle.py). */
-static double betacf(double a, double b, double x)
-{
-    const double tiny = 1e-300;
-    double qab = a + b, qap = a + 1.0, qam = a - 1.0, c = 1.0, d = 1.0 - qab * x / qap;
-    if (fabs(d) < tiny) d = tiny;
-    d = 1.0 / d;
-    double h = d;
-    for (int m = 1; m <= 10000; ++m) {
-        const int m2 = 2 * m;
-        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
-        d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
-        c = 1.0 + aa / c; if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        h *= d * c;
-        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
-        d = 1.0 + aa * d; if (fabs(d) < tiny) d = tiny;
-        c = 1.0 + aa / c; if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (fabs(del - 1.0) < 1e-16) break;
-    }
-    return h;
-}
-
 /* Stirling-series correction lgamma(x) - [(x - 1/2) log x - x + log sqrt(2 pi)], x >= 10 */
 static double lgammacor(double x)
 {
@@ -380,20 +351,49 @@ static double orc_lbeta(double a, double b)
     return lgamma(p) + lgamma(q) - lgamma(p + q);
 }
 
+/* log B(a, b) in long double (the series' prefactor) */
+static long double lbeta_l(long double a, long double b)
+{
+    return lgammal(a) + lgammal(b) - lgammal(a + b);
+}
+
+/* I_x(a, b) by its hypergeometric power series (DLMF 8.17.8, 15.2.1):
+ *   I_x(a, b) = x^a (1-x)^b / (a B(a, b)) * sum_{n >= 0} (a+b)_n / (a+1)_n x^n,
+ * every term positive, summed in long double until a term no longer moves the
+ * sum.  lx = log x, l1x = log(1 - x), both from the caller's cancellation-free
+ * x and 1 - x.  This is deliberately NOT the continued fraction the GPU kernel
+ * evaluates (scc_select.hip ibeta_cf_den), so the oracle checks the kernel with
+ * an independent algorithm (and both are pinned to scipy in the tests). */
+static long double ibeta_series(long double a, long double b, long double x, long double lx, long double l1x)
+{
+    long double sum = 1.0L, term = 1.0L;
+    for (long k = 0; k < 40000000L; ++k) {
+        term *= (a + b + (long double)k) / (a + 1.0L + (long double)k) * x;
+        const long double s2 = sum + term;
+        if (s2 == sum) break;
+        sum = s2;
+    }
+    return expl(a * lx + b * l1x - lbeta_l(a, b)) / a * sum;
+}
+
 /* I_x(a, b) (lower = 1) or 1 - I_x(a, b) (lower = 0), x given with its
- * complement y = 1 - x computed by the caller without cancellation. */
+ * complement y = 1 - x computed by the caller without cancellation.  The
+ * smaller tail (x below or above the mean a / (a + b)) is summed directly:
+ * its series decreases from the first term; the other tail is 1 minus it.
+ * DEVIATION: R's pbeta is TOMS 708 (bratio); Student t tails agree with scipy
+ * to ~1e-12 relative (tests/test_oracle.py). */
 static double orc_pbeta2(double x, double y, double a, double b, int lower)
 {
     if (x <= 0.0) return lower ? 0.0 : 1.0;
     if (y <= 0.0) return lower ? 1.0 : 0.0;
-    const double lx = x > 0.5 ? log1p(-y) : log(x), ly = y > 0.5 ? log1p(-x) : log(y);
-    const double lbt = a * lx + b * ly - orc_lbeta(a, b);
-    if (x < (a + 1.0) / (a + b + 2.0)) {
-        const double v = exp(lbt) * betacf(a, b, x) / a;
-        return lower ? v : 1.0 - v;
+    const long double lx = x > 0.5 ? log1pl(-(long double)y) : logl((long double)x);
+    const long double ly = y > 0.5 ? log1pl(-(long double)x) : logl((long double)y);
+    if ((long double)x * (a + b) <= (long double)a) { /* lower tail the smaller */
+        const long double lo = ibeta_series(a, b, x, lx, ly);
+        return (double)(lower ? lo : 1.0L - lo);
     }
-    const double v = exp(lbt) * betacf(b, a, y) / b; /* = 1 - I_x(a, b) */
-    return lower ? 1.0 - v : v;
+    const long double up = ibeta_series(b, a, y, ly, lx); /* 1 - I_x(a, b) = I_y(b, a) */
+    return (double)(lower ? 1.0L - up : up);
 }
 
 /* R nmath/pt.c, lower_tail, non-log */

@@ -43,13 +43,13 @@ for s in "$@"; do
     cap6kD) SCC_SC_CAP=6144 step cap6kD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     cap8kD) SCC_SC_CAP=8192 step cap8kD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchD) step benchD 900 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
+    benchBq) step benchBq 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
     benchC) step benchC 900 python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 2 ;;
     benchE) step benchE 900 python bench.py --config E --no-cpu-baseline --steps 3 --warmup 2 ;;
     benchBslow) step benchBslow 600 python bench.py --de slow --no-cpu-baseline --no-transfers --no-pearson --steps 10 --warmup 3 ;;
     benchDslow) step benchDslow 900 python bench.py --config D --de slow --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
     benchdev) SCC_BENCH_DEVICES=0,0 step benchdev 600 python bench.py --route devices --no-cpu-baseline --no-transfers --no-pearson --steps 10 --warmup 3 ;;
     dbgx) AMD_LOG_LEVEL=1 step dbgx 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_exchange.py -x -v --timeout 120 --timeout-method thread ;;
-    sticky) AMD_LOG_LEVEL=2 step sticky 300 python -u scripts/dbg_sticky.py ;;
     rank) step rank 600 python -u -m pytest tests/test_gpu_rank_mfma.py tests/test_gpu_de.py -x -v --timeout 200 --timeout-method thread ;;
     rkstB) SCC_RW_DEBUG=7 step rkstB 300 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 ;;
     rkstD) SCC_RW_DEBUG=7 step rkstD 600 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 1 --warmup 1 ;;
@@ -69,6 +69,12 @@ for s in "$@"; do
     proffsi) SCC_EIG_FSI=1 step proffsi 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proffsi -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 2 ;;
     smalleig) step smalleig 300 rocprofv3 --kernel-trace --stats -d gpurun_out/smalleig -o run --output-format csv -- python3 scripts/small_eig_bench.py ;;
     benchfsi3) SCC_EIG_FSI=1 SCC_EIG_FSI_PASSES=3 SCC_EIG_SI_LOG=1 step benchfsi3 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
+    robust) step robust 600 python -u -m pytest tests/test_gpu_robust.py tests/test_gpu_fsi.py -x -v --timeout 200 --timeout-method thread ;;
+    seg) step seg 600 python -u -m pytest tests/test_gpu_rank_seg.py tests/test_gpu_robust.py -x -v --timeout 200 --timeout-method thread ;;
+    de) step de 900 python -u -m pytest tests/test_gpu_de.py tests/test_gpu_rank_mfma.py tests/test_gpu_grouped.py -x -v --timeout 300 --timeout-method thread ;;
+    cfg) step cfg 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_large.py -x -v --timeout 600 --timeout-method thread ;;
+    benchB) step benchB 600 python bench.py --no-cpu-baseline --steps 20 --warmup 5 ;;
+    benchEq) step benchEq 900 python bench.py --config E --no-cpu-baseline --steps 2 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -407,6 +407,8 @@ class Engine:
             nodg = np.zeros(ds.N, np.int32)
             self._check(self.lib.scc_de_result_nodg(r, _ptr(nodg)))
             out.nodg = nodg
+            if fetch == "nodg":  # what the R glue's C_scc_de_fast returns: the union and nodg
+                return out
             P, G = npairs.value, ds.G
             if mode == SCC_DE_FAST:
                 n = nrows.value

@@ -383,7 +383,8 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
             unsigned long long* st_buf = nullptr;
             if (env_int("SCC_STAMPS", 0)) WS("d_estamps", 24, st_buf);
             int nwg_used = 0;
-            HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, marks, st_buf, s0));
+            HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, marks, st_buf,
+                                            eig_graph_key(c), s0));
             if (st_buf) {
                 unsigned long long h[24];
                 HIPCHK(c, hipMemcpyAsync(h, st_buf, sizeof(h), hipMemcpyDeviceToHost, s0));
@@ -675,7 +676,8 @@ extern "C" int scc_pca_shard_eigen(scc_ctx* c, const void* gram_sum, int32_t nco
     {
         Scope sc(c, "eigen", s0);
         int nwg_used = 0;
-        HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, nullptr, nullptr, s0));
+        HIPCHK(c, scc_launch_eigen_topk(d_C, nu, ld, k, d_escr, d_Z, d_W, &d_eig_err, &nwg_used, nullptr, nullptr,
+                                        eig_graph_key(c), s0));
     }
     HIPCHK(c, hipMemcpyAsync(vecs, d_Z, sizeof(double) * (size_t)nu * 16, hipMemcpyDeviceToDevice, s0));
     HIPCHK(c, hipMemcpyAsync(&c->eig_err, d_eig_err, sizeof(unsigned int), hipMemcpyDeviceToHost, s0));

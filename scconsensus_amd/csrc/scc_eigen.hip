@@ -1837,12 +1837,14 @@ extern "C" int scc_fsi_wanted(int n);
 extern "C" size_t scc_fsi_scratch_doubles(int n);
 extern "C" void scc_fsi_forget(const void* p, size_t bytes);
 extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
-                                    int* ok, hipStream_t st);
+                                    int* ok, unsigned long long key, hipStream_t st);
 extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
                                    int* ok, hipStream_t st);
 
 // which solver answered the calling thread's last scc_launch_eigen_topk:
-// 0 direct, 1 subspace iteration, 2 filtered subspace iteration (diagnostic)
+// 0 direct, 1 subspace iteration, 2 filtered subspace iteration (a launch per
+// step), 3 the same in the persistent engine, 4 the direct solver rerun
+// without cooperative waits after a hand-off time-out (diagnostic)
 static thread_local int g_eig_last_path = 0;
 extern "C" SCC_API int scc_diag_eig_last_path() { return g_eig_last_path; }
 
@@ -1866,21 +1868,18 @@ extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 
 // A: n x n symmetric (full), row-major, lda (read only).  scratch: see
 // scc_eigen_scratch_doubles.  Z: n x 16 out, W: k out (descending).
-// *err_dev (device u32 inside scratch) is set to 1 if a hand-off timed out.
-// marks (optional): 6 events recorded before/after each of the three launches
-// (a null entry is skipped).
+// *err_dev (device u32 inside scratch) is set to 1 if a hand-off timed out
+// even on the non-cooperative rerun.  key: the caller's identity for the
+// filtered iteration's graph cache (context serial and workspace generation;
+// 0: no graph).  marks (optional): 6 events recorded before/after each of the
+// three launches (a null entry is skipped).
+static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
+                             hipEvent_t* marks, unsigned long long* stamps, bool safe, hipStream_t st);
+
 extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
                                             double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
-                                            unsigned long long* stamps, hipStream_t st)
+                                            unsigned long long* stamps, unsigned long long key, hipStream_t st)
 {
-    // the side stream and its fork / join events are shared by every context
-    // on a device: one host thread at a time enqueues this launch sequence, so
-    // another context cannot re-record fork_ev / join_ev between our record
-    // and the wait on it (launches are asynchronous: the lock is held briefly).
-    // Recursive: the subspace iteration's Rayleigh-Ritz step solves its 64 x 64
-    // matrix through this same entry point on the same thread.
-    static std::recursive_mutex launch_mu;
-    std::lock_guard<std::recursive_mutex> guard(launch_mu);
     int nwg;
     bool rows_lds, lu_lds;
     eig_plan(n, nwg, rows_lds, lu_lds);
@@ -1896,7 +1895,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
         // accepted only when every test passes (else the direct solver below)
         if (marks && marks[0]) hipEventRecord(marks[0], st);
         int ok = 0;
-        e = scc_eigen_fsi(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, st);
+        e = scc_eigen_fsi(A, n, lda, k, scratch + scc_eigen_topk_scratch_direct(n, lda, k), Z, W, &ok, key, st);
         if (e != hipSuccess) return e;
         if (ok) {
             g_eig_last_path = ok == 2 ? 3 : 2;  // 3: the persistent engine ran the filter loop
@@ -1922,6 +1921,51 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
             return hipSuccess;
         }
     }
+    if ((e = eig_direct(A, n, lda, k, scratch, Z, W, marks, stamps, false, st)) != hipSuccess) return e;
+    // The direct solver's tridiagonalisation hands off between co-resident
+    // workgroups (bounded polls).  On a shared device they may not all become
+    // resident: the time-out flag is read here, and the same solve reruns on
+    // ONE workgroup with no cooperative wait (slower, same algorithm).
+    // SCC_EIG_FORCE_TIMEOUT=1 (tests) takes the rerun as if the flag were set.
+    u32 herr = 0;
+    if ((e = hipMemcpyAsync(&herr, flags + 1, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    const char* ft = getenv("SCC_EIG_FORCE_TIMEOUT");
+    if (herr || (ft && atoi(ft))) {
+        if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc eig] direct solver hand-off timed out: one-workgroup rerun\n");
+        if ((e = hipMemsetAsync(flags, 0, 64, st)) != hipSuccess) return e;
+        if ((e = eig_direct(A, n, lda, k, scratch, Z, W, nullptr, nullptr, true, st)) != hipSuccess) return e;
+        g_eig_last_path = 4;
+    }
+    return hipSuccess;
+}
+
+// The direct solver: k_tridiag, then k_tri_vectors beside the reflectors'
+// T factors / explicit Q on the per-device side stream, the back-transform
+// and k_eig_finish.  safe: one workgroup, rows anywhere, no XCD pinning and no
+// co-resident waits (the rerun after a hand-off time-out).
+static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
+                             hipEvent_t* marks, unsigned long long* stamps, bool safe, hipStream_t st)
+{
+    // the side stream and its fork / join events are shared by every context
+    // on a device: one host thread at a time enqueues this sequence on a
+    // device, so another context cannot re-record fork_ev / join_ev between
+    // our record and the wait on it (launches are asynchronous: the lock is
+    // held while they are queued, not while they run)
+    static std::mutex dev_mu[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> guard(dev_mu[(dev >= 0 && dev < 64) ? dev : 0]);
+    int nwg;
+    bool rows_lds, lu_lds;
+    eig_plan(n, nwg, rows_lds, lu_lds);
+    const EigLayout L = eig_layout(n, lda, k, nwg, rows_lds, lu_lds);
+    u32* flags = (u32*)(scratch + L.flags);
+    hipError_t e;
+    if (safe) {
+        nwg = 1;
+        rows_lds = tri_lds_bytes(n, std::max(n - tri_reg_rows(n), 0), true) <= EIG_LDS_MAX;
+    }
     // granule tags restart at 1 every launch
     e = hipMemsetAsync(scratch + L.pg, 0, sizeof(double) * (L.zq - L.pg), st);
     if (e != hipSuccess) return e;
@@ -1941,7 +1985,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     t.work = scratch + L.work;
     t.counter = flags;
     t.reg = flags + 2;
-    t.xcd_local = eig_local(n) ? 1 : 0;
+    t.xcd_local = (!safe && eig_local(n)) ? 1 : 0;
     t.stamps = stamps;
     t.err = flags + 1;
     const int R = (n + nwg - 1) / nwg;
@@ -1999,7 +2043,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     const char* pin_env = getenv("SCC_EIG_PIN");
     const int pin_mode = pin_env ? atoi(pin_env) : 2;
     // (measured at config B: eig_vec 0.37 ms anywhere, 0.42 claim loop, 0.32 wait)
-    const bool pin = t.xcd_local != 0 && pin_mode != 0;
+    const bool pin = !safe && t.xcd_local != 0 && pin_mode != 0;
     v.wait = pin_mode == 2;
     v.xcd = pin && (pin_mode == 1 || 8 * k <= 256) ? t.reg : nullptr;  // wait needs co-residency
     v.vcount = flags + 5;
@@ -2077,6 +2121,7 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     return hipGetLastError();
 }
 
+
 // diagnostic (tests): top-k eigenpairs of a device matrix A (n x n, lda) into
 // Z (n x 16) and W (k) through scc_launch_eigen_topk; returns 0 on success,
 // *path = scc_diag_eig_last_path()
@@ -2087,7 +2132,7 @@ extern "C" SCC_API int scc_diag_eigen_topk(const double* A, int n, int lda, int 
     const size_t sz = sizeof(double) * scc_eigen_scratch_doubles(n, lda, k);
     if (hipMalloc((void**)&scr, sz) != hipSuccess) return 1;
     unsigned int* err = nullptr;
-    hipError_t e = scc_launch_eigen_topk(A, n, lda, k, scr, Z, W, &err, nullptr, nullptr, nullptr, nullptr);
+    hipError_t e = scc_launch_eigen_topk(A, n, lda, k, scr, Z, W, &err, nullptr, nullptr, nullptr, 0, nullptr);
     unsigned int h = 0;
     if (e == hipSuccess && err) e = hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipDeviceSynchronize();

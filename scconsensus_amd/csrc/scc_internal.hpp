@@ -55,13 +55,16 @@ struct scc_ctx {
     // exact-test table
     double* d_wtab = nullptr;
     int* d_woff = nullptr;
-    bool wtab_ready = false;
+    int wtab_m = 0;  // cluster sizes up to wtab_m are in the table (0: none yet)
     // profiling
     bool profile = false;
     std::vector<scc_rt::PendingEv> pending;
     std::vector<hipEvent_t> ev_pool;
     std::map<std::string, scc_rt::Timer> timers;
     uint64_t generation = 0;
+    uint64_t serial = 0;  // unique per context in this process (never reused, unlike its address)
+    uint64_t ws_gen = 0;  // bumped by every workspace (re)allocation
+    bool rank_legacy = false;  // the bucket rank engine for this run (a segment overflowed)
     std::vector<int> host_tables;  // cell permutation + chunk tables of the last scc_de_run
     int* h_stage = nullptr;        // pinned: the DE result header, tested counts and union, one D2H
     size_t h_stage_n = 0;
@@ -191,6 +194,7 @@ inline int ws_get(scc_ctx* c, const char* name, size_t bytes, void** out)
         return fail(c, SCC_ERR_OOM, std::string("hipMalloc failed for workspace ") + name);
     }
     c->ws[name] = {p, grow};
+    c->ws_gen++;
     *out = p;
     return SCC_OK;
 }
@@ -222,8 +226,17 @@ inline int ws_keep(scc_ctx* c, const char* name, size_t bytes, size_t used, void
         c->ws.erase(it);
     }
     c->ws[name] = {p, grow};
+    c->ws_gen++;
     *out = p;
     return SCC_OK;
+}
+
+// The filtered eigensolver's graph-cache key: this context and the state of
+// its workspace (a graph bakes in workspace pointers; any reallocation makes
+// every earlier graph of the context unreachable)
+inline unsigned long long eig_graph_key(const scc_ctx* c)
+{
+    return ((unsigned long long)c->serial << 32) ^ (unsigned long long)(c->ws_gen & 0xffffffffu);
 }
 
 template <class T>
@@ -335,19 +348,39 @@ inline void resolve_timers(scc_ctx* c)
     c->pending.clear();
 }
 
-inline int ensure_wtab(scc_ctx* c)
+// R's exact Wilcoxon distribution (cwilcox counts) for cluster sizes up to
+// mmax: built the first time a run has two clusters of fewer than 50 cells
+// (the only pairs wilcox.test.default tests exactly), and grown when a later
+// run has larger ones.  Runs without such a pair build nothing.
+inline int ensure_wtab(scc_ctx* c, int mmax)
 {
-    if (c->wtab_ready) return SCC_OK;
-    std::vector<int> woff(50 * 50);
-    const int total = scc_wilcox_table_layout(woff.data());
-    int rc = ws(c, "wtab", (size_t)total, &c->d_wtab);
-    if (rc) return rc;
-    rc = ws(c, "woff", woff.size(), &c->d_woff);
-    if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->d_woff, woff.data(), woff.size() * sizeof(int), hipMemcpyHostToDevice, c->s0));
-    HIPCHK(c, scc_launch_wilcox_table(c->d_wtab, c->d_woff, c->s0));
-    c->wtab_ready = true;
+    mmax = std::min(mmax, 49);
+    if (!c->d_woff) {
+        std::vector<int> woff(50 * 50);
+        const int total = scc_wilcox_table_layout(woff.data());
+        int rc = ws(c, "wtab", (size_t)total, &c->d_wtab);
+        if (rc) return rc;
+        rc = ws(c, "woff", woff.size(), &c->d_woff);
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(c->d_woff, woff.data(), woff.size() * sizeof(int), hipMemcpyHostToDevice, c->s0));
+    }
+    if (mmax <= c->wtab_m) return SCC_OK;
+    HIPCHK(c, scc_launch_wilcox_table(c->d_wtab, c->d_woff, mmax, c->s0));
+    c->wtab_m = mmax;
     return SCC_OK;
+}
+
+// the largest cluster size a pair of clusters that both hold < 50 cells can
+// have (0: no such pair, no exact test in this run)
+inline int exact_test_max_size(const std::vector<int>& nclu)
+{
+    int n_small = 0, m = 0;
+    for (int v : nclu)
+        if (v < 50) {
+            ++n_small;
+            m = std::max(m, v);
+        }
+    return n_small >= 2 ? m : 0;
 }
 
 }  // namespace scc_rt

@@ -98,6 +98,45 @@ struct ScRankLaunch {
     size_t tp_scr_stride;
 };
 
+// The segment rank engine (scc_rank_seg.hip): ranked genes cut into value
+// segments of <= SG_CAP nonzeros, each sorted and counted by one workgroup.
+#define SG_CAP 2048              // elements of a sorted segment
+#define SG_TGT 1024              // the splitter's target segment size (mean)
+#define SCC_SEG_OVERFLOW 0x4000  // error word: a segment outgrew SG_CAP (the run reruns on the bucket engine)
+
+struct ScSeg {
+    long long base;  // first element (keys / keys2 index)
+    int n, gene;
+    int kind;        // 0: a whole gene in keys (codes from the cluster offsets), 1: keys2 / codes2,
+                     // 2: one repeated value (keys2 / codes2; closed form)
+    int hrow;        // row of hseg (the segment's cluster counts) for the cross-segment part; -1: none
+};
+
+struct ScSegLaunch {
+    const long long* gstart;
+    const unsigned long long* keys;
+    int G, K, P, all_pairs;
+    const uint32_t* coff;
+    const int* cl_cc;
+    const uint8_t* flags;       // [P][G] bit0: the pair tests the gene
+    unsigned long long* keys2;  // [nnz] segment-ordered keys of split genes
+    uint8_t* codes2;            // [nnz]
+    ScSeg* segs;                // [seg_cap]
+    int seg_cap;
+    int* counts;                // [0] segments, [1] split genes, [2] hseg rows, [3] splitter queue
+    int* big;                   // [G] genes for the splitter
+    int4* gseg;                 // [G] per split gene: {first hseg row, segments, gene, 0}
+    uint32_t* hseg;             // [hrow_cap][K]
+    int hrow_cap;
+    size_t cross_lds;
+    unsigned long long* accS;
+    unsigned long long* accE;
+    unsigned long long* accX;
+    unsigned long long* accF;
+    int* err;
+};
+hipError_t scc_launch_seg_rank(const ScSegLaunch* L, int ncu, hipStream_t st);
+
 struct ScTestLaunch {
     int K, G, P, mode;
     int glo, ghi;          // genes [glo, ghi): a run's gene shard (all genes: 0, G)
@@ -198,9 +237,9 @@ hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st);
 size_t scc_eigen_scratch_doubles(int n, int lda, int k);
 hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
                                  unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
-                                 unsigned long long* stamps, hipStream_t st);
+                                 unsigned long long* stamps, unsigned long long key, hipStream_t st);
 
-hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st);
+hipError_t scc_launch_wilcox_table(double* W, const int* woff, int mmax, hipStream_t st);
 int scc_wilcox_table_layout(int* woff);
 hipError_t scc_launch_pair_test(const ScTestLaunch* L, hipStream_t st);
 hipError_t scc_launch_count_tested(const uint8_t* flags, int G, int P, int* tested, long long* row_off,

@@ -8,6 +8,7 @@
 // device every entry point returns SCC_ERR_HIP.
 #include "scc_internal.hpp"
 
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -24,7 +25,9 @@ static int ctx_create_one(int device, bool profile, scc_ctx** out)
         return SCC_ERR_HIP;
     }
     if (device < 0 || device >= ndev) return SCC_ERR_INVALID;
+    static std::atomic<uint64_t> next_serial{1};
     scc_ctx* c = new scc_ctx();
+    c->serial = next_serial.fetch_add(1);
     c->device = device;
     c->profile = profile;
     if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->s0, hipStreamNonBlocking) != hipSuccess ||
@@ -488,9 +491,32 @@ struct RecIO {  // the compact exchange's buffers (DE_SHARD_REC out, DE_FINISH_R
     void* first_out = nullptr;
 };
 
+// de_run_body's answer when a segment of the segment rank engine outgrew
+// SG_CAP (a value stretch the splitter's sample missed): the same run again on
+// the bucket engine (never returned by the C ABI)
+static constexpr int kRankRetry = -1000;
+
+static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
+                       int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
+                       const RecIO* rio);
+
 static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
                        const RecIO* rio = nullptr)
+{
+    int rc = de_run_body(c, ds, code, K, prm, stage, glo64, ghi64, shard, out, rio);
+    if (rc == kRankRetry) {
+        if (env_int("SCC_SEG_LOG", 0)) fprintf(stderr, "[scc seg] segment overflow: bucket engine rerun\n");
+        c->rank_legacy = true;
+        rc = de_run_body(c, ds, code, K, prm, stage, glo64, ghi64, shard, out, rio);
+        c->rank_legacy = false;
+    }
+    return rc;
+}
+
+static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
+                       int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
+                       const RecIO* rio)
 {
     const bool shard_stage = stage == DE_SHARD || stage == DE_SHARD_REC;
     const bool finish_stage = stage == DE_FINISH || stage == DE_FINISH_REC;
@@ -621,6 +647,8 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     WS("cntpos", GK, d_cntpos);
     WS("cntneg", GK, d_cntneg);
     const bool ttest = fast && prm->test == SCC_TEST_T;  // DiffTTest (Fast:185-196): no rank stage
+    // the segment rank engine (SCC_RANK_SEG=0 or an overflow rerun: the bucket engine)
+    const bool use_seg = !ttest && !c->rank_legacy && env_int("SCC_RANK_SEG", 0) != 0;
     double* d_vx;
     WS("vx", ttest ? GK : 1, d_vx);
     // rank accumulators: S, E, X per (pair, gene), F per (cluster, gene)
@@ -661,7 +689,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     WS("first", G, d_first);
     WS("union", G, d_union);
     WS("nu", 4, d_nu);
-    if ((rc = ensure_wtab(c))) return rc;
+    if ((rc = ensure_wtab(c, exact_test_max_size(nclu)))) return rc;
     hipStream_t s0 = c->s0, s1 = c->s1;
     c->generation++;
     const int* d_perm = d_tab;
@@ -810,7 +838,38 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         Scope sc(c, "pair_filter", s0);
         HIPCHK(c, scc_launch_pair_filter(&T, s0));
     }
-    if (!ttest) {
+    if (use_seg) {
+        // the segment engine (scc_rank_seg.hip): value segments of <= SG_CAP
+        // nonzeros, each sorted and counted on the matrix cores by one workgroup
+        Scope sc(c, "gene_rank", s0);
+        if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
+        ScSegLaunch SL{};
+        SL.gstart = d_gstart;
+        SL.keys = d_keys;
+        SL.G = (int)G;
+        SL.K = K;
+        SL.P = P;
+        SL.all_pairs = all_pairs ? 1 : 0;
+        SL.coff = d_cnt;
+        SL.cl_cc = d_clcc;
+        SL.flags = d_flags;
+        SL.keys2 = d_keys2;
+        SL.codes2 = d_codes2;
+        SL.seg_cap = (int)std::min<int64_t>(2 * G + nnz1 / (SG_TGT / 2) + 64, 1 << 30);
+        SL.hrow_cap = (int)std::min<int64_t>(G + nnz1 / (SG_TGT / 2) + 64, 1 << 30);
+        WS("segs", (size_t)SL.seg_cap, SL.segs);
+        WS("segcnt", 8, SL.counts);
+        WS("segbig", (size_t)G, SL.big);
+        WS("gseg", (size_t)G, SL.gseg);
+        WS("hseg", (size_t)SL.hrow_cap * K, SL.hseg);
+        SL.accS = accS;
+        SL.accE = accE;
+        SL.accX = accX;
+        SL.accF = accF;
+        SL.err = d_err;
+        HIPCHK(c, hipMemsetAsync(SL.counts, 0, sizeof(int) * 8, s0));
+        HIPCHK(c, scc_launch_seg_rank(&SL, c->n_cu > 0 ? c->n_cu : 256, s0));
+    } else if (!ttest) {
         Scope sc(c, "gene_rank", s0);
         if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
         ScRankLaunch L{};
@@ -991,6 +1050,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         int e = 0;
         HIPCHK(c, hipMemcpy(&e, d_err, sizeof(int), hipMemcpyDeviceToHost));
         if (e & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
+        if (use_seg && (e & SCC_SEG_OVERFLOW)) return kRankRetry;
         if (e & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
         if (e & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
         if (e & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
@@ -1114,6 +1174,7 @@ static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
     if (hdr[1] & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
     if (hdr[1] & 16) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: record out of range");
+    if (use_seg && (hdr[1] & SCC_SEG_OVERFLOW)) return kRankRetry;
     if ((rc = note_validated(hdr[1]))) return rc;
     scc_de_result* r = new scc_de_result();
     r->ctx = c;

@@ -37,22 +37,31 @@ __device__ inline double cw_lookup(int k, int m, int n, const double* W, const i
     }
 }
 
-// single workgroup; level s = i + j ascending, all entries of a level in parallel
-__global__ void __launch_bounds__(1024) k_wilcox_table(double* W, const int* woff)
+// single workgroup; level s = i + j ascending, every entry of a level (all
+// its (i, j) rows at once, flattened over the threads) in parallel.  Only the
+// sizes i <= j <= mmax are built: the exact test runs for a pair of clusters
+// that both hold fewer than 50 cells (wilcox.test.default's rule), and
+// cwilcox(k, m, n) reads only rows with i <= m, j <= n.
+__global__ void __launch_bounds__(1024) k_wilcox_table(double* W, const int* woff, int mmax)
 {
-    for (int s = 2; s <= 2 * (WT_DIM - 1); ++s) {
-        for (int i = 1; i < WT_DIM; ++i) {
-            const int j = s - i;
-            if (j < i || j >= WT_DIM) continue;
-            const int c = (i * j) / 2;
-            double* row = W + woff[i * WT_DIM + j];
-            for (int k = threadIdx.x; k <= c; k += blockDim.x) {
-                if (k < j) {
-                    row[k] = -1.0;  // never read (reduced to cwilcox(k, i, k))
-                } else {
-                    row[k] = cw_lookup(k - j, i - 1, j, W, woff) + cw_lookup(k, i, j - 1, W, woff);
-                }
+    for (int s = 2; s <= 2 * mmax; ++s) {
+        const int ilo = max(1, s - mmax), ihi = s / 2;  // rows (i, s - i) with i <= j <= mmax
+        int tot = 0;
+        for (int i = ilo; i <= ihi; ++i) tot += (i * (s - i)) / 2 + 1;
+        for (int f = threadIdx.x; f < tot; f += blockDim.x) {
+            int i = ilo, k = f;
+            for (;;) {
+                const int len = (i * (s - i)) / 2 + 1;
+                if (k < len) break;
+                k -= len;
+                ++i;
             }
+            const int j = s - i;
+            double* row = W + woff[i * WT_DIM + j];
+            if (k < j)
+                row[k] = -1.0;  // never read (reduced to cwilcox(k, i, k))
+            else
+                row[k] = cw_lookup(k - j, i - 1, j, W, woff) + cw_lookup(k, i, j - 1, W, woff);
         }
         __syncthreads();
     }
@@ -113,8 +122,9 @@ __device__ inline double wilcox_p(i64 u2, i64 tie, int nx, int ny, const double*
 // -------------------------------------------------------- Welch t test
 // stats::t.test(x, y)$p.value (R/t.test.R, two-sided, var.equal = FALSE) for
 // the DiffTTest path (Fast:185-196): 2 * pt(-|t|, df) with R nmath/pt.c's
-// regimes; pbeta by Lentz's continued fraction with R's lbeta (the oracle's
-// restatement, oracle/scc_oracle.c; TOMS 708 in R agrees to ~1e-11).
+// regimes; pbeta by the continued fraction below with R's lbeta (R's own
+// pbeta is TOMS 708; the oracle checks this with the power series and both are
+// pinned to scipy).
 __device__ inline double t_lgammacor(double x)
 {
     const double r = 1.0 / (x * x);
@@ -137,34 +147,30 @@ __device__ inline double t_lbeta(double a, double b)
     return lgamma(p) + lgamma(q) - lgamma(p + q);
 }
 
-__device__ inline double t_betacf(double a, double b, double x)
+// The continued fraction of I_x(a, b) (DLMF 8.17.22):
+//   I_x(a, b) = x^a (1-x)^b / (a B(a, b)) / K,  K = 1 + d_1 / (1 + d_2 / (1 + ...)),
+//   d_{2m+1} = -(a+m)(a+b+m) x / ((a+2m)(a+2m+1)),  d_{2m} = m(b-m) x / ((a+2m-1)(a+2m)),
+// evaluated forward by the modified Lentz method (Thompson & Barnett 1986):
+// K_j = K_{j-1} C_j D_j, C_j = 1 + d_j / C_{j-1}, D_j = 1 / (1 + d_j D_{j-1})
+// (C_0 = K_0 = 1, D_0 = 0), one coefficient per step, until C_j D_j = 1 to
+// working precision.  Returns K.  (The oracle sums the power series instead.)
+__device__ inline double ibeta_cf_den(double a, double b, double x)
 {
     const double tiny = 1e-300;
-    const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
-    double c = 1.0, d = 1.0 - qab * x / qap;
-    if (fabs(d) < tiny) d = tiny;
-    d = 1.0 / d;
-    double h = d;
-    for (int m = 1; m <= 10000; ++m) {
-        const int m2 = 2 * m;
-        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
-        d = 1.0 + aa * d;
-        if (fabs(d) < tiny) d = tiny;
-        c = 1.0 + aa / c;
-        if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        h *= d * c;
-        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
-        d = 1.0 + aa * d;
-        if (fabs(d) < tiny) d = tiny;
-        c = 1.0 + aa / c;
-        if (fabs(c) < tiny) c = tiny;
-        d = 1.0 / d;
-        const double del = d * c;
-        h *= del;
-        if (fabs(del - 1.0) < 1e-16) break;
+    double K = 1.0, C = 1.0, D = 0.0;
+    for (int j = 1; j <= 20000; ++j) {
+        const int m = j >> 1;
+        const double dj = (j & 1) ? -(a + m) * (a + b + m) * x / ((a + 2 * m) * (a + 2 * m + 1))
+                                  : m * (b - m) * x / ((a + 2 * m - 1) * (a + 2 * m));
+        D = 1.0 + dj * D;
+        D = 1.0 / (fabs(D) < tiny ? tiny : D);
+        C = 1.0 + dj / C;
+        if (fabs(C) < tiny) C = tiny;
+        const double cd = C * D;
+        K *= cd;
+        if (fabs(cd - 1.0) < 1e-16) break;
     }
-    return h;
+    return K;
 }
 
 // I_x(a, b) (lower) or 1 - I_x(a, b), with y = 1 - x from the caller
@@ -175,10 +181,10 @@ __device__ inline double t_pbeta2(double x, double y, double a, double b, bool l
     const double lx = x > 0.5 ? log1p(-y) : log(x), ly = y > 0.5 ? log1p(-x) : log(y);
     const double lbt = a * lx + b * ly - t_lbeta(a, b);
     if (x < (a + 1.0) / (a + b + 2.0)) {
-        const double v = exp(lbt) * t_betacf(a, b, x) / a;
+        const double v = exp(lbt) / (a * ibeta_cf_den(a, b, x));
         return lower ? v : 1.0 - v;
     }
-    const double v = exp(lbt) * t_betacf(b, a, y) / b;
+    const double v = exp(lbt) / (b * ibeta_cf_den(b, a, y));
     return lower ? 1.0 - v : v;
 }
 
@@ -693,9 +699,10 @@ __global__ void __launch_bounds__(T) k_union(const u64* first_occ, int G, KeyRec
 }
 
 // -------------------------------------------------------- launchers
-extern "C" hipError_t scc_launch_wilcox_table(double* W, const int* woff, hipStream_t st)
+extern "C" hipError_t scc_launch_wilcox_table(double* W, const int* woff, int mmax, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_wilcox_table, dim3(1), dim3(1024), 0, st, W, woff);
+    if (mmax < 1) return hipSuccess;
+    hipLaunchKernelGGL(k_wilcox_table, dim3(1), dim3(1024), 0, st, W, woff, min(mmax, WT_DIM - 1));
     return hipGetLastError();
 }
 

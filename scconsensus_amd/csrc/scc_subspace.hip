@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -459,7 +460,7 @@ extern "C" int scc_si_wanted(int n)
 
 extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int k, double* scratch, double* Z,
                                             double* W, unsigned int** err_dev, int* nwg_out, hipEvent_t* marks,
-                                            unsigned long long* stamps, hipStream_t st);
+                                            unsigned long long* stamps, unsigned long long key, hipStream_t st);
 
 // ===========================================================================
 // Filtered subspace iteration (Chebyshev-accelerated; the default for
@@ -819,6 +820,9 @@ __global__ void k_fsi_coef0(double* __restrict__ coef)
 #define FX_NPRES 672    // C tile (16 x np doubles) and the Cholesky's 2 x 64 x CB_S side by side in LDS
 #define FX_NPMAX 1024   // above FX_NPRES the Cholesky borrows the C tile's LDS (reloaded after each CholQR)
 #define FX_SPIN (1u << 22)
+// the polls' bound (FX_SPIN; tests lower it through SCC_EIG_FX_SPIN to drive the
+// time-out path on an idle device)
+__device__ u32 g_fx_spin_limit = FX_SPIN;
 #define FX_LB 12  // k-steps per operand load batch (the MFMA order is k_fsi_mul's whatever the batch)
 
 struct FxArgs {
@@ -876,6 +880,7 @@ __device__ __forceinline__ bool fx_wait(const u32* flags, u32* err, int base, in
 {
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
+        const u32 lim = *(volatile const u32*)&g_fx_spin_limit;
         u32 spins = 0;
         bool bad = false;
         for (;;) {
@@ -885,7 +890,7 @@ __device__ __forceinline__ bool fx_wait(const u32* flags, u32* err, int base, in
                                           __HIP_MEMORY_SCOPE_AGENT) >= ph;
             if (__all(mine)) break;
             ++spins;
-            if (spins > FX_SPIN ||
+            if (spins > lim ||
                 ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 bad = true;
                 break;
@@ -1489,8 +1494,9 @@ __global__ void __launch_bounds__(256) k_fsi_engine(FxArgs a)
 // The engine's verdict words (acceptance flag, hand-off error) written by one
 // small kernel into mapped pinned memory: the host reads them after the
 // stream sync instead of two device-to-host copies (each ~5 us of copy-engine
-// latency plus its gap on the stream).  One buffer per device; every use is
-// under scc_launch_eigen_topk's lock.
+// latency plus its gap on the stream).  One buffer per (host thread, device):
+// two contexts on one device driven from two threads never share it, and one
+// thread's calls are sequential (it is read before the next call writes it).
 __global__ void k_fsi_verdict(const u32* __restrict__ flag, const u32* __restrict__ err, volatile u32* out)
 {
     if (threadIdx.x == 0) {
@@ -1499,26 +1505,39 @@ __global__ void k_fsi_verdict(const u32* __restrict__ flag, const u32* __restric
     }
 }
 
+namespace {
+struct VerdictBufs {
+    u32* host[64] = {};
+    u32* devp[64] = {};
+    ~VerdictBufs()
+    {
+        for (int d = 0; d < 64; ++d)
+            if (host[d]) (void)hipHostFree(host[d]);
+    }
+};
+}  // namespace
+
 static volatile u32* fsi_verdict_buf(int dev, u32** dptr)
 {
-    static std::mutex mu;
-    static u32* host[64] = {};
-    static u32* devp[64] = {};
+    static thread_local VerdictBufs vb;
     if (dev < 0 || dev >= 64) return nullptr;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!host[dev]) {
+    if (!vb.host[dev]) {
         u32* h = nullptr;
-        if (hipHostMalloc((void**)&h, 64, hipHostMallocMapped) != hipSuccess) return nullptr;
+        if (hipHostMalloc((void**)&h, 64, hipHostMallocMapped) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
         u32* d = nullptr;
         if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
             (void)hipHostFree(h);
             return nullptr;
         }
-        host[dev] = h;
-        devp[dev] = d;
+        vb.host[dev] = h;
+        vb.devp[dev] = d;
     }
-    *dptr = devp[dev];
-    return host[dev];
+    *dptr = vb.devp[dev];
+    return vb.host[dev];
 }
 
 static int fsi_env(const char* name, int dflt)
@@ -1557,15 +1576,40 @@ extern "C" size_t scc_fsi_scratch_doubles(int n)
            3 * nblk * 16 + 64 + 2 * np + 2 * nt * SGF_W + 64 + 64 * nt + 64;
 }
 
-// the persistent engine for n <= FX_NPMAX (SCC_EIG_FSI_ENGINE=0: the launch per step)
-static bool fx_usable(int n)
-{
-    return fsi_env("SCC_EIG_FSI_ENGINE", 1) != 0 && (int)si_npad(n) <= FX_NPMAX;
-}
 static size_t fx_lds_bytes(int np)
 {
     const size_t own = np > FX_NPRES ? (size_t)16 * np + 768 + 64 : (size_t)16 * np + 2 * 64 * CB_S + 64;
     return sizeof(double) * std::max(own, (size_t)SE_LDS_TOTAL);
+}
+static void fx_prepare();
+
+// After a hand-off time-out the engine stays off on that device for the next
+// FX_COOL calls (the launch path answers them; a contended device would pay
+// the bounded polls again on every call), then is tried again.
+#define FX_COOL 32
+static std::atomic<int> g_fx_cool[64];
+
+// the persistent engine for n <= FX_NPMAX (SCC_EIG_FSI_ENGINE=0: the launch
+// per step): only when all 4 nt workgroups can be resident at once on this
+// device (occupancy at the engine's LDS size times the CUs), and not while a
+// recent time-out cools down
+static bool fx_usable(int n, int dev)
+{
+    if (fsi_env("SCC_EIG_FSI_ENGINE", 1) == 0 || (int)si_npad(n) > FX_NPMAX) return false;
+    if (dev >= 0 && dev < 64 && g_fx_cool[dev].load() > 0) {
+        g_fx_cool[dev].fetch_sub(1);
+        return false;
+    }
+    const int np = (int)si_npad(n), nwg = 4 * (np / 16);
+    fx_prepare();
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_fsi_engine, 256, fx_lds_bytes(np)) !=
+            hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return (long long)per_cu * cus >= nwg;
 }
 static void fx_prepare()
 {
@@ -1578,7 +1622,8 @@ static void fx_prepare()
 
 namespace {
 struct FsiGraphEntry {
-    int dev, n, ldc, k, S, m, passes, live, guard, engine;
+    unsigned long long key;  // the caller's context serial and workspace generation
+    int dev, n, ldc, k, S, m, passes, live, guard, engine, rr, stamps;
     const void *C, *scr, *Z, *W;
     hipGraphExec_t exec;
 };
@@ -1623,7 +1668,7 @@ hipStream_t fsi_capture_stream(int dev)
 // test (Z, W written; 2: the persistent engine ran the filter loop, 1: a launch
 // per step), 0: run the direct solver.  Synchronises st.
 extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, double* scr, double* Z, double* Wout,
-                                    int* ok, hipStream_t st)
+                                    int* ok, unsigned long long key, hipStream_t st)
 {
     *ok = 0;
     if (n < FSI_NMIN || k > 16 || k < 1) return hipSuccess;
@@ -1655,7 +1700,25 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     scc_small_syev_prepare();  // kernel attributes, outside any capture
     fx_prepare();
     const dim3 gt((unsigned)nt, SI_B / 16), gg(SI_B / 16, SI_B / 16);
-    int use_engine = fx_usable(n) ? 1 : 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int use_engine = fx_usable(n, dev) ? 1 : 0;
+    const int rr_on = fsi_env("SCC_EIG_FSI_ENGINE_RR", 1) != 0, stamps_on = fsi_env("SCC_EIG_FSI_STAMPS", 0) != 0;
+    if (use_engine) {  // the polls' bound (tests: SCC_EIG_FX_SPIN); written only when it changes
+        static std::mutex spin_mu;
+        static u32 spin_set[64];
+        static bool spin_init[64];
+        const u32 want = (u32)fsi_env("SCC_EIG_FX_SPIN", (int)FX_SPIN);
+        std::lock_guard<std::mutex> lk(spin_mu);
+        if (dev >= 0 && dev < 64 && (!spin_init[dev] || spin_set[dev] != want)) {
+            hipError_t se = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fx_spin_limit), &want, sizeof(u32), 0,
+                                                   hipMemcpyHostToDevice, st);
+            if (se != hipSuccess) return se;
+            if ((se = hipStreamSynchronize(st)) != hipSuccess) return se;
+            spin_set[dev] = want;
+            spin_init[dev] = true;
+        }
+    }
     auto rayleigh_ritz = [&](hipStream_t s) -> hipError_t {
         hipError_t e;
         // Rayleigh-Ritz on span(Q): W = C Q (Ya), H = Q^T W, its top-k eigenpairs
@@ -1715,7 +1778,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             fa.coef = coef;
             fa.flag = flag;
             fa.err = fxerr;
-            fa.rr = fsi_env("SCC_EIG_FSI_ENGINE_RR", 1) != 0;
+            fa.rr = rr_on;
             fa.k = k;
             fa.guard = guard;
             fa.tol = FSI_TOL;
@@ -1727,7 +1790,7 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
             fa.Z = Z;
             fa.Wout = Wout;
             fa.stamps = nullptr;
-            if (fsi_env("SCC_EIG_FSI_STAMPS", 0)) {
+            if (stamps_on) {
                 void* sp = nullptr;
                 if (hipGetSymbolAddress(&sp, HIP_SYMBOL(g_fx_stamps)) == hipSuccess) {
                     fa.stamps = (u64*)sp;
@@ -1777,15 +1840,14 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         return rayleigh_ritz(s);
     };
     hipError_t e = hipSuccess;
-    int dev = 0;
-    hipGetDevice(&dev);
     bool launched = false;
-    if (fsi_env("SCC_EIG_FSI_GRAPH", 1)) {
+    if (key != 0 && fsi_env("SCC_EIG_FSI_GRAPH", 1)) {
         std::lock_guard<std::mutex> lk(g_fsi_mu);
         hipGraphExec_t ex = nullptr;
         for (const auto& g : g_fsi_graphs)
-            if (g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m && g.passes == passes &&
-                g.live == live && g.guard == guard && g.engine == use_engine && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
+            if (g.key == key && g.dev == dev && g.n == n && g.ldc == ldc && g.k == k && g.S == S && g.m == m &&
+                g.passes == passes && g.live == live && g.guard == guard && g.engine == use_engine && g.rr == rr_on &&
+                g.stamps == stamps_on && g.C == C && g.scr == scr && g.Z == Z && g.W == Wout) {
                 ex = g.exec;
                 if (fsi_env("SCC_EIG_FSI_DEBUG", 0)) fprintf(stderr, "[scc fsi dbg] graph hit scr=%p flag=%p\n", scr, (void*)flag);
                 break;
@@ -1802,7 +1864,8 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
                         hipGraphExecDestroy(g_fsi_graphs.front().exec);
                         g_fsi_graphs.erase(g_fsi_graphs.begin());
                     }
-                    g_fsi_graphs.push_back({dev, n, ldc, k, S, m, passes, live, guard, use_engine, C, scr, Z, Wout, ex});
+                    g_fsi_graphs.push_back({key, dev, n, ldc, k, S, m, passes, live, guard, use_engine, rr_on, stamps_on,
+                                            C, scr, Z, Wout, ex});
                 } else {
                     ex = nullptr;
                 }
@@ -1847,10 +1910,24 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
         for (size_t g = 0; g < (size_t)4 * nt; ++g) fprintf(stderr, " %u", fl[g * FX_FS]);
         fprintf(stderr, "\n");
     }
+    if (use_engine && fsi_env("SCC_EIG_FSI_FORCE_HERR", 0)) herr = 1;  // tests: take the time-out path
     if (herr) {
         // a hand-off of the persistent engine timed out (the device was shared and
-        // its workgroups were not co-resident): the same solve, a launch per step
+        // its workgroups were not co-resident): the same solve, a launch per step;
+        // the engine cools down on this device and its graphs here are dropped
         if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc fsi] engine hand-off timed out: launch path\n");
+        if (dev >= 0 && dev < 64) g_fx_cool[dev].store(std::max(0, fsi_env("SCC_EIG_FX_COOL", FX_COOL)));
+        {
+            std::lock_guard<std::mutex> lk(g_fsi_mu);
+            for (size_t i = 0; i < g_fsi_graphs.size();) {
+                if (g_fsi_graphs[i].dev == dev && g_fsi_graphs[i].engine) {
+                    (void)hipGraphExecDestroy(g_fsi_graphs[i].exec);
+                    g_fsi_graphs.erase(g_fsi_graphs.begin() + i);
+                } else {
+                    ++i;
+                }
+            }
+        }
         use_engine = 0;
         launched = false;
         if ((e = enqueue(st)) != hipSuccess) return e;
@@ -1948,7 +2025,7 @@ extern "C" hipError_t scc_eigen_si(const double* C, int n, int ldc, int k, doubl
     hipLaunchKernelGGL(k_si_hsym, dim3(16), dim3(256), 0, st, part, H);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     unsigned int* inner_err = nullptr;
-    if ((e = scc_launch_eigen_topk(H, SI_B, SI_B, k, escr, Y, theta, &inner_err, nullptr, nullptr, nullptr, st)) !=
+    if ((e = scc_launch_eigen_topk(H, SI_B, SI_B, k, escr, Y, theta, &inner_err, nullptr, nullptr, nullptr, 0, st)) !=
         hipSuccess)
         return e;
     hipLaunchKernelGGL(k_si_ritz, dim3(nblk), dim3(256), 0, st, a, b, Y, theta, n, k, Z, rpart, mpart);

@@ -161,7 +161,15 @@ def _de_sharded(eng, ds, code, K, dist, device, fetch, weights, exchange, pair_s
         # the status word is copied behind the union's own read-back (same
         # stream), so checking it costs no extra host round trip
         st_host = _stage_to_host(first[-1:])
-        union = eng.de_union_first_occ(keys.data_ptr(), ds.G)
+        try:
+            union = eng.de_union_first_occ(keys.data_ptr(), ds.G)
+        except Exception:
+            # a failed rank's keys are garbage, so the union call may fail on them
+            # first: the job's status word names the real failure
+            if getattr(first, "is_cuda", False):
+                torch.cuda.current_stream(device).synchronize()
+            _raise_if([-int(st_host[0])], msg)
+            raise
         _raise_if([-int(st_host[0])], msg)
         return nat.DeResult(nat.SCC_DE_FAST, K, P, union, np.zeros(0, np.int32))
     return eng.de_finish_records(ds, code, K, recs.data_ptr(), counts, stride, fetch=fetch, **shard_kw)
@@ -250,7 +258,9 @@ def distance_sharded(eng, ds, genes, dist: parallel.Dist, device=None, f32=False
     """This rank's column slice of the job's packed PCA-Euclidean distance,
     from the sharded PCA (or given ``scores``), kept in HBM (device_out_ptr 0:
     the engine's workspace; or a device pointer) or streamed to a host array
-    (device_out_ptr None).  Returns (col_lo, col_hi, host array or None)."""
+    (device_out_ptr None).  Returns (col_lo, col_hi, host array or None).
+    When the call fails (ShardError), the output may already have been
+    overwritten with scores from the failed PCA."""
     import torch
 
     if device is None:
@@ -263,7 +273,14 @@ def distance_sharded(eng, ds, genes, dist: parallel.Dist, device=None, f32=False
             # behind them: the job's one host read
             scores, status, msgs = _pca_sharded(eng, ds, genes, dist, device, ncomp)
             st_host = _stage_to_host(status)
-        out = eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, f32=f32, device_out_ptr=device_out_ptr)
+        try:
+            out = eng.distance_scores(scores.data_ptr(), ds.N, lo, hi, f32=f32, device_out_ptr=device_out_ptr)
+        except Exception:
+            if status is not None:  # a failed PCA stage is the real error
+                if getattr(status, "is_cuda", False):
+                    torch.cuda.current_stream(device).synchronize()
+                _raise_if(st_host.numpy(), msgs[0] if msgs else "another rank's PCA stage failed")
+            raise
         if status is not None:
             if getattr(status, "is_cuda", False):
                 torch.cuda.current_stream(device).synchronize()

@@ -150,7 +150,7 @@ def test_t_test_tails_and_constant():
 def test_pt_vs_scipy(df):
     from scipy import stats
     for t in [-40.0, -8.0, -3.0, -1.0, -0.1, 0.0, 0.5, 2.0, 6.0]:
-        assert O.pt(t, df) == pytest.approx(stats.t.cdf(t, df), rel=1e-10, abs=1e-300)  # CF vs cephes
+        assert O.pt(t, df) == pytest.approx(stats.t.cdf(t, df), rel=1e-10, abs=1e-300)  # power series vs cephes
 
 
 def test_de_fast_t_matches_scipy_per_row():
