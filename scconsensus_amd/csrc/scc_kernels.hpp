@@ -100,15 +100,15 @@ struct ScRankLaunch {
 
 // The segment rank engine (scc_rank_seg.hip): ranked genes cut into value
 // segments of <= SG_CAP nonzeros, each sorted and counted by one workgroup.
-#define SG_CAP 2048              // elements of a sorted segment
-#define SG_TGT 1024              // the splitter's target segment size (mean)
+#define SG_CAP 1024              // elements of a sorted segment (one wave: 16 per lane)
+#define SG_TGT 512               // the splitter's target segment size (mean)
 #define SCC_SEG_OVERFLOW 0x4000  // error word: a segment outgrew SG_CAP (the run reruns on the bucket engine)
 
 struct ScSeg {
     long long base;  // first element (keys / keys2 index)
     int n, gene;
     int kind;        // 0: a whole gene in keys (codes from the cluster offsets), 1: keys2 / codes2,
-                     // 2: one repeated value (keys2 / codes2; closed form)
+                     // 2: one repeated value (keys2 / codes2; closed form), 3: cut into sub-segments
     int hrow;        // row of hseg (the segment's cluster counts) for the cross-segment part; -1: none
 };
 
@@ -119,11 +119,21 @@ struct ScSegLaunch {
     const uint32_t* coff;
     const int* cl_cc;
     const uint8_t* flags;       // [P][G] bit0: the pair tests the gene
+    uint8_t* tbg;               // [G][P] the same, gene-major (0 / 1)
     unsigned long long* keys2;  // [nnz] segment-ordered keys of split genes
     uint8_t* codes2;            // [nnz]
     ScSeg* segs;                // [seg_cap]
     int seg_cap;
-    int* counts;                // [0] segments, [1] split genes, [2] hseg rows, [3] splitter queue
+    int* counts;                // [0] segments, [1] split genes, [2] hseg rows, [3] splitter queue, [4] oversized segments,
+                                // [5] wide segments
+    int* ovf;                   // [ovf_cap] oversized interval segments (k_seg_refine)
+    int sample_os;              // splitter sample keys per segment (32; SCC_SEG_OVERSAMPLE)
+    int dbg;                    // SCC_SEG_DEBUG timing cuts (1: no sort, 2: no blocks, 4: no ties); results invalid
+    int stamps;                 // SCC_SEG_STAMPS: per-phase clocks (g_seg_stamps)
+    int* wide;                  // [wide_cap] segments whose key range does not fit the composite key (counts[5])
+    int wide_cap;
+    int wide_mode;              // k_seg_rank: 1 = only the wide list (after the wave kernel)
+    int ovf_cap;
     int* big;                   // [G] genes for the splitter
     int4* gseg;                 // [G] per split gene: {first hseg row, segments, gene, 0}
     uint32_t* hseg;             // [hrow_cap][K]

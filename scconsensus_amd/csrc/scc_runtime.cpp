@@ -499,6 +499,7 @@ static constexpr int kRankRetry = -1000;
 static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
                        const RecIO* rio);
+extern "C" void scc_seg_stamps(hipStream_t st, int print);
 
 static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
@@ -862,13 +863,23 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         WS("segbig", (size_t)G, SL.big);
         WS("gseg", (size_t)G, SL.gseg);
         WS("hseg", (size_t)SL.hrow_cap * K, SL.hseg);
+        SL.ovf_cap = 16384;
+        SL.wide_cap = (int)std::min<int64_t>(SL.seg_cap, 1 << 26);
+        WS("segwide", (size_t)SL.wide_cap, SL.wide);
+        WS("segtbg", PG, SL.tbg);
+        SL.sample_os = std::max(1, env_int("SCC_SEG_OVERSAMPLE", 32));
+        SL.dbg = env_int("SCC_SEG_DEBUG", 0);
+        WS("segovf", (size_t)SL.ovf_cap, SL.ovf);
         SL.accS = accS;
         SL.accE = accE;
         SL.accX = accX;
         SL.accF = accF;
         SL.err = d_err;
         HIPCHK(c, hipMemsetAsync(SL.counts, 0, sizeof(int) * 8, s0));
+        SL.stamps = env_int("SCC_SEG_STAMPS", 0);
+        if (SL.stamps) scc_seg_stamps(s0, 0);
         HIPCHK(c, scc_launch_seg_rank(&SL, c->n_cu > 0 ? c->n_cu : 256, s0));
+        if (SL.stamps) scc_seg_stamps(s0, 1);
     } else if (!ttest) {
         Scope sc(c, "gene_rank", s0);
         if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));

@@ -99,3 +99,23 @@ def test_segment_engine_repeat_bitwise(monkeypatch):
         assert np.array_equal(a.u2, b.u2) and np.array_equal(a.p, b.p, equal_nan=True)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("mode", [nat.SCC_DE_FAST, nat.SCC_DE_SLOW])
+def test_oversized_segments_refined(mode, monkeypatch):
+    """One sample key per segment (SCC_SEG_OVERSAMPLE=1): many interval
+    segments outgrow SG_CAP and are re-cut by k_seg_refine (sorted in LDS, cut
+    at value changes, the cross-sub-segment part added there)."""
+    N, G, K = 16000, 24, 11
+    X = _matrix(N, G, seed=9)
+    code = (np.arange(N) * 7 % K).astype(np.int32)
+    eng = nat.Engine(0)
+    try:
+        ds = eng.dataset_csc(*_csc(X), G, N)
+        old = _run(eng, ds, code, K, mode, monkeypatch, False)
+        monkeypatch.setenv("SCC_SEG_OVERSAMPLE", "1")
+        new = _run(eng, ds, code, K, mode, monkeypatch, True)
+        assert np.array_equal(new.u2, old.u2)
+        assert np.array_equal(new.p, old.p, equal_nan=True)
+    finally:
+        eng.close()

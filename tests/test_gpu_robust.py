@@ -158,7 +158,7 @@ def _explicit_zeros(d, frac=0.05, seed=3):
     vals = d.data.copy()
     vals[rng.random(len(vals)) < frac] = 0.0
     with_z = (d.indptr.copy(), d.indices.copy(), vals)
-    m = sp.csc_matrix((vals, d.indices, d.indptr), shape=(d.G, d.N))
+    m = sp.csc_matrix((vals.copy(), d.indices.copy(), d.indptr.copy()), shape=(d.G, d.N))  # (compacted in place)
     m.eliminate_zeros()
     m.sort_indices()
     no_z = (m.indptr.astype(d.indptr.dtype), m.indices.astype(d.indices.dtype), m.data)
