@@ -1127,6 +1127,66 @@ extern "C" hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, i
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ host output
+// Device-to-host copy on the CUs into pinned (host-coherent) memory: loads
+// from HBM, nontemporal stores that leave over PCIe.  A bounded grid (256
+// workgroups, four 16-B loads in flight per lane) reaches the link rate (55 GB/s measured, scripts/d2h_overlap.hip;
+// the SDMA engine hipMemcpyAsync picks in a plain process gives 30 GB/s, and
+// the runtime's own blit kernel, picked in a torch process, 54 GB/s with a
+// 131072-thread grid).  W = the widest unit src and dst share the alignment
+// of; the head and tail bytes go one per thread in workgroup 0.
+typedef unsigned int d2h_u32x4 __attribute__((ext_vector_type(4)));
+template <class T>
+__global__ void __launch_bounds__(256) k_d2h(const char* __restrict__ src, char* __restrict__ dst, size_t head,
+                                             size_t units, size_t n)
+{
+    const T* s = reinterpret_cast<const T*>(src + head);
+    T* d = reinterpret_cast<T*>(dst + head);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < units; i += 4 * stride) {  // four loads in flight per lane
+        const T v0 = s[i], v1 = s[i + stride], v2 = s[i + 2 * stride], v3 = s[i + 3 * stride];
+        __builtin_nontemporal_store(v0, d + i);
+        __builtin_nontemporal_store(v1, d + i + stride);
+        __builtin_nontemporal_store(v2, d + i + 2 * stride);
+        __builtin_nontemporal_store(v3, d + i + 3 * stride);
+    }
+    for (; i < units; i += stride) __builtin_nontemporal_store(s[i], d + i);
+    if (blockIdx.x == 0) {
+        const size_t tail0 = head + units * sizeof(T);
+        for (size_t b = threadIdx.x; b < head; b += blockDim.x) dst[b] = src[b];
+        for (size_t b = tail0 + threadIdx.x; b < n; b += blockDim.x) dst[b] = src[b];
+    }
+}
+
+static int env_int_d2h()  // workgroups of the copy (SCC_D2H_WG, default 256)
+{
+    const char* e = getenv("SCC_D2H_WG");
+    const int v = (e && *e) ? atoi(e) : 256;
+    return v > 0 ? v : 256;
+}
+
+extern "C" hipError_t scc_launch_d2h(const void* src, void* dst, size_t n, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    const uintptr_t a = (uintptr_t)src, b = (uintptr_t)dst;
+    const size_t w = ((a ^ b) & 15) == 0 ? 16 : ((a ^ b) & 7) == 0 ? 8 : ((a ^ b) & 3) == 0 ? 4 : 1;
+    const size_t head = std::min(n, (size_t)((w - (a & (w - 1))) & (w - 1)));
+    const size_t units = (n - head) / w;
+    const int grid = (int)std::max<size_t>(1, std::min<size_t>((size_t)env_int_d2h(), (units + 255) / 256));
+    const char* s = (const char*)src;
+    char* d = (char*)dst;
+    if (w == 16)
+        hipLaunchKernelGGL(k_d2h<d2h_u32x4>, dim3(grid), dim3(256), 0, st, s, d, head, units, n);
+    else if (w == 8)
+        hipLaunchKernelGGL(k_d2h<unsigned long long>, dim3(grid), dim3(256), 0, st, s, d, head, units, n);
+    else if (w == 4)
+        hipLaunchKernelGGL(k_d2h<unsigned int>, dim3(grid), dim3(256), 0, st, s, d, head, units, n);
+    else
+        hipLaunchKernelGGL(k_d2h<unsigned char>, dim3(grid), dim3(256), 0, st, s, d, head, units, n);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t scc_launch_zscore(const double* Xc, int N, int nu, int ld, float* Z, int ldz, hipStream_t st)
 {
     hipLaunchKernelGGL(k_zscore, dim3((N + 3) / 4), dim3(256), 0, st, Xc, N, nu, ld, ldz, Z);

@@ -38,28 +38,12 @@ hipError_t scc_launch_dist_euclid(const double* P, int N, int c_lo, int c_hi, vo
 hipError_t scc_launch_zscore(const double* Xc, int N, int nu, int ld, float* Z, int ldz, hipStream_t st);
 hipError_t scc_launch_pearson(const double* Xc, int N, int nu, int ld, float* Z, int ldz, int c_lo, int c_hi,
                               void* out, int f32, hipStream_t st);
+hipError_t scc_launch_d2h(const void* src, void* dst, size_t n, hipStream_t st);
 }
 
 extern "C" void scc_distance_release(scc_ctx*) {}
 
 namespace {
-
-// Column tiles of the packed slice [col_lo, col_hi) with about `target`
-// entries each (column j holds N - 1 - j entries).
-std::vector<int64_t> column_tiles(int64_t N, int64_t col_lo, int64_t col_hi, int64_t target)
-{
-    std::vector<int64_t> t{col_lo};
-    int64_t acc = 0;
-    for (int64_t j = col_lo; j < col_hi; ++j) {
-        acc += N - 1 - j;
-        if (acc >= target && j + 1 < col_hi) {
-            t.push_back(j + 1);
-            acc = 0;
-        }
-    }
-    t.push_back(col_hi);
-    return t;
-}
 
 // host copy of one staged chunk, split over a few threads (a single core
 // copies pageable memory at ~10 GB/s, well below the PCIe rate)
@@ -83,92 +67,88 @@ void parallel_copy(char* dst, const char* src, size_t n)
 }  // namespace
 
 // Stream the packed distance slice to the caller's host buffer (north_star:
-// "the distance tiles stream back through pinned hipMemcpyAsync"): the
-// output kernel runs per column tile on s0; s1 copies each finished tile over
-// PCIe while s0 computes the next.  A pinned caller buffer (hipHostMalloc /
-// hipHostRegister / torch pin_memory) receives the DMA directly; a pageable
-// one goes through a 2-slot pinned staging ring whose host-side copy of slot
-// s overlaps the DMA into the other slot.  `emit(a, b, dst)` launches the
-// output kernel for columns [a, b) writing at dst.
+// "the distance tiles stream back through pinned" memory).  The output kernel
+// runs once over the slice on s0 (≈1% of the PCIe time: 0.55 ms against 50 ms
+// at config B), then the bytes leave in chunks, copied on the CUs by
+// k_d2h (scc_dist.hip) in stream order behind it.  A pinned caller buffer
+// (hipHostMalloc / hipHostRegister / torch pin_memory) is written directly; a
+// pageable one goes through a 2-slot pinned staging ring whose host-side copy
+// of slot s overlaps the device copy into the other slot.
+// Why not column tiles overlapped with hipMemcpyAsync on a second stream (the
+// round-1..4 design): in a torch process the runtime ran each copy as its own
+// 131072-thread blit kernel, and a tile kernel sharing the CUs with it ran 24x
+// slower (1.18 ms against 49 us per 128 MB tile, profiles/r05_streamed_tiles.md);
+// in a plain process it picked the SDMA engine at 30 GB/s.  k_d2h gives the
+// link rate (55 GB/s) in either process.  SCC_D2H_KERNEL=0: hipMemcpyAsync
+// (the runtime's choice of engine), same stream order.
 template <class Emit>
 static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi, size_t es, char* d_out,
                           char* host, Emit emit)
 {
-    hipStream_t s0 = c->s0, s1 = c->s1;
+    hipStream_t s0 = c->s0;
     auto colbase = [&](int64_t j) { return (size_t)j * (2 * (size_t)N - j - 1) / 2; };
-    const size_t base0 = colbase(col_lo);
-    const size_t total = (colbase(col_hi) - base0) * es;
-    const int64_t tile_entries = std::max<int64_t>(1, (int64_t)env_int("SCC_DIST_TILE_MB", 128) * (1 << 20) / (int64_t)es);
-    const std::vector<int64_t> tiles = column_tiles(N, col_lo, col_hi, tile_entries);
-    const int nt = (int)tiles.size() - 1;
-    std::vector<hipEvent_t> ev(nt);
-    std::vector<size_t> tile_end(nt);
-    for (int t = 0; t < nt; ++t) {
-        ev[t] = ev_take(c);
-        const size_t off = (colbase(tiles[t]) - base0) * es;
-        tile_end[t] = (colbase(tiles[t + 1]) - base0) * es;
-        HIPCHK(c, emit(tiles[t], tiles[t + 1], d_out + off));
-        HIPCHK(c, hipEventRecord(ev[t], s0));
-    }
-    auto release = [&]() {
-        for (auto e : ev) c->ev_pool.push_back(e);
+    const size_t total = (colbase(col_hi) - colbase(col_lo)) * es;
+    HIPCHK(c, emit(col_lo, col_hi, d_out));
+    const bool kern = env_int("SCC_D2H_KERNEL", 1) != 0;
+    auto copy = [&](char* dst, char* dst_dev, const char* src, size_t n) -> hipError_t {
+        if (kern && dst_dev) return scc_launch_d2h(src, dst_dev, n, s0);
+        return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s0);
+    };
+    auto dev_ptr = [](char* h) -> char* {  // the device address of pinned host memory
+        void* p = nullptr;
+        if (hipHostGetDevicePointer(&p, h, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return (char*)p;
     };
     hipPointerAttribute_t pa{};
     const bool pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost;
-    hipGetLastError();
+    (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
-    if (pinned) {  // DMA straight into the caller's buffer, tile by tile
-        size_t off = 0;
-        for (int t = 0; t < nt; ++t) {
-            HIPCHK(c, hipStreamWaitEvent(s1, ev[t], 0));
-            HIPCHK(c, hipMemcpyAsync(host + off, d_out + off, tile_end[t] - off, hipMemcpyDeviceToHost, s1));
-            off = tile_end[t];
-        }
-        const hipError_t e = hipStreamSynchronize(s1);
-        release();
-        HIPCHK(c, e);
+    if (pinned) {  // straight into the caller's buffer
+        char* hd = dev_ptr(host);
+        const size_t C = (size_t)std::max(1, env_int("SCC_DIST_CHUNK_MB", 1024)) << 20;
+        for (size_t a = 0; a < total; a += C)
+            HIPCHK(c, copy(host + a, hd ? hd + a : nullptr, d_out + a, std::min(C, total - a)));
+        HIPCHK(c, hipStreamSynchronize(s0));
     } else {
         const size_t S = (size_t)std::max(1, env_int("SCC_DIST_STAGE_MB", 64)) << 20;
         if (c->dstage_bytes < S) {
-            if (c->h_dstage) hipHostFree(c->h_dstage);
+            if (c->h_dstage) (void)hipHostFree(c->h_dstage);
             c->h_dstage = nullptr;
             c->dstage_bytes = 0;
             if (hipHostMalloc((void**)&c->h_dstage, 2 * S, hipHostMallocDefault) != hipSuccess) {
-                hipGetLastError();
+                (void)hipGetLastError();
                 c->h_dstage = nullptr;
-                release();
                 return fail(c, SCC_ERR_OOM, "pinned distance staging allocation failed");
             }
             c->dstage_bytes = S;
         }
+        char* sd = dev_ptr(c->h_dstage);
         const size_t nch = (total + S - 1) / S;
         hipEvent_t done[2] = {ev_take(c), ev_take(c)};
-        int waited = 0;  // tiles s1 already waits for
         auto enqueue = [&](size_t ch) -> hipError_t {
-            const size_t a = ch * S, b = std::min(total, a + S);
-            while (waited < nt && tile_end[waited] < b) ++waited;  // tiles that cover [a, b)
-            hipError_t e = hipStreamWaitEvent(s1, ev[std::min(waited, nt - 1)], 0);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(c->h_dstage + (ch & 1) * S, d_out + a, b - a, hipMemcpyDeviceToHost, s1);
-            if (e == hipSuccess) e = hipEventRecord(done[ch & 1], s1);
+            const size_t a = ch * S, b = std::min(total, a + S), slot = (ch & 1) * S;
+            hipError_t e = copy(c->h_dstage + slot, sd ? sd + slot : nullptr, d_out + a, b - a);
+            if (e == hipSuccess) e = hipEventRecord(done[ch & 1], s0);
             return e;
         };
         hipError_t e = nch ? enqueue(0) : hipSuccess;
         for (size_t ch = 0; ch < nch && e == hipSuccess; ++ch) {
-            if (ch + 1 < nch) e = enqueue(ch + 1);  // DMA of the next chunk overlaps this chunk's host copy
+            if (ch + 1 < nch) e = enqueue(ch + 1);  // the next chunk's device copy overlaps this chunk's host copy
             if (e == hipSuccess) e = hipEventSynchronize(done[ch & 1]);
             if (e == hipSuccess) {
                 const size_t a = ch * S, b = std::min(total, a + S);
                 parallel_copy(host + a, c->h_dstage + (ch & 1) * S, b - a);
             }
         }
-        if (e == hipSuccess) e = hipStreamSynchronize(s1);
+        if (e == hipSuccess) e = hipStreamSynchronize(s0);
         c->ev_pool.push_back(done[0]);
         c->ev_pool.push_back(done[1]);
-        release();
         HIPCHK(c, e);
     }
-    if (c->profile) {  // wall time of the streamed output (kernel tiles + PCIe + host copy)
+    if (c->profile) {  // wall time of the streamed output (output kernel + PCIe + host copy)
         auto& tm = c->timers[pinned ? "d2h_pinned" : "d2h"];
         tm.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         tm.n += 1;

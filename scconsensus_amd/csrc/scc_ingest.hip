@@ -102,11 +102,15 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
     const int a = cc_code[ch];
     const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
     const int t0r = glo / gt, t1r = min(ntile, (ghi + gt - 1) / gt);  // rng: the tiles [t0r, t1r) cover [glo, ghi)
-    const int nwin = (G + hw - 1) / hw;
+    // rng: the count rows cover only the shard's tiles [gb, ge) (zero outside
+    // [glo, ghi) inside them: the scatter reads its tiles' edge genes); the
+    // column scan runs over the same range and the rest of the row is never read
+    const int gb = rng ? t0r * gt : 0, ge = rng ? min(G, t1r * gt) : G;
+    const int nwin = (ge - gb + hw - 1) / hw;
     dd se{0.0, 0.0};
     int bad = 0;
     for (int win = 0; win < nwin; ++win) {
-        const int wlo = win * hw, whi = min(G, wlo + hw);
+        const int wlo = gb + win * hw, whi = min(ge, wlo + hw);
         const int clo = max(glo, wlo), chi = min(ghi, whi);  // genes this pass counts
         const u32 nwq = (u32)(whi - wlo + 3) >> 2;
         const u64 mq = ((1ull << 40) + nwq - 1) / nwq;  // l / nwq = (l * mq) >> 40 for l < 2^18
@@ -215,21 +219,22 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
 // (unkept cells) hold the total.  Three passes over [segment of CS_SEG
 // chunks] x [256 genes] blocks so the whole chip works on it.
 #define CS_SEG 32
-__global__ void __launch_bounds__(256) k_ing_colsum(const u32* __restrict__ cnt, int nc_kept, int G,
+__global__ void __launch_bounds__(256) k_ing_colsum(const u32* __restrict__ cnt, int nc_kept, int G, int gb, int ge,
                                                     u32* __restrict__ part)
 {
-    const int g = blockIdx.y * 256 + threadIdx.x;
-    if (g >= G) return;
+    const int g = gb + blockIdx.y * 256 + threadIdx.x;
+    if (g >= ge) return;
     const int w0 = blockIdx.x * CS_SEG, w1 = min(nc_kept, w0 + CS_SEG);
     u32 s = 0;
     for (int w = w0; w < w1; ++w) s += cnt[(size_t)w * G + g];
     part[(size_t)blockIdx.x * G + g] = s;
 }
 
-__global__ void __launch_bounds__(256) k_ing_segscan(u32* __restrict__ part, int nseg, int G, u32* __restrict__ total)
+__global__ void __launch_bounds__(256) k_ing_segscan(u32* __restrict__ part, int nseg, int G, int gb, int ge,
+                                                     u32* __restrict__ total)
 {
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= G) return;
+    const int g = gb + blockIdx.x * 256 + threadIdx.x;
+    if (g >= ge) return;
     u32 run = 0;
     for (int q = 0; q < nseg; ++q) {
         const u32 v = part[(size_t)q * G + g];
@@ -239,11 +244,12 @@ __global__ void __launch_bounds__(256) k_ing_segscan(u32* __restrict__ part, int
     total[g] = run;
 }
 
-__global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int nc, int nc_kept, int G,
-                                                      const u32* __restrict__ part, const u32* __restrict__ total)
+__global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int nc, int nc_kept, int G, int gb,
+                                                      int ge, const u32* __restrict__ part,
+                                                      const u32* __restrict__ total)
 {
-    const int g = blockIdx.y * 256 + threadIdx.x;
-    if (g >= G) return;
+    const int g = gb + blockIdx.y * 256 + threadIdx.x;
+    if (g >= ge) return;
     const int w0 = blockIdx.x * CS_SEG;
     // Unkept chunks add nothing.  Of their rows only nc_kept (the end offset of
     // the last kept cluster, cl_cc[K]) and the totals row nc are ever read, so
@@ -540,26 +546,32 @@ __global__ void k_reduce_dd(const dd* __restrict__ parts, int n, dd* __restrict_
 // before, each ~5 us on the stream at config B.
 __global__ void __launch_bounds__(256) k_de_clear(int* __restrict__ err, int* __restrict__ counts,
                                                   unsigned long long* __restrict__ acc, long long acc_n,
-                                                  unsigned long long* __restrict__ first, int G)
+                                                  unsigned long long* __restrict__ first, int G, int glo, int ghi)
 {
     const long long t = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
     if (t < 4) err[t] = 0;
     if (t < 16) counts[t] = 0;
-    if (acc) {
+    if (acc && glo == 0 && ghi == G) {
         typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
         for (long long e = t; e < acc_n / 2; e += stride) ((u2v*)acc)[e] = u2v{0ull, 0ull};
         if ((acc_n & 1) && t == 0) acc[acc_n - 1] = 0ull;
+    } else if (acc && ghi > glo) {
+        // a gene shard: the accumulator rows' [glo, ghi) columns (the rank
+        // stage and the test touch no other gene)
+        const long long w = ghi - glo, n = (acc_n / G) * w;
+        for (long long e = t; e < n; e += stride) acc[(e / w) * G + glo + e % w] = 0ull;
     }
     if (first)
         for (long long e = t; e < G; e += stride) first[e] = ~0ull;
 }
 
 extern "C" hipError_t scc_launch_de_clear(int* err, int* counts, unsigned long long* acc, long long acc_n,
-                                          unsigned long long* first, int G, hipStream_t st)
+                                          unsigned long long* first, int G, int glo, int ghi, hipStream_t st)
 {
-    const long long work = std::max(acc ? acc_n / 2 : 0ll, (long long)G);
+    const long long accw = !acc ? 0ll : (glo == 0 && ghi == G) ? acc_n / 2 : (acc_n / G) * std::max(0, ghi - glo);
+    const long long work = std::max(accw, (long long)G);
     const int grid = (int)std::max(1ll, std::min(4096ll, (work + 255) / 256));
-    hipLaunchKernelGGL(k_de_clear, dim3(grid), dim3(256), 0, st, err, counts, acc, acc_n, first, G);
+    hipLaunchKernelGGL(k_de_clear, dim3(grid), dim3(256), 0, st, err, counts, acc, acc_n, first, G, glo, ghi);
     return hipGetLastError();
 }
 
@@ -598,17 +610,32 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
 
 extern "C" int scc_ingest_colscan_scratch(int nc, int G) { return ((nc + 1 + CS_SEG - 1) / CS_SEG + 1) * G; }
 
-extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, int G, u32* scratch, hipStream_t st)
+// genes [g0, g1) of the count rows (a gene shard's tiles in range mode,
+// scc_ingest_count_range; all genes otherwise)
+extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, int G, int g0, int g1, u32* scratch,
+                                                hipStream_t st)
 {
+    if (g1 <= g0) return hipSuccess;
     const int nseg_k = (nc_kept + CS_SEG - 1) / CS_SEG;
     const int nseg_all = (nc + 1 + CS_SEG - 1) / CS_SEG;
     u32* part = scratch;
     u32* total = scratch + (size_t)nseg_all * G;
-    const int gb = (G + 255) / 256;
-    if (nseg_k > 0) hipLaunchKernelGGL(k_ing_colsum, dim3(nseg_k, gb), dim3(256), 0, st, cnt, nc_kept, G, part);
-    hipLaunchKernelGGL(k_ing_segscan, dim3(gb), dim3(256), 0, st, part, nseg_k, G, total);
-    hipLaunchKernelGGL(k_ing_colapply, dim3(nseg_all, gb), dim3(256), 0, st, cnt, nc, nc_kept, G, part, total);
+    const int gbk = (g1 - g0 + 255) / 256;
+    if (nseg_k > 0)
+        hipLaunchKernelGGL(k_ing_colsum, dim3(nseg_k, gbk), dim3(256), 0, st, cnt, nc_kept, G, g0, g1, part);
+    hipLaunchKernelGGL(k_ing_segscan, dim3(gbk), dim3(256), 0, st, part, nseg_k, G, g0, g1, total);
+    hipLaunchKernelGGL(k_ing_colapply, dim3(nseg_all, gbk), dim3(256), 0, st, cnt, nc, nc_kept, G, g0, g1, part,
+                       total);
     return hipGetLastError();
+}
+
+// the genes whose count rows a range-mode (rng) counting pass writes: the
+// gene tiles covering [glo, ghi)
+extern "C" void scc_ingest_count_range(int G, int glo, int ghi, int* g0, int* g1)
+{
+    const int ntile = (G + SC_GT - 1) / SC_GT;
+    *g0 = (glo / SC_GT) * SC_GT;
+    *g1 = std::min(G, std::min(ntile, (ghi + SC_GT - 1) / SC_GT) * SC_GT);
 }
 
 extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* rows, const double* vals,

@@ -32,6 +32,7 @@ struct ScStatsLaunch {
     int test;           // SCC_TEST_WILCOX | SCC_TEST_T (FAST)
     uint32_t* cnt_pos;  // [K][G]
     uint32_t* cnt_neg;  // [K][G]
+    int glo, gn;        // the genes [glo, glo + gn) (a gene shard; nothing else is read downstream)
 };
 
 // one unit of rank work: a whole gene (src 0: the ingest's cluster-grouped
@@ -207,14 +208,16 @@ struct ScSelectLaunch {
 extern "C" {
 int scc_ingest_gene_tile(void);
 hipError_t scc_launch_de_clear(int* err, int* counts, unsigned long long* acc, long long acc_n,
-                               unsigned long long* first, int G, hipStream_t st);
+                               unsigned long long* first, int G, int glo, int ghi, hipStream_t st);
 int scc_ingest_hist_window(int G);
 hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
                                   int G, const int* perm, const int* cc_p0, const int* cc_code, int nc, int ntile,
                                   uint32_t* cnt, long long* bnd, int* nodg, dd* wave_expm1, int want_expm1, int glo,
                                   int ghi, int rng, int* err, hipStream_t st);
 int scc_ingest_colscan_scratch(int nc, int G);
-hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nc, int nc_kept, int G, uint32_t* scratch, hipStream_t st);
+hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nc, int nc_kept, int G, int g0, int g1, uint32_t* scratch,
+                                     hipStream_t st);
+void scc_ingest_count_range(int G, int glo, int ghi, int* g0, int* g1);
 hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, const double* vals,
                                      const double* dense, int G, const int* perm, const int* cc_p0, const int* sc_cc0,
                                      int ns, const uint32_t* cnt, const long long* gstart, const long long* bnd,

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 {
     __shared__ int off[SCC_MAX_K + 1];
     __shared__ StatItem item[SCC_MAX_K + ST_W + 4];
-    const int g = blockIdx.x, K = A.K, tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
+    const int g = A.glo + blockIdx.x, K = A.K, tid = threadIdx.x, lane = tid & 63, w = scc_wave_id();
     const i64 base = A.gstart[g];
     const int n = (int)(A.gstart[g + 1] - base);
     const u64* key = A.keys + base;
@@ -170,14 +170,15 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
 
 extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st)
 {
-    if (L->G <= 0) return hipSuccess;
+    if (L->G <= 0 || L->gn <= 0 || L->glo < 0 || L->glo + L->gn > L->G) return hipSuccess;
+    const dim3 grid(L->gn);
     if (L->mode == SCC_DE_FAST && L->test == SCC_TEST_T) {
-        hipLaunchKernelGGL((k_gene_stats<true, true, false>), dim3(L->G), dim3(ST_T), 0, st, *L);
-        hipLaunchKernelGGL((k_gene_stats<false, false, true>), dim3(L->G), dim3(ST_T), 0, st, *L);
+        hipLaunchKernelGGL((k_gene_stats<true, true, false>), grid, dim3(ST_T), 0, st, *L);
+        hipLaunchKernelGGL((k_gene_stats<false, false, true>), grid, dim3(ST_T), 0, st, *L);
     } else if (L->mode == SCC_DE_FAST) {
-        hipLaunchKernelGGL((k_gene_stats<true, false, false>), dim3(L->G), dim3(ST_T), 0, st, *L);
+        hipLaunchKernelGGL((k_gene_stats<true, false, false>), grid, dim3(ST_T), 0, st, *L);
     } else {
-        hipLaunchKernelGGL((k_gene_stats<false, true, false>), dim3(L->G), dim3(ST_T), 0, st, *L);
+        hipLaunchKernelGGL((k_gene_stats<false, true, false>), grid, dim3(ST_T), 0, st, *L);
     }
     return hipGetLastError();
 }

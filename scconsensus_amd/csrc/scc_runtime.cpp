@@ -751,7 +751,8 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     {
         Scope sc(c, "ingest", s0);
         // error words, counters, rank accumulators and first-occurrence keys in one launch
-        HIPCHK(c, scc_launch_de_clear(d_err, d_counts, ttest ? nullptr : d_acc, (long long)acc_n, d_first, (int)G, s0));
+        HIPCHK(c, scc_launch_de_clear(d_err, d_counts, ttest ? nullptr : d_acc, (long long)acc_n, d_first, (int)G, glo,
+                                      ghi, s0));
         de_cleared = true;
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
@@ -760,7 +761,14 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             HIPCHK(c, hipMemcpyAsync(d_nodg, ds->d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
         uint32_t* d_cscr;
         WS("colscan", scc_ingest_colscan_scratch(nc, G), d_cscr);
-        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, d_cscr, s0));
+        // range mode: count rows and their column scan over the shard's gene
+        // tiles only; the totals row is zero elsewhere (gstart: empty genes)
+        int cg0 = 0, cg1 = G;
+        if (hist_rng) {
+            scc_ingest_count_range(G, glo, ghi, &cg0, &cg1);
+            HIPCHK(c, hipMemsetAsync(d_cnt + (size_t)nc * G, 0, sizeof(uint32_t) * G, s0));
+        }
+        HIPCHK(c, scc_launch_ingest_colscan(d_cnt, nc, nc_kept, G, cg0, cg1, d_cscr, s0));
         const uint32_t* d_total = d_cnt + (size_t)nc * G;
         HIPCHK(c, scc_launch_scan(d_total, G, d_gstart, d_scan, d_gstart + G, s0));
         HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
@@ -784,6 +792,8 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         S.mode = prm->mode;
         S.test = ttest ? SCC_TEST_T : SCC_TEST_WILCOX;
         S.var_x = d_vx;
+        S.glo = glo;
+        S.gn = ghi - glo;
         HIPCHK(c, scc_launch_gene_stats(&S, s0));
     }
     // SLOW: log(meanScalingFactor * mean(expm1(X))) (slow:36) gates the pair

@@ -1,6 +1,7 @@
 """Per-rank ingest of a gene shard (1/W of the genes) on a validated dataset:
-range read (k_ing_hist rng) vs every entry (SCC_INGEST_FULL=1), and the whole
-per-rank DE stage times.  python scripts/shard_ingest_time.py D 8"""
+range read (k_ing_hist rng) vs every entry (SCC_INGEST_FULL=1), the whole
+per-rank DE stage times, and the distance side of each rank (cell-shard PCA
+column sums, Gram, projection; its column slice of dist; one eigensolve).  python scripts/shard_ingest_time.py D 8"""
 import os
 import sys
 
@@ -14,6 +15,7 @@ from scconsensus_amd import api, sharded, synth  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "D"
 W = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+parts_run = sys.argv[3].split(",") if len(sys.argv) > 3 else ["full", "range", "dist"]  # (a profile of one part)
 if cfg in ("C", "D"):
     d = synth.generate_device(cfg, "cuda:0", layout="csc")
     torch.cuda.synchronize()
@@ -31,7 +33,7 @@ else:
     w = np.bincount(d.indices, minlength=d.G)
 eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")  # validates the dataset
 fams = ["ingest", "gene_stats", "gene_rank", "pair_test"]
-for full in ("1", "0"):
+for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
     os.environ["SCC_INGEST_FULL"] = full
     out = {}
     for r in range(W):
@@ -50,3 +52,63 @@ for full in ("1", "0"):
         del buf
     print(f"config {cfg}, {W} gene shards, {'full read' if full == '1' else 'range read'}: "
           + ", ".join(f"{f} max {max(v):.3f} mean {np.mean(v):.3f} ms" for f, v in out.items()), flush=True)
+
+# ---- the distance side of one rank (cell shard of the PCA, its column slice
+# of dist), wall-clock around each call on the synchronised stream
+import time  # noqa: E402
+
+if "dist" not in parts_run:
+    sys.exit(0)
+
+os.environ.pop("SCC_INGEST_FULL", None)
+union = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union").union
+nu = len(union)
+f64 = dict(dtype=torch.float64, device="cuda:0")
+eng.distance(ds, union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=0)  # the one-GPU eigensolve, for its path
+eng.synchronize()
+print(f"one-GPU distance: eigen path {int(eng.lib.scc_diag_eig_last_path())}", flush=True)
+
+
+def timed(fn, reps=3):
+    fn()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    eng.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+parts = torch.zeros((W, 2 * nu), **f64)
+res = {"colsum": [], "gram": [], "project": [], "dist": []}
+for r in range(W):
+    lo, hi = sharded.cell_shard(d.N, r, W)
+    res["colsum"].append(timed(lambda: eng.pca_shard_colsum(ds, union, lo, hi, parts[r].data_ptr())))
+gram = torch.zeros(nu * nu, **f64)
+gsum = torch.zeros(nu * nu, **f64)  # the all-reduced Gram (what rank 0's eigensolve sees)
+for r in range(W):
+    lo, hi = sharded.cell_shard(d.N, r, W)
+    # the Gram call centres the gathered block in place: each timed call gets a fresh gather
+    t_both = timed(lambda: (eng.pca_shard_colsum(ds, union, lo, hi, parts[r].data_ptr()),
+                            eng.pca_shard_gram(parts.data_ptr(), W, gram.data_ptr())))
+    res["gram"].append(t_both - res["colsum"][r])
+    eng.pca_shard_colsum(ds, union, lo, hi, parts[r].data_ptr())
+    eng.pca_shard_gram(parts.data_ptr(), W, gram.data_ptr())
+    gsum += gram
+vecs = torch.zeros(nu * 16, **f64)
+t_eig = timed(lambda: eng.pca_shard_eigen(gsum.data_ptr(), vecs.data_ptr()))
+path = int(eng.lib.scc_diag_eig_last_path())
+eng.reset_timers()
+eng.pca_shard_eigen(gsum.data_ptr(), vecs.data_ptr())
+t_eig_dev = eng.kernel_time("eigen")[0]
+scores = torch.zeros(d.N * 16, **f64)
+for r in range(W):
+    lo, hi = sharded.cell_shard(d.N, r, W)
+    eng.pca_shard_colsum(ds, union, lo, hi, parts[r].data_ptr())  # the context keeps this rank's cells
+    eng.pca_shard_gram(parts.data_ptr(), W, gram.data_ptr())
+    res["project"].append(timed(lambda: eng.pca_shard_project(vecs.data_ptr(), scores.data_ptr())))
+for r in range(W):
+    clo, chi = sharded.column_shard(d.N, r, W)
+    res["dist"].append(timed(lambda: eng.distance_scores(scores.data_ptr(), d.N, clo, chi, device_out_ptr=0)))
+print(f"config {cfg}, {W} ranks, distance side (|U| = {nu}): eigen {t_eig:.3f} ms wall, {t_eig_dev:.3f} ms on the stream (one rank, path {path}); "
+      + ", ".join(f"{k} max {max(v):.3f} mean {np.mean(v):.3f} ms" for k, v in res.items()), flush=True)

@@ -223,8 +223,10 @@ def test_sharded_pca_matches_unsharded(cfg_a, world):
 
 @pytest.mark.parametrize("metric", [nat.SCC_DIST_PCA_EUCLID, nat.SCC_DIST_PEARSON])
 @pytest.mark.parametrize("f32", [False, True])
-def test_streamed_output_matches_device(eng, cfg_a, metric, f32, monkeypatch):
-    monkeypatch.setenv("SCC_DIST_TILE_MB", "1")   # ~20 column tiles at config A
+@pytest.mark.parametrize("kernel_copy", ["1", "0"])
+def test_streamed_output_matches_device(eng, cfg_a, metric, f32, kernel_copy, monkeypatch):
+    monkeypatch.setenv("SCC_D2H_KERNEL", kernel_copy)  # k_d2h on the CUs, or hipMemcpyAsync
+    monkeypatch.setenv("SCC_DIST_CHUNK_MB", "1")  # ~20 chunks into a pinned buffer at config A
     monkeypatch.setenv("SCC_DIST_STAGE_MB", "1")  # ~10-20 staging chunks through the 2-slot ring
     d, names, code = cfg_a
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
@@ -241,6 +243,11 @@ def test_streamed_output_matches_device(eng, cfg_a, metric, f32, monkeypatch):
     pinned = torch.empty(n, dtype=dt, pin_memory=True)
     eng.distance(ds, union, metric, f32=f32, out=pinned.numpy())
     np.testing.assert_array_equal(pinned.numpy(), ref)
+    # a pinned destination one element off its 16-B alignment (the copy's head/tail path)
+    off = torch.zeros(n + 2, dtype=dt, pin_memory=True)
+    eng.distance(ds, union, metric, f32=f32, out=off.numpy()[1:n + 1])
+    np.testing.assert_array_equal(off.numpy()[1:n + 1], ref)
+    assert off[0].item() == 0 and off[n + 1].item() == 0
     # a column slice, streamed
     lo, hi = 100, 1700
     s0, s1 = lo * (2 * N - lo - 1) // 2, hi * (2 * N - hi - 1) // 2
