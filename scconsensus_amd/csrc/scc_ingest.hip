@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
                                                     int* __restrict__ nodg, dd* __restrict__ wave_expm1,
                                                     int want_expm1, int glo, int ghi, int rng_in, int hw,
-                                                    int* __restrict__ err)
+                                                    const i64* __restrict__ tbnd, int* __restrict__ err)
 {
     // rng_in 1: a gene-shard range of a validated dataset (below); 2: the whole
     // range of a validated dataset with no explicit zeros (FAST): the counts
@@ -134,9 +134,18 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                     ke = wave_lower_bound(rows, kb, e, chi);
                 }
             } else if (!DENSE && rng) {
-                kb = wave_lower_bound(rows, b, e, t0r * gt);
-                ke = wave_lower_bound(rows, kb, e, t1r * gt);
+                if (tbnd) {  // the dataset's tile starts: two loads, and the run's tile boundaries copied
+                    const i64* tb = tbnd + (size_t)c * (ntile + 1);
+                    kb = tb[t0r];
+                    ke = tb[t1r];
+                    if (a >= 0)
+                        for (int t = t0r + lane; t <= t1r; t += 64) bp[t] = tb[t];
+                } else {
+                    kb = wave_lower_bound(rows, b, e, t0r * gt);
+                    ke = wave_lower_bound(rows, kb, e, t1r * gt);
+                }
             }
+            const bool tiles_known = rng && tbnd != nullptr;
             for (i64 k0 = kb; k0 < ke; k0 += 4 * 64) {  // four loads in flight per lane
                 double xs[4];
                 int gs[4], gps[4];
@@ -153,7 +162,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                         gps[u] = -1;
                     } else {
                         const int r = rows[kc];
-                        const int rp = rows[kc > b ? kc - 1 : b];
+                        const int rp = tiles_known ? -1 : rows[kc > b ? kc - 1 : b];
                         gs[u] = k < ke ? r : -1;
                         gps[u] = (k < ke && k > b) ? rp : -1;
                     }
@@ -176,7 +185,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                         pos += (x > 0.0);
                         if (want_expm1) se = dd_add_d(se, expm1(x));
                     }
-                    if (!DENSE && a >= 0) {
+                    if (!DENSE && a >= 0 && !tiles_known) {
                         // tile boundaries: tiles t in (tile(prev), tile(g)] start at k
                         const int gp = gps[u];
                         if (k > b && gp >= g) bad |= 4;
@@ -187,7 +196,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indpt
                 }
             }
             if (win > 0) continue;
-            if (!DENSE && a >= 0) {
+            if (!DENSE && a >= 0 && !tiles_known) {
                 // tiles after the last entry read (and every tile of an empty cell) end
                 // at ke (= e, or in rng mode the first entry past tile t1r - 1)
                 const int gl = (ke > b) ? rows[ke - 1] : -1;
@@ -588,22 +597,55 @@ extern "C" int scc_ingest_hist_window(int G)
     return std::max(1, std::min(G, cap));
 }
 
+// Every cell's gene-tile starts (tb[c][t] = first entry of cell c with row >=
+// t * gt, tb[c][ntile] = the cell's end): a wave per cell over its row
+// indices, the same rule k_ing_hist applies while it counts.
+__global__ void __launch_bounds__(256) k_ing_tile_bounds(const i64* __restrict__ indptr, const int* __restrict__ rows,
+                                                         int N, int gt, int ntile, i64* __restrict__ tbnd)
+{
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + scc_wave_id();
+    if (c >= N) return;
+    const i64 b = indptr[c], e = indptr[c + 1];
+    i64* tb = tbnd + (size_t)c * (ntile + 1);
+    for (i64 k = b + lane; k < e; k += 64) {
+        const int g = rows[k];
+        const int gp = k > b ? rows[k - 1] : -1;
+        const int tp = gp < 0 ? -1 : min(gp / gt, ntile - 1);
+        const int tg = min(max(g, 0) / gt, ntile - 1);
+        for (int t = tp + 1; t <= tg; ++t) tb[t] = k;
+    }
+    const int gl = e > b ? rows[e - 1] : -1;
+    const int tl = gl < 0 ? -1 : min(max(gl, 0) / gt, ntile - 1);
+    for (int t = tl + 1 + lane; t <= ntile; t += 64) tb[t] = e;
+}
+
+extern "C" hipError_t scc_launch_tile_bounds(const i64* indptr, const int* rows, int N, int gt, int ntile, i64* tbnd,
+                                             hipStream_t st)
+{
+    if (N <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ing_tile_bounds, dim3((N + 3) / 4), dim3(256), 0, st, indptr, rows, N, gt, ntile, tbnd);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows, const double* vals,
                                              const double* dense, int G, const int* perm, const int* cc_p0,
                                              const int* cc_code, int nc, int ntile, u32* cnt, i64* bnd, int* nodg,
-                                             dd* wave_expm1, int want_expm1, int glo, int ghi, int rng, int* err,
-                                             hipStream_t st)
+                                             dd* wave_expm1, int want_expm1, int glo, int ghi, int rng,
+                                             const i64* tbnd, int* err, hipStream_t st)
 {
     const int hw = scc_ingest_hist_window(G);
     const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
     if (dense) {
         hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw, nullptr,
+                           err);
     } else {
         hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, err);
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, tbnd,
+                           err);
     }
     return hipGetLastError();
 }

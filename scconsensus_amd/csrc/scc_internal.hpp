@@ -124,6 +124,10 @@ struct scc_dataset {
     mutable bool validated = false;
     mutable bool no_zeros = false;  // the validating read saw no explicit (stored) zero
     mutable int* d_nodg = nullptr;  // [N], always owned
+    // [N][ntile + 1] entry offsets where each cell's gene tiles start
+    // (clustering-independent), built by the first range-mode run: later
+    // gene-shard runs read a cell's shard entries without binary searches
+    mutable long long* d_tbnd = nullptr;
     // device list: the replica on each peer engine of the context (same order
     // as scc_ctx::peers), and the stored values per gene that balance the
     // gene row-blocks (computed on the first sharded run)

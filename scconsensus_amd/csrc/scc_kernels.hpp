@@ -54,6 +54,7 @@ struct ScRankLaunch {
     int wave_target;       // split: bins are packed into buckets of < 2 * wave_target elements
     int rw_slots;          // wave kernel: tested pairs per gene held in registers, 64 * rw_slots (2, 4, 8 or 16)
     int dbg;               // SCC_RW_DEBUG timing experiments (1: no pair counts, 2: no sort); results invalid
+    int rw_ch;             // k_rank_waves: consecutive buckets per wave visit (SCC_RW_CH, <= 64)
     int bucket_cap;        // capacity of sbuckets / hbg rows
     ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)
     unsigned int* hbg;     // [bucket_cap][K] per-bucket cluster counts
@@ -213,7 +214,9 @@ int scc_ingest_hist_window(int G);
 hipError_t scc_launch_ingest_hist(const long long* indptr, const int* rows, const double* vals, const double* dense,
                                   int G, const int* perm, const int* cc_p0, const int* cc_code, int nc, int ntile,
                                   uint32_t* cnt, long long* bnd, int* nodg, dd* wave_expm1, int want_expm1, int glo,
-                                  int ghi, int rng, int* err, hipStream_t st);
+                                  int ghi, int rng, const long long* tbnd, int* err, hipStream_t st);
+hipError_t scc_launch_tile_bounds(const long long* indptr, const int* rows, int N, int gt, int ntile, long long* tbnd,
+                                  hipStream_t st);
 int scc_ingest_colscan_scratch(int nc, int G);
 hipError_t scc_launch_ingest_colscan(uint32_t* cnt, int nc, int nc_kept, int G, int g0, int g1, uint32_t* scratch,
                                      hipStream_t st);

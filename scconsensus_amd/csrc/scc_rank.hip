@@ -38,6 +38,10 @@
 //        T  = F_a + F_b + f(z_a) + f(z_b) + 3 z_a z_b (z_a + z_b) + 3 X.
 #include "scc_common.hpp"
 #include "scc_kernels.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
 #include <type_traits>
 
 __device__ inline u64 f_tie(u64 c) { return c * c * c - c; }
@@ -1132,6 +1136,11 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     __syncthreads();
 }
 
+// SCC_RW_DEBUG=9: per split gene (stored values, cycles) of the first
+// SPLIT_DIAG_MAX genes, printed as a distribution (scc_rank_split_diag)
+#define SPLIT_DIAG_MAX 65536
+__device__ unsigned long long g_split_diag[SPLIT_DIAG_MAX][2];
+
 __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1142,8 +1151,36 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
         __syncthreads();
         const int i = L.next;
         if (i >= cnt) break;
+        const u64 t0 = A.dbg == 9 ? __builtin_amdgcn_s_memtime() : 0;
         split_one_gene(A, A.split_genes[i], L);
+        if (A.dbg == 9 && threadIdx.x == 0 && i < SPLIT_DIAG_MAX) {
+            const int g = A.split_genes[i];
+            g_split_diag[i][0] = (unsigned long long)(A.gstart[g + 1] - A.gstart[g]);
+            g_split_diag[i][1] = __builtin_amdgcn_s_memtime() - t0;
+        }
     }
+}
+
+extern "C" void scc_rank_split_diag(hipStream_t st, int ngenes)
+{
+    static unsigned long long h[SPLIT_DIAG_MAX][2];
+    const int n = ngenes < SPLIT_DIAG_MAX ? ngenes : SPLIT_DIAG_MAX;
+    if (n <= 0 || hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpyFromSymbol(h, HIP_SYMBOL(g_split_diag), sizeof(unsigned long long) * 2 * n, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    std::vector<int> ix(n);
+    for (int i = 0; i < n; ++i) ix[i] = i;
+    std::sort(ix.begin(), ix.end(), [&](int a, int b) { return h[a][1] > h[b][1]; });
+    unsigned long long tot = 0, totn = 0;
+    for (int i = 0; i < n; ++i) {
+        tot += h[i][1];
+        totn += h[i][0];
+    }
+    fprintf(stderr, "[scc split diag] genes %d values %llu cycles %llu (mean %.0f per gene, %.1f per value); slowest:", n,
+            totn, tot, (double)tot / n, (double)tot / std::max(1ull, totn));
+    for (int q = 0; q < std::min(n, 12); ++q) fprintf(stderr, " %llu/%llu", h[ix[q]][0], h[ix[q]][1]);
+    fprintf(stderr, "\n");
 }
 
 // ===================================================================== re-split
@@ -1903,7 +1940,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
     const int cnt = min(A.counts[4], A.bucket_cap);
     const int K = A.K, G = A.G, P = A.P;
-    constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality)
+    const int CH = A.rw_ch > 0 && A.rw_ch <= 64 ? A.rw_ch : 16;  // consecutive buckets per wave visit (gene locality)
     int cur = -1, ntp = 0;
     u64 gk = ~0ull;
     u32 pa[RW_SLOTS], pb[RW_SLOTS], pp[RW_SLOTS];

@@ -439,7 +439,7 @@ extern "C" void scc_dataset_destroy(scc_dataset* d)
     if (!d) return;
     for (scc_dataset* r : d->reps) scc_dataset_destroy(r);
     d->reps.clear();
-    if (d->owned || d->d_nodg) {
+    if (d->owned || d->d_nodg || d->d_tbnd) {
         hipSetDevice(d->device);
         hipDeviceSynchronize();
     }
@@ -450,6 +450,7 @@ extern "C" void scc_dataset_destroy(scc_dataset* d)
         hipFree(d->d_dense);
     }
     hipFree(d->d_nodg);
+    hipFree(d->d_tbnd);
     delete d;
 }
 
@@ -500,6 +501,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
                        const RecIO* rio);
 extern "C" void scc_seg_stamps(hipStream_t st, int print);
+extern "C" void scc_rank_split_diag(hipStream_t st, int ngenes);
 
 static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
@@ -754,9 +756,18 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_de_clear(d_err, d_counts, ttest ? nullptr : d_acc, (long long)acc_n, d_first, (int)G, glo,
                                       ghi, s0));
         de_cleared = true;
+        if (hist_rng && !ds->d_tbnd) {  // once per dataset: every cell's gene-tile starts
+            if (hipMalloc((void**)&ds->d_tbnd, sizeof(long long) * (size_t)N * (ntile + 1)) != hipSuccess) {
+                (void)hipGetLastError();
+                ds->d_tbnd = nullptr;
+            } else {
+                HIPCHK(c, scc_launch_tile_bounds(ds->d_indptr, ds->d_rows, N, gt, ntile, ds->d_tbnd, s0));
+            }
+        }
         HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                          d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
-                                         hist_rng ? 1 : (hist_ro ? 2 : 0), d_err, s0));
+                                         hist_rng ? 1 : (hist_ro ? 2 : 0), hist_rng ? ds->d_tbnd : nullptr, d_err,
+                                         s0));
         if (hist_rng || hist_ro)
             HIPCHK(c, hipMemcpyAsync(d_nodg, ds->d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
         uint32_t* d_cscr;
@@ -910,6 +921,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.wave_target = wave_target;
         L.rw_slots = P <= 128 ? 2 : P <= 256 ? 4 : P <= 512 ? 8 : 16;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
+        L.rw_ch = env_int("SCC_RW_CH", 16);
         L.rw_mfma = env_int("SCC_RANK_MFMA", 1);
         L.rw_mfma16 = env_int("SCC_RANK_MFMA16", -1);
         L.cross_wave = env_int("SCC_CROSS_WAVE", 0);
@@ -963,6 +975,12 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_rank_classify(&L, s0));
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
         HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
+        if (L.dbg == 9) {  // per-gene split clocks (diagnostic)
+            int nsg = 0;
+            HIPCHK(c, hipMemcpyAsync(&nsg, d_counts + 3, sizeof(int), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            scc_rank_split_diag(s0, nsg);
+        }
         if (stamps) {  // re-split phase clocks (summed over parents): 8 u64 after the item stamps
             ScRankLaunch R = L;
             R.stamps = st_buf + (size_t)3 * item_cap * 8 - 8;

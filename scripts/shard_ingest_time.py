@@ -52,6 +52,7 @@ for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
         del buf
     print(f"config {cfg}, {W} gene shards, {'full read' if full == '1' else 'range read'}: "
           + ", ".join(f"{f} max {max(v):.3f} mean {np.mean(v):.3f} ms" for f, v in out.items()), flush=True)
+    print("per rank: " + "; ".join(f"{f} " + " ".join(f"{x:.3f}" for x in v) for f, v in out.items()), flush=True)
 
 # ---- the distance side of one rank (cell shard of the PCA, its column slice
 # of dist), wall-clock around each call on the synchronised stream
@@ -112,3 +113,4 @@ for r in range(W):
     res["dist"].append(timed(lambda: eng.distance_scores(scores.data_ptr(), d.N, clo, chi, device_out_ptr=0)))
 print(f"config {cfg}, {W} ranks, distance side (|U| = {nu}): eigen {t_eig:.3f} ms wall, {t_eig_dev:.3f} ms on the stream (one rank, path {path}); "
       + ", ".join(f"{k} max {max(v):.3f} mean {np.mean(v):.3f} ms" for k, v in res.items()), flush=True)
+print("per rank: " + "; ".join(f"{k} " + " ".join(f"{x:.3f}" for x in v) for k, v in res.items()), flush=True)
