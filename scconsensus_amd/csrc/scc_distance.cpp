@@ -72,8 +72,10 @@ void parallel_copy(char* dst, const char* src, size_t n)
 // at config B), then the bytes leave in chunks, copied on the CUs by
 // k_d2h (scc_dist.hip) in stream order behind it.  A pinned caller buffer
 // (hipHostMalloc / hipHostRegister / torch pin_memory) is written directly; a
-// pageable one goes through a 2-slot pinned staging ring whose host-side copy
-// of slot s overlaps the device copy into the other slot.
+// pageable one goes through a 2-slot pinned staging ring (2 x 32 MB: its
+// allocation is a context's first-call cost, ~25 ms at 2 x 64 MB; 2 x 16 MB
+// chunks are slower, profiles/r05_streamed_tiles.md) whose host-side copy of
+// slot s overlaps the device copy into the other slot.
 // Why not column tiles overlapped with hipMemcpyAsync on a second stream (the
 // round-1..4 design): in a torch process the runtime ran each copy as its own
 // 131072-thread blit kernel, and a tile kernel sharing the CUs with it ran 24x
@@ -113,7 +115,7 @@ static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi,
             HIPCHK(c, copy(host + a, hd ? hd + a : nullptr, d_out + a, std::min(C, total - a)));
         HIPCHK(c, hipStreamSynchronize(s0));
     } else {
-        const size_t S = (size_t)std::max(1, env_int("SCC_DIST_STAGE_MB", 64)) << 20;
+        const size_t S = (size_t)std::max(1, env_int("SCC_DIST_STAGE_MB", 32)) << 20;
         if (c->dstage_bytes < S) {
             if (c->h_dstage) (void)hipHostFree(c->h_dstage);
             c->h_dstage = nullptr;

@@ -55,6 +55,7 @@ struct ScRankLaunch {
     int rw_slots;          // wave kernel: tested pairs per gene held in registers, 64 * rw_slots (2, 4, 8 or 16)
     int dbg;               // SCC_RW_DEBUG timing experiments (1: no pair counts, 2: no sort); results invalid
     int rw_ch;             // k_rank_waves: consecutive buckets per wave visit (SCC_RW_CH, <= 64)
+    int split2;            // k_rank_split: two-level scatter of genes past one register chunk (SCC_SPLIT2)
     int bucket_cap;        // capacity of sbuckets / hbg rows
     ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)
     unsigned int* hbg;     // [bucket_cap][K] per-bucket cluster counts

@@ -40,6 +40,7 @@
 #include "scc_kernels.hpp"
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <vector>
 #include <type_traits>
@@ -866,6 +867,8 @@ __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 #define SP_BMAX (2 * SP_BINS + 1)  // a bucket starts at a bin, or right after a fat bin
 #define SP_KPT 8                    // keys per thread held in registers across the passes
 #define SP_CHUNK (SP_T * SP_KPT)
+#define SP_SUP 4096  // two-level scatter: group width (a group holds < 2 * SP_SUP = SP_CHUNK values)
+#define SP_NSUP 1022 // groups a gene may have (three [SP_NSUP + 1] u32 tables fit the excl table)
 
 struct SplitLds {
     u32 hist[SP_BINS];
@@ -881,6 +884,7 @@ struct SplitLds {
     int off[SCC_MAX_K + 1];
     int nb, bk0, next;
     int nfat, fat0, nwav, wav0;
+    int nsup;
 };
 // the split's LDS: its tables, then the bucket-order staging of a gene that
 // fits one register chunk (SP_CHUNK keys + codes)
@@ -1042,11 +1046,104 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     // the order inside a bucket is arbitrary (its ranker sorts by key and cluster).
     // A gene of one register chunk is ordered in LDS and leaves as whole lines
     // (scattered 8-byte / 1-byte stores wrote each line several times over:
-    // 3.8x the keys2 + codes2 bytes at config D); larger genes store directly.
+    // 3.8x the keys2 + codes2 bytes at config D).  A larger gene goes in two
+    // levels: its buckets grouped into super-buckets (runs of buckets whose
+    // starts share floor(offset / SP_SUP); a bucket of more than SP_SUP values
+    // alone, so a group holds < SP_CHUNK), the values scattered into group
+    // order (a chunk's values land in a few dozen runs: whole lines), then each
+    // group of two or more buckets reloaded, ordered in LDS and written back.
+    // The one-level scatter's scattered stores were ~2/3 of a large gene's
+    // split time (8.4 -> 3.0 cycles per value without them at config D).
+    // SCC_SPLIT2=0, or a gene past SP_NSUP groups: the one-level scatter.
     const bool staged = n <= SP_CHUNK;
     u64* stk = (u64*)((char*)&L + kSplitStageOff);
     u8* stc = (u8*)(stk + SP_CHUNK);
-    for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
+    // group tables over the bin tables the layout no longer needs (hist and
+    // excl, adjacent: 4096 words): the bins' group ids in the first 1024, then
+    // three [SP_NSUP + 1] tables
+    static_assert(offsetof(SplitLds, excl) == offsetof(SplitLds, hist) + sizeof(u32) * SP_BINS, "hist | excl");
+    static_assert(SP_BINS / 2 + 3 * (SP_NSUP + 1) <= 2 * SP_BINS, "group tables");
+    unsigned short* supbin = (unsigned short*)L.hist;  // [SP_BINS] group of each bin
+    u32* sbeg = L.hist + SP_BINS / 2;                  // [SP_NSUP + 1] group starts (offsets)
+    u32* sbk = sbeg + (SP_NSUP + 1);                   // [SP_NSUP + 1] first bucket of each group
+    u32* scur = sbk + (SP_NSUP + 1);                   // [SP_NSUP] group cursors
+    bool two = !staged && A.split2;
+    if (two) {
+        // group starts over the bins, 2 per thread (the bucket rule's scan)
+        auto big = [&](u32 b) { return L.boff[b + 1] - L.boff[b] > (u32)SP_SUP; };
+        u32 st[2], bq[2];
+        for (int q = 0; q < 2; ++q) {
+            const int d = 2 * tid + q;
+            const u32 b = L.bid[d];
+            bq[q] = b;
+            const u32 bp = d > 0 ? L.bid[d - 1] : b;
+            st[q] = (d == 0) || (bp != b && (big(b) || big(bp) || L.boff[b] / SP_SUP != L.boff[bp] / SP_SUP));
+        }
+        const u32 v = st[0] + st[1];
+        u32 incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.wsum2[w] = incl;
+        __syncthreads();
+        u32 sb = incl - v;
+        for (int q = 0; q < w; ++q) sb += L.wsum2[q];
+        const u32 ns = [&] {
+            u32 t = 0;
+            for (int q = 0; q < SP_W; ++q) t += L.wsum2[q];
+            return t;
+        }();
+        if (ns <= SP_NSUP) {
+            for (int q = 0; q < 2; ++q) {
+                sb += st[q];
+                if (st[q]) {
+                    sbeg[sb - 1] = L.boff[bq[q]];
+                    sbk[sb - 1] = bq[q];
+                    scur[sb - 1] = L.boff[bq[q]];
+                }
+            }
+            // (the writes above use the per-thread running index; store the bin's group after)
+        }
+        __syncthreads();  // every thread has read the bin tables' old contents (hist / excl no longer read)
+        if (ns <= SP_NSUP) {
+            u32 sb2 = incl - v;
+            for (int q = 0; q < w; ++q) sb2 += L.wsum2[q];
+            for (int q = 0; q < 2; ++q) {
+                sb2 += st[q];
+                supbin[2 * tid + q] = (unsigned short)(sb2 - 1);
+            }
+            if (tid == 0) {
+                sbeg[ns] = (u32)n;
+                sbk[ns] = (u32)nb;
+            }
+        }
+        two = ns <= SP_NSUP;  // (block-uniform)
+        if (tid == 0) L.nsup = (int)ns;
+        __syncthreads();
+    }
+    if (two) {  // first level: straight to the group cursors
+        // (staging each chunk in LDS by group first, for whole-line stores,
+        // measured no faster at config D for genes from 32k, 64k or 128k values)
+        for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
+            load_chunk(c0);
+            int a = 0;
+#pragma unroll
+            for (int q = 0; q < SP_KPT; ++q) {
+                const int i = c0 + q * SP_T + tid;
+                if (i < n) {
+                    while (a + 1 < K && L.off[a + 1] <= i) ++a;
+                    const u64 k = kr[q];
+                    const u32 d = (u32)((k - kmn) >> sh);
+                    const u32 pos = atomicAdd(&scur[supbin[d]], 1u);
+                    A.keys2[base + pos] = k;
+                    A.codes2[base + pos] = (u8)a;
+                    if (k != L.rep[d]) L.bdiff[L.bid[d]] = 1;
+                }
+            }
+        }
+    }
+    for (int c0 = 0; c0 < n && !two; c0 += SP_CHUNK) {
         if (n > SP_CHUNK) load_chunk(c0);
         int a = 0;
 #pragma unroll
@@ -1061,7 +1158,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
                 if (staged) {
                     stk[pos] = k;
                     stc[pos] = (u8)a;
-                } else {
+                } else if (A.dbg != 10) {  // (SCC_RW_DEBUG=10: timing cut, no unstaged stores; results invalid)
                     A.keys2[base + pos] = k;
                     A.codes2[base + pos] = (u8)a;
                 }
@@ -1074,6 +1171,38 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         for (int i = tid; i < n; i += SP_T) {
             A.keys2[base + i] = stk[i];
             A.codes2[base + i] = stc[i];
+        }
+    }
+    if (two) {  // second level: each group of >= 2 buckets ordered in LDS, in place
+        const int ns = L.nsup;
+        for (int sg = 0; sg < ns; ++sg) {
+            if (sbk[sg + 1] - sbk[sg] < 2) continue;  // one bucket: in place already (block-uniform)
+            const u32 o0 = sbeg[sg], m = sbeg[sg + 1] - o0;  // m < SP_CHUNK
+            if (m == 0) continue;
+            u64 kv[SP_KPT];
+            u8 cv[SP_KPT];
+#pragma unroll
+            for (int q = 0; q < SP_KPT; ++q) {  // clamped unconditional loads (all in flight)
+                const u32 j = (u32)(q * SP_T + tid);
+                const u32 jc = j < m ? j : m - 1;
+                kv[q] = A.keys2[base + o0 + jc];
+                cv[q] = A.codes2[base + o0 + jc];
+            }
+#pragma unroll
+            for (int q = 0; q < SP_KPT; ++q) {
+                if ((u32)(q * SP_T + tid) < m) {
+                    const u32 d = (u32)((kv[q] - kmn) >> sh);
+                    const u32 p = atomicAdd(&L.bcur[L.bid[d]], 1u) - o0;
+                    stk[p] = kv[q];
+                    stc[p] = cv[q];
+                }
+            }
+            __syncthreads();
+            for (u32 j = tid; j < m; j += SP_T) {
+                A.keys2[base + o0 + j] = stk[j];
+                A.codes2[base + o0 + j] = stc[j];
+            }
+            __syncthreads();
         }
     }
     // ---- 5. one work unit per bucket (empty buckets: a zero histogram row).
@@ -1151,9 +1280,9 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
         __syncthreads();
         const int i = L.next;
         if (i >= cnt) break;
-        const u64 t0 = A.dbg == 9 ? __builtin_amdgcn_s_memtime() : 0;
+        const u64 t0 = A.dbg >= 9 ? __builtin_amdgcn_s_memtime() : 0;
         split_one_gene(A, A.split_genes[i], L);
-        if (A.dbg == 9 && threadIdx.x == 0 && i < SPLIT_DIAG_MAX) {
+        if (A.dbg >= 9 && threadIdx.x == 0 && i < SPLIT_DIAG_MAX) {
             const int g = A.split_genes[i];
             g_split_diag[i][0] = (unsigned long long)(A.gstart[g + 1] - A.gstart[g]);
             g_split_diag[i][1] = __builtin_amdgcn_s_memtime() - t0;

@@ -922,6 +922,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.rw_slots = P <= 128 ? 2 : P <= 256 ? 4 : P <= 512 ? 8 : 16;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
         L.rw_ch = env_int("SCC_RW_CH", 16);
+        L.split2 = env_int("SCC_SPLIT2", 1);
         L.rw_mfma = env_int("SCC_RANK_MFMA", 1);
         L.rw_mfma16 = env_int("SCC_RANK_MFMA16", -1);
         L.cross_wave = env_int("SCC_CROSS_WAVE", 0);
@@ -975,7 +976,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_rank_classify(&L, s0));
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
         HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
-        if (L.dbg == 9) {  // per-gene split clocks (diagnostic)
+        if (L.dbg >= 9) {  // per-gene split clocks (diagnostic; 10: without the unstaged stores)
             int nsg = 0;
             HIPCHK(c, hipMemcpyAsync(&nsg, d_counts + 3, sizeof(int), hipMemcpyDeviceToHost, s0));
             HIPCHK(c, hipStreamSynchronize(s0));

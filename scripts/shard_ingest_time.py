@@ -40,7 +40,8 @@ for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
         lo, hi = sharded.gene_shard(d.G, r, W, w)
         cap = max(1, P * (hi - lo))
         buf = torch.empty(cap * 8, dtype=torch.int64, device="cuda:0")
-        eng.de_run_shard_records(ds, code, K, lo, hi, buf.data_ptr(), cap)  # warm-up
+        nrec = eng.de_run_shard_records(ds, code, K, lo, hi, buf.data_ptr(), cap)  # warm-up
+        out.setdefault("records", []).append(nrec)
         eng.synchronize()
         eng.reset_timers()
         for _ in range(3):
@@ -50,9 +51,12 @@ for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
             t, n = eng.kernel_time(f)
             out.setdefault(f, []).append(t / max(n, 1))
         del buf
+    recs = out.pop("records")
     print(f"config {cfg}, {W} gene shards, {'full read' if full == '1' else 'range read'}: "
-          + ", ".join(f"{f} max {max(v):.3f} mean {np.mean(v):.3f} ms" for f, v in out.items()), flush=True)
-    print("per rank: " + "; ".join(f"{f} " + " ".join(f"{x:.3f}" for x in v) for f, v in out.items()), flush=True)
+          + ", ".join(f"{f} max {max(v):.3f} mean {np.mean(v):.3f} ms" for f, v in out.items())
+          + f"; records {sum(recs)} ({64 * sum(recs) / 1e6:.1f} MB, 64 B each)", flush=True)
+    print("per rank: " + "; ".join(f"{f} " + " ".join(f"{x:.3f}" for x in v) for f, v in out.items())
+          + "; DE total " + " ".join(f"{sum(v[r] for v in out.values()):.3f}" for r in range(W)), flush=True)
 
 # ---- the distance side of one rank (cell shard of the PCA, its column slice
 # of dist), wall-clock around each call on the synchronised stream
@@ -111,6 +115,10 @@ for r in range(W):
 for r in range(W):
     clo, chi = sharded.column_shard(d.N, r, W)
     res["dist"].append(timed(lambda: eng.distance_scores(scores.data_ptr(), d.N, clo, chi, device_out_ptr=0)))
+clo, chi = sharded.column_shard(d.N, 0, W)  # rank 0 again, after the others (first-slice effects)
+t_again = timed(lambda: eng.distance_scores(scores.data_ptr(), d.N, clo, chi, device_out_ptr=0))
+print(f"dist rank 0 again: {t_again:.3f} ms (columns {clo}..{chi}; last rank {sharded.column_shard(d.N, W - 1, W)})",
+      flush=True)
 print(f"config {cfg}, {W} ranks, distance side (|U| = {nu}): eigen {t_eig:.3f} ms wall, {t_eig_dev:.3f} ms on the stream (one rank, path {path}); "
       + ", ".join(f"{k} max {max(v):.3f} mean {np.mean(v):.3f} ms" for k, v in res.items()), flush=True)
 print("per rank: " + "; ".join(f"{k} " + " ".join(f"{x:.3f}" for x in v) for k, v in res.items()), flush=True)
