@@ -10,6 +10,10 @@ checked end to end:
   avg_logFC, pct.1/pct.2 — depends on that gene alone, so for the sampled
   genes the engine's rows must equal the oracle's exactly (and in the same
   relative order inside each pair).
+* ``check_p_from_counts`` — every tested row's p at FULL size, restated in numpy
+  from the row's exact 2U and tie term and the two cluster sizes
+  (``wilcox.test.default``'s exact / normal rule), so that a wrong p on a gene
+  the subset oracle does not sample cannot pass.
 * ``check_selection`` — the per-pair selection at FULL size, restated in numpy
   from the engine's own per-row statistics: R's row order ``order(p,
   -avg_logFC)`` (Fast:346), BH with the lazy n (Fast:347-350), the
@@ -63,6 +67,37 @@ def check_selection(rows, union, K, q_val_thrs=0.1, top_n=30):
     top_genes = np.concatenate(top_rows) if top_rows else np.zeros(0, np.int32)
     _, first = np.unique(top_genes, return_index=True)
     np.testing.assert_array_equal(union, top_genes[np.sort(first)])
+
+
+def check_p_from_counts(rows, code, K, rtol=1e-9):
+    """R's wilcox.test.default p-value (two-sided, correct = TRUE, exact
+    for n.x < 50 and n.y < 50 without ties) restated in numpy for EVERY
+    tested row from the engine's exact W = u2 / 2, its tie term
+    sum(NTIES^3 - NTIES) and the cluster sizes; the normal tail by
+    scipy's ndtr with R's pnorm underflow (|z| > 37.5193 gives 0).  Returns the
+    number of rows checked (the exact ones through the oracle's pwilcox)."""
+    from scipy.special import ndtr
+    P = K * (K - 1) // 2
+    n = np.bincount(np.asarray(code)[np.asarray(code) >= 0], minlength=K).astype(np.float64)
+    pa = np.array([i for i in range(K - 1) for j in range(i + 1, K)])
+    pb = np.array([j for i in range(K - 1) for j in range(i + 1, K)])
+    row_pair = np.repeat(np.arange(P), np.asarray(rows.pair_tested, np.int64))
+    nx, ny = n[pa[row_pair]], n[pb[row_pair]]
+    W = np.asarray(rows.u2, np.float64) / 2.0
+    ties = np.asarray(rows.ties, np.float64)
+    exact = (nx < 50) & (ny < 50) & (ties == 0)
+    z = W - nx * ny / 2.0
+    sigma = np.sqrt((nx * ny / 12.0) * ((nx + ny + 1.0) - ties / ((nx + ny) * (nx + ny - 1.0))))
+    z = (z - np.sign(z) * 0.5) / sigma
+    tail = np.where(-np.abs(z) < -37.5193, 0.0, ndtr(-np.abs(z)))
+    want = np.minimum(1.0, 2.0 * tail)
+    for k in np.flatnonzero(exact):  # (rare at B-E: clusters of < 50 cells)
+        m, nn, q = int(nx[k]), int(ny[k]), W[k]
+        p = O.pwilcox(q, m, nn) if q <= m * nn / 2 else O.pwilcox(q - 1, m, nn, lower_tail=False)
+        want[k] = min(1.0, 2.0 * p)
+    got = np.asarray(rows.p, np.float64)
+    np.testing.assert_allclose(got, want, rtol=rtol, atol=1e-300, err_msg="p from (2U, ties, n.x, n.y)")
+    return len(got)
 
 
 def check_rows_against_oracle_subset(rows, Xsub, genes, code, K, **params):

@@ -8,16 +8,17 @@ test_gpu_de.py, D in test_gpu_large.py).
   exact-SVD oracle; 2e5 sampled entries of the Pearson `1 - cor` distance.
 * C (100k x 15k, K = 30) and E (1M-cell CSR, K = 100): the oracle on a seeded
   gene subset over all cells and pairs (exact tested sets, U, ties, pct; p and
-  logFC within the bar), the full-size selection restated from the engine's
-  own rows, and at C sampled `dist` entries against the exact SVD.
+  logFC within the bar), every row's p restated from its exact 2U / ties and
+  the cluster sizes, the full-size selection restated from the engine's own
+  rows, and at C sampled `dist` entries against the exact SVD.
 """
 import numpy as np
 import pytest
 import torch  # before the engine loads (torch's HIP runtime first)
 
 import oracle as O
-from parity_helpers import (check_rows_against_oracle_subset, check_selection, packed_index, rows_of_gene_major,
-                            sample_cell_pairs)
+from parity_helpers import (check_p_from_counts, check_rows_against_oracle_subset, check_selection, packed_index,
+                            rows_of_gene_major, sample_cell_pairs)
 from scconsensus_amd import api, synth
 
 pytestmark = pytest.mark.gpu
@@ -100,6 +101,7 @@ def _de_large(name, n_genes_sample, seed, dist_pairs=0):
     assert np.all((r.ties >= 0))
     assert 100 < len(g.union) <= 30 * P
     check_selection(r, g.union, K)
+    assert check_p_from_counts(r, code, K) == len(r.gene)  # every row's p from its exact counts
     # the oracle on a seeded gene sample: half drawn from the tested rows, half uniform
     rng = np.random.default_rng(seed)
     tg = np.unique(r.gene)

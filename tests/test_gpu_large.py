@@ -13,7 +13,8 @@ import pytest
 import torch  # before the engine loads (torch's HIP runtime first)
 
 import oracle as O
-from parity_helpers import (check_rows_against_oracle_subset, check_selection, check_slow_against_oracle_subset,
+from parity_helpers import (check_p_from_counts, check_rows_against_oracle_subset, check_selection,
+                            check_slow_against_oracle_subset,
                             check_slow_selection, packed_index, rows_of_gene_major, sample_cell_pairs, slow_gate,
                             slow_log_threshold)
 from scconsensus_amd import api, synth
@@ -42,6 +43,7 @@ def test_config_d_parity(monkeypatch):
     assert np.all(r.u2 >= 0) and np.all(r.u2 <= 2 * nn[r.row_pair])
     assert 100 < len(g.union) <= 30 * len(pairs)
     check_selection(r, g.union, K)
+    assert check_p_from_counts(r, code, K) == len(r.gene)  # every row's p from its exact counts
     # the same DE with the re-split route off (fat buckets ranked as LDS items)
     # and the gene-level cross terms by the per-(gene, pair) wave kernel
     monkeypatch.setenv("SCC_RESPLIT", "0")

@@ -7,8 +7,8 @@ import numpy as np
 import pytest
 
 import oracle as O
-from parity_helpers import (check_rows_against_oracle_subset, check_selection, packed_index, rows_of_gene_major,
-                            sample_cell_pairs)
+from parity_helpers import (check_p_from_counts, check_rows_against_oracle_subset, check_selection, packed_index,
+                            rows_of_gene_major, sample_cell_pairs)
 from scconsensus_amd import api, synth
 
 
@@ -52,6 +52,40 @@ def test_subset_oracle_accepts_and_rejects(small):
     bad.u2[k] += 1
     with pytest.raises(AssertionError):
         check_rows_against_oracle_subset(bad, X[genes], genes, code, K)
+
+
+def test_p_from_counts_accepts_oracle_and_rejects(small):
+    d, X, code, K, o, rows = small
+    assert check_p_from_counts(rows, code, K) == len(rows.p)
+    bad = SimpleNamespace(**vars(rows))
+    bad.p = rows.p.copy()
+    k = int(np.flatnonzero(rows.p > 1e-10)[0])
+    bad.p[k] *= 1.0 + 1e-6
+    with pytest.raises(AssertionError):
+        check_p_from_counts(bad, code, K)
+
+
+def test_p_from_counts_exact_branch():
+    """Small clusters without ties (wilcox.test's exact branch) and tied
+    data (the normal branch), each row's p against the oracle's wilcox.test."""
+    rng = np.random.default_rng(1)
+    K, sizes = 4, [30, 45, 60, 200]
+    code = np.repeat(np.arange(K), sizes).astype(np.int32)
+    rng.shuffle(code)
+    u2, ties, p, tested = [], [], [], []
+    for i in range(K - 1):
+        for j in range(i + 1, K):
+            for g in range(20):
+                x = np.where(rng.random(len(code)) < 0.6, np.round(rng.gamma(1, 2, len(code)), 1), 0.0)
+                if g % 4 == 0:
+                    x = rng.random(len(code))  # no ties: exact below 50 cells
+                pv, W, T, _ = O.wilcox_test(x[code == i], x[code == j])
+                u2.append(int(round(2 * W)))
+                ties.append(T)
+                p.append(pv)
+            tested.append(20)
+    rows = SimpleNamespace(pair_tested=np.array(tested), u2=np.array(u2), ties=np.array(ties), p=np.array(p))
+    assert check_p_from_counts(rows, code, K) == len(p)
 
 
 def test_packed_index_and_rows():
