@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(256) k_rec_scatter(const scc_de_record* __rest
                                                      double* __restrict__ p_, double* __restrict__ lfc,
                                                      double* __restrict__ pct1, double* __restrict__ pct2,
                                                      long long* __restrict__ u2, long long* __restrict__ t,
-                                                     u8* __restrict__ flags, int* __restrict__ err)
+                                                     u8* __restrict__ flags, int* __restrict__ err, int plo, int phi)
 {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const scc_de_record r = rec[i];
@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(256) k_rec_scatter(const scc_de_record* __rest
             atomicOr(err, 16);  // a malformed record
             continue;
         }
+        if (r.pair < plo || r.pair >= phi) continue;  // another rank's pair block (pair-split selection)
         const size_t e = (size_t)r.pair * G + r.gene;
         p_[e] = r.p;
         lfc[e] = r.avg_logfc;
@@ -143,11 +144,11 @@ extern "C" hipError_t scc_launch_rec_pack(const uint8_t* flags, int G, int P, in
 
 extern "C" hipError_t scc_launch_rec_scatter(const scc_de_record* rec, long long n, int G, int P, double* p,
                                              double* lfc, double* pct1, double* pct2, long long* u2, long long* t,
-                                             uint8_t* flags, int* err, hipStream_t st)
+                                             uint8_t* flags, int* err, int plo, int phi, hipStream_t st)
 {
     if (n <= 0) return hipSuccess;
     const long long nb = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
     hipLaunchKernelGGL(k_rec_scatter, dim3((unsigned)nb), dim3(256), 0, st, rec, n, G, P, p, lfc, pct1, pct2, u2, t,
-                       flags, err);
+                       flags, err, plo, phi);
     return hipGetLastError();
 }

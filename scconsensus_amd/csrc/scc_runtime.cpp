@@ -475,7 +475,7 @@ hipError_t scc_launch_rec_pack(const uint8_t* flags, int G, int P, int glo, int 
                                const long long* u2, const long long* t, scc_de_record* out, hipStream_t st);
 hipError_t scc_launch_rec_scatter(const scc_de_record* rec, long long n, int G, int P, double* p, double* lfc,
                                   double* pct1, double* pct2, long long* u2, long long* t, uint8_t* flags, int* err,
-                                  hipStream_t st);
+                                  int plo, int phi, hipStream_t st);
 }
 
 struct RecIO {  // the compact exchange's buffers (DE_SHARD_REC out, DE_FINISH_REC in)
@@ -562,8 +562,9 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     std::vector<int> start(K + 1, 0);
     for (int a = 0; a < K; ++a) start[a + 1] = start[a] + nclu[a];
     const int nkept = start[K];
-    std::vector<int> perm(N), fill(start.begin(), start.end() - 1);
-    {
+    // (a finish stage reads no cell order: the records carry every statistic)
+    std::vector<int> perm(finish_stage ? 0 : N), fill(start.begin(), start.end() - 1);
+    if (!finish_stage) {
         int u = nkept;
         for (int i = 0; i < N; ++i) perm[code[i] >= 0 ? fill[code[i]]++ : u++] = i;
     }
@@ -1103,14 +1104,24 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             src += PG * f.es;
         }
     } else if (stage == DE_FINISH_REC) {
-        for (const Field& f : fields)
-            if (f.p) HIPCHK(c, hipMemsetAsync(f.p, 0, PG * f.es, s0));
+        // pair-split selection (first_out): only this rank's pair rows are
+        // read, so only they are cleared and scattered (the flags, which size
+        // every pair's row offsets, are cleared in full)
+        const bool pb = rio->first_out != nullptr;
+        const int plo = pb ? rio->pair_lo : 0, phi = pb ? rio->pair_hi : P;
+        for (const Field& f : fields) {
+            if (!f.p) continue;
+            if (f.p == (void*)d_flags || !pb)
+                HIPCHK(c, hipMemsetAsync(f.p, 0, PG * f.es, s0));
+            else if (phi > plo)
+                HIPCHK(c, hipMemsetAsync((char*)f.p + (size_t)plo * G * f.es, 0, (size_t)(phi - plo) * G * f.es, s0));
+        }
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
         const scc_de_record* rec = (const scc_de_record*)rio->in;
         for (int b = 0; b < rio->nblocks; ++b)
             HIPCHK(c, scc_launch_rec_scatter(rec + (size_t)b * rio->stride, rio->counts[b], G, P, d_p, d_lfc,
                                              fast ? d_pct1 : nullptr, fast ? d_pct2 : nullptr, d_u2, d_t, d_flags,
-                                             d_err, s0));
+                                             d_err, plo, phi, s0));
     }
     // rows (FAST) / per-pair vectors (SLOW)
     int* d_row_gene = nullptr;

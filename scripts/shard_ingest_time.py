@@ -33,6 +33,7 @@ else:
     w = np.bincount(d.indices, minlength=d.G)
 eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union")  # validates the dataset
 fams = ["ingest", "gene_stats", "gene_rank", "pair_test"]
+kept = []  # (records buffer, count) of each rank's range-read run
 for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
     os.environ["SCC_INGEST_FULL"] = full
     out = {}
@@ -50,7 +51,10 @@ for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
         for f in fams:
             t, n = eng.kernel_time(f)
             out.setdefault(f, []).append(t / max(n, 1))
-        del buf
+        if full == "0":
+            kept.append((buf, nrec))
+        else:
+            del buf
     recs = out.pop("records")
     print(f"config {cfg}, {W} gene shards, {'full read' if full == '1' else 'range read'}: "
           + ", ".join(f"{f} max {max(v):.3f} mean {np.mean(v):.3f} ms" for f, v in out.items())
@@ -61,6 +65,42 @@ for full in [f for f, n in (("1", "full"), ("0", "range")) if n in parts_run]:
 # ---- the distance side of one rank (cell shard of the PCA, its column slice
 # of dist), wall-clock around each call on the synchronised stream
 import time  # noqa: E402
+
+if kept:
+    # the records all-gather emulated (blocks of the common stride), then each
+    # rank's selection of its pair block (scc_de_finish_records_pairs) and the
+    # union from the MIN-combined first-occurrence keys (scc_de_union_first_occ)
+    REC_WORDS = 8
+    counts = np.array([c for _, c in kept], np.int64)
+    stride = int(counts.max())
+    recs = torch.zeros(W * stride * REC_WORDS, dtype=torch.int64, device="cuda:0")
+    for r, (b, c) in enumerate(kept):
+        recs[r * stride * REC_WORDS: (r * stride + c) * REC_WORDS] = b[: c * REC_WORDS]
+    del kept
+    firsts = []
+    tsel = []
+    for r in range(W):
+        plo, phi = sharded.parallel.shard_range(P, r, W)
+        first = torch.empty(d.G + 1, dtype=torch.int64, device="cuda:0")
+        eng.de_finish_records_pairs(ds, code, K, recs.data_ptr(), counts, stride, plo, phi, first.data_ptr())
+        eng.synchronize()
+        t0 = time.perf_counter()
+        eng.de_finish_records_pairs(ds, code, K, recs.data_ptr(), counts, stride, plo, phi, first.data_ptr())
+        eng.synchronize()
+        tsel.append((time.perf_counter() - t0) * 1e3)
+        firsts.append(first[: d.G].clone())
+    keys = torch.stack(firsts)
+    keys[keys == -1] = torch.iinfo(torch.int64).max
+    keys = keys.min(dim=0).values
+    keys[keys == torch.iinfo(torch.int64).max] = -1
+    t0 = time.perf_counter()
+    un = eng.de_union_first_occ(keys.data_ptr(), d.G)
+    tun = (time.perf_counter() - t0) * 1e3
+    ref = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="union").union
+    print(f"selection of 1/{W} of the pairs from all records: max {max(tsel):.3f} mean {np.mean(tsel):.3f} ms "
+          f"(wall, synchronised); union from the keys {tun:.3f} ms; union identical to one GPU: "
+          f"{bool(np.array_equal(un, ref))}", flush=True)
+    del recs
 
 if "dist" not in parts_run:
     sys.exit(0)
