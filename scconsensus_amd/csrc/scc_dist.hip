@@ -196,6 +196,21 @@ __global__ void __launch_bounds__(256) k_center(double* __restrict__ Xc, int N, 
 }
 
 // ------------------------------------------------------------------ Gram (fp64 MFMA)
+// Dispatch slot -> (output tile, cell chunk).  Slot x runs on XCD x % 8; the
+// slots of one XCD take whole chunks, all tiles of a chunk together, so the
+// chunk's rows of Xc come from HBM once into that XCD's L2 and every tile
+// reading them hits there (with chunk-major slots across the grid, a chunk's
+// tiles sat on all eight XCDs and each fetched the rows: 5.7x the operand at
+// B, 8x at D).  The grid is ceil(nchunk / 8) * 8 * ntl slots; the spare ones exit.
+__device__ inline bool gram_slot(int ntl, int nchunk, int& tile, int& chunk)
+{
+    const int x = blockIdx.x, xcd = x & 7, q = x >> 3;
+    chunk = (q / ntl) * 8 + xcd;
+    tile = q % ntl;
+    return chunk < nchunk;
+}
+static inline unsigned gram_grid(int ntl, int nchunk) { return (unsigned)(((nchunk + 7) / 8) * 8 * ntl); }
+
 #define GR_U 4  // 4-row k-steps whose loads are issued together (8: B 0.13, C 0.88, D 4.51 ms)
 // WG = 4 waves -> 64x64 tile of C (upper tiles only); wave -> 32x32 = 2x2 MFMA
 // 16x16x4 tiles.  Lane l holds A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15];
@@ -205,17 +220,19 @@ __global__ void __launch_bounds__(256) k_center(double* __restrict__ Xc, int N, 
 // bits), rows past nval zero.  (The 128-wide kernel below keeps an explicit
 // centring pass: eight more registers took it from two waves per SIMD to one.)
 __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc, int Npad, int ld, int ntile,
-                                                  int rows_per_chunk, double* __restrict__ slabs,
+                                                  int nchunk, int rows_per_chunk, double* __restrict__ slabs,
                                                   const double* __restrict__ mean, int nval)
 {
-    // upper-triangular tile index -> (ti, tj), ti <= tj
-    int t = blockIdx.x, ti = 0;
+    // upper-triangular tile index -> (ti, tj), ti <= tj; every tile of one
+    // chunk on one XCD (gram_slot)
+    int t, chunk;
+    if (!gram_slot(ntile * (ntile + 1) / 2, nchunk, t, chunk)) return;
+    int ti = 0;
     while (t >= ntile - ti) {
         t -= ntile - ti;
         ++ti;
     }
     const int tj = ti + t;
-    const int chunk = blockIdx.y;
     const int lane = threadIdx.x & 63, w = scc_wave_id();
     const int wi = (w >> 1) * 32, wj = (w & 1) * 32;
     const int i0 = ti * 64 + wi, j0 = tj * 64 + wj;
@@ -276,15 +293,16 @@ __global__ void __launch_bounds__(256) k_gram_f64(const double* __restrict__ Xc,
 // 128 tile is not computed (its mirror is), and a tile whose second 64-block
 // falls past ld (ld % 128 == 64) leaves those waves idle.
 __global__ void __launch_bounds__(256) k_gram_f64_128(const double* __restrict__ Xc, int Npad, int ld, int ntile,
-                                                      int rows_per_chunk, double* __restrict__ slabs)
+                                                      int nchunk, int rows_per_chunk, double* __restrict__ slabs)
 {
-    int t = blockIdx.x, ti = 0;
+    int t, chunk;
+    if (!gram_slot(ntile * (ntile + 1) / 2, nchunk, t, chunk)) return;
+    int ti = 0;
     while (t >= ntile - ti) {
         t -= ntile - ti;
         ++ti;
     }
     const int tj = ti + t;
-    const int chunk = blockIdx.y;
     const int lane = threadIdx.x & 63, w = scc_wave_id();
     const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
     const int i0 = ti * 128 + wi, j0 = tj * 128 + wj;
@@ -333,7 +351,11 @@ __global__ void __launch_bounds__(256) k_gram_f64_128(const double* __restrict__
             }
 }
 
-// C[i][j] = sum_k slabs[k][i][j] in chunk order for tiles ti <= tj, mirrored
+// C[i][j] = sum_k slabs[k][i][j] in chunk order for 64-blocks ti <= tj, and
+// the same sum stored at C[j][i]: the slabs are read only where they were
+// computed, in whole lines (reading the mirror column-wise for the lower
+// blocks fetched a line per element: 3.5x the slabs at B); the transposed
+// stores of one block come from one workgroup and merge in its XCD's L2
 __global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ slabs, int nchunk, int ld,
                                                      double* __restrict__ C)
 {
@@ -341,10 +363,12 @@ __global__ void __launch_bounds__(256) k_gram_reduce(const double* __restrict__ 
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
         const int i = (int)(e / ld), j = (int)(e % ld);
         const int ti = i >> 6, tj = j >> 6;
-        const size_t src = (ti <= tj) ? e : ((size_t)j * ld + i);
+        if (ti > tj) continue;
         double s = 0.0;
-        for (int k = 0; k < nchunk; ++k) s += slabs[(size_t)k * total + src];
+#pragma unroll 8
+        for (int k = 0; k < nchunk; ++k) s += slabs[(size_t)k * total + e];
         C[e] = s;
+        if (ti < tj) C[(size_t)j * ld + i] = s;
     }
 }
 
@@ -1077,12 +1101,12 @@ extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nc
     if (mean && tw != 64) return hipErrorInvalidValue;
     if (tw == 128) {
         const int nt = (ld + 127) / 128;
-        hipLaunchKernelGGL(k_gram_f64_128, dim3(nt * (nt + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, nt, rpc,
-                           slabs);
+        hipLaunchKernelGGL(k_gram_f64_128, dim3(gram_grid(nt * (nt + 1) / 2, nchunk)), dim3(256), 0, st, Xc, Npad,
+                           ld, nt, nchunk, rpc, slabs);
     } else {
         const int ntile = ld / 64;
-        hipLaunchKernelGGL(k_gram_f64, dim3(ntile * (ntile + 1) / 2, nchunk), dim3(256), 0, st, Xc, Npad, ld, ntile,
-                           rpc, slabs, mean, nval);
+        hipLaunchKernelGGL(k_gram_f64, dim3(gram_grid(ntile * (ntile + 1) / 2, nchunk)), dim3(256), 0, st, Xc, Npad,
+                           ld, ntile, nchunk, rpc, slabs, mean, nval);
     }
     hipLaunchKernelGGL(k_gram_reduce, dim3(2048), dim3(256), 0, st, slabs, nchunk, ld, C);
     return hipGetLastError();

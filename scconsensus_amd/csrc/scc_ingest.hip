@@ -76,8 +76,9 @@ __device__ inline i64 wave_lower_bound(const int* __restrict__ rows, i64 lo, i64
 // `hw` genes: the first pass reads every entry (nodg, expm1, input checks,
 // tile boundaries, counts of window 0), later passes read each cell's entries
 // of their window only (two wave-parallel binary searches; dense: the range).
-template <bool DENSE>
-__global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
+template <bool DENSE, int MINB>
+__global__ void __launch_bounds__(IH_T) __attribute__((amdgpu_waves_per_eu(MINB * IH_T / 256)))
+k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                     const double* __restrict__ vals, int G, const int* __restrict__ perm,
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
@@ -287,16 +288,16 @@ __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int
 #define SC_GT 256       // genes per tile
 #define SC_CAP 4096     // default staged entries per round (u64 key + u16 gene = 10 B each): 3 blocks per CU
 #define SC_CMAX 128     // cells per scatter chunk (kScatterCC * kCountChunk)
-#define SC_RUN 8        // consecutive gene tiles of one chunk dealt to one XCD
+#define SC_RUN 8        // consecutive gene tiles of one chunk dealt to one XCD (SCC_SC_RUN)
 
-template <bool DENSE>
+template <bool DENSE, int U>
 __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                        const double* __restrict__ vals, int G,
                                                        const int* __restrict__ perm, const int* __restrict__ cc_p0,
                                                        const int* __restrict__ sc_cc0, const u32* __restrict__ cnt,
                                                        const i64* __restrict__ gstart, const i64* __restrict__ bnd,
                                                        int ntile, int cap, int glo, int ghi, int t0, int nsc, int ntl,
-                                                       u64* __restrict__ keys)
+                                                       int run, u64* __restrict__ keys)
 {
     __shared__ u32 loff[SC_GT + 1];
     __shared__ u32 cur[SC_GT];
@@ -316,7 +317,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
     // line a cell's entries of tiles t and t + 1 share is fetched once into
     // that XCD's L2 instead of twice from HBM
     const long long lin = blockIdx.x, kq = lin >> 3, xq = lin & 7;
-    const long long L = ((kq / SC_RUN) * 8 + xq) * SC_RUN + kq % SC_RUN;
+    const long long L = ((kq / run) * 8 + xq) * run + kq % run;
     if (L >= (long long)nsc * ntl) return;
     const int s = (int)(L / ntl), t = t0 + (int)(L % ntl);  // gene tiles from t0 (a gene shard's tiles)
     const int g0 = t * SC_GT, g1 = min(G, g0 + SC_GT), ng = g1 - g0;
@@ -428,11 +429,11 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
         // entry e - cof[c] of cell c, found by a binary search of cof): every
         // lane loads, however few entries a cell has in the tile (~8 at 1M-cell
         // density; a lane per cell entry left most lanes idle)
-        for (u32 e0 = (u32)wv * 256; e0 < E; e0 += 4 * ING_T) {
-            double x[4];
-            int gq[4];
+        for (u32 e0 = (u32)wv * (64 * U); e0 < E; e0 += U * ING_T) {
+            double x[U];
+            int gq[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 // clamped to the last entry (e0 < E) so the loads are
                 // unconditional and all four stay in flight (as in k_ing_hist)
                 const u32 e = e0 + (u32)(u * 64 + lane);
@@ -451,7 +452,7 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
                 gq[u] = e < E ? gv : -1;
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) put(x[u], gq[u]);
+            for (int u = 0; u < U; ++u) put(x[u], gq[u]);
         }
         __syncthreads();
         const int Er = (int)(loff[r1] - base);
@@ -636,14 +637,23 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
 {
     const int hw = scc_ingest_hist_window(G);
     const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
+    static const int minb = [] {
+        const char* v = getenv("SCC_IH_MINB");
+        return (v && *v) ? atoi(v) : 1;
+    }();
     if (dense) {
-        hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_hist<true>, dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw, nullptr,
+        hipFuncSetAttribute((const void*)k_ing_hist<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_ing_hist<true, 1>), dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm,
+                           cc_p0, cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw,
+                           nullptr, err);
+    } else if (minb == 2) {
+        hipFuncSetAttribute((const void*)k_ing_hist<false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_ing_hist<false, 2>), dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, tbnd,
                            err);
     } else {
-        hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(k_ing_hist<false>, dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+        hipFuncSetAttribute((const void*)k_ing_hist<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_ing_hist<false, 1>), dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
                            cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, tbnd,
                            err);
     }
@@ -689,21 +699,37 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
     if (ns <= 0 || ghi <= glo) return hipSuccess;
     const int t0 = glo / SC_GT, t1 = (ghi + SC_GT - 1) / SC_GT;  // the gene tiles of [glo, ghi)
     const int ntl = t1 - t0;
-    const long long nrun = ((long long)ns * ntl + SC_RUN - 1) / SC_RUN;
-    const dim3 grid((unsigned)(((nrun + 7) / 8) * 8 * SC_RUN));
+    static const int run = [] {
+        const char* v = getenv("SCC_SC_RUN");
+        return (v && *v) ? std::max(1, atoi(v)) : SC_RUN;
+    }();
+    const long long nrun = ((long long)ns * ntl + run - 1) / run;
+    const dim3 grid((unsigned)(((nrun + 7) / 8) * 8 * run));
     static const int cap = [] {
         const char* v = getenv("SCC_SC_CAP");
         return (v && *v) ? std::max(SC_GT, atoi(v)) : SC_CAP;
     }();
     const size_t lds = (size_t)cap * (8 + 2);
-    hipFuncSetAttribute((const void*)k_ing_scatter<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_ing_scatter<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    static const int unroll = [] {
+        const char* v = getenv("SCC_SC_U");
+        return (v && *v) ? atoi(v) : 4;
+    }();
+    hipFuncSetAttribute((const void*)k_ing_scatter<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_ing_scatter<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_ing_scatter<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute((const void*)k_ing_scatter<false, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (dense)
-        hipLaunchKernelGGL(k_ing_scatter<true>, grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, keys);
+        hipLaunchKernelGGL((k_ing_scatter<true, 4>), grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm,
+                           cc_p0, sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
+    else if (unroll == 16)
+        hipLaunchKernelGGL((k_ing_scatter<false, 16>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
+    else if (unroll == 8)
+        hipLaunchKernelGGL((k_ing_scatter<false, 8>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     else
-        hipLaunchKernelGGL(k_ing_scatter<false>, grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0, sc_cc0,
-                           cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, keys);
+        hipLaunchKernelGGL((k_ing_scatter<false, 4>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     return hipGetLastError();
 }
 

@@ -49,6 +49,9 @@ struct scc_ctx {
     hipStream_t s0 = nullptr, s1 = nullptr;
     hipStream_t own_s0 = nullptr;  // the context's own stream (s0 unless scc_ctx_set_stream)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t sw[2] = {nullptr, nullptr};        // side streams of the wave kernels' slot classes
+    hipEvent_t ev_wj[2] = {nullptr, nullptr};      // their joins
+    hipEvent_t ev_wfork = nullptr;                 // and fork
     std::string err;
     // workspace slots (grow-only)
     std::map<std::string, std::pair<void*, size_t>> ws;

@@ -245,10 +245,15 @@ int scc_rank_tables_global(int ntp_max, int K);
 size_t scc_rank_tables_stride(int ntp_max, int K);
 hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int grid, hipStream_t st);
-hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st);
+// the slot classes' launches go round st, side[0], side[1], ... (nside 0: all
+// on st); a side stream is forked from st (event fork) when it first gets a
+// launch and joined back (its event in join[]) at the end
+hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st, const hipStream_t* side = nullptr,
+                                 int nside = 0, hipEvent_t fork = nullptr, const hipEvent_t* join = nullptr);
 void scc_rank_mfma_stamps(hipStream_t st, int print);
 hipError_t scc_launch_rank_cross(const ScRankLaunch* L, int grid_genes, hipStream_t st);
-hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st);
+hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st, const hipStream_t* side = nullptr,
+                                   int nside = 0, hipEvent_t fork = nullptr, const hipEvent_t* join = nullptr);
 hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid, hipStream_t st);
 hipError_t scc_launch_pair_filter(const ScTestLaunch* L, hipStream_t st);
 size_t scc_eigen_scratch_doubles(int n, int lda, int k);

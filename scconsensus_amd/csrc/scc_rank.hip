@@ -86,6 +86,9 @@ __device__ inline u64 match_bits(u32 d, u64 act)
 // ===================================================================== stats
 #define ST_T 256
 #define ST_W (ST_T / 64)
+#ifndef ST_U
+#define ST_U 4
+#endif
 
 struct StatItem {
     double sx_hi, sx_lo, se_hi, se_lo;
@@ -122,15 +125,19 @@ __global__ void __launch_bounds__(ST_T) k_gene_stats(ScStatsLaunch A)
         const double ma = VAR ? A.mean_x[(size_t)a * A.G + g] : 0.0;
         dd sx{0.0, 0.0}, se{0.0, 0.0};
         u32 pos = 0, neg = 0;
-        for (int i = s0 + lane; i < s1; i += 256) {
-            double x[4];  // 4 loads in flight; past the end adds +0 (exact no-op)
+        // ST_U loads in flight per lane (16 measured slower: B 0.18 -> 0.28 ms,
+        // D 2.06 -> 2.75: the stage is VALU-bound on fp64 expm1 + double-double
+        // adds, and the wider unroll cost occupancy); the per-lane summation
+        // order (i, i + 64, i + 128, ...) does not depend on ST_U
+        for (int i = s0 + lane; i < s1; i += 64 * ST_U) {
+            double x[ST_U];  // past the end adds +0 (exact no-op)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {  // clamped unconditional load + select (i < s1)
+            for (int q = 0; q < ST_U; ++q) {  // clamped unconditional load + select (i < s1)
                 const double v = scc_val_of(key[min(i + 64 * q, s1 - 1)]);
                 x[q] = (i + 64 * q < s1) ? v : 0.0;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < ST_U; ++q) {
                 if (EXPM1) se = dd_add_d(se, expm1(x[q]));
                 if (SUMX) sx = dd_add_d(sx, x[q]);
                 if (VAR && i + 64 * q < s1) sx = dd_add(sx, dd_two_prod(x[q] - ma, x[q] - ma));
@@ -3223,8 +3230,63 @@ extern "C" size_t scc_rank_split_lds(int K)
     return kSplitStageOff + (size_t)SP_CHUNK * (sizeof(u64) + 1);
 }
 
-extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st)
+// Launches that may run concurrently taken round st0, side[0], side[1], ...:
+// a side stream waits on the fork event (recorded on st0 before the first
+// launch: a record costs no wait) when it first gets a launch, and st0 waits on
+// its join event at the end.  nside 0: everything on st0.
+struct SideStreams {
+    hipStream_t st0;
+    const hipStream_t* side;
+    int nside;
+    hipEvent_t fork;
+    const hipEvent_t* join;
+    bool used[4] = {false, false, false, false};
+    int turn = 0;
+    SideStreams(hipStream_t s, const hipStream_t* sd, int n, hipEvent_t f, const hipEvent_t* j)
+        : st0(s), side(sd), nside((f && j && sd) ? std::min(n, 4) : 0), fork(f), join(j)
+    {
+        if (nside > 0) hipEventRecord(fork, st0);
+    }
+    hipStream_t next()
+    {
+        const int t = turn++;
+        if (nside <= 0 || t % (nside + 1) == 0) return st0;
+        const int i = t % (nside + 1) - 1;
+        if (!used[i]) hipStreamWaitEvent(side[i], fork, 0);
+        used[i] = true;
+        return side[i];
+    }
+    void end()
+    {
+        for (int i = 0; i < nside; ++i)
+            if (used[i]) {
+                hipEventRecord(join[i], side[i]);
+                hipStreamWaitEvent(st0, join[i], 0);
+                used[i] = false;
+            }
+    }
+};
+
+static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStreams& ss);
+
+extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hipStream_t st0, const hipStream_t* side,
+                                            int nside, hipEvent_t fork, const hipEvent_t* join)
 {
+    SideStreams ss(st0, side, nside, fork, join);
+    const hipError_t e = rank_waves_launches(L, grid, ss);
+    ss.end();
+    return e != hipSuccess ? e : hipGetLastError();
+}
+
+static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStreams& ss)
+{
+    // the launches below touch disjoint genes' accumulator cells (each gene is
+    // in one class) or, for the windows of one gene, disjoint pair rows, and
+    // read only what the split wrote: they may run concurrently, so each takes
+    // the next stream in turn and their tails overlap (a gene shard's grid is
+    // an eighth of the whole job's and each launch ended on a long tail)
+    auto next_stream = [&]() { return ss.next(); };
+    hipStream_t st = ss.st0;
     // one launch per slot class present: genes with <= 128 tested pairs on the
     // 2-slot kernel, <= 256 on 4, <= 512 on 8, <= 1024 on 16
     // the matrix-core kernel (K <= 64) counts all K^2 pairs of a bucket at a
@@ -3242,6 +3304,7 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
         ScRankLaunch M = *L;
         M.wv_filter = L->rw_mfma == 2 ? 0 : 1;
         M.wv_lo = mfma_min;
+        st = next_stream();
         if (L->K <= 32)
             hipLaunchKernelGGL(k_rank_mfma<1>, dim3(grid), dim3(256), 0, st, M);
         else
@@ -3271,6 +3334,7 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
         A.wv_hi = hi[c];
         A.wv_base = 0;
         A.wv_filter = L->rw_slots > 2 ? 1 : 0;  // rw_slots 2: class 0 is the only launch and holds every gene
+        st = next_stream();
         if (c == 0)
             hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, A);
         else if (c == 1)
@@ -3287,6 +3351,7 @@ extern "C" hipError_t scc_launch_rank_waves(const ScRankLaunch* L, int grid, hip
     if (L->rw_slots >= RW_SLOTS_MAX) {
         const int per = 64 * RW_SLOTS_MAX;
         const int npass = (std::min(L->ntp_max, RW_PAIRS_MAX) + per - 1) / per;
+        st = next_stream();  // (the windows in one stream)
         for (int k = 0; k < npass; ++k) {
             A.wv_lo = std::max(per, k * per);
             A.wv_hi = RW_PAIRS_MAX;
@@ -3321,9 +3386,15 @@ extern "C" hipError_t scc_launch_rank_cross_seg(const ScRankLaunch* L, int grid,
     return hipGetLastError();
 }
 
-extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st)
+extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, hipStream_t st0, const hipStream_t* side,
+                                              int nside, hipEvent_t fork, const hipEvent_t* join)
 {
     if (!L->fatbk || grid <= 0) return hipSuccess;
+    // the first level's three launches take disjoint parents (<= RSW_CAP
+    // elements by tested-pair class, larger ones) and meet only in atomic
+    // allocation counters: concurrent; the second level reads the first's fat2
+    SideStreams ss(st0, side, nside, fork, join);
+    hipStream_t st = st0;
     // wave-private allocation chunks sized so that the unused tails of all
     // waves stay a small part of the bucket capacity
     ScRankLaunch W = *L;
@@ -3333,11 +3404,13 @@ extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, h
     // K > 64 (config E): most genes hold more than 512 tested pairs, one launch
     // of the wide variant takes every parent (a second pass over the list cost more)
     W.rsw_all = L->K > 64 ? 1 : 0;
-    if (!W.rsw_all) hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);
-    if (L->P > 64 * RSW_TS_SMALL) hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, st, W);
+    if (!W.rsw_all) hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, ss.next(), W);
+    if (L->P > 64 * RSW_TS_SMALL)
+        hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, ss.next(), W);
     const size_t acc_lds = sizeof(u64) * (size_t)std::max(L->P, 1);
     hipFuncSetAttribute((const void*)k_rank_resplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_lds);
-    hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), acc_lds, st, *L);
+    hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), acc_lds, ss.next(), *L);
+    ss.end();
     if (L->fat2) {  // sub-buckets the first level left with > 64 distinct values
         W.rs_level = 1;
         if (!W.rsw_all) hipLaunchKernelGGL(k_rank_resplit_w<RSW_TS_SMALL>, dim3(2 * grid), dim3(256), 0, st, W);

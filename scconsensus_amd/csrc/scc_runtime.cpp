@@ -33,7 +33,12 @@ static int ctx_create_one(int device, bool profile, scc_ctx** out)
     if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->s0, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->s1, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sw[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->sw[1], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_wj[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_wj[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_wfork, hipEventDisableTiming) != hipSuccess) {
         hipGetLastError();
         delete c;
         return SCC_ERR_HIP;
@@ -117,6 +122,12 @@ extern "C" void scc_ctx_destroy(scc_ctx* c)
     if (c->h_dstage) hipHostFree(c->h_dstage);
     hipEventDestroy(c->ev_fork);
     hipEventDestroy(c->ev_join);
+    for (int i = 0; i < 2; ++i) {
+        hipStreamSynchronize(c->sw[i]);
+        hipStreamDestroy(c->sw[i]);
+        hipEventDestroy(c->ev_wj[i]);
+    }
+    hipEventDestroy(c->ev_wfork);
     hipStreamSynchronize(c->s0);
     hipStreamDestroy(c->own_s0);
     hipStreamDestroy(c->s1);
@@ -997,7 +1008,10 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
                     h[4] / (double)std::max(1ull, h[7]));
             HIPCHK(c, hipMemsetAsync(R.stamps, 0, 64, s0));
         } else {
-            HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0));
+            // (not on small jobs: at config B the fork and join cost more than
+            // the overlap of two ~10-us launches)
+            const int rs_side = (env_int("SCC_RW_STREAMS", 1) != 0 && ds->nnz > (64ll << 20)) ? 2 : 0;
+            HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0, c->sw, rs_side, c->ev_wfork, c->ev_wj));
         }
         // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS
         // items; SCC_ITEMS_SERIAL=1 runs them after the waves on one stream)
@@ -1008,7 +1022,10 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             HIPCHK(c, hipStreamWaitEvent(s1, c->ev_fork, 0));
         }
         if (L.dbg == 7) scc_rank_mfma_stamps(s0, 0);
-        HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0));
+        // the slot classes on s0 and two side streams (SCC_RW_STREAMS=0: all on s0)
+        // (forked only when a second class launch exists: config B has one)
+        const int rw_side = (env_int("SCC_RW_STREAMS", 1) != 0 && L.dbg != 7) ? 2 : 0;
+        HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0, c->sw, rw_side, c->ev_wfork, c->ev_wj));
         if (L.dbg == 7) scc_rank_mfma_stamps(s0, 1);
         HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, si));
         HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, si));
@@ -1105,15 +1122,19 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         }
     } else if (stage == DE_FINISH_REC) {
         // pair-split selection (first_out): only this rank's pair rows are
-        // read, so only they are cleared and scattered (the flags, which size
-        // every pair's row offsets, are cleared in full)
+        // read, so only they are cleared and scattered.  FAST reads a cell's
+        // statistics only where its flag is set (k_pair_select), so of the
+        // range only the flags are cleared; SLOW clears every field of the
+        // range.  Outside the range the flags keep older contents: they only
+        // size the other pairs' row offsets (at most one row per cell, so the
+        // range's rows stay inside the row buffers) and no row there is read.
         const bool pb = rio->first_out != nullptr;
         const int plo = pb ? rio->pair_lo : 0, phi = pb ? rio->pair_hi : P;
         for (const Field& f : fields) {
             if (!f.p) continue;
-            if (f.p == (void*)d_flags || !pb)
+            if (!pb)
                 HIPCHK(c, hipMemsetAsync(f.p, 0, PG * f.es, s0));
-            else if (phi > plo)
+            else if (phi > plo && (f.p == (void*)d_flags || !fast))
                 HIPCHK(c, hipMemsetAsync((char*)f.p + (size_t)plo * G * f.es, 0, (size_t)(phi - plo) * G * f.es, s0));
         }
         HIPCHK(c, hipMemsetAsync(d_err, 0, sizeof(int) * 4, s0));
