@@ -135,18 +135,16 @@ k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
                     ke = wave_lower_bound(rows, kb, e, chi);
                 }
             } else if (!DENSE && rng) {
-                if (tbnd) {  // the dataset's tile starts: two loads, and the run's tile boundaries copied
+                if (tbnd) {  // the dataset's tile starts: two loads (the scatter reads the cache itself)
                     const i64* tb = tbnd + (size_t)c * (ntile + 1);
                     kb = tb[t0r];
                     ke = tb[t1r];
-                    if (a >= 0)
-                        for (int t = t0r + lane; t <= t1r; t += 64) bp[t] = tb[t];
                 } else {
                     kb = wave_lower_bound(rows, b, e, t0r * gt);
                     ke = wave_lower_bound(rows, kb, e, t1r * gt);
                 }
             }
-            const bool tiles_known = rng && tbnd != nullptr;
+            const bool tiles_known = tbnd != nullptr;  // (rng or ro: the dataset's cache, read by the scatter)
             for (i64 k0 = kb; k0 < ke; k0 += 4 * 64) {  // four loads in flight per lane
                 double xs[4];
                 int gs[4], gps[4];
@@ -225,6 +223,63 @@ k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
     if (bad) atomicOr(err, bad);
 }
 
+// The counting pass of a validated, zero-free dataset over all genes (FAST):
+// row indices only (4 of the 12 bytes per stored value), the cells' tile
+// starts from the dataset's cache (the scatter reads them there), nodg from
+// the dataset's cache -- so only the counts remain: no value, boundary or
+// check logic (k_ing_hist's 81 registers left one workgroup per CU; this one
+// runs two).  Same histogram layout and count rows as k_ing_hist.
+__global__ void __launch_bounds__(IH_T) k_ing_count_ro(const i64* __restrict__ indptr, const int* __restrict__ rows,
+                                                       int G, const int* __restrict__ perm,
+                                                       const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
+                                                       int hw, u32* __restrict__ cnt)
+{
+    extern __shared__ __attribute__((aligned(16))) u32 hist[];
+    const int lane = threadIdx.x & 63, wv = scc_wave_id();
+    const int ch = blockIdx.x;
+    if (cc_code[ch] < 0) return;  // unkept cells: nothing to count (block-uniform)
+    const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
+    for (int wlo = 0; wlo < G; wlo += hw) {
+        const int whi = min(G, wlo + hw);
+        const u32 nwq = (u32)(whi - wlo + 3) >> 2;
+        const u64 mq = ((1ull << 40) + nwq - 1) / nwq;
+        for (u32 q = threadIdx.x; q < nwq; q += IH_T) hist[q] = 0;
+        __syncthreads();
+        for (int p = p0 + wv; p < p1; p += IH_T / 64) {
+            const int c = perm[p];
+            i64 kb = indptr[c], ke = indptr[c + 1];
+            if (wlo > 0 || whi < G) {
+                kb = wave_lower_bound(rows, kb, ke, wlo);
+                ke = wave_lower_bound(rows, kb, ke, whi);
+            }
+            for (i64 k0 = kb; k0 < ke; k0 += 4 * 64) {
+                int gs[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {  // clamped unconditional loads, all in flight
+                    const i64 k = k0 + u * 64 + lane;
+                    gs[u] = rows[k < ke ? k : ke - 1];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (k0 + u * 64 + lane < ke) {
+                        const u32 l = (u32)(gs[u] - wlo);
+                        const u32 q = (u32)(((u64)l * mq) >> 40);
+                        atomicAdd(&hist[l - q * nwq], 1u << (8 * q));
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        u32* row = cnt + (size_t)ch * G;
+        for (int g = wlo + threadIdx.x; g < whi; g += IH_T) {
+            const u32 l = (u32)(g - wlo);
+            const u32 q = (u32)(((u64)l * mq) >> 40);
+            row[g] = (hist[l - q * nwq] >> (8 * q)) & 0xFFu;
+        }
+        __syncthreads();
+    }
+}
+
 // per gene: exclusive prefix over the count chunks (in place); rows >= nc_kept
 // (unkept cells) hold the total.  Three passes over [segment of CS_SEG
 // chunks] x [256 genes] blocks so the whole chip works on it.
@@ -296,8 +351,9 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
                                                        const int* __restrict__ perm, const int* __restrict__ cc_p0,
                                                        const int* __restrict__ sc_cc0, const u32* __restrict__ cnt,
                                                        const i64* __restrict__ gstart, const i64* __restrict__ bnd,
-                                                       int ntile, int cap, int glo, int ghi, int t0, int nsc, int ntl,
-                                                       int run, u64* __restrict__ keys)
+                                                       const i64* __restrict__ tbnd, int ntile, int cap, int glo,
+                                                       int ghi, int t0, int nsc, int ntl, int run,
+                                                       u64* __restrict__ keys)
 {
     __shared__ u32 loff[SC_GT + 1];
     __shared__ u32 cur[SC_GT];
@@ -335,7 +391,8 @@ __global__ void __launch_bounds__(ING_T) k_ing_scatter(const i64* __restrict__ i
         } else {
             // clamp: bnd is only trustworthy when the hist pass saw sorted
             // rows (err bit 4 otherwise); reads must stay in bounds anyway
-            const i64* bp = bnd + (size_t)(p0 + tid) * (ntile + 1);
+            // (the run's boundaries by cell order, or the dataset's cache by cell)
+            const i64* bp = tbnd ? tbnd + (size_t)c * (ntile + 1) : bnd + (size_t)(p0 + tid) * (ntile + 1);
             const i64 cb = indptr[c], ce = indptr[c + 1];
             kb = min(max(bp[t], cb), ce);
             ke = min(max(bp[t + 1], kb), ce);
@@ -660,6 +717,16 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
     return hipGetLastError();
 }
 
+extern "C" hipError_t scc_launch_ingest_count_ro(const i64* indptr, const int* rows, int G, const int* perm,
+                                                 const int* cc_p0, const int* cc_code, int nc, u32* cnt, hipStream_t st)
+{
+    const int hw = scc_ingest_hist_window(G);
+    const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
+    hipFuncSetAttribute((const void*)k_ing_count_ro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_ing_count_ro, dim3(nc), dim3(IH_T), lds, st, indptr, rows, G, perm, cc_p0, cc_code, hw, cnt);
+    return hipGetLastError();
+}
+
 extern "C" int scc_ingest_colscan_scratch(int nc, int G) { return ((nc + 1 + CS_SEG - 1) / CS_SEG + 1) * G; }
 
 // genes [g0, g1) of the count rows (a gene shard's tiles in range mode,
@@ -693,8 +760,8 @@ extern "C" void scc_ingest_count_range(int G, int glo, int ghi, int* g0, int* g1
 extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* rows, const double* vals,
                                                 const double* dense, int G, const int* perm, const int* cc_p0,
                                                 const int* sc_cc0, int ns, const u32* cnt, const i64* gstart,
-                                                const i64* bnd, int ntile, int glo, int ghi, u64* keys,
-                                                hipStream_t st)
+                                                const i64* bnd, const i64* tbnd, int ntile, int glo, int ghi,
+                                                u64* keys, hipStream_t st)
 {
     if (ns <= 0 || ghi <= glo) return hipSuccess;
     const int t0 = glo / SC_GT, t1 = (ghi + SC_GT - 1) / SC_GT;  // the gene tiles of [glo, ghi)
@@ -720,16 +787,16 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
     hipFuncSetAttribute((const void*)k_ing_scatter<false, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (dense)
         hipLaunchKernelGGL((k_ing_scatter<true, 4>), grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm,
-                           cc_p0, sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
+                           cc_p0, sc_cc0, cnt, gstart, bnd, nullptr, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     else if (unroll == 16)
         hipLaunchKernelGGL((k_ing_scatter<false, 16>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
+                           sc_cc0, cnt, gstart, bnd, tbnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     else if (unroll == 8)
         hipLaunchKernelGGL((k_ing_scatter<false, 8>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
+                           sc_cc0, cnt, gstart, bnd, tbnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     else
         hipLaunchKernelGGL((k_ing_scatter<false, 4>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
+                           sc_cc0, cnt, gstart, bnd, tbnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     return hipGetLastError();
 }
 

@@ -225,7 +225,12 @@ void scc_ingest_count_range(int G, int glo, int ghi, int* g0, int* g1);
 hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, const double* vals,
                                      const double* dense, int G, const int* perm, const int* cc_p0, const int* sc_cc0,
                                      int ns, const uint32_t* cnt, const long long* gstart, const long long* bnd,
-                                     int ntile, int glo, int ghi, unsigned long long* keys, hipStream_t st);
+                                     const long long* tbnd, int ntile, int glo, int ghi, unsigned long long* keys,
+                                     hipStream_t st);
+// the counting pass of a validated zero-free dataset over all genes (FAST; the
+// tile starts come from the dataset's cache, nodg from its cache)
+hipError_t scc_launch_ingest_count_ro(const long long* indptr, const int* rows, int G, const int* perm,
+                                      const int* cc_p0, const int* cc_code, int nc, uint32_t* cnt, hipStream_t st);
 hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
                            long long* total, hipStream_t st);
 int scc_scan_scratch_blocks(long long n);

@@ -768,7 +768,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_de_clear(d_err, d_counts, ttest ? nullptr : d_acc, (long long)acc_n, d_first, (int)G, glo,
                                       ghi, s0));
         de_cleared = true;
-        if (hist_rng && !ds->d_tbnd) {  // once per dataset: every cell's gene-tile starts
+        if ((hist_rng || hist_ro) && !ds->d_tbnd) {  // once per dataset: every cell's gene-tile starts
             if (hipMalloc((void**)&ds->d_tbnd, sizeof(long long) * (size_t)N * (ntile + 1)) != hipSuccess) {
                 (void)hipGetLastError();
                 ds->d_tbnd = nullptr;
@@ -776,10 +776,14 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
                 HIPCHK(c, scc_launch_tile_bounds(ds->d_indptr, ds->d_rows, N, gt, ntile, ds->d_tbnd, s0));
             }
         }
-        HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
-                                         d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
-                                         hist_rng ? 1 : (hist_ro ? 2 : 0), hist_rng ? ds->d_tbnd : nullptr, d_err,
-                                         s0));
+        // (the tile-start cache: the scatter reads it instead of the run's bnd)
+        const long long* tbnd = (hist_rng || hist_ro) ? ds->d_tbnd : nullptr;
+        if (hist_ro && tbnd && env_int("SCC_COUNT_RO", 1) != 0)
+            HIPCHK(c, scc_launch_ingest_count_ro(ds->d_indptr, ds->d_rows, G, d_perm, d_ccp0, d_cccode, nc, d_cnt, s0));
+        else
+            HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
+                                             d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
+                                             hist_rng ? 1 : (hist_ro ? 2 : 0), tbnd, d_err, s0));
         if (hist_rng || hist_ro)
             HIPCHK(c, hipMemcpyAsync(d_nodg, ds->d_nodg, sizeof(int) * N, hipMemcpyDeviceToDevice, s0));
         uint32_t* d_cscr;
@@ -795,7 +799,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         const uint32_t* d_total = d_cnt + (size_t)nc * G;
         HIPCHK(c, scc_launch_scan(d_total, G, d_gstart, d_scan, d_gstart + G, s0));
         HIPCHK(c, scc_launch_ingest_scatter(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
-                                            d_sccc0, ns, d_cnt, d_gstart, d_bnd, ntile, glo, ghi, d_keys, s0));
+                                            d_sccc0, ns, d_cnt, d_gstart, d_bnd, tbnd, ntile, glo, ghi, d_keys, s0));
         if (!fast) HIPCHK(c, scc_launch_reduce_dd(d_wexp, nwaves, d_gexp, s0));
     }
     {
