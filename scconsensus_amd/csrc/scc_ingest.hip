@@ -229,26 +229,42 @@ k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
 // the dataset's cache -- so only the counts remain: no value, boundary or
 // check logic (k_ing_hist's 81 registers left one workgroup per CU; this one
 // runs two).  Same histogram layout and count rows as k_ing_hist.
+// A gene shard [glo, ghi) (rng) counts the genes of its range over its gene
+// tiles [gb, ge) (count rows zero elsewhere in them, as k_ing_hist), each
+// cell's entries of those tiles found from the tile-start cache tbnd.
 __global__ void __launch_bounds__(IH_T) k_ing_count_ro(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                        int G, const int* __restrict__ perm,
                                                        const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
-                                                       int hw, u32* __restrict__ cnt)
+                                                       int hw, int glo, int ghi, int gt, int ntile,
+                                                       const i64* __restrict__ tbnd, u32* __restrict__ cnt)
 {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int ch = blockIdx.x;
     if (cc_code[ch] < 0) return;  // unkept cells: nothing to count (block-uniform)
     const int p0 = cc_p0[ch], p1 = cc_p0[ch + 1];
-    for (int wlo = 0; wlo < G; wlo += hw) {
-        const int whi = min(G, wlo + hw);
+    const bool rng = glo > 0 || ghi < G;
+    const int t0r = glo / gt, t1r = min(ntile, (ghi + gt - 1) / gt);
+    const int gb = rng ? t0r * gt : 0, ge = rng ? min(G, t1r * gt) : G;
+    for (int wlo = gb; wlo < ge; wlo += hw) {
+        const int whi = min(ge, wlo + hw);
+        const int clo = max(glo, wlo), chi = min(ghi, whi);  // genes this pass counts
         const u32 nwq = (u32)(whi - wlo + 3) >> 2;
         const u64 mq = ((1ull << 40) + nwq - 1) / nwq;
         for (u32 q = threadIdx.x; q < nwq; q += IH_T) hist[q] = 0;
         __syncthreads();
         for (int p = p0 + wv; p < p1; p += IH_T / 64) {
             const int c = perm[p];
-            i64 kb = indptr[c], ke = indptr[c + 1];
-            if (wlo > 0 || whi < G) {
+            i64 kb, ke;
+            if (rng) {
+                const i64* tb = tbnd + (size_t)c * (ntile + 1);
+                kb = tb[t0r];
+                ke = tb[t1r];
+            } else {
+                kb = indptr[c];
+                ke = indptr[c + 1];
+            }
+            if (wlo > gb || whi < ge) {
                 kb = wave_lower_bound(rows, kb, ke, wlo);
                 ke = wave_lower_bound(rows, kb, ke, whi);
             }
@@ -261,7 +277,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_count_ro(const i64* __restrict__ i
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    if (k0 + u * 64 + lane < ke) {
+                    if (k0 + u * 64 + lane < ke && gs[u] >= clo && gs[u] < chi) {
                         const u32 l = (u32)(gs[u] - wlo);
                         const u32 q = (u32)(((u64)l * mq) >> 40);
                         atomicAdd(&hist[l - q * nwq], 1u << (8 * q));
@@ -274,7 +290,7 @@ __global__ void __launch_bounds__(IH_T) k_ing_count_ro(const i64* __restrict__ i
         for (int g = wlo + threadIdx.x; g < whi; g += IH_T) {
             const u32 l = (u32)(g - wlo);
             const u32 q = (u32)(((u64)l * mq) >> 40);
-            row[g] = (hist[l - q * nwq] >> (8 * q)) & 0xFFu;
+            row[g] = (hist[l - q * nwq] >> (8 * q)) & 0xFFu;  // genes outside [glo, ghi) count 0
         }
         __syncthreads();
     }
@@ -295,18 +311,28 @@ __global__ void __launch_bounds__(256) k_ing_colsum(const u32* __restrict__ cnt,
     part[(size_t)blockIdx.x * G + g] = s;
 }
 
+// one wave per gene, 64 segments a step (a thread per gene walked the
+// segments one dependent load at a time: 48 us for a gene shard of config D's
+// 195 segments)
 __global__ void __launch_bounds__(256) k_ing_segscan(u32* __restrict__ part, int nseg, int G, int gb, int ge,
                                                      u32* __restrict__ total)
 {
-    const int g = gb + blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int g = gb + blockIdx.x * 4 + scc_wave_id();
     if (g >= ge) return;
     u32 run = 0;
-    for (int q = 0; q < nseg; ++q) {
-        const u32 v = part[(size_t)q * G + g];
-        part[(size_t)q * G + g] = run;
-        run += v;
+    for (int q0 = 0; q0 < nseg; q0 += 64) {
+        const int q = q0 + lane;
+        const u32 v = q < nseg ? part[(size_t)q * G + g] : 0u;
+        u32 inc = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (q < nseg) part[(size_t)q * G + g] = run + inc - v;
+        run += __shfl(inc, 63, 64);
     }
-    total[g] = run;
+    if (lane == 0) total[g] = run;
 }
 
 __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int nc, int nc_kept, int G, int gb,
@@ -718,12 +744,16 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
 }
 
 extern "C" hipError_t scc_launch_ingest_count_ro(const i64* indptr, const int* rows, int G, const int* perm,
-                                                 const int* cc_p0, const int* cc_code, int nc, u32* cnt, hipStream_t st)
+                                                 const int* cc_p0, const int* cc_code, int nc, int glo, int ghi,
+                                                 const i64* tbnd, u32* cnt, hipStream_t st)
 {
+    if ((glo > 0 || ghi < G) && !tbnd) return hipErrorInvalidValue;
     const int hw = scc_ingest_hist_window(G);
     const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
+    const int ntile = (G + SC_GT - 1) / SC_GT;
     hipFuncSetAttribute((const void*)k_ing_count_ro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_ing_count_ro, dim3(nc), dim3(IH_T), lds, st, indptr, rows, G, perm, cc_p0, cc_code, hw, cnt);
+    hipLaunchKernelGGL(k_ing_count_ro, dim3(nc), dim3(IH_T), lds, st, indptr, rows, G, perm, cc_p0, cc_code, hw, glo,
+                       ghi, SC_GT, ntile, tbnd, cnt);
     return hipGetLastError();
 }
 
@@ -742,7 +772,7 @@ extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, i
     const int gbk = (g1 - g0 + 255) / 256;
     if (nseg_k > 0)
         hipLaunchKernelGGL(k_ing_colsum, dim3(nseg_k, gbk), dim3(256), 0, st, cnt, nc_kept, G, g0, g1, part);
-    hipLaunchKernelGGL(k_ing_segscan, dim3(gbk), dim3(256), 0, st, part, nseg_k, G, g0, g1, total);
+    hipLaunchKernelGGL(k_ing_segscan, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, part, nseg_k, G, g0, g1, total);
     hipLaunchKernelGGL(k_ing_colapply, dim3(nseg_all, gbk), dim3(256), 0, st, cnt, nc, nc_kept, G, g0, g1, part,
                        total);
     return hipGetLastError();

@@ -229,8 +229,10 @@ hipError_t scc_launch_ingest_scatter(const long long* indptr, const int* rows, c
                                      hipStream_t st);
 // the counting pass of a validated zero-free dataset over all genes (FAST; the
 // tile starts come from the dataset's cache, nodg from its cache)
+// (a gene shard [glo, ghi) of a validated dataset too: its tiles' entries from tbnd)
 hipError_t scc_launch_ingest_count_ro(const long long* indptr, const int* rows, int G, const int* perm,
-                                      const int* cc_p0, const int* cc_code, int nc, uint32_t* cnt, hipStream_t st);
+                                      const int* cc_p0, const int* cc_code, int nc, int glo, int ghi,
+                                      const long long* tbnd, uint32_t* cnt, hipStream_t st);
 hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
                            long long* total, hipStream_t st);
 int scc_scan_scratch_blocks(long long n);

@@ -778,8 +778,9 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         }
         // (the tile-start cache: the scatter reads it instead of the run's bnd)
         const long long* tbnd = (hist_rng || hist_ro) ? ds->d_tbnd : nullptr;
-        if (hist_ro && tbnd && env_int("SCC_COUNT_RO", 1) != 0)
-            HIPCHK(c, scc_launch_ingest_count_ro(ds->d_indptr, ds->d_rows, G, d_perm, d_ccp0, d_cccode, nc, d_cnt, s0));
+        if ((hist_ro || (hist_rng && ds->no_zeros)) && tbnd && env_int("SCC_COUNT_RO", 1) != 0)
+            HIPCHK(c, scc_launch_ingest_count_ro(ds->d_indptr, ds->d_rows, G, d_perm, d_ccp0, d_cccode, nc,
+                                                 hist_rng ? glo : 0, hist_rng ? ghi : G, tbnd, d_cnt, s0));
         else
             HIPCHK(c, scc_launch_ingest_hist(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, d_perm, d_ccp0,
                                              d_cccode, nc, ntile, d_cnt, d_bnd, d_nodg, d_wexp, fast ? 0 : 1, glo, ghi,
