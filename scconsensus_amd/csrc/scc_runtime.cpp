@@ -580,6 +580,14 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         for (int i = 0; i < N; ++i) perm[code[i] >= 0 ? fill[code[i]]++ : u++] = i;
     }
     std::vector<int> cc_p0, cc_code, sc_cc0, cl_cc(K + 1);
+    // scatter chunks of 2 count chunks (64 cells) when a cell has >= 16 stored
+    // values per gene tile (config B / D: ~29; ingest B 0.45 -> 0.40 ms, D 5.97
+    // -> 5.79), else 4 (config E: ~8 per tile, where 64-cell chunks left the
+    // workgroups too little work: 12.7 -> 16.5 ms); SCC_SC_CC overrides
+    const int64_t ntile_h = (ds->G + scc_ingest_gene_tile() - 1) / scc_ingest_gene_tile();
+    const bool dense_tiles = ds->nnz >= 16 * (int64_t)std::max(1, N) * std::max<int64_t>(1, ntile_h);
+    const int scatter_cc =
+        std::min(kScatterCC, std::max(1, env_int("SCC_SC_CC", dense_tiles ? kScatterCC / 2 : kScatterCC)));
     for (int a = 0; a < K; ++a) {
         cl_cc[a] = (int)cc_code.size();
         for (int p = start[a]; p < start[a + 1]; p += kCountChunk) {
@@ -590,7 +598,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     const int nc_kept = (int)cc_code.size();
     cl_cc[K] = nc_kept;
     for (int a = 0; a < K; ++a)
-        for (int q = cl_cc[a]; q < cl_cc[a + 1]; q += kScatterCC) sc_cc0.push_back(q);
+        for (int q = cl_cc[a]; q < cl_cc[a + 1]; q += scatter_cc) sc_cc0.push_back(q);
     const int ns = (int)sc_cc0.size();
     sc_cc0.push_back(nc_kept);
     for (int p = nkept; p < N; p += kCountChunk) {
