@@ -311,28 +311,37 @@ __global__ void __launch_bounds__(256) k_ing_colsum(const u32* __restrict__ cnt,
     part[(size_t)blockIdx.x * G + g] = s;
 }
 
-// one wave per gene, 64 segments a step (a thread per gene walked the
-// segments one dependent load at a time: 48 us for a gene shard of config D's
-// 195 segments)
-__global__ void __launch_bounds__(256) k_ing_segscan(u32* __restrict__ part, int nseg, int G, int gb, int ge,
-                                                     u32* __restrict__ total)
+// 64 genes per workgroup (a lane per gene: coalesced rows), the segments cut
+// into 16 runs, one per wave: each wave sums its run, the waves' sums are
+// scanned in LDS, and each wave rewrites its run from its offset.  (A thread
+// per gene walking every segment was a chain of nseg dependent loads: 48 us
+// for a gene shard of config D; a wave per gene broke the chain but read each
+// line for one 4-byte value, 15x the part array at config E.)
+#define SS_T 1024
+__global__ void __launch_bounds__(SS_T) k_ing_segscan(u32* __restrict__ part, int nseg, int G, int gb, int ge,
+                                                      u32* __restrict__ total)
 {
-    const int lane = threadIdx.x & 63;
-    const int g = gb + blockIdx.x * 4 + scc_wave_id();
-    if (g >= ge) return;
+    __shared__ u32 ws[SS_T / 64][64];
+    const int lane = threadIdx.x & 63, w = scc_wave_id();
+    const int g = gb + blockIdx.x * 64 + lane;
+    const bool ok = g < ge;
+    const int per = (nseg + SS_T / 64 - 1) / (SS_T / 64);
+    const int q0 = min(nseg, w * per), q1 = min(nseg, q0 + per);
+    u32 s = 0;
+    if (ok)
+        for (int q = q0; q < q1; ++q) s += part[(size_t)q * G + g];
+    ws[w][lane] = s;
+    __syncthreads();
     u32 run = 0;
-    for (int q0 = 0; q0 < nseg; q0 += 64) {
-        const int q = q0 + lane;
-        const u32 v = q < nseg ? part[(size_t)q * G + g] : 0u;
-        u32 inc = v;
-        for (int o = 1; o < 64; o <<= 1) {
-            const u32 y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
+    for (int v = 0; v < w; ++v) run += ws[v][lane];
+    if (ok) {
+        for (int q = q0; q < q1; ++q) {
+            const u32 v = part[(size_t)q * G + g];
+            part[(size_t)q * G + g] = run;
+            run += v;
         }
-        if (q < nseg) part[(size_t)q * G + g] = run + inc - v;
-        run += __shfl(inc, 63, 64);
+        if (w == SS_T / 64 - 1) total[g] = run;
     }
-    if (lane == 0) total[g] = run;
 }
 
 __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int nc, int nc_kept, int G, int gb,
@@ -772,7 +781,7 @@ extern "C" hipError_t scc_launch_ingest_colscan(u32* cnt, int nc, int nc_kept, i
     const int gbk = (g1 - g0 + 255) / 256;
     if (nseg_k > 0)
         hipLaunchKernelGGL(k_ing_colsum, dim3(nseg_k, gbk), dim3(256), 0, st, cnt, nc_kept, G, g0, g1, part);
-    hipLaunchKernelGGL(k_ing_segscan, dim3((g1 - g0 + 3) / 4), dim3(256), 0, st, part, nseg_k, G, g0, g1, total);
+    hipLaunchKernelGGL(k_ing_segscan, dim3((g1 - g0 + 63) / 64), dim3(SS_T), 0, st, part, nseg_k, G, g0, g1, total);
     hipLaunchKernelGGL(k_ing_colapply, dim3(nseg_all, gbk), dim3(256), 0, st, cnt, nc, nc_kept, G, g0, g1, part,
                        total);
     return hipGetLastError();
