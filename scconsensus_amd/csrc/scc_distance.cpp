@@ -27,6 +27,7 @@ hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nc
                              hipStream_t st);
 hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C, const double* mean,
                            int nval, hipStream_t st);
+
 int scc_gram_tile_width(int ld);
 hipError_t scc_launch_scores(const double* Xc, int N, int nu, int ld, const double* Z16, int k, double* P,
                              const double* mean,
@@ -42,6 +43,17 @@ hipError_t scc_launch_d2h(const void* src, void* dst, size_t n, hipStream_t st);
 }
 
 extern "C" void scc_distance_release(scc_ctx*) {}
+
+// cell chunks of the split-K Gram (slabs reduced in a fixed order); SCC_GRAM_CHUNKS overrides
+static int gram_chunks(int npad)
+{
+    static const int forced = [] {
+        const char* e = getenv("SCC_GRAM_CHUNKS");
+        return (e && *e) ? atoi(e) : 0;
+    }();
+    const int cap = forced > 0 ? std::min(forced, 64) : 32;
+    return std::max(1, std::min(cap, npad / 512));
+}
 
 namespace {
 
@@ -332,7 +344,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     if (metric == SCC_DIST_PCA_EUCLID) {
         double *d_slabs, *d_C, *d_W, *d_Z, *d_P, *d_escr;
         const bool fused = env_int("SCC_CENTER_FUSED", 1) != 0 && scc_gram_tile_width(ld) == 64;
-        const int nchunk = std::max(1, std::min(32, Npad / 512));
+        const int nchunk = gram_chunks(Npad);
         WS("d_slabs", (size_t)nchunk * ld * ld, d_slabs);
         WS("d_C", (size_t)ld * ld, d_C);
         WS("d_W", ld, d_W);
@@ -613,7 +625,7 @@ extern "C" int scc_pca_shard_gram(scc_ctx* c, const void* parts, int32_t world, 
     double *d_X, *d_mean, *d_slabs, *d_C;
     if ((rc = ws(c, "d_X", (size_t)npad * ld, &d_X))) return rc;
     if ((rc = ws(c, "d_mean", ld, &d_mean))) return rc;
-    const int nchunk = std::max(1, std::min(32, npad / 512));
+    const int nchunk = gram_chunks(npad);
     if ((rc = ws(c, "d_slabs", (size_t)nchunk * ld * ld, &d_slabs))) return rc;
     if ((rc = ws(c, "d_C", (size_t)ld * ld, &d_C))) return rc;
     {
