@@ -76,9 +76,8 @@ __device__ inline i64 wave_lower_bound(const int* __restrict__ rows, i64 lo, i64
 // `hw` genes: the first pass reads every entry (nodg, expm1, input checks,
 // tile boundaries, counts of window 0), later passes read each cell's entries
 // of their window only (two wave-parallel binary searches; dense: the range).
-template <bool DENSE, int MINB>
-__global__ void __launch_bounds__(IH_T) __attribute__((amdgpu_waves_per_eu(MINB * IH_T / 256)))
-k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
+template <bool DENSE>
+__global__ void __launch_bounds__(IH_T) k_ing_hist(const i64* __restrict__ indptr, const int* __restrict__ rows,
                                                     const double* __restrict__ vals, int G, const int* __restrict__ perm,
                                                     const int* __restrict__ cc_p0, const int* __restrict__ cc_code,
                                                     int gt, int ntile, u32* __restrict__ cnt, i64* __restrict__ bnd,
@@ -729,23 +728,14 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
 {
     const int hw = scc_ingest_hist_window(G);
     const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
-    static const int minb = [] {
-        const char* v = getenv("SCC_IH_MINB");
-        return (v && *v) ? atoi(v) : 1;
-    }();
     if (dense) {
-        hipFuncSetAttribute((const void*)k_ing_hist<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_ing_hist<true, 1>), dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm,
-                           cc_p0, cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw,
-                           nullptr, err);
-    } else if (minb == 2) {
-        hipFuncSetAttribute((const void*)k_ing_hist<false, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_ing_hist<false, 2>), dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, tbnd,
+        hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_ing_hist<true>), dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
+                           cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw, nullptr,
                            err);
     } else {
-        hipFuncSetAttribute((const void*)k_ing_hist<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((k_ing_hist<false, 1>), dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
+        hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_ing_hist<false>), dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
                            cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, tbnd,
                            err);
     }
@@ -816,23 +806,12 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
         return (v && *v) ? std::max(SC_GT, atoi(v)) : SC_CAP;
     }();
     const size_t lds = (size_t)cap * (8 + 2);
-    static const int unroll = [] {
-        const char* v = getenv("SCC_SC_U");
-        return (v && *v) ? atoi(v) : 4;
-    }();
+    // (4 loads in flight per lane: 8 and 16 measured slower at config B)
     hipFuncSetAttribute((const void*)k_ing_scatter<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipFuncSetAttribute((const void*)k_ing_scatter<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_ing_scatter<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_ing_scatter<false, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (dense)
         hipLaunchKernelGGL((k_ing_scatter<true, 4>), grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm,
                            cc_p0, sc_cc0, cnt, gstart, bnd, nullptr, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
-    else if (unroll == 16)
-        hipLaunchKernelGGL((k_ing_scatter<false, 16>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, tbnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
-    else if (unroll == 8)
-        hipLaunchKernelGGL((k_ing_scatter<false, 8>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
-                           sc_cc0, cnt, gstart, bnd, tbnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
     else
         hipLaunchKernelGGL((k_ing_scatter<false, 4>), grid, dim3(ING_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
                            sc_cc0, cnt, gstart, bnd, tbnd, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);
