@@ -81,30 +81,33 @@ __global__ void __launch_bounds__(256) k_gather_csc(const i64* __restrict__ indp
 }
 
 // The same gather with the union map in LDS (u16 slots, 0xffff = not in the
-// union): persistent workgroups load the map once and walk cells, so a row
-// index costs one LDS lookup instead of a dependent global load of umap[row]
-// (three dependent global round trips per batch of 512 entries become two).
-// Used when the map and four LDS rows fit (G * 2 + 4 * ld * 8 bytes).
+// union): persistent workgroups build the map from the union's gene list and
+// walk cells, so a row index costs one LDS lookup instead of a dependent global
+// load of umap[row] (three dependent global round trips per batch of 512
+// entries become two).  Rows [N, Npad) (padding) leave as zeros, so a call
+// needs no memset and no global union map before it (two launches and ~60 us
+// of GPU idle at config B).  Used when the map and four LDS rows fit (G * 2 +
+// 4 * ld * 8 bytes).
 __global__ void __launch_bounds__(1024) k_gather_csc_lm(const i64* __restrict__ indptr, const int* __restrict__ rows,
-                                                       const double* __restrict__ vals, int N, int G,
-                                                       const int* __restrict__ umap, int ld, double* __restrict__ Xc)
+                                                       const double* __restrict__ vals, int N, int Npad, int G,
+                                                       const int* __restrict__ genes, int nu, int ld,
+                                                       double* __restrict__ Xc)
 {
     extern __shared__ __attribute__((aligned(16))) double grow[];  // [waves][ld], then the map
     const int nw = blockDim.x >> 6;
     unsigned short* lmap = (unsigned short*)(grow + nw * (size_t)ld);
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-        const int u = umap[g];
-        lmap[g] = (unsigned short)(u >= 0 ? u : 0xffff);
-    }
+    for (int g = threadIdx.x; g < G; g += blockDim.x) lmap[g] = 0xffff;
+    __syncthreads();
+    for (int u = threadIdx.x; u < nu; u += blockDim.x) lmap[genes[u]] = (unsigned short)u;  // genes checked by the host
     __syncthreads();
     double* row = grow + (size_t)wv * ld;
-    for (int c = blockIdx.x * nw + wv; c < N; c += gridDim.x * nw) {
+    for (int c = blockIdx.x * nw + wv; c < Npad; c += gridDim.x * nw) {
         for (int u = lane; u < ld; u += 64) row[u] = 0.0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const i64 b = indptr[c], e = indptr[c + 1];
+        const i64 b = c < N ? indptr[c] : 0, e = c < N ? indptr[c + 1] : 0;
         for (i64 k0 = b + lane; k0 < e; k0 += 512) {
             int r[8];
 #pragma unroll
@@ -991,14 +994,27 @@ extern "C" hipError_t scc_launch_union_map(int* umap, int G, const int* genes, i
     return hipGetLastError();
 }
 
+// X[U, ] of cells [0, N) into Xc rows [0, N), rows [N, Npad) zero: the union
+// map and the padding clear included (the LDS-map kernel builds its own map
+// and writes the padding rows; the other forms get a global map and a memset)
 extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, const double* vals, const double* dense,
-                                        int G, int N, const int* umap, const int* genes, int nu, int ld, double* Xc,
-                                        hipStream_t st)
+                                        int G, int N, int Npad, int* umap, const int* genes, int nu, int ld,
+                                        double* Xc, hipStream_t st)
 {
+    const bool lm = !dense && ld <= GATHER_LDS_LD && sizeof(double) * 4 * (size_t)ld + 2 * (size_t)G <= 120 * 1024 &&
+                    !(getenv("SCC_GATHER_LM") && atoi(getenv("SCC_GATHER_LM")) == 0);
+    if (!lm) {
+        // the CSC gathers write whole rows when they stage them in LDS: only the padding then
+        const size_t r0 = (dense || ld > GATHER_LDS_LD) ? 0 : (size_t)N;
+        hipError_t e = hipSuccess;
+        if ((size_t)Npad > r0) e = hipMemsetAsync(Xc + r0 * ld, 0, sizeof(double) * ((size_t)Npad - r0) * ld, st);
+        if (e == hipSuccess && !dense) e = scc_launch_union_map(umap, G, genes, nu, st);
+        if (e != hipSuccess) return e;
+    }
+    if (N <= 0 && !lm) return hipSuccess;
     if (dense)
         hipLaunchKernelGGL(k_gather_dense, dim3(2048), dim3(256), 0, st, dense, G, N, genes, nu, ld, Xc);
-    else if (ld <= GATHER_LDS_LD && sizeof(double) * 4 * (size_t)ld + 2 * (size_t)G <= 120 * 1024 &&
-             !(getenv("SCC_GATHER_LM") && atoi(getenv("SCC_GATHER_LM")) == 0)) {
+    else if (lm) {
         // waves per workgroup (4, 8 or 16 rows in LDS beside one copy of the
         // map): the most resident waves per CU (a wave per cell is latency
         // bound: indptr, then rows, then the hits' values), the fewer waves on a tie
@@ -1015,8 +1031,9 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
         const size_t lds = sizeof(double) * W * (size_t)ld + mapb;
         const int wgs = std::max(1, std::min((int)(cu_lds / lds), 32 / W));
         hipFuncSetAttribute((const void*)k_gather_csc_lm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        const int grid = std::max(1, std::min((N + W - 1) / W, wgs * cus));
-        hipLaunchKernelGGL(k_gather_csc_lm, dim3(grid), dim3(64 * W), lds, st, indptr, rows, vals, N, G, umap, ld, Xc);
+        const int grid = std::max(1, std::min((Npad + W - 1) / W, wgs * cus));
+        hipLaunchKernelGGL(k_gather_csc_lm, dim3(grid), dim3(64 * W), lds, st, indptr, rows, vals, N, Npad, G, genes, nu,
+                           ld, Xc);
     } else if (ld <= GATHER_LDS_LD)
         hipLaunchKernelGGL(k_gather_csc<true>, dim3((N + 3) / 4), dim3(256), sizeof(double) * 4 * (size_t)ld, st,
                            indptr, rows, vals, N, G, umap, ld, Xc);

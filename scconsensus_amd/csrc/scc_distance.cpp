@@ -21,7 +21,7 @@ extern "C" {
 hipError_t scc_launch_union_map(int* umap, int G, const int* genes, int nu, hipStream_t st);
 int scc_gather_writes_rows(int ld);
 hipError_t scc_launch_gather(const long long* indptr, const int* rows, const double* vals, const double* dense,
-                             int G, int N, const int* umap, const int* genes, int nu, int ld, double* Xc,
+                             int G, int N, int Npad, int* umap, const int* genes, int nu, int ld, double* Xc,
                              hipStream_t st);
 hipError_t scc_launch_center(double* Xc, int N, int nu, int ld, dd* part, int nchunk, double* mean, int apply,
                              hipStream_t st);
@@ -333,12 +333,9 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
         return rc;
     {
         Scope sc(c, "gather", s0);
-        // the CSC gather writes whole rows (zeros included): only the padding rows need clearing
-        const size_t r0 = (ds->dense || !scc_gather_writes_rows(ld)) ? 0 : (size_t)N;
-        if ((size_t)Npad > r0) HIPCHK(c, hipMemsetAsync(d_X + r0 * ld, 0, sizeof(double) * ((size_t)Npad - r0) * ld, s0));
-        HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
-        HIPCHK(c, scc_launch_gather(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, N, d_umap, d_genes, nu, ld,
-                                    d_X, s0));
+        // (the union map and the padding rows' clear included)
+        HIPCHK(c, scc_launch_gather(ds->d_indptr, ds->d_rows, ds->d_vals, ds->d_dense, G, N, Npad, d_umap, d_genes, nu,
+                                    ld, d_X, s0));
     }
     unsigned int* d_eig_err = nullptr;  // the hand-off's time-out flag, read back after the last launch
     if (metric == SCC_DIST_PCA_EUCLID) {
@@ -590,13 +587,9 @@ extern "C" int scc_pca_shard_colsum(scc_ctx* c, const scc_dataset* ds, const int
     if ((rc = genes_h2d(c, d_genes, genes, nu, s0))) return rc;
     {
         Scope sc(c, "gather", s0);
-        const size_t r0 = (ds->dense || !scc_gather_writes_rows(ld)) ? 0 : (size_t)n;  // CSC: whole rows written
-        HIPCHK(c, hipMemsetAsync(d_X + r0 * ld, 0, sizeof(double) * ((size_t)npad - r0) * ld, s0));
-        HIPCHK(c, scc_launch_union_map(d_umap, G, d_genes, nu, s0));
-        if (n > 0)
-            HIPCHK(c, scc_launch_gather(ds->dense ? nullptr : ds->d_indptr + cell_lo, ds->d_rows, ds->d_vals,
-                                        ds->dense ? ds->d_dense + (size_t)cell_lo * G : nullptr, G, n, d_umap, d_genes,
-                                        nu, ld, d_X, s0));
+        HIPCHK(c, scc_launch_gather(ds->dense ? nullptr : ds->d_indptr + cell_lo, ds->d_rows, ds->d_vals,
+                                    ds->dense ? ds->d_dense + (size_t)cell_lo * G : nullptr, G, n, npad, d_umap,
+                                    d_genes, nu, ld, d_X, s0));
     }
     {
         Scope sc(c, "center", s0);
