@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <atomic>
+#include <map>
+#include <mutex>
+#include <utility>
 
 typedef unsigned long long u64;
 typedef long long i64;
@@ -19,6 +22,29 @@ typedef uint8_t u8;
 #define SCC_MAX_K 128
 #define SCC_CODE_BITS 7
 #define SCC_CODE_MASK 127u
+
+// ------------------------------------------------------------ launch attributes
+// A kernel's dynamic-LDS limit, set once per (kernel, device) and raised only
+// when a launch needs more: hipFuncSetAttribute costs ~23 us a call on this
+// runtime (HIP API trace of the config-B bench: 134 calls, 3.1 ms over 12
+// steps), and the per-call settings kept the host behind the GPU.
+static inline hipError_t scc_set_lds(const void* fn, size_t bytes)
+{
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, size_t> set;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(fn, dev);
+    const auto it = set.find(key);
+    if (it != set.end() && it->second >= bytes) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) set[key] = bytes;
+    return e;
+}
 
 // ------------------------------------------------------------ orderable keys
 // Bijective map fp64 -> u64 whose unsigned order is the IEEE total order for

@@ -1030,7 +1030,7 @@ extern "C" hipError_t scc_launch_gather(const i64* indptr, const int* rows, cons
         }
         const size_t lds = sizeof(double) * W * (size_t)ld + mapb;
         const int wgs = std::max(1, std::min((int)(cu_lds / lds), 32 / W));
-        hipFuncSetAttribute((const void*)k_gather_csc_lm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        scc_set_lds((const void*)k_gather_csc_lm, (int)lds);
         const int grid = std::max(1, std::min((Npad + W - 1) / W, wgs * cus));
         hipLaunchKernelGGL(k_gather_csc_lm, dim3(grid), dim3(64 * W), lds, st, indptr, rows, vals, N, Npad, G, genes, nu,
                            ld, Xc);

@@ -1710,7 +1710,7 @@ static void launch_eig_finish(double* Zq, int n, int lda, int k, const double* W
 {
     const size_t lds = sizeof(double) * (size_t)k * n;
     if (lds <= 150 * 1024) {
-        hipFuncSetAttribute((const void*)k_eig_finish_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        scc_set_lds((const void*)k_eig_finish_lds, (int)lds);
         hipLaunchKernelGGL(k_eig_finish_lds, dim3(1), dim3(FIN_T), lds, st, Zq, n, lda, k, W, tnorm, Z);
     } else {
         hipLaunchKernelGGL(k_eig_finish, dim3(1), dim3(FIN_T), 0, st, Zq, n, lda, k, W, tnorm, Z);
@@ -2010,7 +2010,7 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
                  : nj == 8  ? (const void*)(k_tridiag<false, 8>)
                  : nj == 14 ? (const void*)(k_tridiag<false, 14>)
                             : (const void*)(k_tridiag<false, 0>);
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        scc_set_lds(fn, (int)lds);
         const dim3 grid(t.xcd_local ? std::min(8 * nwg, cus) : nwg);
         void* args[] = {&t};
         e = hipLaunchKernel(fn, grid, dim3(TRI_T), args, lds, st);
@@ -2049,7 +2049,7 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
     v.vcount = flags + 5;
     v.err = flags + 1;
     const size_t vlds = sizeof(double) * (lu_lds ? 10 : 4) * (size_t)n;
-    hipFuncSetAttribute((const void*)k_tri_vectors, hipFuncAttributeMaxDynamicSharedMemorySize, (int)vlds);
+    scc_set_lds((const void*)k_tri_vectors, (int)vlds);
     // Back-transformation: the explicit Q formed on a side stream beside
     // k_tri_vectors, then Z = Q Y (SCC_EIG_BT=2, the default where its LDS
     // fits); SCC_EIG_BT=1: one workgroup applying the reflector blocks to all
@@ -2081,7 +2081,7 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
         }
         const size_t rlds = sizeof(double) * BT_NB * (size_t)n;
         if (rlds + 20 * 1024 <= EIG_LDS_MAX) {  // + the static G, T (one coalesced read: no XCD pinning)
-            hipFuncSetAttribute((const void*)k_refl_T_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds);
+            scc_set_lds((const void*)k_refl_T_lds, (int)rlds);
             hipLaunchKernelGGL(k_refl_T_lds, dim3(nblk), dim3(1024), rlds, rs, t.refl, t.tau, n, lda,
                                scratch + L.tf);
         } else {
@@ -2091,7 +2091,7 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (q_form) {
             const size_t qlds = form_q_lds(n);
-            hipFuncSetAttribute((const void*)k_form_q, hipFuncAttributeMaxDynamicSharedMemorySize, (int)qlds);
+            scc_set_lds((const void*)k_form_q, (int)qlds);
             hipLaunchKernelGGL(k_form_q, dim3((n + QF_R - 1) / QF_R), dim3(QF_T), qlds, rs, t.refl, scratch + L.tf, n,
                                lda, scratch + L.q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2110,7 +2110,7 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
         zfin = scratch + L.zt;
     } else if (bt_one) {
         const size_t blds = tri_back_lds(n, k);
-        hipFuncSetAttribute((const void*)k_tri_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds);
+        scc_set_lds((const void*)k_tri_back, (int)blds);
         hipLaunchKernelGGL(k_tri_back, dim3(1), dim3(TB_T), blds, st, v.Zq, n, lda, k, v.refl, v.tf, stamps);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

@@ -729,12 +729,12 @@ extern "C" hipError_t scc_launch_ingest_hist(const i64* indptr, const int* rows,
     const int hw = scc_ingest_hist_window(G);
     const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
     if (dense) {
-        hipFuncSetAttribute((const void*)k_ing_hist<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        scc_set_lds((const void*)k_ing_hist<true>, (int)lds);
         hipLaunchKernelGGL((k_ing_hist<true>), dim3(nc), dim3(IH_T), lds, st, nullptr, nullptr, dense, G, perm, cc_p0,
                            cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, 0, hw, nullptr,
                            err);
     } else {
-        hipFuncSetAttribute((const void*)k_ing_hist<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        scc_set_lds((const void*)k_ing_hist<false>, (int)lds);
         hipLaunchKernelGGL((k_ing_hist<false>), dim3(nc), dim3(IH_T), lds, st, indptr, rows, vals, G, perm, cc_p0,
                            cc_code, SC_GT, ntile, cnt, bnd, nodg, wave_expm1, want_expm1, glo, ghi, rng, hw, tbnd,
                            err);
@@ -750,7 +750,7 @@ extern "C" hipError_t scc_launch_ingest_count_ro(const i64* indptr, const int* r
     const int hw = scc_ingest_hist_window(G);
     const size_t lds = sizeof(u32) * (size_t)((hw + 3) / 4);
     const int ntile = (G + SC_GT - 1) / SC_GT;
-    hipFuncSetAttribute((const void*)k_ing_count_ro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    scc_set_lds((const void*)k_ing_count_ro, (int)lds);
     hipLaunchKernelGGL(k_ing_count_ro, dim3(nc), dim3(IH_T), lds, st, indptr, rows, G, perm, cc_p0, cc_code, hw, glo,
                        ghi, SC_GT, ntile, tbnd, cnt);
     return hipGetLastError();
@@ -807,8 +807,8 @@ extern "C" hipError_t scc_launch_ingest_scatter(const i64* indptr, const int* ro
     }();
     const size_t lds = (size_t)cap * (8 + 2);
     // (4 loads in flight per lane: 8 and 16 measured slower at config B)
-    hipFuncSetAttribute((const void*)k_ing_scatter<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipFuncSetAttribute((const void*)k_ing_scatter<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    scc_set_lds((const void*)k_ing_scatter<true, 4>, (int)lds);
+    scc_set_lds((const void*)k_ing_scatter<false, 4>, (int)lds);
     if (dense)
         hipLaunchKernelGGL((k_ing_scatter<true, 4>), grid, dim3(ING_T), lds, st, nullptr, nullptr, dense, G, perm,
                            cc_p0, sc_cc0, cnt, gstart, bnd, nullptr, ntile, cap, glo, ghi, t0, ns, ntl, run, keys);

@@ -3408,7 +3408,7 @@ extern "C" hipError_t scc_launch_rank_resplit(const ScRankLaunch* L, int grid, h
     if (L->P > 64 * RSW_TS_SMALL)
         hipLaunchKernelGGL(k_rank_resplit_w<RSW_PACC / 64>, dim3(2 * grid), dim3(256), 0, ss.next(), W);
     const size_t acc_lds = sizeof(u64) * (size_t)std::max(L->P, 1);
-    hipFuncSetAttribute((const void*)k_rank_resplit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_lds);
+    scc_set_lds((const void*)k_rank_resplit, (int)acc_lds);
     hipLaunchKernelGGL(k_rank_resplit, dim3(grid), dim3(RS_T), acc_lds, ss.next(), *L);
     ss.end();
     if (L->fat2) {  // sub-buckets the first level left with > 64 distinct values
@@ -3424,7 +3424,7 @@ extern "C" hipError_t scc_launch_rank_split(const ScRankLaunch* L, int grid, hip
 {
     if (grid <= 0) return hipSuccess;
     const size_t lds = scc_rank_split_lds(L->K);
-    hipFuncSetAttribute((const void*)k_rank_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    scc_set_lds((const void*)k_rank_split, (int)lds);
     hipLaunchKernelGGL(k_rank_split, dim3(grid), dim3(SP_T), lds, st, *L);
     return hipGetLastError();
 }
@@ -3436,26 +3436,22 @@ extern "C" hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int 
     if (cls == 0) {
         A.cap_lds = L->cap_s;
         const size_t lds = scc_rank_item_lds(0, L->cap_s, L->ntp_max, L->K);
-        hipFuncSetAttribute((const void*)k_rank_item<RK_T0, false, RK_KPT0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+        scc_set_lds((const void*)k_rank_item<RK_T0, false, RK_KPT0>, (int)lds);
         hipLaunchKernelGGL((k_rank_item<RK_T0, false, RK_KPT0>), dim3(grid), dim3(RK_T0), lds, st, A, 0);
     } else if (cls == 1 && L->med_wide) {
         A.cap_lds = L->cap_m;
         const size_t lds = scc_rank_item_lds(3, L->cap_m, L->ntp_max, L->K);
-        hipFuncSetAttribute((const void*)k_rank_item<RK_T1W, false, RK_KPT1>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        scc_set_lds((const void*)k_rank_item<RK_T1W, false, RK_KPT1>, (int)lds);
         hipLaunchKernelGGL((k_rank_item<RK_T1W, false, RK_KPT1>), dim3(grid / 2), dim3(RK_T1W), lds, st, A, 1);
     } else if (cls == 1) {
         A.cap_lds = L->cap_m;
         const size_t lds = scc_rank_item_lds(1, L->cap_m, L->ntp_max, L->K);
-        hipFuncSetAttribute((const void*)k_rank_item<RK_T1, false, RK_KPT1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+        scc_set_lds((const void*)k_rank_item<RK_T1, false, RK_KPT1>, (int)lds);
         hipLaunchKernelGGL((k_rank_item<RK_T1, false, RK_KPT1>), dim3(grid), dim3(RK_T1), lds, st, A, 1);
     } else {
         A.cap_lds = 0;
         const size_t lds = scc_rank_item_lds(2, 0, L->ntp_max, L->K);
-        hipFuncSetAttribute((const void*)k_rank_item<RK_T2, true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+        scc_set_lds((const void*)k_rank_item<RK_T2, true, 1>, (int)lds);
         hipLaunchKernelGGL((k_rank_item<RK_T2, true, 1>), dim3(grid), dim3(RK_T2), lds, st, A, 2);
     }
     return hipGetLastError();

@@ -1584,8 +1584,7 @@ static hipError_t launch_rank(const ScSegLaunch* L, int ncu, hipStream_t st)
     const size_t lds = scc_seg_rank_lds(L->K);
     static bool attr = false;  // (one attribute call per instantiation and process: the largest K of the tile count)
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_seg_rank<KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)scc_seg_rank_lds(16 * KT));
+        scc_set_lds((const void*)k_seg_rank<KT>, (int)scc_seg_rank_lds(16 * KT));
         attr = true;
     }
     const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
@@ -1598,7 +1597,7 @@ static hipError_t launch_wave(const ScSegLaunch* L, int ncu, hipStream_t st)
 {
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_seg_wave<KT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        scc_set_lds((const void*)k_seg_wave<KT>, 160 * 1024);
         attr = true;
     }
     const size_t wb = sw_layout(L->K).bytes;
@@ -1623,9 +1622,9 @@ hipError_t scc_launch_seg_rank(const ScSegLaunch* L, int ncu, hipStream_t st)
     hipLaunchKernelGGL(k_seg_flags_t, dim3((L->G + 31) / 32, (L->P + 31) / 32), dim3(256), 0, st, *L);
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_seg_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Sp2Lds));
-        hipFuncSetAttribute((const void*)k_seg_cross, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-        hipFuncSetAttribute((const void*)k_seg_refine, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RefLds));
+        scc_set_lds((const void*)k_seg_split, (int)sizeof(Sp2Lds));
+        scc_set_lds((const void*)k_seg_cross, 64 * 1024);
+        scc_set_lds((const void*)k_seg_refine, (int)sizeof(RefLds));
         attr = true;
     }
     hipLaunchKernelGGL(k_seg_split, dim3(ncu), dim3(SP2_T), sizeof(Sp2Lds), st, *L);

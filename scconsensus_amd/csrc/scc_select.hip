@@ -786,7 +786,7 @@ extern "C" hipError_t scc_launch_pair_select(const ScSelectLaunch* L, hipStream_
     A.first_occ = L->first_occ;
     A.err = L->err;
     const size_t lds = scc_select_lds_bytes(L->cap);
-    hipFuncSetAttribute((const void*)k_pair_select<SEL_T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    scc_set_lds((const void*)k_pair_select<SEL_T>, (int)lds);
     if (L->phi <= L->plo) return hipSuccess;
     hipLaunchKernelGGL(k_pair_select<SEL_T>, dim3(L->phi - L->plo), dim3(SEL_T), lds, st, A);
     return hipGetLastError();
@@ -798,7 +798,7 @@ extern "C" hipError_t scc_launch_union(const u64* first_occ, int G, void* scratc
     // one workgroup over all G genes: 1024 threads (a quarter of the chunk rounds of 256)
     constexpr int UT = 1024;
     const size_t lds = (size_t)cap * sizeof(KeyRec) + sizeof(int) * UT;
-    hipFuncSetAttribute((const void*)k_union<UT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    scc_set_lds((const void*)k_union<UT>, (int)lds);
     hipLaunchKernelGGL(k_union<UT>, dim3(1), dim3(UT), lds, st, first_occ, G, (KeyRec*)scratch, cap, out, n_out);
     return hipGetLastError();
 }

@@ -40,8 +40,7 @@ extern "C" void scc_small_syev_prepare()
 {
     static std::once_flag once;
     std::call_once(once, [] {
-        (void)hipFuncSetAttribute((const void*)k_small_syev, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)scc_small_syev_lds_bytes());
+        (void)scc_set_lds((const void*)k_small_syev, (int)scc_small_syev_lds_bytes());
     });
 }
 

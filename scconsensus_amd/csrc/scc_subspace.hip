@@ -1615,8 +1615,7 @@ static void fx_prepare()
 {
     static std::once_flag once;
     std::call_once(once, [] {
-        (void)hipFuncSetAttribute((const void*)k_fsi_engine, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)std::max(fx_lds_bytes(FX_NPRES), fx_lds_bytes(FX_NPMAX)));
+        (void)scc_set_lds((const void*)k_fsi_engine, (int)std::max(fx_lds_bytes(FX_NPRES), fx_lds_bytes(FX_NPMAX)));
     });
 }
 
