@@ -205,7 +205,7 @@ def cold_call(d, code, K, gpu, de_mode):
     return out
 
 
-def de_only(a, eng, ds, d, code, K, dist, world):
+def de_only(a, eng, ds, d, code, K, dist, world, dataset_ms=None):
     """Config E (BASELINE: "1M-cell sparse CSR input, 100 clusters (4950
     pairs), DE-only"): the FAST DE over all pairs, rows fetched to the host."""
     from scconsensus_amd import _native as nat
@@ -277,6 +277,25 @@ def de_only(a, eng, ds, d, code, K, dist, world):
                       "engine_runs_per_step": 1 if K <= 128 else (-(-K // 64)) * (-(-K // 64) - 1) // 2,
                       "parallelism": f"jobs{world}" if world > 1 else "single"},
            "stage_ms_per_step": stage_ms, "roofline": roof, "kernels": kernels}
+    if dataset_ms:
+        # the CSR -> CSC build: minimum traffic = the CSR read once (12 B per
+        # stored value + 8 B per gene) + the CSC written once (12 B per stored
+        # value + 8 B per cell)
+        t_b = sum(dataset_ms[1:]) / max(1, len(dataset_ms) - 1)
+        mn = 12.0 * nnz + 8.0 * (G + 1) + 12.0 * nnz + 8.0 * (N + 1)
+        dsb = {"first_ms": dataset_ms[0], "ms": t_b, "runs_ms": dataset_ms,
+               "min_bytes": mn, "achieved_gbs": mn / (t_b / 1e3) / 1e9,
+               "frac": mn / (t_b / 1e3) / 1e9 / PEAK_HBM_GBS,
+               "note": "scc_dataset_create_csr_device wall time (synchronised), CSR -> resident CSC; not in value"}
+        if os.path.exists(tpath):
+            tk = json.load(open(tpath))["kernels"]
+            hits = {k: v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith("k_csr")}
+            if hits:
+                dsb["traffic"] = sum(hits.values())
+                dsb["traffic_kernels"] = hits
+                dsb["traffic_vs_min"] = sum(hits.values()) / mn
+        out["dataset_ms"] = dsb
+        out["de_plus_dataset_ms"] = s_step * 1e3 + t_b
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
     dist.close()
@@ -385,8 +404,21 @@ def main():
     eng = nat.Engine(gpu, profile=not a.no_stage_events,
                      devices=devices if route_devices and len(devices) > 1 else None)
     if a.config == "E":
-        ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
-        return de_only(a, eng, ds, d, code, K, dist, world)
+        # the gene-major CSR is transposed into the resident CSC when the
+        # dataset is created (k_csr_count / k_csr_scatter): an R call on a
+        # dgRMatrix pays it once per call, so it is timed and reported beside
+        # the DE (first build: allocations; then the mean of repeated builds)
+        build = []
+        for i in range(3):
+            eng.synchronize()
+            t0 = time.perf_counter()
+            ds = eng.dataset_csr_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N,
+                                        d.nnz)
+            eng.synchronize()
+            build.append((time.perf_counter() - t0) * 1e3)
+            if i < 2:
+                ds.close()
+        return de_only(a, eng, ds, d, code, K, dist, world, dataset_ms=build)
     if a.config in DEVICE_GEN:
         ds = eng.dataset_csc_device(d.indptr.data_ptr(), d.indices.data_ptr(), d.data.data_ptr(), d.G, d.N, d.nnz)
     else:
@@ -512,7 +544,9 @@ def main():
     stage_ms[dom] = t_dom[0] / max(t_dom[1], 1)
     os.environ["SCC_PROFILE_STAGES"] = "-"  # the side measurements below: no stage events
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{a.config}.json")
+    # counters of THIS DE mode only (a SLOW line never borrows FAST's kernels' traffic)
+    ttag = a.config + ("_slow" if a.de == "slow" else "")
+    tpath = os.path.join(ROOT, "profiles", f"pmc_traffic_{ttag}.json")
     if os.path.exists(tpath) and not multi:
         tk = json.load(open(tpath))["kernels"]
         kpre = {"dist": "k_dist", "ingest": "k_ing", "gene_stats": "k_gene_stats", "gene_rank": "k_rank",
@@ -592,7 +626,7 @@ def main():
 
     roof_dom = roof(dom)
     roof_dom["traffic"] = traffic
-    roof_dom["traffic_source"] = (f"profiles/pmc_traffic_{a.config}.json (scripts/pmc_traffic.sh)"
+    roof_dom["traffic_source"] = (f"profiles/pmc_traffic_{ttag}.json (scripts/pmc_traffic.sh {a.config} {a.de})"
                                   if traffic is not None else None)
     if alg[dom][2].endswith("stage") or " stage" in alg[dom][2]:
         roof_dom["note"] = "avg_launch_ms is the whole stage (its kernels back to back), not one kernel"

@@ -136,8 +136,9 @@ SCC_API int scc_dataset_create_csc(scc_ctx* ctx, const int64_t* indptr, const in
  * input): indptr[G+1], cols[nnz] (0-based cells), vals[nnz].  Transposed once
  * on the device into the resident CSC over cells above (the dgCMatrix R
  * would hold for the same matrix), so every result equals the CSC path's.
- * Column indices outside [0, N) fail with SCC_ERR_INVALID; a repeated
- * (gene, cell) fails like unsorted dgCMatrix rows at scc_de_run.  No
+ * Column indices outside [0, N), or not strictly ascending within a gene
+ * (unsorted, or a repeated (gene, cell)), fail with SCC_ERR_INVALID here;
+ * more than 524,288 genes with SCC_ERR_UNSUPPORTED.  No
  * reference interface: the reference takes dataMatrix as an R matrix
  * (Fast:22, :368); this is the R-free caller's equivalent. */
 SCC_API int scc_dataset_create_csr(scc_ctx* ctx, const int64_t* indptr, const int32_t* cols, const double* vals,
@@ -148,6 +149,11 @@ SCC_API int scc_dataset_create_dense(scc_ctx* ctx, const double* x_colmajor, int
                              int32_t ptr_kind, scc_dataset** out);
 /* Destroy every dataset before the context it was created on. */
 SCC_API void scc_dataset_destroy(scc_dataset* ds);
+/* Copy a sparse dataset's resident dgCMatrix (indptr[N+1], rows[nnz],
+ * vals[nnz]) to host arrays: what the CSR transpose built, for checks and
+ * for callers that want the CSC back (rows = vals = NULL: indptr only).  No
+ * reference interface (the R side already holds its matrix). */
+SCC_API int scc_dataset_read_csc(scc_dataset* ds, int64_t* indptr, int32_t* rows, double* vals);
 
 /* ---- stage 1+2: per-cluster statistics, all-pairs Wilcoxon, BH, union --- */
 SCC_API int scc_de_run(scc_ctx* ctx, const scc_dataset* ds, const int32_t* code /* host, [N] */, int32_t K,

@@ -37,6 +37,7 @@ EXPORTS = [
     "scc_ctx_create", "scc_device_count", "scc_ctx_destroy", "scc_ctx_last_error", "scc_ctx_synchronize", "scc_ctx_set_stream",
     "scc_ctx_kernel_time",
     "scc_ctx_reset_timers", "scc_dataset_create_csc", "scc_dataset_create_csr", "scc_dataset_create_dense", "scc_dataset_destroy",
+    "scc_dataset_read_csc",
     "scc_de_run", "scc_de_shard_bytes", "scc_de_run_shard", "scc_de_finish", "scc_de_run_shard_records",
     "scc_de_finish_records", "scc_de_finish_records_pairs", "scc_de_union_first_occ", "scc_de_result_counts", "scc_de_result_union", "scc_de_result_rows",
     "scc_de_result_pair_vectors", "scc_de_result_log_threshold", "scc_de_result_nodg", "scc_de_result_destroy",
@@ -107,6 +108,7 @@ def load():
         "scc_dataset_create_csr": (ctypes.c_int, [vp, vp, vp, vp, i64, i64, i64, i32, P(vp)]),
         "scc_dataset_create_dense": (ctypes.c_int, [vp, vp, i64, i64, i32, P(vp)]),
         "scc_dataset_destroy": (None, [vp]),
+        "scc_dataset_read_csc": (ctypes.c_int, [vp, vp, vp, vp]),
         "scc_de_run": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), P(vp)]),
         "scc_de_shard_bytes": (i64, [i32, i64]),
         "scc_de_run_shard": (ctypes.c_int, [vp, vp, vp, i32, P(DeParams), i64, i64, vp]),
@@ -280,6 +282,16 @@ class Engine:
                                                     ctypes.c_void_p(vals_ptr), G, N, nnz, SCC_PTR_DEVICE,
                                                     ctypes.byref(h)))
         return Dataset(self, h, G, N)
+
+    def read_csc(self, ds: Dataset):
+        """The dataset's resident dgCMatrix (indptr, rows, vals) on the host."""
+        indptr = np.empty(ds.N + 1, np.int64)
+        self._check(self.lib.scc_dataset_read_csc(ds.handle, _ptr(indptr), None, None))
+        nnz = int(indptr[-1])
+        rows = np.empty(max(nnz, 1), np.int32)
+        vals = np.empty(max(nnz, 1), np.float64)
+        self._check(self.lib.scc_dataset_read_csc(ds.handle, _ptr(indptr), _ptr(rows), _ptr(vals)))
+        return indptr, rows[:nnz], vals[:nnz]
 
     def dataset_dense(self, X_gene_major) -> Dataset:
         """X as a genes x cells array; passed to the engine in R's column-major layout."""

@@ -236,11 +236,22 @@ hipError_t scc_launch_ingest_count_ro(const long long* indptr, const int* rows, 
 hipError_t scc_launch_scan(const uint32_t* in, long long n, long long* out, long long* bsum_scratch,
                            long long* total, hipStream_t st);
 int scc_scan_scratch_blocks(long long n);
-#define SCC_CSR_TG 32  // genes per tile of the CSR -> CSC transpose
-size_t scc_csr_scratch_words(long long G, long long N);
-hipError_t scc_launch_csr_to_csc(const long long* indptr, const int* cols, const double* vals, int G, int N,
-                                 uint32_t* scratch, long long* scan_scratch, long long* csc_indptr, int* csc_rows,
-                                 double* csc_vals, int* err, int check_only, hipStream_t st);
+// CSR -> CSC transpose (scc_csr.hip): a plan sized on the host from (G, N,
+// nnz), one scratch blob, a validating pass, then the two-pass transpose
+struct ScCsrPlan {
+    long long G, N, nnz;
+    int SB, NS;      // cells per superblock, superblocks
+    int T;           // gene tiles of 256
+    int CG, NG;      // cells per output group, groups
+    size_t off_bnd, off_rs, off_tt, off_ts, off_off, off_gm, off_gb, off_scan, off_meta, off_ival, bytes;
+};
+int scc_csr_plan(long long G, long long N, long long nnz, ScCsrPlan* P);
+// validation (columns in [0, N), strictly ascending per gene) + superblock bounds
+hipError_t scc_launch_csr_check(const ScCsrPlan* P, const long long* indptr, const int* cols, void* scratch,
+                                int* err, hipStream_t st);
+hipError_t scc_launch_csr_to_csc(const ScCsrPlan* P, const long long* indptr, const int* cols, const double* vals,
+                                 void* scratch, long long* csc_indptr, int* csc_rows, double* csc_vals,
+                                 hipStream_t st);
 hipError_t scc_launch_reduce_dd(const dd* parts, int n, dd* out, hipStream_t st);
 
 hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t st);

@@ -365,12 +365,16 @@ extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const i
             cleanup();
             return fail(c, SCC_ERR_INVALID, "CSR indptr is not non-decreasing");
         }
-    uint32_t* scratch = nullptr;
-    long long* scan_scr = nullptr;
+    // the transpose's plan and scratch (scc_csr.hip: bounds, region and group
+    // offsets, the 10-B-per-entry intermediate)
+    ScCsrPlan plan;
+    if (scc_csr_plan(G, N, nnz, &plan) != 0) {
+        cleanup();
+        return fail(c, SCC_ERR_UNSUPPORTED, "scc_dataset_create_csr: more than 524,288 genes");
+    }
+    void* scratch = nullptr;
     int* d_err = nullptr;
-    if (!dalloc((void**)&scratch, sizeof(uint32_t) * scc_csr_scratch_words(G, N)) ||
-        !dalloc((void**)&scan_scr, sizeof(long long) * (scc_scan_scratch_blocks(N) + 1)) ||
-        !dalloc((void**)&d_err, sizeof(int))) {
+    if (!dalloc(&scratch, plan.bytes) || !dalloc((void**)&d_err, sizeof(int))) {
         cleanup();
         return fail(c, SCC_ERR_OOM, "CSR transpose scratch allocation failed");
     }
@@ -389,21 +393,20 @@ extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const i
         scc_dataset_destroy(d);
         return fail(c, SCC_ERR_OOM, "dataset allocation failed");
     }
+    // validation first (columns in range, strictly ascending per gene), then
+    // the transpose only over a valid matrix
     int herr = 0;
     hipError_t e = hipMemsetAsync(d_err, 0, sizeof(int), s0);
-    if (e == hipSuccess)
-        e = scc_launch_csr_to_csc(d_ip, d_cols, d_vals, (int)G, (int)N, scratch, scan_scr, d->d_indptr, d->d_rows,
-                                  d->d_vals, d_err, 1, s0);
+    if (e == hipSuccess) e = scc_launch_csr_check(&plan, d_ip, d_cols, scratch, d_err, s0);
     if (e == hipSuccess) e = hipMemcpyAsync(&herr, d_err, sizeof(int), hipMemcpyDeviceToHost, s0);
     if (e == hipSuccess) e = hipStreamSynchronize(s0);
     if (e == hipSuccess && herr) {
         cleanup();
         scc_dataset_destroy(d);
-        return fail(c, SCC_ERR_INVALID, "CSR column index out of range");
+        return fail(c, SCC_ERR_INVALID, "CSR column index out of range or not strictly ascending within a gene");
     }
     if (e == hipSuccess)
-        e = scc_launch_csr_to_csc(d_ip, d_cols, d_vals, (int)G, (int)N, scratch, scan_scr, d->d_indptr, d->d_rows,
-                                  d->d_vals, d_err, 0, s0);
+        e = scc_launch_csr_to_csc(&plan, d_ip, d_cols, d_vals, scratch, d->d_indptr, d->d_rows, d->d_vals, s0);
     if (e == hipSuccess) e = hipStreamSynchronize(s0);
     cleanup();
     if (e != hipSuccess) {
@@ -443,6 +446,26 @@ extern "C" int scc_dataset_create_dense(scc_ctx* c, const double* x, int64_t G, 
         }
     }
     return finish_create(c, d, out);
+}
+
+extern "C" int scc_dataset_read_csc(scc_dataset* d, int64_t* indptr, int32_t* rows, double* vals)
+{
+    if (!d || !indptr || (!rows != !vals))
+        return fail(d ? d->ctx : nullptr, SCC_ERR_INVALID, "scc_dataset_read_csc: bad arguments");
+    if (d->dense || !d->d_indptr) return fail(d->ctx, SCC_ERR_INVALID, "scc_dataset_read_csc: not a sparse dataset");
+    scc_enter(d->ctx);
+    hipStream_t s0 = d->ctx->s0;
+    hipError_t e = hipMemcpyAsync(indptr, d->d_indptr, sizeof(int64_t) * (d->N + 1), hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess && d->nnz > 0 && rows)
+        e = hipMemcpyAsync(rows, d->d_rows, sizeof(int32_t) * d->nnz, hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess && d->nnz > 0 && vals)
+        e = hipMemcpyAsync(vals, d->d_vals, sizeof(double) * d->nnz, hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess) e = hipStreamSynchronize(s0);
+    if (e != hipSuccess) {
+        hipGetLastError();
+        return fail(d->ctx, SCC_ERR_HIP, std::string("scc_dataset_read_csc: ") + hipGetErrorString(e));
+    }
+    return SCC_OK;
 }
 
 extern "C" void scc_dataset_destroy(scc_dataset* d)

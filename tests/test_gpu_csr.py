@@ -106,3 +106,64 @@ def test_api_accepts_scipy_csr(eng):
     b = api.reclusterDEConsensusFast(d.scipy_csc(), d.labels, deepSplitValues=(1,))
     assert a["deGeneUnion"] == b["deGeneUnion"]
     assert list(a["dynamicColors"]["deepsplit: 1"]) == list(b["dynamicColors"]["deepsplit: 1"])
+
+
+# ---------------------------------------------------------------- the transpose itself
+def _expect_csc(m):
+    """scipy's own transpose of the CSR: the dgCMatrix R would hold."""
+    c = m.tocsc()
+    c.sort_indices()
+    return c.indptr.astype(np.int64), c.indices.astype(np.int32), c.data
+
+
+def _check_transpose(eng, m, G, N):
+    ds = eng.dataset_csr(m.indptr, m.indices, m.data, G, N)
+    ip, rows, vals = eng.read_csc(ds)
+    eip, erows, evals = _expect_csc(m)
+    np.testing.assert_array_equal(ip, eip)
+    np.testing.assert_array_equal(rows, erows)
+    np.testing.assert_array_equal(vals, evals)  # bit-identical (values are moved, never computed)
+    ds.close()
+
+
+@pytest.mark.parametrize("G,N,density,seed", [
+    (1, 1, 1.0, 0), (1, 5000, 0.3, 1), (3000, 1, 0.5, 2), (257, 1025, 0.05, 3),
+    (2000, 3000, 0.0325, 4), (600, 700, 1.0, 5), (5000, 20000, 0.002, 6), (300, 4000, 0.0, 7),
+])
+def test_transpose_bit_identical_to_scipy(eng, G, N, density, seed):
+    """Shapes around the tile (256 genes), superblock and group edges, fully
+    dense (pieces split in LDS), very sparse, empty."""
+    rng = np.random.default_rng(seed)
+    m = sp.random(G, N, density=density, format="csr", random_state=rng, dtype=np.float64)
+    m.data = rng.standard_normal(m.nnz)
+    m.sort_indices()
+    _check_transpose(eng, m, G, N)
+
+
+def test_transpose_dense_blocks_and_heavy_cells(eng):
+    """A tile whose genes are dense over a superblock (the pass-1 piece is cut
+    down to fit the LDS staging), a cell holding every gene and empty cells
+    and genes (a pass-2 group past its staging, written in place)."""
+    rng = np.random.default_rng(11)
+    G, N = 30000, 2000
+    m = sp.random(G, N, density=0.01, format="lil", random_state=rng, dtype=np.float64)
+    m[256:512, 0:600] = rng.random((256, 600)) + 1.0  # dense region
+    m[:, 1500] = (rng.random((G, 1)) + 2.0)           # a heavy cell: every gene
+    m[:, 1700] = 0.0
+    m[100, :] = 0.0
+    m = sp.csr_matrix(m)
+    m.eliminate_zeros()
+    m.sort_indices()
+    _check_transpose(eng, m, G, N)
+
+
+def test_transpose_rejects_unsorted_and_repeated_columns(eng):
+    from scconsensus_amd import _native as nat
+    vals = np.ones(4)
+    for cols in ([0, 2, 1, 3], [0, 1, 1, 3]):  # unsorted / repeated (gene, cell) in gene 0
+        with pytest.raises(nat.SccError) as e:
+            eng.dataset_csr(np.array([0, 3, 4], np.int64), np.array(cols, np.int32), vals, 2, 4)
+        assert e.value.code == nat.SCC_ERR_INVALID
+    with pytest.raises(nat.SccError) as e:  # negative column
+        eng.dataset_csr(np.array([0, 1, 2], np.int64), np.array([-1, 0], np.int32), vals[:2], 2, 4)
+    assert e.value.code == nat.SCC_ERR_INVALID
