@@ -70,11 +70,8 @@ for s in "$@"; do
     smalleig) step smalleig 300 rocprofv3 --kernel-trace --stats -d gpurun_out/smalleig -o run --output-format csv -- python3 scripts/small_eig_bench.py ;;
     benchfsi3) SCC_EIG_FSI=1 SCC_EIG_FSI_PASSES=3 SCC_EIG_SI_LOG=1 step benchfsi3 600 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 20 --warmup 5 ;;
     robust) step robust 600 python -u -m pytest tests/test_gpu_robust.py tests/test_gpu_fsi.py -x -v --timeout 200 --timeout-method thread ;;
-    seg) step seg 600 python -u -m pytest tests/test_gpu_rank_seg.py tests/test_gpu_robust.py -x -v --timeout 200 --timeout-method thread ;;
     de) step de 900 python -u -m pytest tests/test_gpu_de.py tests/test_gpu_rank_mfma.py tests/test_gpu_grouped.py -x -v --timeout 300 --timeout-method thread ;;
     cfg) step cfg 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_large.py -x -v --timeout 600 --timeout-method thread ;;
-    segdbg) for v in 0 4 5; do SCC_SEG_DEBUG=$v step segdbg$v 300 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 5 --warmup 3 || exit 1; done ;;
-    segst) SCC_SEG_STAMPS=1 step segstB 300 python bench.py --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1 && SCC_SEG_STAMPS=1 step segstD 600 python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --steps 1 --warmup 1 ;;
     benchB) step benchB 600 python bench.py --no-cpu-baseline --steps 20 --warmup 5 ;;
     benchEq) step benchEq 900 python bench.py --config E --no-cpu-baseline --steps 2 --warmup 1 ;;
     *) echo "unknown step $s"; exit 2 ;;

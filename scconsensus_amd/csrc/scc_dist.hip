@@ -1101,13 +1101,8 @@ extern "C" hipError_t scc_launch_center_parts(double* Xc, int n, int nu, int ld,
     return hipGetLastError();
 }
 
-// output tile width of the Gram: 128 from |U| > 384 (half the operand
-// re-fetch; SCC_GRAM_T=64 / 128 forces either)
-extern "C" int scc_gram_tile_width(int ld)
-{
-    const char* gt = getenv("SCC_GRAM_T");
-    return (gt && *gt) ? (atoi(gt) == 128 ? 128 : 64) : (ld > 384 ? 128 : 64);
-}
+// output tile width of the Gram: 128 from |U| > 384 (half the operand re-fetch)
+extern "C" int scc_gram_tile_width(int ld) { return ld > 384 ? 128 : 64; }
 
 // mean: centre on the fly (64-wide tiles only; the caller centred Xc otherwise)
 extern "C" hipError_t scc_launch_gram(const double* Xc, int Npad, int ld, int nchunk, double* slabs, double* C,
@@ -1200,12 +1195,7 @@ __global__ void __launch_bounds__(256) k_d2h(const char* __restrict__ src, char*
     }
 }
 
-static int env_int_d2h()  // workgroups of the copy (SCC_D2H_WG, default 256)
-{
-    const char* e = getenv("SCC_D2H_WG");
-    const int v = (e && *e) ? atoi(e) : 256;
-    return v > 0 ? v : 256;
-}
+static int env_int_d2h() { return 256; }  // workgroups of the copy (32-1024 measured 53-55 GB/s alike)
 
 extern "C" hipError_t scc_launch_d2h(const void* src, void* dst, size_t n, hipStream_t st)
 {

@@ -117,15 +117,28 @@ static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi,
         return (char*)p;
     };
     hipPointerAttribute_t pa{};
-    const bool pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost;
+    bool pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost;
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
+    // a large pageable buffer (R's allocVector): registered with the runtime
+    // for the call (page-locked in place, mapped for k_d2h) instead of going
+    // through the staging ring and a host memcpy; SCC_DIST_REGISTER=0 keeps
+    // the ring
+    bool registered = false;
+    if (!pinned && total >= ((size_t)256 << 20) && env_int("SCC_DIST_REGISTER", 1) != 0) {
+        registered = hipHostRegister(host, total, hipHostRegisterMapped) == hipSuccess;
+        if (!registered) (void)hipGetLastError();
+        pinned = registered;
+    }
     if (pinned) {  // straight into the caller's buffer
         char* hd = dev_ptr(host);
         const size_t C = (size_t)std::max(1, env_int("SCC_DIST_CHUNK_MB", 1024)) << 20;
-        for (size_t a = 0; a < total; a += C)
-            HIPCHK(c, copy(host + a, hd ? hd + a : nullptr, d_out + a, std::min(C, total - a)));
-        HIPCHK(c, hipStreamSynchronize(s0));
+        hipError_t e = hipSuccess;
+        for (size_t a = 0; a < total && e == hipSuccess; a += C)
+            e = copy(host + a, hd ? hd + a : nullptr, d_out + a, std::min(C, total - a));
+        if (e == hipSuccess) e = hipStreamSynchronize(s0);
+        if (registered && hipHostUnregister(host) != hipSuccess) (void)hipGetLastError();
+        HIPCHK(c, e);
     } else {
         const size_t S = (size_t)std::max(1, env_int("SCC_DIST_STAGE_MB", 32)) << 20;
         if (c->dstage_bytes < S) {
@@ -163,7 +176,7 @@ static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi,
         HIPCHK(c, e);
     }
     if (c->profile) {  // wall time of the streamed output (output kernel + PCIe + host copy)
-        auto& tm = c->timers[pinned ? "d2h_pinned" : "d2h"];
+        auto& tm = c->timers[registered ? "d2h_registered" : (pinned ? "d2h_pinned" : "d2h")];
         tm.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         tm.n += 1;
     }
@@ -340,7 +353,7 @@ static int dist_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* genes, in
     unsigned int* d_eig_err = nullptr;  // the hand-off's time-out flag, read back after the last launch
     if (metric == SCC_DIST_PCA_EUCLID) {
         double *d_slabs, *d_C, *d_W, *d_Z, *d_P, *d_escr;
-        const bool fused = env_int("SCC_CENTER_FUSED", 1) != 0 && scc_gram_tile_width(ld) == 64;
+        const bool fused = scc_gram_tile_width(ld) == 64;  // centring folded into the 64-wide Gram and the scores
         const int nchunk = gram_chunks(Npad);
         WS("d_slabs", (size_t)nchunk * ld * ld, d_slabs);
         WS("d_C", (size_t)ld * ld, d_C);

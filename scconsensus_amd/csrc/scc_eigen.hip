@@ -1873,6 +1873,10 @@ extern "C" size_t scc_eigen_scratch_doubles(int n, int lda, int k)
 // filtered iteration's graph cache (context serial and workspace generation;
 // 0: no graph).  marks (optional): 6 events recorded before/after each of the
 // three launches (a null entry is skipped).
+// set by eig_direct: whether its launches wait on co-resident workgroups
+// (more than one tridiagonalisation workgroup, or follow-ups pinned to its XCD)
+static thread_local bool t_eig_coop = true;
+
 static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scratch, double* Z, double* W,
                              hipEvent_t* marks, unsigned long long* stamps, bool safe, hipStream_t st);
 
@@ -1925,13 +1929,17 @@ extern "C" hipError_t scc_launch_eigen_topk(const double* A, int n, int lda, int
     // The direct solver's tridiagonalisation hands off between co-resident
     // workgroups (bounded polls).  On a shared device they may not all become
     // resident: the time-out flag is read here, and the same solve reruns on
-    // ONE workgroup with no cooperative wait (slower, same algorithm).
+    // ONE workgroup with no cooperative wait (slower, same algorithm).  A plan
+    // of one workgroup without XCD pinning waits on nobody: no read, the call
+    // stays asynchronous.
     // SCC_EIG_FORCE_TIMEOUT=1 (tests) takes the rerun as if the flag were set.
+    const char* ft = getenv("SCC_EIG_FORCE_TIMEOUT");
+    const bool forced = ft && atoi(ft);
+    if (!t_eig_coop && !forced) return hipSuccess;
     u32 herr = 0;
     if ((e = hipMemcpyAsync(&herr, flags + 1, sizeof(u32), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    const char* ft = getenv("SCC_EIG_FORCE_TIMEOUT");
-    if (herr || (ft && atoi(ft))) {
+    if (herr || forced) {
         if (getenv("SCC_EIG_SI_LOG")) fprintf(stderr, "[scc eig] direct solver hand-off timed out: one-workgroup rerun\n");
         if ((e = hipMemsetAsync(flags, 0, 64, st)) != hipSuccess) return e;
         if ((e = eig_direct(A, n, lda, k, scratch, Z, W, nullptr, nullptr, true, st)) != hipSuccess) return e;
@@ -1993,6 +2001,7 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
     size_t lds = tri_lds_bytes(n, std::max(R - tri_reg_rows(n), 0), rows_lds);
     if (lds < 82 * 1024) lds = 82 * 1024;
     t.lds_rows_cap = rows_lds ? (int)((lds / sizeof(double) - (5 * (size_t)n + 64 + EIG_MAX_WG)) / n) : 0;
+    t_eig_coop = nwg > 1 || t.xcd_local;
     if (marks && marks[0]) hipEventRecord(marks[0], st);
     const int cus = scc_device_cus(64);
     {
@@ -2038,11 +2047,9 @@ static hipError_t eig_direct(const double* A, int n, int lda, int k, double* scr
     v.stamps = stamps;
     v.tf = scratch + L.tf;
     // follow-up kernels on the tridiagonalisation's XCD (its reflectors are in that L2)
-    // SCC_EIG_PIN: 0 = anywhere, 1 = claim loop (xcd_next), 2 (default) = one
-    // item per workgroup with a co-resident wait when 8 x k workgroups fit
-    const char* pin_env = getenv("SCC_EIG_PIN");
-    const int pin_mode = pin_env ? atoi(pin_env) : 2;
+    // one item per workgroup with a co-resident wait when 8 x k workgroups fit
     // (measured at config B: eig_vec 0.37 ms anywhere, 0.42 claim loop, 0.32 wait)
+    constexpr int pin_mode = 2;
     const bool pin = !safe && t.xcd_local != 0 && pin_mode != 0;
     v.wait = pin_mode == 2;
     v.xcd = pin && (pin_mode == 1 || 8 * k <= 256) ? t.reg : nullptr;  // wait needs co-residency

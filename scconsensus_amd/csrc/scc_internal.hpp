@@ -67,7 +67,6 @@ struct scc_ctx {
     uint64_t generation = 0;
     uint64_t serial = 0;  // unique per context in this process (never reused, unlike its address)
     uint64_t ws_gen = 0;  // bumped by every workspace (re)allocation
-    bool rank_legacy = false;  // the bucket rank engine for this run (a segment overflowed)
     std::vector<int> host_tables;  // cell permutation + chunk tables of the last scc_de_run
     int* h_stage = nullptr;        // pinned: the DE result header, tested counts and union, one D2H
     size_t h_stage_n = 0;

@@ -50,12 +50,9 @@ struct ScRankLaunch {
     const int* cl_cc;
     const uint8_t* flags;  // [P][G] bit0: the pair tests the gene
     int cap_s, cap_m, cap_lds, bucket_target, ntp_max, item_cap;
-    int med_wide;          // medium items: 1024 threads, one workgroup per CU
     int wave_target;       // split: bins are packed into buckets of < 2 * wave_target elements
     int rw_slots;          // wave kernel: tested pairs per gene held in registers, 64 * rw_slots (2, 4, 8 or 16)
     int dbg;               // SCC_RW_DEBUG timing experiments (1: no pair counts, 2: no sort); results invalid
-    int rw_ch;             // k_rank_waves: consecutive buckets per wave visit (SCC_RW_CH, <= 64)
-    int split2;            // k_rank_split: two-level scatter of genes past one register chunk (SCC_SPLIT2)
     int bucket_cap;        // capacity of sbuckets / hbg rows
     ScRankItem* sbuckets;  // [bucket_cap] buckets of <= 64 elements (one wave each)
     unsigned int* hbg;     // [bucket_cap][K] per-bucket cluster counts
@@ -101,54 +98,6 @@ struct ScRankLaunch {
     size_t tp_scr_stride;
 };
 
-// The segment rank engine (scc_rank_seg.hip): ranked genes cut into value
-// segments of <= SG_CAP nonzeros, each sorted and counted by one workgroup.
-#define SG_CAP 1024              // elements of a sorted segment (one wave: 16 per lane)
-#define SG_TGT 512               // the splitter's target segment size (mean)
-#define SCC_SEG_OVERFLOW 0x4000  // error word: a segment outgrew SG_CAP (the run reruns on the bucket engine)
-
-struct ScSeg {
-    long long base;  // first element (keys / keys2 index)
-    int n, gene;
-    int kind;        // 0: a whole gene in keys (codes from the cluster offsets), 1: keys2 / codes2,
-                     // 2: one repeated value (keys2 / codes2; closed form), 3: cut into sub-segments
-    int hrow;        // row of hseg (the segment's cluster counts) for the cross-segment part; -1: none
-};
-
-struct ScSegLaunch {
-    const long long* gstart;
-    const unsigned long long* keys;
-    int G, K, P, all_pairs;
-    const uint32_t* coff;
-    const int* cl_cc;
-    const uint8_t* flags;       // [P][G] bit0: the pair tests the gene
-    uint8_t* tbg;               // [G][P] the same, gene-major (0 / 1)
-    unsigned long long* keys2;  // [nnz] segment-ordered keys of split genes
-    uint8_t* codes2;            // [nnz]
-    ScSeg* segs;                // [seg_cap]
-    int seg_cap;
-    int* counts;                // [0] segments, [1] split genes, [2] hseg rows, [3] splitter queue, [4] oversized segments,
-                                // [5] wide segments
-    int* ovf;                   // [ovf_cap] oversized interval segments (k_seg_refine)
-    int sample_os;              // splitter sample keys per segment (32; SCC_SEG_OVERSAMPLE)
-    int dbg;                    // SCC_SEG_DEBUG timing cuts (1: no sort, 2: no blocks, 4: no ties); results invalid
-    int stamps;                 // SCC_SEG_STAMPS: per-phase clocks (g_seg_stamps)
-    int* wide;                  // [wide_cap] segments whose key range does not fit the composite key (counts[5])
-    int wide_cap;
-    int wide_mode;              // k_seg_rank: 1 = only the wide list (after the wave kernel)
-    int ovf_cap;
-    int* big;                   // [G] genes for the splitter
-    int4* gseg;                 // [G] per split gene: {first hseg row, segments, gene, 0}
-    uint32_t* hseg;             // [hrow_cap][K]
-    int hrow_cap;
-    size_t cross_lds;
-    unsigned long long* accS;
-    unsigned long long* accE;
-    unsigned long long* accX;
-    unsigned long long* accF;
-    int* err;
-};
-hipError_t scc_launch_seg_rank(const ScSegLaunch* L, int ncu, hipStream_t st);
 
 struct ScTestLaunch {
     int K, G, P, mode;

@@ -888,6 +888,7 @@ struct SplitLds {
     u32 wsum[SP_W + 1];
     u32 wsum2[SP_W + 1];
     u64 rmn[SP_W], rmx[SP_W];
+    u32 cdf[SP_BINS + 1];  // the linear window's counts, scanned: the equalized bins' map
     int off[SCC_MAX_K + 1];
     int nb, bk0, next;
     int nfat, fat0, nwav, wav0;
@@ -978,14 +979,68 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     const int bits = range ? 64 - __clzll((long long)range) : 0;
     const int sh = bits > 11 ? bits - 11 : 0;
     if (tid == 0) A.gkmin[g] = bits <= 64 - SCC_CODE_BITS ? kmn : ~0ull;  // wave kernel: (key - kmin) << 7 | cluster
-    // ---- 1. histogram of the top 11 bits of the key window (one LDS atomic per
-    // element; any key of a bin is kept as its representative)
+    // ---- 1. equalized bins.  A linear 2048-bin window over the gene's whole
+    // key range puts hundreds of distinct values into one bin where the values
+    // crowd (at 200k cells: the count-1 band of a dense gene), and every such
+    // bin cost a re-split (k_rank_resplit*: 8 ms of config D's rank stage).
+    // So the linear histogram is a first look: where a bin holds more than 64
+    // elements, its scan (cdf) maps a key
+    // to  floor(2048 (cdf[j] + f h_j) / n)  (j its linear bin, f its place in
+    // it, h_j the bin's count) -- the gene's empirical CDF, interpolated --
+    // and the buckets are cut on those bins.  The map is non-decreasing in the
+    // key (every operation is a correctly rounded monotone one), so a bin is a
+    // key interval: equal values never straddle bins and order is kept.
+    // A gene whose linear bins all hold <= 64 elements keeps them (no second pass).
     for (int c0 = 0; c0 < n; c0 += SP_CHUNK) {
         if (n > SP_CHUNK) load_chunk(c0);
 #pragma unroll
         for (int q = 0; q < SP_KPT; ++q) {
             if (c0 + q * SP_T + tid < n) {
                 const u32 d = (u32)((kr[q] - kmn) >> sh);
+                atomicAdd(&L.hist[d], 1u);
+                L.rep[d] = kr[q];
+            }
+        }
+    }
+    __syncthreads();
+    const bool equalize = __syncthreads_or(L.hist[2 * tid] > 64u || L.hist[2 * tid + 1] > 64u) != 0;
+    if (equalize) {
+        const u32 h0 = L.hist[2 * tid], h1 = L.hist[2 * tid + 1];
+        const u32 v = h0 + h1;
+        u32 incl = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const u32 y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) L.wsum[w] = incl;
+        __syncthreads();
+        u32 b = incl - v;
+        for (int q = 0; q < w; ++q) b += L.wsum[q];
+        L.cdf[2 * tid] = b;
+        L.cdf[2 * tid + 1] = b + h0;
+        if (tid == SP_T - 1) L.cdf[SP_BINS] = (u32)n;
+        L.hist[2 * tid] = 0;
+        L.hist[2 * tid + 1] = 0;
+    }
+    __syncthreads();
+    const double inv_w = ldexp(1.0, -sh), bin_scale = (double)SP_BINS / (double)max(n, 1);
+    auto binof = [&](u64 k) -> u32 {
+        const u64 x = k - kmn;
+        const u32 j = (u32)(x >> sh);
+        if (!equalize) return j;
+        const u32 lo = L.cdf[j], h = L.cdf[j + 1] - lo;
+        const double f = (double)(x - ((u64)j << sh)) * inv_w;
+        const u32 d = (u32)(((double)lo + f * (double)h) * bin_scale);
+        return d < SP_BINS ? d : SP_BINS - 1;
+    };
+    // histogram of the equalized bins (one LDS atomic per element; any key of
+    // a bin is kept as its representative)
+    for (int c0 = 0; c0 < n && equalize; c0 += SP_CHUNK) {
+        if (n > SP_CHUNK) load_chunk(c0);
+#pragma unroll
+        for (int q = 0; q < SP_KPT; ++q) {
+            if (c0 + q * SP_T + tid < n) {
+                const u32 d = binof(kr[q]);
                 atomicAdd(&L.hist[d], 1u);
                 L.rep[d] = kr[q];
             }
@@ -1061,7 +1116,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     // group of two or more buckets reloaded, ordered in LDS and written back.
     // The one-level scatter's scattered stores were ~2/3 of a large gene's
     // split time (8.4 -> 3.0 cycles per value without them at config D).
-    // SCC_SPLIT2=0, or a gene past SP_NSUP groups: the one-level scatter.
+    // A gene past SP_NSUP groups: the one-level scatter.
     const bool staged = n <= SP_CHUNK;
     u64* stk = (u64*)((char*)&L + kSplitStageOff);
     u8* stc = (u8*)(stk + SP_CHUNK);
@@ -1074,7 +1129,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     u32* sbeg = L.hist + SP_BINS / 2;                  // [SP_NSUP + 1] group starts (offsets)
     u32* sbk = sbeg + (SP_NSUP + 1);                   // [SP_NSUP + 1] first bucket of each group
     u32* scur = sbk + (SP_NSUP + 1);                   // [SP_NSUP] group cursors
-    bool two = !staged && A.split2;
+    bool two = !staged;
     if (two) {
         // group starts over the bins, 2 per thread (the bucket rule's scan)
         auto big = [&](u32 b) { return L.boff[b + 1] - L.boff[b] > (u32)SP_SUP; };
@@ -1141,7 +1196,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
                 if (i < n) {
                     while (a + 1 < K && L.off[a + 1] <= i) ++a;
                     const u64 k = kr[q];
-                    const u32 d = (u32)((k - kmn) >> sh);
+                    const u32 d = binof(k);
                     const u32 pos = atomicAdd(&scur[supbin[d]], 1u);
                     A.keys2[base + pos] = k;
                     A.codes2[base + pos] = (u8)a;
@@ -1159,7 +1214,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
             if (i < n) {
                 while (a + 1 < K && L.off[a + 1] <= i) ++a;
                 const u64 k = kr[q];
-                const u32 d = (u32)((k - kmn) >> sh);
+                const u32 d = binof(k);
                 const u32 bk = L.bid[d];
                 const u32 pos = atomicAdd(&L.bcur[bk], 1u);
                 if (staged) {
@@ -1198,7 +1253,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
 #pragma unroll
             for (int q = 0; q < SP_KPT; ++q) {
                 if ((u32)(q * SP_T + tid) < m) {
-                    const u32 d = (u32)((kv[q] - kmn) >> sh);
+                    const u32 d = binof(kv[q]);
                     const u32 p = atomicAdd(&L.bcur[L.bid[d]], 1u) - o0;
                     stk[p] = kv[q];
                     stc[p] = cv[q];
@@ -2076,7 +2131,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
     const int cnt = min(A.counts[4], A.bucket_cap);
     const int K = A.K, G = A.G, P = A.P;
-    const int CH = A.rw_ch > 0 && A.rw_ch <= 64 ? A.rw_ch : 16;  // consecutive buckets per wave visit (gene locality)
+    constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality; 8 / 32 / 64 measured no better)
     int cur = -1, ntp = 0;
     u64 gk = ~0ull;
     u32 pa[RW_SLOTS], pb[RW_SLOTS], pp[RW_SLOTS];
@@ -3198,14 +3253,12 @@ static size_t item_lds_fixed(int ntp_max, int K)
 
 #define RK_T0 256   // small items
 #define RK_T1 512   // medium items (two workgroups per CU)
-#define RK_T1W 1024 // medium items, wide variant (one workgroup per CU)
 #define RK_T2 1024  // HBM-resident items
 
 extern "C" size_t scc_rank_item_lds(int cls, int cap, int ntp_max, int K)
 {
     if (cls == 0) return item_lds_fixed<RK_T0 / 64>(ntp_max, K) + (size_t)cap * (4 + 2 + 2 + 1 + 1);
     if (cls == 1) return item_lds_fixed<RK_T1 / 64>(ntp_max, K) + (size_t)cap * (4 + 2 + 2 + 1 + 1);
-    if (cls == 3) return item_lds_fixed<RK_T1W / 64>(ntp_max, K) + (size_t)cap * (4 + 2 + 2 + 1 + 1);
     return item_lds_fixed<RK_T2 / 64>(ntp_max, K);
 }
 
@@ -3218,7 +3271,6 @@ extern "C" int scc_rank_item_cap(int cls, int want, int ntp_max, int K, int lim)
     int cap = want & ~63;
     if (cls == 0 && cap > RK_KPT0 * RK_T0) cap = RK_KPT0 * RK_T0;
     if (cls == 1 && cap > RK_KPT1 * RK_T1) cap = RK_KPT1 * RK_T1;
-    if (cls == 3 && cap > RK_KPT1 * RK_T1W) cap = RK_KPT1 * RK_T1W;
     while (cap > 64 && scc_rank_item_lds(cls, cap, ntp_max, K) > (size_t)lim) cap -= 64;
     if (cap > 65535) cap = 65535 & ~63;
     return cap;
@@ -3293,11 +3345,8 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
     // fixed cost: it takes the genes with more than 512 tested pairs (SLOW at
     // config D: every gene, 1225 pairs), the slot kernels the others
     // (SCC_RANK_MFMA=2: every gene on the matrix cores, 0: none)
-    static const int mfma_min = [] {  // SCC_RANK_MFMA_MIN: the tested-pair count past which a gene goes there
-        const char* e = getenv("SCC_RANK_MFMA_MIN");
-        const int v = (e && *e) ? atoi(e) : 512;
-        return v == 128 || v == 256 ? v : 512;
-    }();
+    // (from 256 or 128 tested pairs measured slower at config D: 37.2 / 53.0 vs 34.2 ms)
+    constexpr int mfma_min = 512;  // the tested-pair count past which a gene goes there
     const int hi[4] = {128, 256, 512, 1024};
     const bool mfma = L->rw_mfma && L->K <= 64 && (L->rw_mfma == 2 || 64 * L->rw_slots > mfma_min);
     if (mfma) {
@@ -3438,11 +3487,6 @@ extern "C" hipError_t scc_launch_rank_items(const ScRankLaunch* L, int cls, int 
         const size_t lds = scc_rank_item_lds(0, L->cap_s, L->ntp_max, L->K);
         scc_set_lds((const void*)k_rank_item<RK_T0, false, RK_KPT0>, (int)lds);
         hipLaunchKernelGGL((k_rank_item<RK_T0, false, RK_KPT0>), dim3(grid), dim3(RK_T0), lds, st, A, 0);
-    } else if (cls == 1 && L->med_wide) {
-        A.cap_lds = L->cap_m;
-        const size_t lds = scc_rank_item_lds(3, L->cap_m, L->ntp_max, L->K);
-        scc_set_lds((const void*)k_rank_item<RK_T1W, false, RK_KPT1>, (int)lds);
-        hipLaunchKernelGGL((k_rank_item<RK_T1W, false, RK_KPT1>), dim3(grid / 2), dim3(RK_T1W), lds, st, A, 1);
     } else if (cls == 1) {
         A.cap_lds = L->cap_m;
         const size_t lds = scc_rank_item_lds(1, L->cap_m, L->ntp_max, L->K);

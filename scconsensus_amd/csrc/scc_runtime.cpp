@@ -526,29 +526,16 @@ struct RecIO {  // the compact exchange's buffers (DE_SHARD_REC out, DE_FINISH_R
     void* first_out = nullptr;
 };
 
-// de_run_body's answer when a segment of the segment rank engine outgrew
-// SG_CAP (a value stretch the splitter's sample missed): the same run again on
-// the bucket engine (never returned by the C ABI)
-static constexpr int kRankRetry = -1000;
-
 static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
                        const RecIO* rio);
-extern "C" void scc_seg_stamps(hipStream_t st, int print);
 extern "C" void scc_rank_split_diag(hipStream_t st, int ngenes);
 
 static int de_run_impl(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
                        int stage, int64_t glo64, int64_t ghi64, void* shard, scc_de_result** out,
                        const RecIO* rio = nullptr)
 {
-    int rc = de_run_body(c, ds, code, K, prm, stage, glo64, ghi64, shard, out, rio);
-    if (rc == kRankRetry) {
-        if (env_int("SCC_SEG_LOG", 0)) fprintf(stderr, "[scc seg] segment overflow: bucket engine rerun\n");
-        c->rank_legacy = true;
-        rc = de_run_body(c, ds, code, K, prm, stage, glo64, ghi64, shard, out, rio);
-        c->rank_legacy = false;
-    }
-    return rc;
+    return de_run_body(c, ds, code, K, prm, stage, glo64, ghi64, shard, out, rio);
 }
 
 static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, int32_t K, const scc_de_params* prm,
@@ -693,8 +680,6 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     WS("cntpos", GK, d_cntpos);
     WS("cntneg", GK, d_cntneg);
     const bool ttest = fast && prm->test == SCC_TEST_T;  // DiffTTest (Fast:185-196): no rank stage
-    // the segment rank engine (SCC_RANK_SEG=0 or an overflow rerun: the bucket engine)
-    const bool use_seg = !ttest && !c->rank_legacy && env_int("SCC_RANK_SEG", 0) != 0;
     double* d_vx;
     WS("vx", ttest ? GK : 1, d_vx);
     // rank accumulators: S, E, X per (pair, gene), F per (cluster, gene)
@@ -705,11 +690,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     const int ntp_max = P;
     // small items: 4 workgroups per CU; medium: 2 per CU (LDS budget per workgroup)
     const int cap_s = scc_rank_item_cap(0, env_int("SCC_CAP_SMALL", kCapSmall), ntp_max, K, 40 * 1024);
-    const int med_wide = env_int("SCC_RANK_WIDE", 0);
-    const int cap_m = std::max(cap_s, med_wide ? scc_rank_item_cap(3, env_int("SCC_CAP_MEDIUM", kCapMedium), ntp_max, K,
-                                                                   160 * 1024)
-                                               : scc_rank_item_cap(1, env_int("SCC_CAP_MEDIUM", kCapMedium), ntp_max, K,
-                                                                   80 * 1024));
+    const int cap_m = std::max(cap_s, scc_rank_item_cap(1, env_int("SCC_CAP_MEDIUM", kCapMedium), ntp_max, K, 80 * 1024));
     const int wave_target = 32;  // value buckets of < 64 elements: one wave each
     const int bucket_cap = (int)std::min<int64_t>(3 * nnz1 / wave_target + 2 * (int64_t)G + 64, 1 << 29);
     const int item_cap = bucket_cap;
@@ -800,7 +781,15 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
                                       ghi, s0));
         de_cleared = true;
         if ((hist_rng || hist_ro) && !ds->d_tbnd) {  // once per dataset: every cell's gene-tile starts
-            if (hipMalloc((void**)&ds->d_tbnd, sizeof(long long) * (size_t)N * (ntile + 1)) != hipSuccess) {
+            // (8 B per (cell, tile): ~0.6 GB at config E, held until the dataset
+            // is destroyed, outside the workspace; taken only while it leaves
+            // three quarters of the free memory to the runs' workspaces, else
+            // the counting pass keeps its per-run binary searches: INTEGRATION.md)
+            const size_t tb_bytes = sizeof(long long) * (size_t)N * (ntile + 1);
+            size_t mfree = 0, mtot = 0;
+            const bool room = hipMemGetInfo(&mfree, &mtot) == hipSuccess && tb_bytes <= mfree / 4;
+            (void)hipGetLastError();
+            if (!room || hipMalloc((void**)&ds->d_tbnd, tb_bytes) != hipSuccess) {
                 (void)hipGetLastError();
                 ds->d_tbnd = nullptr;
             } else {
@@ -908,48 +897,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         Scope sc(c, "pair_filter", s0);
         HIPCHK(c, scc_launch_pair_filter(&T, s0));
     }
-    if (use_seg) {
-        // the segment engine (scc_rank_seg.hip): value segments of <= SG_CAP
-        // nonzeros, each sorted and counted on the matrix cores by one workgroup
-        Scope sc(c, "gene_rank", s0);
-        if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
-        ScSegLaunch SL{};
-        SL.gstart = d_gstart;
-        SL.keys = d_keys;
-        SL.G = (int)G;
-        SL.K = K;
-        SL.P = P;
-        SL.all_pairs = all_pairs ? 1 : 0;
-        SL.coff = d_cnt;
-        SL.cl_cc = d_clcc;
-        SL.flags = d_flags;
-        SL.keys2 = d_keys2;
-        SL.codes2 = d_codes2;
-        SL.seg_cap = (int)std::min<int64_t>(2 * G + nnz1 / (SG_TGT / 2) + 64, 1 << 30);
-        SL.hrow_cap = (int)std::min<int64_t>(G + nnz1 / (SG_TGT / 2) + 64, 1 << 30);
-        WS("segs", (size_t)SL.seg_cap, SL.segs);
-        WS("segcnt", 8, SL.counts);
-        WS("segbig", (size_t)G, SL.big);
-        WS("gseg", (size_t)G, SL.gseg);
-        WS("hseg", (size_t)SL.hrow_cap * K, SL.hseg);
-        SL.ovf_cap = 16384;
-        SL.wide_cap = (int)std::min<int64_t>(SL.seg_cap, 1 << 26);
-        WS("segwide", (size_t)SL.wide_cap, SL.wide);
-        WS("segtbg", PG, SL.tbg);
-        SL.sample_os = std::max(1, env_int("SCC_SEG_OVERSAMPLE", 32));
-        SL.dbg = env_int("SCC_SEG_DEBUG", 0);
-        WS("segovf", (size_t)SL.ovf_cap, SL.ovf);
-        SL.accS = accS;
-        SL.accE = accE;
-        SL.accX = accX;
-        SL.accF = accF;
-        SL.err = d_err;
-        HIPCHK(c, hipMemsetAsync(SL.counts, 0, sizeof(int) * 8, s0));
-        SL.stamps = env_int("SCC_SEG_STAMPS", 0);
-        if (SL.stamps) scc_seg_stamps(s0, 0);
-        HIPCHK(c, scc_launch_seg_rank(&SL, c->n_cu > 0 ? c->n_cu : 256, s0));
-        if (SL.stamps) scc_seg_stamps(s0, 1);
-    } else if (!ttest) {
+    if (!ttest) {
         Scope sc(c, "gene_rank", s0);
         if (!de_cleared) HIPCHK(c, hipMemsetAsync(d_acc, 0, sizeof(unsigned long long) * acc_n, s0));
         ScRankLaunch L{};
@@ -964,13 +912,10 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         L.flags = d_flags;
         L.cap_s = cap_s;
         L.cap_m = cap_m;
-        L.med_wide = med_wide;
         L.bucket_target = bucket_target;
         L.wave_target = wave_target;
         L.rw_slots = P <= 128 ? 2 : P <= 256 ? 4 : P <= 512 ? 8 : 16;
         L.dbg = env_int("SCC_RW_DEBUG", 0);
-        L.rw_ch = env_int("SCC_RW_CH", 16);
-        L.split2 = env_int("SCC_SPLIT2", 1);
         L.rw_mfma = env_int("SCC_RANK_MFMA", 1);
         L.rw_mfma16 = env_int("SCC_RANK_MFMA16", -1);
         L.cross_wave = env_int("SCC_CROSS_WAVE", 0);
@@ -1046,7 +991,9 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         } else {
             // (not on small jobs: at config B the fork and join cost more than
             // the overlap of two ~10-us launches)
-            const int rs_side = (env_int("SCC_RW_STREAMS", 1) != 0 && ds->nnz > (64ll << 20)) ? 2 : 0;
+            // (SCC_RW_STREAMS=2 forces them at any size: the streams test)
+            const int rw_mode = env_int("SCC_RW_STREAMS", 1);
+            const int rs_side = (rw_mode >= 2 || (rw_mode != 0 && ds->nnz > (64ll << 20))) ? 2 : 0;
             HIPCHK(c, scc_launch_rank_resplit(&L, 4 * ncu, s0, c->sw, rs_side, c->ev_wfork, c->ev_wj));
         }
         // buckets of <= 64 elements (one wave each) beside the fat buckets (LDS
@@ -1144,7 +1091,6 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         int e = 0;
         HIPCHK(c, hipMemcpy(&e, d_err, sizeof(int), hipMemcpyDeviceToHost));
         if (e & 1) return fail(c, SCC_ERR_NONFINITE, "input holds non-finite values");
-        if (use_seg && (e & SCC_SEG_OVERFLOW)) return kRankRetry;
         if (e & 2) return fail(c, SCC_ERR_INVALID, "row index out of range");
         if (e & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
         if (e & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
@@ -1188,7 +1134,11 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     double* d_slow_q = nullptr;
     uint8_t* d_slow_de = nullptr;
     void *d_rec = nullptr, *d_key = nullptr;
+    // FAST rows: one per (pair, gene) flag at most, so PG rows hold every row
+    // offset count_tested can produce from any flag contents -- including the
+    // stale flags a pair-range finish leaves outside its range
     const size_t rowcap = fast ? PG : 1;
+    if (fast && rowcap < PG) return fail(c, SCC_ERR_INVALID, "internal: FAST row buffers smaller than P x G");
     WS("row_gene", rowcap, d_row_gene);
     WS("row_p", rowcap, d_row_p);
     WS("row_q", rowcap, d_row_q);
@@ -1282,7 +1232,6 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     if (hdr[1] & 4) return fail(c, SCC_ERR_INVALID, "row indices not strictly increasing within a column (dgCMatrix)");
     if (hdr[1] & 8) return fail(c, SCC_ERR_RSTOP, "t.test: data are essentially constant (R stop())");
     if (hdr[1] & 16) return fail(c, SCC_ERR_INVALID, "scc_de_finish_records: record out of range");
-    if (use_seg && (hdr[1] & SCC_SEG_OVERFLOW)) return kRankRetry;
     if ((rc = note_validated(hdr[1]))) return rc;
     scc_de_result* r = new scc_de_result();
     r->ctx = c;

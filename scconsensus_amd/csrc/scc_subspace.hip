@@ -1589,11 +1589,17 @@ static void fx_prepare();
 #define FX_COOL 32
 static std::atomic<int> g_fx_cool[64];
 
+// engines in flight per device (each call waits for its own engine's verdict
+// before it returns, so a count taken around that span is exact)
+static std::atomic<int> g_fx_users[64];
+
 // the persistent engine for n <= FX_NPMAX (SCC_EIG_FSI_ENGINE=0: the launch
-// per step): only when all 4 nt workgroups can be resident at once on this
-// device (occupancy at the engine's LDS size times the CUs), and not while a
-// recent time-out cools down
-static bool fx_usable(int n, int dev)
+// per step): only when the 4 nt workgroups of every engine in flight on this
+// device, this one included, can be resident at once (occupancy at the
+// engine's LDS size times the CUs: two threads or contexts sharing a device
+// must not both spin to the time-out), and not while a recent
+// time-out cools down.  `users`: the engines in flight counting this one.
+static bool fx_usable(int n, int dev, int users = 1)
 {
     if (fsi_env("SCC_EIG_FSI_ENGINE", 1) == 0 || (int)si_npad(n) > FX_NPMAX) return false;
     if (dev >= 0 && dev < 64 && g_fx_cool[dev].load() > 0) {
@@ -1609,7 +1615,7 @@ static bool fx_usable(int n, int dev)
         (void)hipGetLastError();
         return false;
     }
-    return (long long)per_cu * cus >= nwg;
+    return (long long)per_cu * cus >= (long long)nwg * std::max(1, users);
 }
 static void fx_prepare()
 {
@@ -1701,7 +1707,18 @@ extern "C" hipError_t scc_eigen_fsi(const double* C, int n, int ldc, int k, doub
     const dim3 gt((unsigned)nt, SI_B / 16), gg(SI_B / 16, SI_B / 16);
     int dev = 0;
     (void)hipGetDevice(&dev);
-    int use_engine = fx_usable(n, dev) ? 1 : 0;
+    // reserve a place among this device's engines first, then check that all fit
+    const bool devok = dev >= 0 && dev < 64;
+    const int users = devok ? g_fx_users[dev].fetch_add(1) + 1 : 1;
+    int use_engine = fx_usable(n, dev, users) ? 1 : 0;
+    if (devok && !use_engine) g_fx_users[dev].fetch_sub(1);
+    struct FxUser {  // released when this call returns (its engine has answered by then)
+        int dev;
+        ~FxUser()
+        {
+            if (dev >= 0) g_fx_users[dev].fetch_sub(1);
+        }
+    } fx_user{devok && use_engine ? dev : -1};
     const int rr_on = fsi_env("SCC_EIG_FSI_ENGINE_RR", 1) != 0, stamps_on = fsi_env("SCC_EIG_FSI_STAMPS", 0) != 0;
     if (use_engine) {  // the polls' bound (tests: SCC_EIG_FX_SPIN); written only when it changes
         static std::mutex spin_mu;

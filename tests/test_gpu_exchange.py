@@ -252,3 +252,29 @@ def test_streamed_output_matches_device(eng, cfg_a, metric, f32, kernel_copy, mo
     lo, hi = 100, 1700
     s0, s1 = lo * (2 * N - lo - 1) // 2, hi * (2 * N - hi - 1) // 2
     np.testing.assert_array_equal(eng.distance_cols(ds, union, lo, hi, metric, f32=f32), ref[s0:s1])
+
+
+@pytest.mark.parametrize("register", ["1", "0"])
+def test_large_pageable_output_registered(eng, register, monkeypatch):
+    """A pageable output of >= 256 MB (R's allocVector at scale) is registered
+    with the runtime for the call and written directly by k_d2h
+    (SCC_DIST_REGISTER=0: the staging ring); both bit-identical to the
+    device output, the buffer's neighbours untouched (one element off the
+    16-B alignment, as inside an R vector)."""
+    monkeypatch.setenv("SCC_DIST_REGISTER", register)
+    d = synth.generate("A", G=600, N=8300, K=6, seed=21)
+    names, code = api.select_clusters(d.labels, 10)
+    ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
+    union = eng.de_run(ds, code, len(names), nat.SCC_DE_FAST, fetch="union").union
+    n = d.N * (d.N - 1) // 2
+    assert 8 * n >= 256 << 20
+    dev = torch.empty(n, dtype=torch.float64, device="cuda:0")
+    eng.distance(ds, union, nat.SCC_DIST_PCA_EUCLID, device_out_ptr=dev.data_ptr())
+    eng.synchronize()
+    ref = dev.cpu().numpy()
+    del dev
+    buf = np.full(n + 2, -7.0)
+    eng.distance(ds, union, nat.SCC_DIST_PCA_EUCLID, out=buf[1:n + 1])
+    np.testing.assert_array_equal(buf[1:n + 1], ref)
+    assert buf[0] == -7.0 and buf[n + 1] == -7.0
+    ds.close()

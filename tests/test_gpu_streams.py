@@ -1,6 +1,7 @@
 """Round-5 scheduling and ingest paths against their references, bit for bit:
-the wave kernels' slot-class launches on side streams (SCC_RW_STREAMS=1, the
-default) against one stream, and the validated dataset's lean counting pass
+the wave kernels' slot-class launches and the re-splits on side streams
+(SCC_RW_STREAMS=2: the re-splits' too, which the default takes only past 64 M
+stored values) against one stream, and the validated dataset's lean counting pass
 (`k_ing_count_ro`, tile starts from the dataset cache) against the full
 counting pass (SCC_COUNT_RO=0 / SCC_INGEST_FULL=1), whole-range and in forced
 small gene windows (reference: R/reclusterDEConsensusFast.R:78-91, the rank
@@ -41,7 +42,7 @@ def test_side_streams_bitwise(eng, monkeypatch):
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     monkeypatch.setenv("SCC_RW_STREAMS", "0")
     one = eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows")
-    monkeypatch.setenv("SCC_RW_STREAMS", "1")
+    monkeypatch.setenv("SCC_RW_STREAMS", "2")  # (2: the re-splits' side streams too, at any size)
     for _ in range(2):
         _same(eng.de_run(ds, code, K, nat.SCC_DE_FAST, fetch="rows"), one)
     # SLOW: every gene tested by every pair (the wide slot classes and windows)
@@ -50,7 +51,7 @@ def test_side_streams_bitwise(eng, monkeypatch):
     kw = dict(q_val_thrs=0.05, fc_thrs=1.5, mean_scaling_factor=5.0)
     monkeypatch.setenv("SCC_RW_STREAMS", "0")
     slow1 = eng.de_run(dss, code, K, nat.SCC_DE_SLOW, fetch="all", **kw)
-    monkeypatch.setenv("SCC_RW_STREAMS", "1")
+    monkeypatch.setenv("SCC_RW_STREAMS", "2")
     slow2 = eng.de_run(dss, code, K, nat.SCC_DE_SLOW, fetch="all", **kw)
     for f in ("union", "p", "q", "logfc", "u2", "de"):
         np.testing.assert_array_equal(getattr(slow2, f), getattr(slow1, f), err_msg=f)
