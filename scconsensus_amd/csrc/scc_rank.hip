@@ -2133,12 +2133,21 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
     const int K = A.K, G = A.G, P = A.P;
     constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality; 8 / 32 / 64 measured no better)
     int cur = -1, ntp = 0;
+    u64 xbud = 0;  // a bound on the largest slot sum of the current run
     u64 gk = ~0ull;
-    u32 pa[RW_SLOTS], pb[RW_SLOTS], pp[RW_SLOTS];
-    u64 aS[RW_SLOTS], aE[RW_SLOTS], aX[RW_SLOTS];
+    // per slot: the tested pair as the split packed it (p | a << 16 | b << 24)
+    // and its sums over the buckets of the current run of one gene, in 32 bits
+    // (a wave bucket adds S <= 32 * 32, E <= 32 * 32, X <= 32 * 32 * 64 to one
+    // pair, a ties-only bucket of n values E <= n^2 / 4, X <= n^3 / 4: a run is
+    // cut before the bound passes 2^32; a ties-only bucket past 2048 values
+    // goes straight out in 64 bits):
+    // half the registers of u64 sums and three pair words, so the 16-slot
+    // variant fits two waves per SIMD
+    u32 tp[RW_SLOTS];
+    u32 aS[RW_SLOTS], aE[RW_SLOTS], aX[RW_SLOTS];
 #pragma unroll
     for (int q = 0; q < RW_SLOTS; ++q) {
-        pa[q] = pb[q] = pp[q] = 0;
+        tp[q] = 0;
         aS[q] = aE[q] = aX[q] = 0;
     }
     for (int c0 = W * CH; c0 < cnt; c0 += NW * CH) {
@@ -2189,13 +2198,15 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 nkey = lane < n1 ? A.keys2[b1 + lane] : ~0ull;
                 ncode = lane < n1 ? (u32)A.codes2[b1 + lane] : 255u;
             }
-            if (g != cur) {
-                // flush the previous gene's sums: one integer atomic per pair
+            const bool big_ties = src == 2 && n > 2048;
+            const u64 xadd = src == 2 ? (big_ties ? 0ull : (u64)n * n * n / 4 + 1) : 65536ull;
+            if (g != cur || xbud + xadd > 0xffffffffull) {
+                // flush the previous run's sums: one integer atomic per pair
                 if (cur >= 0) {
 #pragma unroll
                     for (int q = 0; q < RW_SLOTS; ++q) {
                         if (q * 64 + lane < ntp) {
-                            const size_t o = (size_t)pp[q] * G + cur;
+                            const size_t o = (size_t)(tp[q] & 0xffffu) * G + cur;
                             if (aS[q]) atomicAdd((unsigned long long*)&A.accS[o], (unsigned long long)aS[q]);
                             if (aE[q]) atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)aE[q]);
                             if (aX[q]) atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)aX[q]);
@@ -2203,6 +2214,10 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                         aS[q] = aE[q] = aX[q] = 0;
                     }
                 }
+                xbud = 0;
+            }
+            xbud += xadd;
+            if (g != cur) {
                 cur = g;
                 gk = A.gkmin[g];
                 // tested pairs of g in pair order (compacted by the split)
@@ -2214,11 +2229,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                 for (int q = 0; q < RW_SLOTS; ++q) {
                     const int j = q * 64 + lane;
                     const u32 v = tl[j < ntp ? j : 0];
-                    if (j < ntp) {
-                        pp[q] = v & 0xffffu;
-                        pa[q] = (v >> 16) & 0xffu;
-                        pb[q] = v >> 24;
-                    }
+                    if (j < ntp) tp[q] = v;
                 }
             }
             if (src == 2) {
@@ -2251,19 +2262,27 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
                             atomicAdd((unsigned long long*)&A.accF[(size_t)c * G + g], (unsigned long long)f_tie(mc));
                     }
                 }
+                // (past 2048 values its counts can pass 32 bits: straight out in 64)
 #pragma unroll
                 for (int q = 0; q < RW_SLOTS; ++q) {
-                    u64 ca = (u32)__shfl((int)myc, (int)(pa[q] & 63u), 64);
-                    u64 cb = (u32)__shfl((int)myc, (int)(pb[q] & 63u), 64);
+                    const u32 pa = (tp[q] >> 16) & 0xffu, pb = tp[q] >> 24;
+                    u64 ca = (u32)__shfl((int)myc, (int)(pa & 63u), 64);
+                    u64 cb = (u32)__shfl((int)myc, (int)(pb & 63u), 64);
                     if (K > 64) {
-                        const u64 ca1 = (u32)__shfl((int)myc1, (int)(pa[q] & 63u), 64);
-                        const u64 cb1 = (u32)__shfl((int)myc1, (int)(pb[q] & 63u), 64);
-                        ca = pa[q] >= 64 ? ca1 : ca;
-                        cb = pb[q] >= 64 ? cb1 : cb;
+                        const u64 ca1 = (u32)__shfl((int)myc1, (int)(pa & 63u), 64);
+                        const u64 cb1 = (u32)__shfl((int)myc1, (int)(pb & 63u), 64);
+                        ca = pa >= 64 ? ca1 : ca;
+                        cb = pb >= 64 ? cb1 : cb;
                     }
-                    if (q * 64 + lane < ntp) {
-                        aE[q] += ca * cb;
-                        aX[q] += ca * cb * (ca + cb);
+                    if (q * 64 + lane < ntp && ca && cb) {
+                        if (big_ties) {
+                            const size_t o = (size_t)(tp[q] & 0xffffu) * G + g;
+                            atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)(ca * cb));
+                            atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)(ca * cb * (ca + cb)));
+                        } else {
+                            aE[q] += (u32)(ca * cb);
+                            aX[q] += (u32)(ca * cb * (ca + cb));
+                        }
                     }
                 }
                 continue;
@@ -2336,17 +2355,14 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
             for (int q = 0; q < RW_SLOTS; ++q) {
                 if (q * 64 >= ntp || A.dbg == 1) break;
                 u64 ma, mb;
-                if (K > 16 && K <= 64) {  // the pair's masks straight from the leaders' LDS posts (two reads, no lane moves)
-                    ma = cms[wv][pa[q]];
-                    mb = cms[wv][pb[q]];
+                const u32 pa = (tp[q] >> 16) & 0xffu, pb = tp[q] >> 24;
+                if (K > 16) {  // the pair's masks straight from the leaders' LDS posts (two reads, no lane moves;
+                               // clusters 64..127 too: 8 lane moves a slot before at K > 64)
+                    ma = cms[wv][pa];
+                    mb = cms[wv][pb];
                 } else {
-                    ma = shfl_u64(cm, (int)(pa[q] & 63u));
-                    mb = shfl_u64(cm, (int)(pb[q] & 63u));
-                    if (K > 64) {
-                        const u64 ma1 = shfl_u64(cm1, (int)(pa[q] & 63u)), mb1 = shfl_u64(cm1, (int)(pb[q] & 63u));
-                        ma = pa[q] >= 64 ? ma1 : ma;
-                        mb = pb[q] >= 64 ? mb1 : mb;
-                    }
+                    ma = shfl_u64(cm, (int)(pa & 63u));
+                    mb = shfl_u64(cm, (int)(pb & 63u));
                 }
                 if (q * 64 + lane < ntp && ma && mb) {
                     u32 S, E, X;
@@ -2363,7 +2379,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 #pragma unroll
         for (int q = 0; q < RW_SLOTS; ++q) {
             if (q * 64 + lane < ntp) {
-                const size_t o = (size_t)pp[q] * G + cur;
+                const size_t o = (size_t)(tp[q] & 0xffffu) * G + cur;
                 if (aS[q]) atomicAdd((unsigned long long*)&A.accS[o], (unsigned long long)aS[q]);
                 if (aE[q]) atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)aE[q]);
                 if (aX[q]) atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)aX[q]);
@@ -3145,11 +3161,17 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 // tested pairs (<= XC_J per thread) in registers: one atomic per (gene, pair).
 // (The per-(gene, pair) wave version re-read the rows once per pair.)
 #define XC_T 256
-#define XC_Q 32                 // buckets per LDS round
+#define XC_Q 64                 // buckets per LDS round
 #define XC_KC SCC_MAX_K         // cluster columns held
 #define XC_J 8                  // tested pairs per thread per pass over the rows (2048)
+#define XC_PF ((XC_Q * XC_KC + XC_T - 1) / XC_T)  // histogram words a thread prefetches per round
 // SEG: the same sum over the sub-buckets of each re-split parent (the
 // in-parent cross term; segments from k_rank_resplit*, rsseg).
+// Each round's rows are loaded into registers while the previous round is
+// summed (its latency off the per-gene chain), and every pair's sum over a
+// round runs as four independent partial sums (the LDS reads in flight
+// together): one workgroup walks a gene's buckets in order, so the per-round
+// chain is what its time was (config D: 2.5 ms, D SLOW 7.8 ms before).
 template <bool SEG>
 __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
 {
@@ -3174,6 +3196,19 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
         }
         const int ntp = min(A.gene_nt[g], P);
         const u32* tl = A.gene_tp + (size_t)g * P;
+        const int nw = XC_Q * K;  // histogram words of a full round
+        // one round's rows into registers (clamped loads, masked past the gene)
+        u32 hv[XC_PF];
+        auto prefetch = [&](int q0) {
+            const unsigned int* h = A.hbg + (size_t)(bk0 + q0) * K;
+            const int lim = (min(XC_Q, nb - q0)) * K;
+#pragma unroll
+            for (int r = 0; r < XC_PF; ++r) {
+                const int e = r * XC_T + tid;
+                hv[r] = h[min(e, max(lim - 1, 0))];
+                if (e >= lim) hv[r] = 0u;
+            }
+        };
         for (int j0 = 0; j0 < ntp; j0 += XC_J * XC_T) {  // windows of 2048 tested pairs
             u32 pv[XC_J];
             u64 acc[XC_J];
@@ -3183,16 +3218,21 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
                 pv[u] = j < ntp ? tl[j] : 0u;
                 acc[u] = 0;
             }
+            if (nb > 0) prefetch(0);
             __syncthreads();
             if (tid < XC_KC) carry[tid] = 0;
             for (int q0 = 0; q0 < nb; q0 += XC_Q) {
                 const int nq = min(XC_Q, nb - q0);
                 __syncthreads();
-                const unsigned int* h = A.hbg + (size_t)(bk0 + q0) * K;
-                for (int e = tid; e < XC_Q * K; e += XC_T) {
-                    const int q = e / K, c = e - q * K;
-                    Hs[q][c] = q < nq ? h[e] : 0u;
+#pragma unroll
+                for (int r = 0; r < XC_PF; ++r) {
+                    const int e = r * XC_T + tid;
+                    if (e < nw) {
+                        const int q = e / K, c = e - q * K;
+                        Hs[q][c] = hv[r];
+                    }
                 }
+                if (q0 + XC_Q < nb) prefetch(q0 + XC_Q);  // the next round's rows, in flight meanwhile
                 __syncthreads();
                 // column scan: thread (c, part) sums RPP rows, parts combined through LDS
                 const int c = tid % XC_KC, part = tid / XC_KC;
@@ -3216,11 +3256,18 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
                 for (int u = 0; u < XC_J; ++u) {
                     if (j0 + u * XC_T + tid < ntp) {
                         const int a = (int)((pv[u] >> 16) & 0xffu), b = (int)(pv[u] >> 24);
-                        u64 sacc = 0;
-                        for (int q = 0; q < nq; ++q) sacc += (u64)Hs[q][a] * Cs[q][b];
-                        acc[u] += sacc;
+                        u64 s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // (rows past nq are zero)
+#pragma unroll 4
+                        for (int q = 0; q < XC_Q; q += 4) {
+                            s0 += (u64)Hs[q][a] * Cs[q][b];
+                            s1 += (u64)Hs[q + 1][a] * Cs[q + 1][b];
+                            s2 += (u64)Hs[q + 2][a] * Cs[q + 2][b];
+                            s3 += (u64)Hs[q + 3][a] * Cs[q + 3][b];
+                        }
+                        acc[u] += (s0 + s1) + (s2 + s3);
                     }
                 }
+                (void)nq;
             }
 #pragma unroll
             for (int u = 0; u < XC_J; ++u) {
@@ -3303,7 +3350,11 @@ struct SideStreams {
     {
         const int t = turn++;
         if (nside <= 0 || t % (nside + 1) == 0) return st0;
-        const int i = t % (nside + 1) - 1;
+        return pick(t % (nside + 1) - 1);
+    }
+    hipStream_t pick(int i)  // -1: st0; i: side[i] (st0 when there are fewer sides)
+    {
+        if (i < 0 || i >= nside) return st0;
         if (!used[i]) hipStreamWaitEvent(side[i], fork, 0);
         used[i] = true;
         return side[i];
@@ -3337,7 +3388,17 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
     // read only what the split wrote: they may run concurrently, so each takes
     // the next stream in turn and their tails overlap (a gene shard's grid is
     // an eighth of the whole job's and each launch ended on a long tail)
+    // With two sides (the runtime passes {a side stream, the LDS items'
+    // stream}: three hardware queues) the launches take fixed places, longest
+    // chains apart (config D timeline, profiles/r06_timeline_rank_d_*.txt):
+    // matrix-core genes on side 1 ahead of the items, <= 128 and <= 512
+    // tested pairs on side 0, <= 256 on st0.  Otherwise round robin.
     auto next_stream = [&]() { return ss.next(); };
+    auto place = [&](int role) {  // 0..3: slot class, 4: matrix cores, 5: windows
+        if (ss.nside < 2) return ss.next();
+        static const int where[6] = {0, -1, 0, 1, 1, -1};
+        return ss.pick(where[role]);
+    };
     hipStream_t st = ss.st0;
     // one launch per slot class present: genes with <= 128 tested pairs on the
     // 2-slot kernel, <= 256 on 4, <= 512 on 8, <= 1024 on 16
@@ -3353,7 +3414,7 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
         ScRankLaunch M = *L;
         M.wv_filter = L->rw_mfma == 2 ? 0 : 1;
         M.wv_lo = mfma_min;
-        st = next_stream();
+        st = place(4);
         if (L->K <= 32)
             hipLaunchKernelGGL(k_rank_mfma<1>, dim3(grid), dim3(256), 0, st, M);
         else
@@ -3383,7 +3444,7 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
         A.wv_hi = hi[c];
         A.wv_base = 0;
         A.wv_filter = L->rw_slots > 2 ? 1 : 0;  // rw_slots 2: class 0 is the only launch and holds every gene
-        st = next_stream();
+        st = place(c);
         if (c == 0)
             hipLaunchKernelGGL(k_rank_waves<2>, dim3(grid), dim3(256), 0, st, A);
         else if (c == 1)
@@ -3400,7 +3461,7 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
     if (L->rw_slots >= RW_SLOTS_MAX) {
         const int per = 64 * RW_SLOTS_MAX;
         const int npass = (std::min(L->ntp_max, RW_PAIRS_MAX) + per - 1) / per;
-        st = next_stream();  // (the windows in one stream)
+        st = place(5);  // (the windows in one stream)
         for (int k = 0; k < npass; ++k) {
             A.wv_lo = std::max(per, k * per);
             A.wv_hi = RW_PAIRS_MAX;

@@ -1007,8 +1007,11 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         if (L.dbg == 7) scc_rank_mfma_stamps(s0, 0);
         // the slot classes on s0 and two side streams (SCC_RW_STREAMS=0: all on s0)
         // (forked only when a second class launch exists: config B has one)
+        // (sides: one side stream and the items' stream s1 -- a second side
+        // stream shared the first one's hardware queue, GPU_MAX_HW_QUEUES = 4)
         const int rw_side = (env_int("SCC_RW_STREAMS", 1) != 0 && L.dbg != 7) ? 2 : 0;
-        HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0, c->sw, rw_side, c->ev_wfork, c->ev_wj));
+        const hipStream_t wsides[2] = {c->sw[0], si};
+        HIPCHK(c, scc_launch_rank_waves(&L, 8 * ncu, s0, si != s0 ? wsides : c->sw, rw_side, c->ev_wfork, c->ev_wj));
         if (L.dbg == 7) scc_rank_mfma_stamps(s0, 1);
         HIPCHK(c, scc_launch_rank_items(&L, 1, 2 * ncu, si));
         HIPCHK(c, scc_launch_rank_items(&L, 0, 4 * ncu, si));
@@ -1019,6 +1022,13 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         }
         HIPCHK(c, scc_launch_rank_cross(&L, 4 * ncu, s0));
         HIPCHK(c, scc_launch_rank_cross_seg(&L, 4 * ncu, s0));
+        if (env_int("SCC_RANK_LOG", 0)) {  // diagnostic: the rank stage's work lists
+            int h[16];
+            HIPCHK(c, hipMemcpyAsync(h, d_counts, sizeof(h), hipMemcpyDeviceToHost, s0));
+            HIPCHK(c, hipStreamSynchronize(s0));
+            fprintf(stderr, "[scc rank] items %d/%d/%d split genes %d wave buckets %d bucket ids %d parents %d "
+                    "segments %d second-level %d\n", h[0], h[1], h[2], h[3], h[4], h[5], h[8], h[10], h[12]);
+        }
         if (stamps) {
             std::vector<unsigned long long> h((size_t)3 * item_cap * 8);
             int cnts[4];
