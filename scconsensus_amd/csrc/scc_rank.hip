@@ -197,6 +197,15 @@ extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t 
 
 // ===================================================================== classify
 // counts: [0] small items, [1] medium items, [2] global-memory items, [3] split genes
+#define SPLIT_BIG 32768
+// split gene i of split_count(A) (the large ones first)
+__device__ inline int split_count(const ScRankLaunch& A) { return A.counts[3] + A.counts[13]; }
+__device__ inline int split_gene_at(const ScRankLaunch& A, int i)
+{
+    const int nbig = A.counts[13];
+    return i < nbig ? A.split_genes[A.G - 1 - i] : A.split_genes[i - nbig];
+}
+
 __global__ void k_rank_classify(ScRankLaunch A)
 {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -217,8 +226,14 @@ __global__ void k_rank_classify(ScRankLaunch A)
         }
         if (!any) return;
     }
-    const int s = atomicAdd(&A.counts[3], 1);  // every ranked gene is split into value buckets
-    A.split_genes[s] = g;
+    // every ranked gene is split into value buckets; genes of >= SPLIT_BIG
+    // values fill the list from its end (split_gene_at hands them out first:
+    // the split's queue runs longest first, so a gene shard's largest genes
+    // are not its tail)
+    if (n >= SPLIT_BIG)
+        A.split_genes[A.G - 1 - atomicAdd(&A.counts[13], 1)] = g;
+    else
+        A.split_genes[atomicAdd(&A.counts[3], 1)] = g;
 }
 
 extern "C" hipError_t scc_launch_rank_classify(const ScRankLaunch* L, hipStream_t st)
@@ -1336,16 +1351,16 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     SplitLds& L = *(SplitLds*)smem;
-    const int cnt = A.counts[3];
+    const int cnt = split_count(A);
     for (;;) {  // genes from a queue (their sizes vary by orders of magnitude)
         if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[6], 1);
         __syncthreads();
         const int i = L.next;
         if (i >= cnt) break;
         const u64 t0 = A.dbg >= 9 ? __builtin_amdgcn_s_memtime() : 0;
-        split_one_gene(A, A.split_genes[i], L);
+        split_one_gene(A, split_gene_at(A, i), L);
         if (A.dbg >= 9 && threadIdx.x == 0 && i < SPLIT_DIAG_MAX) {
-            const int g = A.split_genes[i];
+            const int g = split_gene_at(A, i);
             g_split_diag[i][0] = (unsigned long long)(A.gstart[g + 1] - A.gstart[g]);
             g_split_diag[i][1] = __builtin_amdgcn_s_memtime() - t0;
         }
@@ -3117,7 +3132,7 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 {
     const int lane = threadIdx.x & 63;
     const int W = blockIdx.x * 4 + scc_wave_id(), NW = gridDim.x * 4;
-    const int ng = SEG ? A.counts[10] : A.counts[3], P = A.P;
+    const int ng = SEG ? A.counts[10] : split_count(A), P = A.P;
     for (int f = W; f < ng * P; f += NW) {
         const int gi = f / P, p = f - gi * P;
         int g, bk0, nb;
@@ -3127,7 +3142,7 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
             bk0 = sg.y;
             nb = sg.z;
         } else {
-            g = A.split_genes[gi];
+            g = split_gene_at(A, gi);
             bk0 = A.gene_bk[2 * g];
             nb = A.gene_bk[2 * g + 1];
         }
@@ -3181,7 +3196,7 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
     __shared__ u32 carry[XC_KC];
     constexpr int NPART = XC_T / XC_KC, RPP = XC_Q / NPART;  // column-scan parts, rows per part
     const int tid = threadIdx.x, K = A.K, G = A.G, P = A.P;
-    const int ng = SEG ? A.counts[10] : A.counts[3];
+    const int ng = SEG ? A.counts[10] : split_count(A);
     for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
         int g, bk0, nb;
         if (SEG) {
@@ -3190,7 +3205,7 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
             bk0 = sg.y;
             nb = sg.z;
         } else {
-            g = A.split_genes[gi];
+            g = split_gene_at(A, gi);
             bk0 = A.gene_bk[2 * g];
             nb = A.gene_bk[2 * g + 1];
         }

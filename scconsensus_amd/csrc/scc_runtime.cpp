@@ -970,10 +970,10 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
         HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
         if (L.dbg >= 9) {  // per-gene split clocks (diagnostic; 10: without the unstaged stores)
-            int nsg = 0;
-            HIPCHK(c, hipMemcpyAsync(&nsg, d_counts + 3, sizeof(int), hipMemcpyDeviceToHost, s0));
+            int hc[16];
+            HIPCHK(c, hipMemcpyAsync(hc, d_counts, sizeof(hc), hipMemcpyDeviceToHost, s0));
             HIPCHK(c, hipStreamSynchronize(s0));
-            scc_rank_split_diag(s0, nsg);
+            scc_rank_split_diag(s0, hc[3] + hc[13]);  // (small split genes + large ones)
         }
         if (stamps) {  // re-split phase clocks (summed over parents): 8 u64 after the item stamps
             ScRankLaunch R = L;
@@ -1027,7 +1027,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
             HIPCHK(c, hipMemcpyAsync(h, d_counts, sizeof(h), hipMemcpyDeviceToHost, s0));
             HIPCHK(c, hipStreamSynchronize(s0));
             fprintf(stderr, "[scc rank] items %d/%d/%d split genes %d wave buckets %d bucket ids %d parents %d "
-                    "segments %d second-level %d\n", h[0], h[1], h[2], h[3], h[4], h[5], h[8], h[10], h[12]);
+                    "segments %d second-level %d\n", h[0], h[1], h[2], h[3] + h[13], h[4], h[5], h[8], h[10], h[12]);
         }
         if (stamps) {
             std::vector<unsigned long long> h((size_t)3 * item_cap * 8);
