@@ -3190,8 +3190,10 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 template <bool SEG>
 __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
 {
-    __shared__ u32 Hs[XC_Q][XC_KC + 1];
-    __shared__ u32 Cs[XC_Q][XC_KC + 1];
+    // cluster-major: a pair's rows of one round are contiguous, read 4 at a time
+    // (16-B LDS reads; the row stride XC_Q + 4 words spreads the clusters over banks)
+    __shared__ __attribute__((aligned(16))) u32 Hs[XC_KC][XC_Q + 4];
+    __shared__ __attribute__((aligned(16))) u32 Cs[XC_KC][XC_Q + 4];
     __shared__ u32 seg[XC_T / XC_KC][XC_KC];
     __shared__ u32 carry[XC_KC];
     constexpr int NPART = XC_T / XC_KC, RPP = XC_Q / NPART;  // column-scan parts, rows per part
@@ -3244,7 +3246,7 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
                     const int e = r * XC_T + tid;
                     if (e < nw) {
                         const int q = e / K, c = e - q * K;
-                        Hs[q][c] = hv[r];
+                        Hs[c][q] = hv[r];
                     }
                 }
                 if (q0 + XC_Q < nb) prefetch(q0 + XC_Q);  // the next round's rows, in flight meanwhile
@@ -3253,15 +3255,15 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
                 const int c = tid % XC_KC, part = tid / XC_KC;
                 u32 ssum = 0;
                 if (c < K)
-                    for (int q = part * RPP; q < part * RPP + RPP; ++q) ssum += Hs[q][c];
+                    for (int q = part * RPP; q < part * RPP + RPP; ++q) ssum += Hs[c][q];
                 seg[part][c] = ssum;
                 __syncthreads();
                 if (c < K) {
                     u32 run = carry[c];
                     for (int v = 0; v < part; ++v) run += seg[v][c];
                     for (int q = part * RPP; q < part * RPP + RPP; ++q) {
-                        Cs[q][c] = run;
-                        run += Hs[q][c];
+                        Cs[c][q] = run;
+                        run += Hs[c][q];
                     }
                 }
                 __syncthreads();
@@ -3272,12 +3274,15 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
                     if (j0 + u * XC_T + tid < ntp) {
                         const int a = (int)((pv[u] >> 16) & 0xffu), b = (int)(pv[u] >> 24);
                         u64 s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // (rows past nq are zero)
+                        const uint4* ha = (const uint4*)Hs[a];
+                        const uint4* cb = (const uint4*)Cs[b];
 #pragma unroll 4
-                        for (int q = 0; q < XC_Q; q += 4) {
-                            s0 += (u64)Hs[q][a] * Cs[q][b];
-                            s1 += (u64)Hs[q + 1][a] * Cs[q + 1][b];
-                            s2 += (u64)Hs[q + 2][a] * Cs[q + 2][b];
-                            s3 += (u64)Hs[q + 3][a] * Cs[q + 3][b];
+                        for (int q4 = 0; q4 < XC_Q / 4; ++q4) {
+                            const uint4 hx = ha[q4], cx = cb[q4];
+                            s0 += (u64)hx.x * cx.x;
+                            s1 += (u64)hx.y * cx.y;
+                            s2 += (u64)hx.z * cx.z;
+                            s3 += (u64)hx.w * cx.w;
                         }
                         acc[u] += (s0 + s1) + (s2 + s3);
                     }
@@ -3406,12 +3411,12 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
     // With two sides (the runtime passes {a side stream, the LDS items'
     // stream}: three hardware queues) the launches take fixed places, longest
     // chains apart (config D timeline, profiles/r06_timeline_rank_d_*.txt):
-    // matrix-core genes on side 1 ahead of the items, <= 128 and <= 512
-    // tested pairs on side 0, <= 256 on st0.  Otherwise round robin.
+    // matrix-core genes on side 1 ahead of the items, <= 128 tested pairs on
+    // side 0 (the largest class), <= 256 then <= 512 on st0.  Otherwise round robin.
     auto next_stream = [&]() { return ss.next(); };
     auto place = [&](int role) {  // 0..3: slot class, 4: matrix cores, 5: windows
         if (ss.nside < 2) return ss.next();
-        static const int where[6] = {0, -1, 0, 1, 1, -1};
+        static const int where[6] = {0, -1, -1, 1, 1, -1};
         return ss.pick(where[role]);
     };
     hipStream_t st = ss.st0;
