@@ -289,7 +289,7 @@ def de_only(a, eng, ds, d, code, K, dist, world, dataset_ms=None):
                "note": "scc_dataset_create_csr_device wall time (synchronised), CSR -> resident CSC; not in value"}
         if os.path.exists(tpath):
             tk = json.load(open(tpath))["kernels"]
-            hits = {k: v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith("k_csr")}
+            hits = {k: v["traffic_bytes_per_launch"] for k, v in tk.items() if k.startswith("k_ct_")}
             if hits:
                 dsb["traffic"] = sum(hits.values())
                 dsb["traffic_kernels"] = hits
@@ -405,7 +405,7 @@ def main():
                      devices=devices if route_devices and len(devices) > 1 else None)
     if a.config == "E":
         # the gene-major CSR is transposed into the resident CSC when the
-        # dataset is created (k_csr_count / k_csr_scatter): an R call on a
+        # dataset is created (k_ct_bounds / k_ct_tiles / k_ct_pass1 / k_ct_pass2): an R call on a
         # dgRMatrix pays it once per call, so it is timed and reported beside
         # the DE (first build: allocations; then the mean of repeated builds)
         build = []

@@ -138,7 +138,7 @@ SCC_API int scc_dataset_create_csc(scc_ctx* ctx, const int64_t* indptr, const in
  * would hold for the same matrix), so every result equals the CSC path's.
  * Column indices outside [0, N), or not strictly ascending within a gene
  * (unsorted, or a repeated (gene, cell)), fail with SCC_ERR_INVALID here;
- * more than 524,288 genes with SCC_ERR_UNSUPPORTED.  No
+ * more than 262,144 genes with SCC_ERR_UNSUPPORTED.  No
  * reference interface: the reference takes dataMatrix as an R matrix
  * (Fast:22, :368); this is the R-free caller's equivalent. */
 SCC_API int scc_dataset_create_csr(scc_ctx* ctx, const int64_t* indptr, const int32_t* cols, const double* vals,

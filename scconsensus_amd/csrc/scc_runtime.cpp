@@ -370,7 +370,7 @@ extern "C" int scc_dataset_create_csr(scc_ctx* c, const int64_t* indptr, const i
     ScCsrPlan plan;
     if (scc_csr_plan(G, N, nnz, &plan) != 0) {
         cleanup();
-        return fail(c, SCC_ERR_UNSUPPORTED, "scc_dataset_create_csr: more than 524,288 genes");
+        return fail(c, SCC_ERR_UNSUPPORTED, "scc_dataset_create_csr: more than 262,144 genes");
     }
     void* scratch = nullptr;
     int* d_err = nullptr;

@@ -8,15 +8,20 @@ test_gpu_de.py, D in test_gpu_large.py).
   exact-SVD oracle; 2e5 sampled entries of the Pearson `1 - cor` distance.
 * C (100k x 15k, K = 30) and E (1M-cell CSR, K = 100): the oracle on a seeded
   gene subset over all cells and pairs (exact tested sets, U, ties, pct; p and
-  logFC within the bar), every row's p restated from its exact 2U / ties and
+  logFC within the bar), EVERY tested row's exact 2U and tie term against an
+  independent full-size torch computation (tests/torch_ranksum.py: one global
+  sort and prefix counts), every row's p restated from its exact 2U / ties and
   the cluster sizes, the full-size selection restated from the engine's own
   rows, and at C sampled `dist` entries against the exact SVD.
 """
+import time
+
 import numpy as np
 import pytest
 import torch  # before the engine loads (torch's HIP runtime first)
 
 import oracle as O
+import torch_ranksum as TR
 from parity_helpers import (check_p_from_counts, check_rows_against_oracle_subset, check_selection, packed_index,
                             rows_of_gene_major, sample_cell_pairs)
 from scconsensus_amd import api, synth
@@ -102,6 +107,17 @@ def _de_large(name, n_genes_sample, seed, dist_pairs=0):
     assert 100 < len(g.union) <= 30 * P
     check_selection(r, g.union, K)
     assert check_p_from_counts(r, code, K) == len(r.gene)  # every row's p from its exact counts
+    # EVERY tested row's exact 2U and tie term against an independent full-size torch computation
+    t0 = time.perf_counter()
+    u2_all, ties_all = TR.pair_stats(d.indptr, d.indices, d.data, code, K, max_chunk=min(16 << 20, (512 << 20) // K))
+    gi = torch.from_numpy(r.gene.astype(np.int64)).to("cuda:0")
+    pi = torch.from_numpy(r.row_pair.astype(np.int64)).to("cuda:0")
+    np.testing.assert_array_equal(u2_all[gi, pi].cpu().numpy(), r.u2)
+    np.testing.assert_array_equal(ties_all[gi, pi].cpu().numpy(), r.ties)
+    print(f"{name}: {len(r.gene)} rows checked against the full-size torch rank sums "
+          f"({time.perf_counter() - t0:.1f} s)")
+    del u2_all, ties_all, gi, pi
+    _free()
     # the oracle on a seeded gene sample: half drawn from the tested rows, half uniform
     rng = np.random.default_rng(seed)
     tg = np.unique(r.gene)

@@ -3,7 +3,9 @@ the device, with the input generated in HBM as a gene-major CSR (so the CSR
 transpose runs at full size too).
 
 DE: full-size properties (U within [0, 2 n_a n_b]; the re-split route and the
-plain LDS-item route bit-identical), the oracle on a seeded gene subset over
+plain LDS-item route bit-identical), every tested row's exact 2U and tie term
+(and under SLOW all 1225 x 20000 2U values) against an independent full-size
+torch computation (tests/torch_ranksum.py), the oracle on a seeded gene subset over
 all cells and pairs (exact tested sets, U, ties, pct; p / logFC within the
 bar), and the full-size per-pair selection restated from the engine's rows.
 Distance: the 2e10-entry packed fp64 `dist` (160 GB, HBM-resident) on 2e5
@@ -13,6 +15,7 @@ import pytest
 import torch  # before the engine loads (torch's HIP runtime first)
 
 import oracle as O
+import torch_ranksum as TR
 from parity_helpers import (check_p_from_counts, check_rows_against_oracle_subset, check_selection,
                             check_slow_against_oracle_subset,
                             check_slow_selection, packed_index, rows_of_gene_major, sample_cell_pairs, slow_gate,
@@ -44,6 +47,14 @@ def test_config_d_parity(monkeypatch):
     assert 100 < len(g.union) <= 30 * len(pairs)
     check_selection(r, g.union, K)
     assert check_p_from_counts(r, code, K) == len(r.gene)  # every row's p from its exact counts
+    # EVERY tested row's exact 2U and tie term against the independent full-size torch rank sums
+    u2_all, ties_all = TR.pair_stats(d.indptr, d.indices, d.data, code, K, max_chunk=(512 << 20) // K)
+    gi = torch.from_numpy(r.gene.astype(np.int64)).to("cuda:0")
+    pi = torch.from_numpy(r.row_pair.astype(np.int64)).to("cuda:0")
+    np.testing.assert_array_equal(u2_all[gi, pi].cpu().numpy(), r.u2)
+    np.testing.assert_array_equal(ties_all[gi, pi].cpu().numpy(), r.ties)
+    _say(f"D: {len(r.gene)} rows match the full-size torch rank sums")
+    del u2_all, ties_all, gi, pi
     # the same DE with the re-split route off (fat buckets ranked as LDS items)
     # and the gene-level cross terms by the per-(gene, pair) wave kernel
     monkeypatch.setenv("SCC_RESPLIT", "0")
@@ -105,6 +116,11 @@ def test_config_d_slow():
     g = eng.de_run(ds, code, K, nat.SCC_DE_SLOW, q_val_thrs=qthr, fc_thrs=fc, mean_scaling_factor=msf, fetch="all")
     assert g.p.shape == (1225, d.G)
     _say("SLOW D engine done")
+    # ALL 1225 x 20000 exact 2U values against the independent full-size torch rank sums
+    u2_all, _ = TR.pair_stats(d.indptr, d.indices, d.data, code, K, max_chunk=(512 << 20) // K)
+    np.testing.assert_array_equal(u2_all.T.cpu().numpy(), g.u2)
+    del u2_all
+    _say("SLOW D: all 24.5 M (pair, gene) 2U values match the torch rank sums")
     assert g.log_thr == pytest.approx(slow_log_threshold(d.data.cpu().numpy(), d.G, d.N, msf), rel=1e-13)
     ip = d.indptr.cpu().numpy()
     rng = np.random.default_rng(12)

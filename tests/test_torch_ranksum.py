@@ -1,0 +1,37 @@
+"""The full-size torch rank-sum checker (tests/torch_ranksum.py) against a
+brute-force count on small CPU cases with heavy ties, empty genes and
+unclustered cells -- the checker is pinned before it judges the engine."""
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+import torch_ranksum as TR
+
+
+def _brute(X, code, K):
+    G = X.shape[0]
+    pairs = [(i, j) for i in range(K - 1) for j in range(i + 1, K)]
+    u2 = np.zeros((G, len(pairs)), np.int64)
+    ties = np.zeros((G, len(pairs)), np.int64)
+    for g in range(G):
+        for p, (a, b) in enumerate(pairs):
+            xa, xb = X[g, code == a], X[g, code == b]
+            u2[g, p] = 2 * (xa[:, None] > xb[None, :]).sum() + (xa[:, None] == xb[None, :]).sum()
+            _, t = np.unique(np.concatenate([xa, xb]), return_counts=True)
+            ties[g, p] = (t ** 3 - t).sum()
+    return u2, ties
+
+
+def test_checker_matches_brute_force():
+    rng = np.random.default_rng(7)
+    for G, N, K, dens, chunk in [(9, 60, 4, 0.4, 16 << 20), (7, 50, 5, 0.7, 23), (5, 40, 3, 0.0, 16 << 20)]:
+        X = np.where(rng.random((G, N)) < dens, rng.integers(1, 5, (G, N)) * 0.5, 0.0)
+        X[2] = 0.0                      # an empty gene
+        code = rng.integers(-1, K, N)   # -1: a cell outside every cluster
+        code[:K] = np.arange(K)
+        A = sp.csr_matrix(X)
+        u2, ties = TR.pair_stats(torch.from_numpy(A.indptr.astype(np.int64)), torch.from_numpy(A.indices.astype(np.int32)),
+                                 torch.from_numpy(A.data), code, K, max_chunk=chunk)
+        bu, bt = _brute(X, code, K)
+        np.testing.assert_array_equal(u2.numpy(), bu)
+        np.testing.assert_array_equal(ties.numpy(), bt)
