@@ -67,7 +67,7 @@ struct ScRankLaunch {
     int wv_lo, wv_hi;      // wave kernel launch: genes with wv_lo < tested pairs <= wv_hi
     int wv_base;           // ... and their tested pairs [wv_base, wv_base + 64 * slots)
     int wv_filter;         // 0: one launch holds every gene (no per-bucket class test)
-    int rw_mfma;           // K <= 64: the wave buckets' pair counts on the int8 matrix cores (k_rank_mfma)
+    int rw_mfma;           // K <= 64: the wave buckets' pair counts on the int8 matrix cores (k_rank_mfma16)
     int rw_mfma16;         // the 16 x 16 x 64 form for the genes the slot kernels take (k_rank_mfma16): -1 at K <= 16, 1 at K <= 32, 0 off
     ScRankItem* fatbk;     // [fat_cap] buckets of > 64 distinct values (re-split into sub-buckets)
     int4* fatg;            // [G] {gene, first fatbk entry, parents}: the re-split work units

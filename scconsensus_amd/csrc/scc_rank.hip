@@ -2415,27 +2415,14 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
 //   E += O^T Q                     sum over groups t_a t_b
 //   X += (D O)^T Q + Q^T (D O)     sum over groups t_a^2 t_b + t_a t_b^2
 // Every operand is 0/1 or a count <= 64 (int8) and one bucket's products fit
-// int32.  A gene's sums stay in the accumulator tiles (the upper 32 x 32 tiles
+// int32.  A gene's sums stay in the accumulator tiles (the upper 16 x 16 tiles
 // of the K x K matrices hold every pair a < b) and leave with one integer
-// atomic per tested pair when the gene changes: 12 MFMAs per bucket at
-// K <= 64 without ties, 36 with, whatever the number of tested pairs (the
-// per-pair walk of k_rank_waves ran 16 slots of 64 pairs per bucket at
-// config D).  Same bucket list, same hbg rows and F terms, same integers.
-//
-// Operand slots: lane l holds row / column l & 31 of a 32 x 32 x 32 step and,
-// in byte t of its fragment (lane half h = l >> 5), the element
-//   pi(h, t) = (t & 3) + 8 (t >> 2) + 4 h        of the step's 32-element block,
-// which is the row the accumulator layout puts in register t of lane half h:
-// an accumulator tile packed to bytes is the next product's operand as it
-// stands (the other operand built in the same slot order).
+// atomic per tested pair when the gene changes: at K <= 64 (NC = 4 cluster
+// tiles) 26 MFMAs 16x16x64 per bucket without ties, 72 with, whatever the
+// number of tested pairs (the per-pair walk of k_rank_waves ran 16 slots of 64
+// pairs per bucket at config D).  Same bucket list, same hbg rows and F terms,
+// same integers.
 typedef int rk_v4i __attribute__((ext_vector_type(4)));
-typedef int rk_v16i __attribute__((ext_vector_type(16)));
-
-__device__ inline rk_v16i rk_mfma(rk_v4i a, rk_v4i b, rk_v16i c)
-{
-    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
-}
-
 // bytes [base + q < x], q = 0..3 (0 / 1 each)
 __device__ inline u32 rk_lt_bytes(int x, int base)
 {
@@ -2450,17 +2437,6 @@ __device__ inline u32 rk_eq_bytes(u32 w, u32 c)
     const u32 x = w ^ (c * 0x01010101u);
     const u32 nz = ((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x;  // bit 7 of a byte: the byte is not zero
     return (~nz >> 7) & 0x01010101u;
-}
-
-// accumulator rows (values < 128) -> operand bytes, register t into byte t
-__device__ inline rk_v4i rk_pack(const rk_v16i& m)
-{
-    rk_v4i r;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-        r[d] = (m[4 * d] & 0xff) | ((m[4 * d + 1] & 0xff) << 8) | ((m[4 * d + 2] & 0xff) << 16) |
-               ((m[4 * d + 3] & 0xff) << 24);
-    return r;
 }
 
 __device__ unsigned long long g_rk_stamps[8];  // SCC_RK_STAMPS diagnostics: summed phase cycles
@@ -2486,328 +2462,11 @@ struct RkWaveLds {
     u64 F[64];    // within-cluster tie terms of the current gene, per cluster
 };
 
-template <int NT>
-__global__ void __launch_bounds__(256) k_rank_mfma(ScRankLaunch A)
-{
-    constexpr int NTL = NT == 1 ? 1 : 3;   // accumulator tiles (ma, nb), ma <= nb: (0,0) (0,1) (1,1)
-    constexpr int TL = NT == 1 ? 8 : 32;   // tested-pair list entries per lane (P <= 496 / 2016)
-    __shared__ __attribute__((aligned(16))) RkWaveLds Ls[4];
-    __shared__ u32 Lbuf[4][NTL * 1024];    // one accumulator matrix of a flush, [tile][a & 31][b & 31]
-    const int lane = threadIdx.x & 63, wv = scc_wave_id();
-    RkWaveLds& Lw = Ls[wv];
-    u32* buf = Lbuf[wv];
-    const int NW = gridDim.x * 4, W = blockIdx.x * 4 + wv;
-    const int cnt = min(A.counts[4], A.bucket_cap);
-    const int K = A.K, G = A.G, P = A.P;
-    // consecutive buckets per wave visit: long runs of one gene (a gene's sums
-    // leave once per run), about four visits per wave
-    const int CH = max(16, min(512, cnt / (4 * NW)));
-    const int h = lane >> 5, i0 = lane & 31;
-    // L[i][j] = [j < i] for rows i0 (+ 32) against columns of the same block
-    rk_v4i Lc;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) Lc[d] = (int)rk_lt_bytes(i0, 8 * d + 4 * h);
-    const rk_v4i ones = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
-    const rk_v16i zero = {};
-    // R = 2 S + E (k_pair_test reads 2 accS + accE only: R goes to accE), X
-    rk_v16i R[NTL], X[NTL];
-#pragma unroll
-    for (int t = 0; t < NTL; ++t) R[t] = X[t] = zero;
-    Lw.F[lane] = 0;
-    int cur = -1, ntp = 0, nrun = 0;
-    bool rtie = false;
-    u64 gk = ~0ull;
-    const bool stm = A.dbg == 7;  // SCC_RW_DEBUG=7: phase clocks into g_rk_stamps
-    u64 tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tprev = stm ? __builtin_amdgcn_s_memtime() : 0;
-    auto stamp = [&](int ph) {
-        if (stm) {
-            const u64 t = __builtin_amdgcn_s_memtime();
-            tph[ph] += t - tprev;
-            tprev = t;
-        }
-    };
-    // the gene's sums out: its tested-pair list into registers first (no load
-    // waits behind the atomics), the tiles through LDS, one integer atomic per
-    // tested pair with a nonzero sum
-    auto flush = [&]() {
-        ++tph[7];
-        const u32* tl = A.gene_tp + (size_t)cur * P;
-        u32 tv[TL];
-#pragma unroll
-        for (int q = 0; q < TL; ++q) tv[q] = tl[min(q * 64 + lane, max(ntp - 1, 0))];
-        auto out = [&](rk_v16i* Mx, unsigned long long* acc) {
-#pragma unroll
-            for (int t = 0; t < NTL; ++t) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) buf[t * 1024 + ((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + i0] = (u32)Mx[t][r];
-                Mx[t] = zero;
-            }
-            wsync();
-#pragma unroll
-            for (int q = 0; q < TL; ++q) {
-                if (q * 64 >= ntp) break;
-                const u32 v = tv[q];
-                const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
-                const u32 x = buf[((a >> 5) + (b >> 5)) * 1024 + (a & 31) * 32 + (b & 31)];
-                if (q * 64 + lane < ntp && x) atomicAdd(&acc[(size_t)(v & 0xffffu) * G + cur], (unsigned long long)x);
-            }
-            wsync();
-        };
-        out(R, (unsigned long long*)A.accE);
-        if (rtie) {
-            out(X, (unsigned long long*)A.accX);
-            const u64 f = Lw.F[lane];
-            if (lane < K && f) atomicAdd((unsigned long long*)&A.accF[(size_t)lane * G + cur], (unsigned long long)f);
-            Lw.F[lane] = 0;
-            wsync();
-        }
-        nrun = 0;
-        rtie = false;
-    };
-    for (int c0 = W * CH; c0 < cnt; c0 += NW * CH) {
-        const int c1 = min(cnt, c0 + CH);
-        for (int s0 = c0; s0 < c1; s0 += 64) {
-            const int s1 = min(c1, s0 + 64);
-            ScRankItem D{0, 0, 0, 0, 0};
-            if (lane < s1 - s0) D = A.sbuckets[s0 + lane];
-            u64 rem;
-            if (A.wv_filter) {  // this launch ranks the buckets of genes with more than wv_lo tested pairs
-                const int ntg = (lane < s1 - s0 && D.n > 0) ? A.gene_nt[D.gene] : -1;
-                rem = __ballot(ntg > A.wv_lo);
-            } else {
-                rem = __ballot(lane < s1 - s0 && D.n > 0);  // n = 0: an unused re-split slot
-            }
-            if (!rem) continue;
-            const u32 dlo = (u32)(u64)D.base, dhi = (u32)((u64)D.base >> 32);
-            auto dbase = [&](int li) {
-                return (i64)(((u64)(u32)__builtin_amdgcn_readlane((int)dhi, li) << 32) |
-                             (u32)__builtin_amdgcn_readlane((int)dlo, li));
-            };
-            u64 nkey;
-            u32 ncode;
-            {
-                const int l0 = __builtin_ctzll(rem);
-                const i64 b0 = dbase(l0);
-                const int n0 = __builtin_amdgcn_readlane(D.n, l0);
-                nkey = lane < n0 ? A.keys2[b0 + lane] : ~0ull;
-                ncode = lane < n0 ? (u32)A.codes2[b0 + lane] : 255u;
-            }
-            while (rem) {
-                const int li = __builtin_ctzll(rem);
-                rem &= rem - 1;
-                const int g = __builtin_amdgcn_readlane(D.gene, li);
-                const int n = __builtin_amdgcn_readlane(D.n, li);
-                const int bucket = __builtin_amdgcn_readlane(D.bucket, li);
-                const int src = __builtin_amdgcn_readlane(D.src, li);
-                const i64 bbase = dbase(li);
-                u64 key = nkey;
-                u32 code = ncode;
-                if (rem) {
-                    const int l1 = __builtin_ctzll(rem);
-                    const i64 b1 = dbase(l1);
-                    const int n1 = __builtin_amdgcn_readlane(D.n, l1);
-                    nkey = lane < n1 ? A.keys2[b1 + lane] : ~0ull;
-                    ncode = lane < n1 ? (u32)A.codes2[b1 + lane] : 255u;
-                }
-                if (g != cur || nrun >= 16384) {  // (16384 buckets keep every int32 sum from wrapping)
-                    if (cur >= 0) flush();
-                    if (g != cur) {
-                        cur = g;
-                        gk = A.gkmin[g];
-                        ntp = A.gene_nt[g];
-                    }
-                }
-                ++nrun;
-                ++tph[6];
-                stamp(4);
-                if (src == 2) {
-                    // one repeated key: only the cluster histogram matters (as in
-                    // k_rank_waves); its products can pass int32, so they go straight out
-                    u32 myc = 0;
-                    for (int i00 = 0; i00 < n; i00 += 256) {
-                        u32 cd[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int i = i00 + u * 64 + lane;
-                            cd[u] = i < n ? (u32)A.codes2[bbase + i] : 255u;
-                        }
-                        for (int c = 0; c < K; ++c) {
-                            u32 t = 0;
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) t += (u32)__popcll(__ballot(cd[u] == (u32)c));
-                            if (lane == c) myc += t;
-                        }
-                    }
-                    if (lane < K) {
-                        A.hbg[(size_t)bucket * K + lane] = myc;
-                        if (myc >= 2) Lw.F[lane] += f_tie(myc);
-                    }
-                    rtie = true;
-                    Lw.cnt[lane] = myc;
-                    wsync();
-                    const u32* tl = A.gene_tp + (size_t)g * P;
-                    for (int j = lane; j < ntp; j += 64) {
-                        const u32 v = tl[j];
-                        const u64 ca = Lw.cnt[(v >> 16) & 0xffu], cb = Lw.cnt[v >> 24];
-                        if (ca && cb) {
-                            const size_t o = (size_t)(v & 0xffffu) * G + g;
-                            atomicAdd((unsigned long long*)&A.accE[o], (unsigned long long)(ca * cb));
-                            atomicAdd((unsigned long long*)&A.accX[o], (unsigned long long)(ca * cb * (ca + cb)));
-                        }
-                    }
-                    wsync();
-                    stamp(5);
-                    continue;
-                }
-                // ---- bitonic sort by (key, code) across the lanes (invalid lanes last)
-                const bool vl = lane < n;
-                if (gk != ~0ull) {
-                    u64 ck = vl ? (((key - gk) << SCC_CODE_BITS) | code) : ~0ull;
-                    if (n > 1) bitonic_merge_ck<1, 2>(ck);
-                    if (n > 2) bitonic_merge_ck<2, 4>(ck);
-                    if (n > 4) bitonic_merge_ck<4, 8>(ck);
-                    if (n > 8) bitonic_merge_ck<8, 16>(ck);
-                    if (n > 16) bitonic_merge_ck<16, 32>(ck);
-                    if (n > 32) bitonic_merge_ck<32, 0>(ck);
-                    key = ck >> SCC_CODE_BITS;
-                    code = vl ? (u32)(ck & SCC_CODE_MASK) : 255u;
-                } else {
-                    if (n > 1) bitonic_merge<1>(key, code, (lane & 2) == 0, lane);
-                    if (n > 2) bitonic_merge<2>(key, code, (lane & 4) == 0, lane);
-                    if (n > 4) bitonic_merge<4>(key, code, (lane & 8) == 0, lane);
-                    if (n > 8) bitonic_merge<8>(key, code, (lane & 16) == 0, lane);
-                    if (n > 16) bitonic_merge<16>(key, code, (lane & 32) == 0, lane);
-                    if (n > 32) bitonic_merge<32>(key, code, true, lane);
-                }
-                stamp(0);
-                // ---- one-hot operand: the sorted codes at their slots
-                const int sg = (lane & 32) | (((lane >> 2) & 1) << 4) | (((lane >> 3) & 3) << 2) | (lane & 3);
-                Lw.code[sg] = (u8)code;
-                wsync();
-                const bool two = n > 32;
-                rk_v4i cw[2];
-                cw[0] = *(const rk_v4i*)(Lw.code + 16 * h);
-                cw[1] = *(const rk_v4i*)(Lw.code + 32 + 16 * h);
-                rk_v4i ob[NT][2];
-#pragma unroll
-                for (int t = 0; t < NT; ++t)
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) ob[t][ks][d] = (int)rk_eq_bytes((u32)cw[ks][d], (u32)(i0 + 32 * t));
-                // the bucket's cluster histogram row (bytes are 0 / 1: byte sums <= 8)
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    u32 sm = 0;
-#pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) sm += (u32)ob[t][ks][d];
-                    u32 c = (sm * 0x01010101u) >> 24;
-                    c += (u32)__shfl_xor((int)c, 32, 64);
-                    if (h == 0 && i0 + 32 * t < K) A.hbg[(size_t)bucket * K + i0 + 32 * t] = c;
-                }
-                stamp(1);
-                // ---- M = L O, R += O^T (2 M)
-                rk_v4i mb[2][NT];
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    rk_v16i m0 = rk_mfma(Lc, ob[t][0], zero);
-                    mb[0][t] = rk_pack(m0 + m0);
-                    if (two) {
-                        rk_v16i m1 = rk_mfma(Lc, ob[t][1], rk_mfma(ones, ob[t][0], zero));
-                        mb[1][t] = rk_pack(m1 + m1);
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < NTL; ++t) {
-                    const int ma = (NT == 1 || t < 2) ? 0 : 1, nb = (NT == 1 || t == 0) ? 0 : 1;
-                    R[t] = rk_mfma(ob[ma][0], mb[0][nb], R[t]);
-                    if (two) R[t] = rk_mfma(ob[ma][1], mb[1][nb], R[t]);
-                }
-                stamp(2);
-                // ---- tie groups (equal keys) and runs (equal key and cluster)
-                const u64 kp = ((u64)(u32)__shfl_up((int)(u32)(key >> 32), 1, 64) << 32) |
-                               (u64)(u32)__shfl_up((int)(u32)key, 1, 64);
-                const u32 cpv = (u32)__shfl_up((int)code, 1, 64);
-                const u64 vmask = (n >= 64) ? ~0ull : ((1ull << n) - 1);
-                const bool gs_me = (lane == 0) || (kp != key);
-                const u64 gst = __ballot(gs_me && vl);
-                const bool anytie = ((~gst) & vmask & ~1ull) != 0;
-                if (anytie) {
-                    rtie = true;
-                    const u64 le = (lane == 63) ? ~0ull : ((2ull << lane) - 1);  // lanes <= me
-                    const bool rs_me = (lane == 0) || (kp != key) || (cpv != code);
-                    const u64 rst = __ballot(rs_me && vl);
-                    const u64 raft = rst & ~le;
-                    const int re = raft ? __builtin_ctzll(raft) : n;
-                    const int rs = 63 - __clzll((long long)((rst & le) | 1ull));
-                    if (rs_me && vl && re - lane >= 2)  // within-cluster runs: F_a += len^3 - len
-                        atomicAdd((unsigned long long*)&Lw.F[code], (unsigned long long)f_tie((u64)(re - lane)));
-                    const int gs = 63 - __clzll((long long)((gst & le) | 1ull));
-                    const u64 gaft = gst & ~le;
-                    const int ge = gaft ? __builtin_ctzll(gaft) : n;
-                    Lw.dcnt[sg] = (u8)(vl ? re - rs : 0);
-                    wsync();
-                    rk_v4i dw[2];
-                    dw[0] = *(const rk_v4i*)(Lw.dcnt + 16 * h);
-                    dw[1] = *(const rk_v4i*)(Lw.dcnt + 32 + 16 * h);
-                    rk_v4i odb[NT][2];
-#pragma unroll
-                    for (int t = 0; t < NT; ++t)
-#pragma unroll
-                        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                            for (int d = 0; d < 4; ++d) odb[t][ks][d] = (int)(((u32)ob[t][ks][d] * 0xffu) & (u32)dw[ks][d]);
-                    // Q = Eq O, rows i0 + 32 mt (their group bounds from the row's lane)
-                    rk_v4i qb[2][NT];
-#pragma unroll
-                    for (int mt = 0; mt < 2; ++mt) {
-                        if (mt == 1 && !two) break;
-                        const int gsr = __shfl(gs, i0 + 32 * mt, 64), ger = __shfl(ge, i0 + 32 * mt, 64);
-                        rk_v4i eq[2];
-#pragma unroll
-                        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-                            for (int d = 0; d < 4; ++d) {
-                                const int base = 32 * ks + 8 * d + 4 * h;
-                                eq[ks][d] = (int)(rk_lt_bytes(ger, base) - rk_lt_bytes(gsr, base));
-                            }
-#pragma unroll
-                        for (int t = 0; t < NT; ++t) {
-                            rk_v16i q = rk_mfma(eq[0], ob[t][0], zero);
-                            if (two) q = rk_mfma(eq[1], ob[t][1], q);
-                            qb[mt][t] = rk_pack(q);
-                        }
-                    }
-#pragma unroll
-                    for (int t = 0; t < NTL; ++t) {
-                        const int ma = (NT == 1 || t < 2) ? 0 : 1, nb = (NT == 1 || t == 0) ? 0 : 1;
-#pragma unroll
-                        for (int mt = 0; mt < 2; ++mt) {
-                            if (mt == 1 && !two) break;
-                            R[t] = rk_mfma(ob[ma][mt], qb[mt][nb], R[t]);
-                            X[t] = rk_mfma(odb[ma][mt], qb[mt][nb], X[t]);
-                            X[t] = rk_mfma(qb[mt][ma], odb[nb][mt], X[t]);
-                        }
-                    }
-                    wsync();
-                }
-                wsync();  // the code slots are rewritten by the next bucket
-                stamp(3);
-            }
-        }
-    }
-    if (cur >= 0) flush();
-    stamp(4);
-    if (stm && lane == 0)
-        for (int q = 0; q < 8; ++q) atomicAdd(&g_rk_stamps[q], (unsigned long long)tph[q]);
-}
-
-// The same products on 16 x 16 x 64 tiles (K <= 16 * NC): one MFMA covers a
+// The products on 16 x 16 x 64 tiles (K <= 16 * NC): one MFMA covers a
 // bucket's 64 elements, a cluster tile is 4 accumulator registers, so the
-// kernel stays small enough for several waves per SIMD (the 32 x 32 form's
-// per-bucket chain was latency-exposed at one or two).  Slots: lane l holds
+// kernel keeps two waves per SIMD even at K = 64 (a 32 x 32 x 32 form of the
+// same products held 1 wave at 422 registers: D SLOW rank 60.8 ms against
+// 42.3 ms for this one, round 6).  Slots: lane l holds
 // row / column l & 15 and, in byte t of its 16-byte fragment (lane group
 // g = l >> 4), element e(g, t) = 16 (t >> 2) + 4 g + (t & 3): the row the
 // accumulator layout puts in register t & 3 of lane group g of row tile
@@ -2824,10 +2483,10 @@ __device__ constexpr int rk_tile16(int ma, int nb)  // upper tiles (ma <= nb) in
 }
 
 template <int NC>
-__global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
+__global__ void __launch_bounds__(256, NC >= 3 ? 2 : 1) k_rank_mfma16(ScRankLaunch A)  // NC >= 3: 2 waves / SIMD (NC = 4: 23 VGPRs spill)
 {
     constexpr int NTL = NC * (NC + 1) / 2;
-    constexpr int TL = NC == 1 ? 2 : 8;  // tested-pair list entries per lane (P <= 120 / 496)
+    constexpr int TL = NC == 1 ? 2 : NC == 2 ? 8 : 32;  // tested-pair list entries per lane (P <= 120 / 496 / 2016)
     __shared__ __attribute__((aligned(16))) RkWaveLds Ls[4];
     __shared__ u32 Lbuf[4][NTL * 256];   // one accumulator matrix of a flush, [tile][a & 15][b & 15]
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
@@ -2839,12 +2498,14 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
     const int CH = max(16, min(512, cnt / (4 * NW)));
     const int g4 = lane >> 4, r16 = lane & 15;
     const rk_v4i zero = {0, 0, 0, 0};
-    // L rows 16 mt + r16: bytes [e(g4, t) < i] (constant per lane)
-    rk_v4i Lm[4];
+    // L rows 16 mt + r16: bytes [e(g4, t) < i] (formed where used: held for the
+    // whole kernel they were 16 registers of the 2-waves-per-SIMD budget at NC = 4)
+    auto Lrow = [&](int mt) {
+        rk_v4i l;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) Lm[mt][d] = (int)rk_lt_bytes(16 * mt + r16, 16 * d + 4 * g4);
+        for (int d = 0; d < 4; ++d) l[d] = (int)rk_lt_bytes(16 * mt + r16, 16 * d + 4 * g4);
+        return l;
+    };
     rk_v4i R[NTL], X[NTL];
 #pragma unroll
     for (int t = 0; t < NTL; ++t) R[t] = X[t] = zero;
@@ -2864,9 +2525,9 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
     auto flush = [&]() {
         ++tph[7];
         const u32* tl = A.gene_tp + (size_t)cur * P;
-        u32 tv[TL];
-#pragma unroll
-        for (int q = 0; q < TL; ++q) tv[q] = tl[min(q * 64 + lane, max(ntp - 1, 0))];
+        // the tested-pair list in register chunks of <= 8 entries a lane (a
+        // whole 2016-pair list in registers would cost the kernel its occupancy)
+        constexpr int TLC = TL < 8 ? TL : 8;
         auto out = [&](rk_v4i* Mx, unsigned long long* acc) {
 #pragma unroll
             for (int ma = 0; ma < NC; ++ma)
@@ -2878,13 +2539,20 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                     Mx[t] = zero;
                 }
             wsync();
+            for (int q0 = 0; q0 < TL; q0 += TLC) {
+                if (q0 * 64 >= ntp) break;
+                u32 tv[TLC];
 #pragma unroll
-            for (int q = 0; q < TL; ++q) {
-                if (q * 64 >= ntp) break;
-                const u32 v = tv[q];
-                const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
-                const u32 x = buf[rk_tile16<NC>(a >> 4, b >> 4) * 256 + (a & 15) * 16 + (b & 15)];
-                if (q * 64 + lane < ntp && x) atomicAdd(&acc[(size_t)(v & 0xffffu) * G + cur], (unsigned long long)x);
+                for (int q = 0; q < TLC; ++q) tv[q] = tl[min((q0 + q) * 64 + lane, max(ntp - 1, 0))];
+#pragma unroll
+                for (int q = 0; q < TLC; ++q) {
+                    if ((q0 + q) * 64 >= ntp) break;
+                    const u32 v = tv[q];
+                    const int a = (int)((v >> 16) & 0xffu), b = (int)(v >> 24);
+                    const u32 x = buf[rk_tile16<NC>(a >> 4, b >> 4) * 256 + (a & 15) * 16 + (b & 15)];
+                    if ((q0 + q) * 64 + lane < ntp && x)
+                        atomicAdd(&acc[(size_t)(v & 0xffffu) * G + cur], (unsigned long long)x);
+                }
             }
             wsync();
         };
@@ -2955,7 +2623,7 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
                 ++nrun;
                 ++tph[6];
                 stamp(4);
-                if (src == 2) {  // one repeated key (as k_rank_mfma)
+                if (src == 2) {  // one repeated key: only the cluster histogram matters (as in k_rank_waves)
                     u32 myc = 0;
                     for (int i00 = 0; i00 < n; i00 += 256) {
                         u32 cd[4];
@@ -3040,9 +2708,10 @@ __global__ void __launch_bounds__(256) k_rank_mfma16(ScRankLaunch A)
 #pragma unroll
                 for (int mt = 0; mt < 4; ++mt) {
                     if (mt >= nmt) break;
+                    const rk_v4i Lmt = Lrow(mt);
 #pragma unroll
                     for (int t = 0; t < NC; ++t) {
-                        const rk_v4i m = rk_mfma16(Lm[mt], ob[t], zero);
+                        const rk_v4i m = rk_mfma16(Lmt, ob[t], zero);
                         mb[t][mt] = (int)((u32)(2 * m[0]) | ((u32)(2 * m[1]) << 8) | ((u32)(2 * m[2]) << 16) |
                                           ((u32)(2 * m[3]) << 24));
                     }
@@ -3426,7 +3095,8 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
     // fixed cost: it takes the genes with more than 512 tested pairs (SLOW at
     // config D: every gene, 1225 pairs), the slot kernels the others
     // (SCC_RANK_MFMA=2: every gene on the matrix cores, 0: none)
-    // (from 256 or 128 tested pairs measured slower at config D: 37.2 / 53.0 vs 34.2 ms)
+    // (from 256 or 128 tested pairs, or every gene, measured slower at config D: rank
+    // 22.6 / 29.0 / 31.9 vs 20.2 ms, round 6)
     constexpr int mfma_min = 512;  // the tested-pair count past which a gene goes there
     const int hi[4] = {128, 256, 512, 1024};
     const bool mfma = L->rw_mfma && L->K <= 64 && (L->rw_mfma == 2 || 64 * L->rw_slots > mfma_min);
@@ -3435,10 +3105,15 @@ static hipError_t rank_waves_launches(const ScRankLaunch* L, int grid, SideStrea
         M.wv_filter = L->rw_mfma == 2 ? 0 : 1;
         M.wv_lo = mfma_min;
         st = place(4);
-        if (L->K <= 32)
-            hipLaunchKernelGGL(k_rank_mfma<1>, dim3(grid), dim3(256), 0, st, M);
+        M.wv_hi = 1 << 30;
+        if (L->K <= 16)
+            hipLaunchKernelGGL(k_rank_mfma16<1>, dim3(grid), dim3(256), 0, st, M);
+        else if (L->K <= 32)
+            hipLaunchKernelGGL(k_rank_mfma16<2>, dim3(grid), dim3(256), 0, st, M);
+        else if (L->K <= 48)
+            hipLaunchKernelGGL(k_rank_mfma16<3>, dim3(grid), dim3(256), 0, st, M);
         else
-            hipLaunchKernelGGL(k_rank_mfma<2>, dim3(grid), dim3(256), 0, st, M);
+            hipLaunchKernelGGL(k_rank_mfma16<4>, dim3(grid), dim3(256), 0, st, M);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess || L->rw_mfma == 2) return e;
     }

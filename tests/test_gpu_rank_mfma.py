@@ -1,4 +1,4 @@
-"""The wave buckets' pair counts on the int8 matrix cores (k_rank_mfma, K <= 64)
+"""The wave buckets' pair counts on the int8 matrix cores (k_rank_mfma16, K <= 64)
 against the per-pair slot kernel (k_rank_waves, SCC_RANK_MFMA=0), every gene on
 the matrix cores (SCC_RANK_MFMA=2; by default only genes past 512 tested pairs): the same
 integers (U for every pair and gene, and the p-values, which carry the tie
@@ -38,8 +38,8 @@ def test_mfma_matches_slot_kernel(eng, K, decimals, monkeypatch):
     Kc = len(names)
     ds = eng.dataset_csc(d.indptr, d.indices, d.data, d.G, d.N)
     res = {}
-    # every gene on the 32-wide matrix-core kernel / the genes past 512 pairs /
-    # none; "16": the 16-wide kernel (K <= 32) for the genes the slot kernels take
+    # every gene on the matrix-core kernel / the genes past 512 pairs /
+    # none; "16": the matrix cores (K <= 32) also for the genes the slot kernels take
     for flag in ("2", "1", "0", "16"):
         monkeypatch.setenv("SCC_RANK_MFMA", "1" if flag == "16" else flag)
         monkeypatch.setenv("SCC_RANK_MFMA16", "1" if flag == "16" else "0")  # (default: on at K <= 16)
