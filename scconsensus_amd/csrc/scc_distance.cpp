@@ -120,12 +120,15 @@ static int stream_to_host(scc_ctx* c, int64_t N, int64_t col_lo, int64_t col_hi,
     bool pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost;
     (void)hipGetLastError();
     const auto t0 = std::chrono::steady_clock::now();
-    // a large pageable buffer (R's allocVector): registered with the runtime
-    // for the call (page-locked in place, mapped for k_d2h) instead of going
-    // through the staging ring and a host memcpy; SCC_DIST_REGISTER=0 keeps
-    // the ring
+    // SCC_DIST_REGISTER=1: a large pageable buffer (R's allocVector) is
+    // registered with the runtime for the call (page-locked in place, mapped
+    // for k_d2h) instead of going through the staging ring and a host memcpy.
+    // Off by default: on a freshly allocated buffer (what R hands over) the
+    // registration faults in and locks every page first, and the cold call at
+    // config B took 164 ms against ~64 ms through the ring (round 6 bench,
+    // cold_call_ms)
     bool registered = false;
-    if (!pinned && total >= ((size_t)256 << 20) && env_int("SCC_DIST_REGISTER", 1) != 0) {
+    if (!pinned && total >= ((size_t)256 << 20) && env_int("SCC_DIST_REGISTER", 0) != 0) {
         registered = hipHostRegister(host, total, hipHostRegisterMapped) == hipSuccess;
         if (!registered) (void)hipGetLastError();
         pinned = registered;

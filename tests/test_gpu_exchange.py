@@ -256,9 +256,9 @@ def test_streamed_output_matches_device(eng, cfg_a, metric, f32, kernel_copy, mo
 
 @pytest.mark.parametrize("register", ["1", "0"])
 def test_large_pageable_output_registered(eng, register, monkeypatch):
-    """A pageable output of >= 256 MB (R's allocVector at scale) is registered
-    with the runtime for the call and written directly by k_d2h
-    (SCC_DIST_REGISTER=0: the staging ring); both bit-identical to the
+    """A pageable output of >= 256 MB (R's allocVector at scale) through the
+    staging ring (the default) or registered with the runtime for the call and
+    written directly by k_d2h (SCC_DIST_REGISTER=1); both bit-identical to the
     device output, the buffer's neighbours untouched (one element off the
     16-B alignment, as inside an R vector)."""
     monkeypatch.setenv("SCC_DIST_REGISTER", register)
