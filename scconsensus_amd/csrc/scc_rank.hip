@@ -200,9 +200,9 @@ extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t 
 #define SPLIT_BIG 32768
 // split gene i of split_count(A) (the large ones first)
 __device__ inline int split_count(const ScRankLaunch& A) { return A.counts[3] + A.counts[13]; }
-__device__ inline int split_gene_at(const ScRankLaunch& A, int i)
+// (nbig = A.counts[13], read once by the caller)
+__device__ inline int split_gene_at(const ScRankLaunch& A, int nbig, int i)
 {
-    const int nbig = A.counts[13];
     return i < nbig ? A.split_genes[A.G - 1 - i] : A.split_genes[i - nbig];
 }
 
@@ -1351,16 +1351,16 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     SplitLds& L = *(SplitLds*)smem;
-    const int cnt = split_count(A);
+    const int cnt = split_count(A), nbig = A.counts[13];
     for (;;) {  // genes from a queue (their sizes vary by orders of magnitude)
         if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[6], 1);
         __syncthreads();
         const int i = L.next;
         if (i >= cnt) break;
         const u64 t0 = A.dbg >= 9 ? __builtin_amdgcn_s_memtime() : 0;
-        split_one_gene(A, split_gene_at(A, i), L);
+        split_one_gene(A, split_gene_at(A, nbig, i), L);
         if (A.dbg >= 9 && threadIdx.x == 0 && i < SPLIT_DIAG_MAX) {
-            const int g = split_gene_at(A, i);
+            const int g = split_gene_at(A, nbig, i);
             g_split_diag[i][0] = (unsigned long long)(A.gstart[g + 1] - A.gstart[g]);
             g_split_diag[i][1] = __builtin_amdgcn_s_memtime() - t0;
         }
@@ -2801,7 +2801,7 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 {
     const int lane = threadIdx.x & 63;
     const int W = blockIdx.x * 4 + scc_wave_id(), NW = gridDim.x * 4;
-    const int ng = SEG ? A.counts[10] : split_count(A), P = A.P;
+    const int ng = SEG ? A.counts[10] : split_count(A), P = A.P, nbig = A.counts[13];
     for (int f = W; f < ng * P; f += NW) {
         const int gi = f / P, p = f - gi * P;
         int g, bk0, nb;
@@ -2811,7 +2811,7 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
             bk0 = sg.y;
             nb = sg.z;
         } else {
-            g = split_gene_at(A, gi);
+            g = split_gene_at(A, nbig, gi);
             bk0 = A.gene_bk[2 * g];
             nb = A.gene_bk[2 * g + 1];
         }
@@ -2867,7 +2867,7 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
     __shared__ u32 carry[XC_KC];
     constexpr int NPART = XC_T / XC_KC, RPP = XC_Q / NPART;  // column-scan parts, rows per part
     const int tid = threadIdx.x, K = A.K, G = A.G, P = A.P;
-    const int ng = SEG ? A.counts[10] : split_count(A);
+    const int ng = SEG ? A.counts[10] : split_count(A), nbig = A.counts[13];
     for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
         int g, bk0, nb;
         if (SEG) {
@@ -2876,7 +2876,7 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
             bk0 = sg.y;
             nb = sg.z;
         } else {
-            g = split_gene_at(A, gi);
+            g = split_gene_at(A, nbig, gi);
             bk0 = A.gene_bk[2 * g];
             nb = A.gene_bk[2 * g + 1];
         }
