@@ -651,7 +651,7 @@ __global__ void __launch_bounds__(256) k_de_clear(int* __restrict__ err, int* __
 {
     const long long t = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
     if (t < 4) err[t] = 0;
-    if (t < 16) counts[t] = 0;
+    if (t < SCC_NCOUNTS) counts[SCC_CNT_STRIDE * t] = 0;
     if (acc && glo == 0 && ghi == G) {
         typedef unsigned long long u2v __attribute__((ext_vector_type(2)));
         for (long long e = t; e < acc_n / 2; e += stride) ((u2v*)acc)[e] = u2v{0ull, 0ull};

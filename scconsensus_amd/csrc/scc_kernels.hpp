@@ -18,6 +18,13 @@
 
 struct dd;
 
+// The rank stage's work counters (ScRankLaunch::counts, 16 of them) sit
+// SCC_CNT_STRIDE ints apart, one 128-B line each: every split workgroup adds
+// to several of them per gene, and on one shared line the atomics (and any
+// load of a neighbour) queued behind each other in L2.
+#define SCC_NCOUNTS 16
+#define SCC_CNT_STRIDE 32
+
 struct ScStatsLaunch {
     const long long* gstart;
     const unsigned long long* keys;

@@ -199,8 +199,8 @@ extern "C" hipError_t scc_launch_gene_stats(const ScStatsLaunch* L, hipStream_t 
 // counts: [0] small items, [1] medium items, [2] global-memory items, [3] split genes
 #define SPLIT_BIG 32768
 // split gene i of split_count(A) (the large ones first)
-__device__ inline int split_count(const ScRankLaunch& A) { return A.counts[3] + A.counts[13]; }
-// (nbig = A.counts[13], read once by the caller)
+__device__ inline int split_count(const ScRankLaunch& A) { return A.counts[SCC_CNT_STRIDE * (3)] + A.counts[SCC_CNT_STRIDE * (13)]; }
+// (nbig = A.counts[SCC_CNT_STRIDE * (13)], read once by the caller)
 __device__ inline int split_gene_at(const ScRankLaunch& A, int nbig, int i)
 {
     return i < nbig ? A.split_genes[A.G - 1 - i] : A.split_genes[i - nbig];
@@ -231,9 +231,9 @@ __global__ void k_rank_classify(ScRankLaunch A)
     // the split's queue runs longest first, so a gene shard's largest genes
     // are not its tail)
     if (n >= SPLIT_BIG)
-        A.split_genes[A.G - 1 - atomicAdd(&A.counts[13], 1)] = g;
+        A.split_genes[A.G - 1 - atomicAdd(&A.counts[SCC_CNT_STRIDE * (13)], 1)] = g;
     else
-        A.split_genes[atomicAdd(&A.counts[3], 1)] = g;
+        A.split_genes[atomicAdd(&A.counts[SCC_CNT_STRIDE * (3)], 1)] = g;
 }
 
 extern "C" hipError_t scc_launch_rank_classify(const ScRankLaunch* L, hipStream_t st)
@@ -856,7 +856,7 @@ template <int T, bool GLOBALMEM, int KPT>
 __global__ void __launch_bounds__(T, 4) k_rank_item(ScRankLaunch A, int cls)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int cnt = A.counts[cls];
+    const int cnt = A.counts[SCC_CNT_STRIDE * (cls)];
     for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
         const ScRankItem it = A.items[(size_t)cls * A.item_cap + i];
         rank_one_item<T, GLOBALMEM, KPT>(A, it, i + A.stamp_base[cls], smem);
@@ -1107,7 +1107,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
         if (tid == SP_T - 1) {
             L.nb = (int)(b + v);
             L.boff[b + v] = (u32)n;
-            L.bk0 = atomicAdd(&A.counts[5], (int)(b + v));
+            L.bk0 = atomicAdd(&A.counts[SCC_CNT_STRIDE * (5)], (int)(b + v));
             A.gene_bk[2 * g] = L.bk0;
             A.gene_bk[2 * g + 1] = (int)(b + v);
         }
@@ -1305,13 +1305,13 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
     }
     __syncthreads();
     if (tid == 0) {
-        L.wav0 = L.nwav ? atomicAdd(&A.counts[4], L.nwav) : 0;
+        L.wav0 = L.nwav ? atomicAdd(&A.counts[SCC_CNT_STRIDE * (4)], L.nwav) : 0;
         L.fat0 = -1;
         if (L.nfat) {
-            const int f0 = atomicAdd(&A.counts[8], L.nfat);
+            const int f0 = atomicAdd(&A.counts[SCC_CNT_STRIDE * (8)], L.nfat);
             if (f0 + L.nfat <= A.fat_cap) {
                 L.fat0 = f0;
-                A.fatg[atomicAdd(&A.counts[11], 1)] = int4{g, f0, L.nfat, 0};
+                A.fatg[atomicAdd(&A.counts[SCC_CNT_STRIDE * (11)], 1)] = int4{g, f0, L.nfat, 0};
             }
         }
         L.nfat = 0;
@@ -1336,7 +1336,7 @@ __device__ void split_one_gene(const ScRankLaunch& A, int g, SplitLds& L)
             A.fatbk[L.fat0 + atomicAdd(&L.nfat, 1)] = itm;
         } else {
             const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
-            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[SCC_CNT_STRIDE * (cls)], 1)] = itm;
         }
     }
     __syncthreads();
@@ -1351,9 +1351,9 @@ __global__ void __launch_bounds__(SP_T) k_rank_split(ScRankLaunch A)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     SplitLds& L = *(SplitLds*)smem;
-    const int cnt = split_count(A), nbig = A.counts[13];
+    const int cnt = split_count(A), nbig = A.counts[SCC_CNT_STRIDE * (13)];
     for (;;) {  // genes from a queue (their sizes vary by orders of magnitude)
-        if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[6], 1);
+        if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[SCC_CNT_STRIDE * (6)], 1);
         __syncthreads();
         const int i = L.next;
         if (i >= cnt) break;
@@ -1419,7 +1419,7 @@ struct ResplitLds {
 // re-split level (k_rank_resplit_w with rs_level 1) while its list has room.
 __device__ inline bool push_fat2(const ScRankLaunch& A, const ScRankItem& itm)
 {
-    const int f = atomicAdd(&A.counts[12], 1);
+    const int f = atomicAdd(&A.counts[SCC_CNT_STRIDE * (12)], 1);
     if (f >= A.fat2_cap) return false;
     A.fat2[f] = itm;
     return true;
@@ -1543,7 +1543,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
         if (tid == RS_T - 1) {
             L.nb = (int)b;
             L.boff[b] = (u32)n;
-            const int bk0 = atomicAdd(&A.counts[5], (int)b);
+            const int bk0 = atomicAdd(&A.counts[SCC_CNT_STRIDE * (5)], (int)b);
             L.ovf = bk0 + (int)b > A.bucket_cap;
             L.bk0 = bk0;
         }
@@ -1554,7 +1554,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
     if (L.ovf) {  // out of bucket ids: rank the parent as one LDS item
         if (tid == 0) {
             const int cls = (n <= A.cap_s) ? 0 : ((n <= A.cap_m) ? 1 : 2);
-            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = it;
+            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[SCC_CNT_STRIDE * (cls)], 1)] = it;
         }
         return;
     }
@@ -1600,7 +1600,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
             u32 t = 0;
             for (int v = 0; v < W; ++v) t += L.wsum[v];
             L.nw = (int)t;
-            L.w0 = t ? atomicAdd(&A.counts[4], (int)t) : 0;
+            L.w0 = t ? atomicAdd(&A.counts[SCC_CNT_STRIDE * (4)], (int)t) : 0;
         }
         __syncthreads();
         u32 o = (u32)L.w0;
@@ -1625,7 +1625,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
                         // still > 64 distinct values: a second re-split level
                     } else {
                         const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
-                        A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+                        A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[SCC_CNT_STRIDE * (cls)], 1)] = itm;
                     }
                 }
             }
@@ -1635,7 +1635,7 @@ __device__ void resplit_one(const ScRankLaunch& A, const ScRankItem it, ResplitL
     }
     RSTAMP(3);
     if (!hist_lds) {  // many sub-buckets: k_rank_cross_seg adds the in-parent cross term
-        if (tid == 0) A.rsseg[atomicAdd(&A.counts[10], 1)] = int4{g, bk0, nb, 0};
+        if (tid == 0) A.rsseg[atomicAdd(&A.counts[SCC_CNT_STRIDE * (10)], 1)] = int4{g, bk0, nb, 0};
         return;
     }
     // in-parent cross term: S_ab += sum_s hs[s][a] * bs[s][b], bs = #(b in
@@ -1675,7 +1675,7 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
     // (8 B x 66 at config B, x 4950 at E), so no gene falls back to one global
     // atomic per (parent, pair)
     extern __shared__ __attribute__((aligned(16))) u64 racc[];
-    const int ng = A.counts[11];
+    const int ng = A.counts[SCC_CNT_STRIDE * (11)];
     // work items from a queue: slice sl of gene i takes the gene's parents
     // ge.y + sl, ge.y + sl + RS_SLICES, ... (a contiguous run of fatbk), so the
     // large parents of one heavy gene spread over RS_SLICES workgroups (one
@@ -1683,7 +1683,7 @@ __global__ void __launch_bounds__(RS_T) k_rank_resplit(ScRankLaunch A)
     // for 1/8 of config D's genes as for all of them).  Every slice adds its
     // in-parent cross terms with integer atomics: order-free.
     for (;;) {
-        if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[9], 1);
+        if (threadIdx.x == 0) L.next = atomicAdd(&A.counts[SCC_CNT_STRIDE * (9)], 1);
         __syncthreads();
         const int wi = L.next;
         if (wi >= ng * RS_SLICES) break;
@@ -1745,7 +1745,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
     ResplitWLds& L = Ls[wv];
     const int K = A.K;
     const ScRankItem* list = A.rs_level ? A.fat2 : A.fatbk;
-    const int cnt = A.rs_level ? min(A.counts[12], A.fat2_cap) : min(A.counts[8], A.fat_cap);
+    const int cnt = A.rs_level ? min(A.counts[SCC_CNT_STRIDE * (12)], A.fat2_cap) : min(A.counts[SCC_CNT_STRIDE * (8)], A.fat_cap);
     constexpr int EPL = RSW_CAP / 64, BPL = RSW_BINS / 64;
     // Bucket ids and wave-list slots come from wave-private chunks: one global
     // atomic per chunk, not per parent (same-address atomics serialise in L2:
@@ -1893,7 +1893,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
         if (nb > id_end - id_cur) {
             const int grab = max(nb, 2 * chunk);
             int b0 = 0;
-            if (lane == 0) b0 = atomicAdd(&A.counts[5], grab);
+            if (lane == 0) b0 = atomicAdd(&A.counts[SCC_CNT_STRIDE * (5)], grab);
             b0 = __shfl(b0, 0, 64);
             ovf = b0 + grab > A.bucket_cap;
             id_cur = b0;
@@ -1904,7 +1904,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
         if (ovf) {  // out of bucket ids: rank the parent as one LDS item
             if (lane == 0) {
                 const int cls = (n <= A.cap_s) ? 0 : ((n <= A.cap_m) ? 1 : 2);
-                A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = it;
+                A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[SCC_CNT_STRIDE * (cls)], 1)] = it;
             }
             continue;
         }
@@ -1944,7 +1944,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
                 fill_null(sl_cur, sl_end);
                 const int grab = max((int)cw, chunk);
                 int s0 = 0;
-                if (lane == 0) s0 = atomicAdd(&A.counts[4], grab);
+                if (lane == 0) s0 = atomicAdd(&A.counts[SCC_CNT_STRIDE * (4)], grab);
                 s0 = __shfl(s0, 0, 64);
                 if (s0 + grab > A.bucket_cap) {  // list full: these sub-buckets go to the LDS items
                     fill_null(min(s0, A.bucket_cap), A.bucket_cap);
@@ -1980,7 +1980,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
                             // still > 64 distinct values: a second re-split level
                         } else {
                             const int cls = (c <= A.cap_s) ? 0 : ((c <= A.cap_m) ? 1 : 2);
-                            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[cls], 1)] = itm;
+                            A.items[(size_t)cls * A.item_cap + atomicAdd(&A.counts[SCC_CNT_STRIDE * (cls)], 1)] = itm;
                         }
                     }
                 }
@@ -1988,7 +1988,7 @@ __global__ void __launch_bounds__(256) k_rank_resplit_w(ScRankLaunch A)
             }
         }
         if (!hist_lds) {  // many sub-buckets: k_rank_cross_seg adds the in-parent cross term
-            if (lane == 0) A.rsseg[atomicAdd(&A.counts[10], 1)] = int4{g, bk0, nb, 0};
+            if (lane == 0) A.rsseg[atomicAdd(&A.counts[SCC_CNT_STRIDE * (10)], 1)] = int4{g, bk0, nb, 0};
             continue;
         }
         for (int c = lane; c < K; c += 64) {
@@ -2144,7 +2144,7 @@ __global__ void __launch_bounds__(256) k_rank_waves(ScRankLaunch A)
     __shared__ u64 cms[4][SCC_MAX_K];  // per-wave cluster masks (K > 16)
     const int lane = threadIdx.x & 63, wv = scc_wave_id();
     const int W = blockIdx.x * 4 + wv, NW = gridDim.x * 4;
-    const int cnt = min(A.counts[4], A.bucket_cap);
+    const int cnt = min(A.counts[SCC_CNT_STRIDE * (4)], A.bucket_cap);
     const int K = A.K, G = A.G, P = A.P;
     constexpr int CH = 16;  // consecutive buckets per wave visit (gene locality; 8 / 32 / 64 measured no better)
     int cur = -1, ntp = 0;
@@ -2493,7 +2493,7 @@ __global__ void __launch_bounds__(256, NC >= 3 ? 2 : 1) k_rank_mfma16(ScRankLaun
     RkWaveLds& Lw = Ls[wv];
     u32* buf = Lbuf[wv];
     const int NW = gridDim.x * 4, W = blockIdx.x * 4 + wv;
-    const int cnt = min(A.counts[4], A.bucket_cap);
+    const int cnt = min(A.counts[SCC_CNT_STRIDE * (4)], A.bucket_cap);
     const int K = A.K, G = A.G, P = A.P;
     const int CH = max(16, min(512, cnt / (4 * NW)));
     const int g4 = lane >> 4, r16 = lane & 15;
@@ -2801,7 +2801,7 @@ __global__ void __launch_bounds__(256) k_rank_cross(ScRankLaunch A)
 {
     const int lane = threadIdx.x & 63;
     const int W = blockIdx.x * 4 + scc_wave_id(), NW = gridDim.x * 4;
-    const int ng = SEG ? A.counts[10] : split_count(A), P = A.P, nbig = A.counts[13];
+    const int ng = SEG ? A.counts[SCC_CNT_STRIDE * (10)] : split_count(A), P = A.P, nbig = A.counts[SCC_CNT_STRIDE * (13)];
     for (int f = W; f < ng * P; f += NW) {
         const int gi = f / P, p = f - gi * P;
         int g, bk0, nb;
@@ -2867,7 +2867,7 @@ __global__ void __launch_bounds__(XC_T) k_rank_cross_gene(ScRankLaunch A)
     __shared__ u32 carry[XC_KC];
     constexpr int NPART = XC_T / XC_KC, RPP = XC_Q / NPART;  // column-scan parts, rows per part
     const int tid = threadIdx.x, K = A.K, G = A.G, P = A.P;
-    const int ng = SEG ? A.counts[10] : split_count(A), nbig = A.counts[13];
+    const int ng = SEG ? A.counts[SCC_CNT_STRIDE * (10)] : split_count(A), nbig = A.counts[SCC_CNT_STRIDE * (13)];
     for (int gi = blockIdx.x; gi < ng; gi += gridDim.x) {
         int g, bk0, nb;
         if (SEG) {

@@ -673,7 +673,7 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         d_gexp = (dd*)((char*)p + sizeof(double) * 2 * nwaves);
     }
     WS("splitg", (size_t)G, d_splitg);
-    WS("counts", 16, d_counts);
+    WS("counts", SCC_NCOUNTS * SCC_CNT_STRIDE, d_counts);
     WS("err", 4, d_err);
     WS("mx", GK, d_mx);
     WS("me", GK, d_me);
@@ -718,6 +718,14 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     WS("nu", 4, d_nu);
     if ((rc = ensure_wtab(c, exact_test_max_size(nclu)))) return rc;
     hipStream_t s0 = c->s0, s1 = c->s1;
+    // the rank stage's work counters on the host (diagnostics; synchronises s0)
+    auto read_counts = [&](int* h) -> hipError_t {
+        int t[SCC_NCOUNTS * SCC_CNT_STRIDE];
+        hipError_t e = hipMemcpyAsync(t, d_counts, sizeof(t), hipMemcpyDeviceToHost, s0);
+        if (e == hipSuccess) e = hipStreamSynchronize(s0);
+        for (int i = 0; i < SCC_NCOUNTS; ++i) h[i] = t[i * SCC_CNT_STRIDE];
+        return e;
+    };
     c->generation++;
     const int* d_perm = d_tab;
     const int* d_ccp0 = d_tab + o_ccp0;
@@ -970,9 +978,8 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         const int ncu = c->n_cu > 0 ? c->n_cu : 256;
         HIPCHK(c, scc_launch_rank_split(&L, 2 * ncu, s0));
         if (L.dbg >= 9) {  // per-gene split clocks (diagnostic; 10: without the unstaged stores)
-            int hc[16];
-            HIPCHK(c, hipMemcpyAsync(hc, d_counts, sizeof(hc), hipMemcpyDeviceToHost, s0));
-            HIPCHK(c, hipStreamSynchronize(s0));
+            int hc[SCC_NCOUNTS];
+            HIPCHK(c, read_counts(hc));
             scc_rank_split_diag(s0, hc[3] + hc[13]);  // (small split genes + large ones)
         }
         if (stamps) {  // re-split phase clocks (summed over parents): 8 u64 after the item stamps
@@ -1023,18 +1030,16 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
         HIPCHK(c, scc_launch_rank_cross(&L, 4 * ncu, s0));
         HIPCHK(c, scc_launch_rank_cross_seg(&L, 4 * ncu, s0));
         if (env_int("SCC_RANK_LOG", 0)) {  // diagnostic: the rank stage's work lists
-            int h[16];
-            HIPCHK(c, hipMemcpyAsync(h, d_counts, sizeof(h), hipMemcpyDeviceToHost, s0));
-            HIPCHK(c, hipStreamSynchronize(s0));
+            int h[SCC_NCOUNTS];
+            HIPCHK(c, read_counts(h));
             fprintf(stderr, "[scc rank] items %d/%d/%d split genes %d wave buckets %d bucket ids %d parents %d "
                     "segments %d second-level %d\n", h[0], h[1], h[2], h[3] + h[13], h[4], h[5], h[8], h[10], h[12]);
         }
         if (stamps) {
             std::vector<unsigned long long> h((size_t)3 * item_cap * 8);
-            int cnts[4];
+            int cnts[SCC_NCOUNTS];
             HIPCHK(c, hipMemcpyAsync(h.data(), st_buf, h.size() * 8, hipMemcpyDeviceToHost, s0));
-            HIPCHK(c, hipMemcpyAsync(cnts, d_counts, sizeof(cnts), hipMemcpyDeviceToHost, s0));
-            HIPCHK(c, hipStreamSynchronize(s0));
+            HIPCHK(c, read_counts(cnts));
             const char* ph[] = {"setup", "sort", "fixup+codes", "partition", "pairs", "ties"};
             fprintf(stderr, "[scc stamps] split genes %d\n", cnts[3]);
             for (int cls = 0; cls < 3; ++cls) {
