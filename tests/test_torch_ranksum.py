@@ -35,3 +35,18 @@ def test_checker_matches_brute_force():
         bu, bt = _brute(X, code, K)
         np.testing.assert_array_equal(u2.numpy(), bu)
         np.testing.assert_array_equal(ties.numpy(), bt)
+
+
+def test_packed_max_err_walks_every_entry():
+    """The full-vector `dist` checker against scipy's condensed order (= R's
+    packed column-major lower triangle), with a planted error found."""
+    from scipy.spatial.distance import pdist
+    rng = np.random.default_rng(3)
+    S = rng.standard_normal((301, 5))
+    N = S.shape[0]
+    out = torch.from_numpy(pdist(S))
+    St = torch.from_numpy(S)
+    fn = TR.euclid_block(St)  # noqa: E731
+    assert TR.packed_max_err(out, fn, N, cols=37) < 1e-12
+    out[N * (N - 1) // 2 - 1] += 0.5  # the last entry: (N-1, N-2)
+    assert abs(TR.packed_max_err(out, fn, N, cols=37) - 0.5) < 1e-9

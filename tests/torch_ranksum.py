@@ -14,7 +14,11 @@ For a gene g and clusters a < b over all cells of a and b (zeros included):
         = F_a + F_b + 3 (Y_ab + Y_ba) + (z_a + z_b)^3 - (z_a + z_b)
   F_a   = sum over groups (t_a^3 - t_a),  Y_ab = sum over groups t_a^2 t_b
 (pos: stored values, all > 0 here; z = cluster size - pos).  Every sum is an
-exact integer (int64)."""
+exact integer (int64).
+
+Also `packed_max_err`: the max error over EVERY entry of a packed `dist`
+vector against fp64 values formed block by block on the GPU (the large
+configurations' distances, checked in full rather than sampled)."""
 import time
 
 import torch
@@ -108,3 +112,42 @@ def pair_stats(indptr, cols, vals, code, K, max_chunk=16 << 20):
         ties[g0:g1] = Fg[:, ia] + Fg[:, ib] + 3 * X + zs * zs * zs - zs
         g0 = g1
     return u2, ties
+
+
+def packed_max_err(out, block_fn, N, cols=256):
+    """Max |out - want| over EVERY entry of a packed `dist` vector on the GPU
+    (R's column-major lower triangle: column j holds rows j+1 .. N-1).
+    block_fn(j0, j1) returns the [j1 - j0, N] fp64 block of wanted values
+    (row r = column j0 + r against every cell); only its entries below the
+    diagonal are compared, in packed order."""
+    dev = out.device
+    ar = torch.arange(N, device=dev)
+    worst = 0.0
+    for j0 in range(0, N - 1, cols):
+        j1 = min(N - 1, j0 + cols)
+        lo = j0 * (2 * N - j0 - 1) // 2
+        hi = j1 * (2 * N - j1 - 1) // 2
+        want = block_fn(j0, j1)
+        mask = ar.view(1, -1) > (j0 + torch.arange(j1 - j0, device=dev)).view(-1, 1)
+        got = out[lo:hi].to(torch.float64)
+        e = (got - want[mask]).abs()
+        m = float(e.max())
+        if m > worst and m > 1e-5 and worst <= 1e-5:  # the first bad block: where (diagnostics)
+            k = int(e.argmax())
+            print(f"[packed_max_err] columns {j0}..{j1}: entry {lo + k} off by {m:.3g} "
+                  f"(got {float(got[k]):.6g}, want {float(want[mask][k]):.6g})", flush=True)
+        worst = max(worst, m)
+    return worst
+
+
+def euclid_block(St):
+    """block_fn for packed_max_err: Euclidean distances of the score rows
+    j0 .. j1-1 to every row, summed component by component in fp64 (no
+    matrix-product shortcut)."""
+    def fn(j0, j1):
+        acc = None
+        for q in range(St.shape[1]):
+            d = St[j0:j1, q].view(-1, 1) - St[:, q].view(1, -1)
+            acc = d * d if acc is None else acc + d * d
+        return torch.sqrt(acc)
+    return fn
