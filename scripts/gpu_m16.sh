@@ -1,4 +1,4 @@
-# matrix-core rank kernel variants: rank parity, then bench lines (round 6 experiment)
+# matrix-core rank kernel: rank parity, then bench lines at D SLOW, D (default and every gene on the matrix cores), C (and the 16-wide kernel for the slot genes), B
 set -u
 mkdir -p gpurun_out/m16
 export TMPDIR=/tmp
@@ -14,8 +14,6 @@ D="python bench.py --config D --no-cpu-baseline --no-transfers --no-pearson --st
 C="python bench.py --config C --no-cpu-baseline --no-transfers --no-pearson --steps 3 --warmup 1"
 run dslow python bench.py --config D --de slow --no-cpu-baseline --no-transfers --no-pearson --steps 2 --warmup 1
 run d $D
-SCC_TMP_MMIN=256 run d_mmin256 $D
-SCC_TMP_MMIN=128 run d_mmin128 $D
 SCC_RANK_MFMA=2 run d_all $D
 run c $C
 SCC_RANK_MFMA16=1 run c_m16 $C
