@@ -376,7 +376,7 @@ __global__ void __launch_bounds__(256) k_ing_colapply(u32* __restrict__ cnt, int
 
 #define SC_GT 256       // genes per tile
 #define SC_CAP 4096     // default staged entries per round (u64 key + u16 gene = 10 B each): 3 blocks per CU
-#define SC_CMAX 128     // cells per scatter chunk (kScatterCC * kCountChunk)
+#define SC_CMAX 256     // cells per scatter chunk (kScatterCC * kCountChunk; <= ING_T: a thread per cell)
 #define SC_RUN 8        // consecutive gene tiles of one chunk dealt to one XCD (SCC_SC_RUN)
 
 template <bool DENSE, int U>

@@ -25,7 +25,7 @@ constexpr int kCapSmall = 2048;    // rank work item in LDS, 256 threads
 constexpr int kCapMedium = 16384;  // rank work item in LDS, 1024 threads (capped by the LDS budget);
                                    // larger genes are split into value buckets
 constexpr int kCountChunk = 32;    // cells per ingest count chunk (one cluster each)
-constexpr int kScatterCC = 4;      // count chunks per ingest scatter chunk
+constexpr int kScatterCC = 8;      // count chunks per ingest scatter chunk (at most)
 constexpr int kSelectCap = 2048;   // per-pair records sorted in LDS
 constexpr int kUnionCap = 4096;
 constexpr int kMaxK = SCC_MAX_K;  // 7-bit cluster codes in the rank kernels: clusters per engine run

@@ -592,12 +592,13 @@ static int de_run_body(scc_ctx* c, const scc_dataset* ds, const int32_t* code, i
     std::vector<int> cc_p0, cc_code, sc_cc0, cl_cc(K + 1);
     // scatter chunks of 2 count chunks (64 cells) when a cell has >= 16 stored
     // values per gene tile (config B / D: ~29; ingest B 0.45 -> 0.40 ms, D 5.97
-    // -> 5.79), else 4 (config E: ~8 per tile, where 64-cell chunks left the
-    // workgroups too little work: 12.7 -> 16.5 ms); SCC_SC_CC overrides
+    // -> 5.79), else 8 (config E: ~8 per tile, where small chunks leave the
+    // workgroups too little work for their fixed cost: 64 cells 16.5 ms, 128
+    // cells 12.0-12.2, 192 cells 11.0, 256 cells 10.4-10.5, round 6); SCC_SC_CC overrides
     const int64_t ntile_h = (ds->G + scc_ingest_gene_tile() - 1) / scc_ingest_gene_tile();
     const bool dense_tiles = ds->nnz >= 16 * (int64_t)std::max(1, N) * std::max<int64_t>(1, ntile_h);
     const int scatter_cc =
-        std::min(kScatterCC, std::max(1, env_int("SCC_SC_CC", dense_tiles ? kScatterCC / 2 : kScatterCC)));
+        std::min(kScatterCC, std::max(1, env_int("SCC_SC_CC", dense_tiles ? 2 : kScatterCC)));
     for (int a = 0; a < K; ++a) {
         cl_cc[a] = (int)cc_code.size();
         for (int p = start[a]; p < start[a + 1]; p += kCountChunk) {
