@@ -167,3 +167,22 @@ def test_transpose_rejects_unsorted_and_repeated_columns(eng):
     with pytest.raises(nat.SccError) as e:  # negative column
         eng.dataset_csr(np.array([0, 1, 2], np.int64), np.array([-1, 0], np.int32), vals[:2], 2, 4)
     assert e.value.code == nat.SCC_ERR_INVALID
+
+
+def test_transpose_at_the_gene_limit_and_past_it(eng):
+    """The transpose's largest gene count (262,144 = 1024 tiles of 256 genes:
+    include/scc.h) is exact; one gene more is refused with SCC_ERR_UNSUPPORTED."""
+    from scconsensus_amd import _native as nat
+    rng = np.random.default_rng(13)
+    G, N = 262_144, 3000
+    m = sp.random(G, N, density=2e-5, format="csr", random_state=rng, dtype=np.float64)
+    m.data = rng.standard_normal(m.nnz)
+    m = m.tolil()
+    m[G - 1, N - 1] = 7.0  # the last gene and cell are present
+    m[0, 0] = 3.0
+    m = sp.csr_matrix(m)
+    m.sort_indices()
+    _check_transpose(eng, m, G, N)
+    with pytest.raises(nat.SccError) as e:
+        eng.dataset_csr(np.zeros(G + 2, np.int64), np.zeros(0, np.int32), np.zeros(0), G + 1, N)
+    assert e.value.code == nat.SCC_ERR_UNSUPPORTED
