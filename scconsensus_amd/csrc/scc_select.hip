@@ -468,43 +468,70 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
     const int G = A.G;
     const size_t pb = (size_t)p * G;
     // 1) compact tested genes (gene order) into records (HBM scratch when
-    // they outgrow the LDS: counted first)
+    // they outgrow the LDS: counted first).  SLOW (every gene, no second key)
+    // sorts 16-B (p key, gene) records instead of 24-B rows, with the whole
+    // record LDS as their staging (4096 of them in the 2048-row budget): a
+    // pair's 20k genes at config D took 10 passes over 24-B records through
+    // HBM / L2, now 6 over 16-B ones.  Same order (p, then gene): same results.
     int m = 0;
     const bool fast = (A.mode == SCC_DE_FAST);
     RowRec* rec = (RowRec*)smem;
+    KeyRec* krec = (KeyRec*)smem;
+    int chk = 1;  // SLOW: KeyRec staging capacity (a power of two)
+    while (2 * chk * sizeof(KeyRec) <= (size_t)A.cap * (sizeof(RowRec) + sizeof(KeyRec))) chk *= 2;
     const int per = (G + T - 1) / T;
     {
         const int g0 = min(G, tid * per), g1 = min(G, g0 + per);
         int c = 0;
         for (int g = g0; g < g1; ++g) c += A.flags[pb + g] & 1;
         int o = block_excl_scan<T>(c, sc, m);
-        if (m > A.cap) rec = A.rec_scratch + pb;
+        if (fast && m > A.cap) rec = A.rec_scratch + pb;
+        if (!fast && m > chk) krec = A.key_scratch + pb;
         for (int g = g0; g < g1; ++g) {
             if (A.flags[pb + g] & 1) {
-                RowRec r;
-                r.k1 = p_key(A.p[pb + g]);
-                r.k2 = fast ? scc_key_of(-A.lfc[pb + g] + 0.0) : 0ull;
-                r.g = (u32)g;
-                r.pad = 0;
-                rec[o++] = r;
+                if (fast) {
+                    RowRec r;
+                    r.k1 = p_key(A.p[pb + g]);
+                    r.k2 = scc_key_of(-A.lfc[pb + g] + 0.0);
+                    r.g = (u32)g;
+                    r.pad = 0;
+                    rec[o++] = r;
+                } else {
+                    KeyRec r;
+                    r.k = p_key(A.p[pb + g]);
+                    r.g = (u32)g;
+                    r.pad = 0;
+                    krec[o++] = r;
+                }
             }
         }
     }
-    const bool big = m > A.cap;
     __syncthreads();
     // 2) sort into R's row order
-    if (big) {
-        AccAoS<RowRec> gacc{rec}, sacc{(RowRec*)smem};
-        block_bitonic_staged(gacc, m, sacc, A.cap, tid, T);
+    if (fast) {
+        if (m > A.cap) {
+            AccAoS<RowRec> gacc{rec}, sacc{(RowRec*)smem};
+            block_bitonic_staged(gacc, m, sacc, A.cap, tid, T);
+        } else {
+            AccAoS<RowRec> acc{rec};
+            block_bitonic(acc, m, tid, T);
+        }
     } else {
-        AccAoS<RowRec> acc{rec};
-        block_bitonic(acc, m, tid, T);
+        if (m > chk) {
+            AccAoS<KeyRec> gacc{krec}, sacc{(KeyRec*)smem};
+            block_bitonic_staged(gacc, m, sacc, chk, tid, T);
+        } else {
+            AccAoS<KeyRec> acc{krec};
+            block_bitonic(acc, m, tid, T);
+        }
     }
+    auto key_at = [&](int i) { return fast ? rec[i].k1 : krec[i].k; };
+    auto gene_at = [&](int i) { return fast ? rec[i].g : krec[i].g; };
     // 3) BH: non-NaN prefix length, then suffix-min of (n / rank) * p
     int mnn = 0;
     {
         int c = 0;
-        for (int i = tid; i < m; i += T) c += (rec[i].k1 != ~0ull);
+        for (int i = tid; i < m; i += T) c += (key_at(i) != ~0ull);
         int tot;
         block_excl_scan<T>(c, sc, tot);
         mnn = tot;
@@ -519,7 +546,7 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
         double pv = 0.0;
         u32 gg = 0;
         if (i < mnn) {
-            gg = rec[i].g;
+            gg = gene_at(i);
             pv = A.p[pb + gg];
             v = (nbh / (double)(i + 1)) * pv;
         }
@@ -551,7 +578,7 @@ __global__ void __launch_bounds__(T) k_pair_select(SelectArgs A)
     }
     for (int i = mnn + tid; i < m; i += T) {
         if (fast) A.row_q[A.row_off[p] + i] = NAN;
-        else A.slow_q[pb + rec[i].g] = NAN;
+        else A.slow_q[pb + gene_at(i)] = NAN;
     }
     __syncthreads();
     __threadfence_block();
